@@ -1,0 +1,278 @@
+// pybind11 bindings of the gfx950 kernels and HIP runtime helpers:
+// module ddl_amd._ddl_hip.
+//
+// Every device/host buffer crosses this boundary as a raw address (int) and
+// every launch takes an explicit hipStream_t handle (torch.cuda.Stream's
+// .cuda_stream); dtype/shape validation lives in ddl_amd/ops/kernels.py.
+// Keeping torch headers out of this TU keeps one HIP runtime (torch/lib's,
+// linked by path) and no libtorch ABI coupling.
+#include <errno.h>
+#include <hip/hip_runtime.h>
+#include <linux/futex.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "launch.h"
+
+namespace py = pybind11;
+
+namespace {
+
+void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+void check_rc(int rc, const char* what) {
+  if (rc == 0) return;
+  if (rc > 0) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(static_cast<hipError_t>(rc)));
+  throw std::invalid_argument(std::string(what) + ": unsupported arguments (code " + std::to_string(rc) + ")");
+}
+
+hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+template <typename T>
+T* as_ptr(uintptr_t a) {
+  return reinterpret_cast<T*>(a);
+}
+
+ddl::FeistelKeys make_keys(const std::vector<uint64_t>& k, uint64_t n, uint32_t half_bits) {
+  if (k.size() != ddl::kFeistelRounds) throw std::invalid_argument("feistel: need 6 round keys");
+  ddl::FeistelKeys f{};
+  for (int i = 0; i < ddl::kFeistelRounds; ++i) f.k[i] = k[i];
+  f.n = n;
+  f.half_bits = half_bits;
+  return f;
+}
+
+ddl::RowIndex make_index(int mode, uintptr_t idx, int64_t base, const std::vector<uint64_t>& keys, uint64_t n,
+                         uint32_t half_bits) {
+  ddl::RowIndex ri{};
+  ri.mode = mode;
+  ri.idx = as_ptr<const int64_t>(idx);
+  ri.base = base;
+  if (mode == 1 && !idx) throw std::invalid_argument("index mode 1 needs an index vector");
+  if (mode == 2) ri.keys = make_keys(keys, n, half_bits);
+  return ri;
+}
+
+ddl::Affine make_affine(const std::vector<float>& scale, const std::vector<float>& bias, int64_t plane) {
+  ddl::Affine a{};
+  if (scale.empty()) return a;
+  if (scale.size() != bias.size() || scale.size() > 8) throw std::invalid_argument("affine: 1..8 channels");
+  if (plane <= 0) throw std::invalid_argument("affine: plane must be > 0");
+  for (size_t i = 0; i < scale.size(); ++i) {
+    a.scale[i] = scale[i];
+    a.bias[i] = bias[i];
+  }
+  a.channels = static_cast<int32_t>(scale.size());
+  a.plane = plane;
+  a.enabled = 1;
+  return a;
+}
+
+// Host callback run by the HIP runtime once every prior op on the stream has
+// retired: hands a shm slot back to its producer (state store + futex wake).
+struct ReleaseReq {
+  std::atomic<uint32_t>* word;
+  uint32_t value;
+};
+
+void release_cb(void* p) {
+  auto* r = static_cast<ReleaseReq*>(p);
+  r->word->store(r->value, std::memory_order_release);
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(r->word), FUTEX_WAKE, INT32_MAX, nullptr, nullptr, 0);
+  delete r;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_ddl_hip, m) {
+  m.doc() = "ddl_amd gfx950 HIP kernels (permute/gather, collate, pad/pack, checksum) and HIP runtime helpers";
+
+  m.def("device_count", [] {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+  });
+  m.def("arch_name", [](int dev) {
+    hipDeviceProp_t p;
+    check(hipGetDeviceProperties(&p, dev), "hipGetDeviceProperties");
+    return std::string(p.gcnArchName);
+  });
+
+  // ---------------------------------------------------------------- memory
+  m.def(
+      "host_register",
+      [](uintptr_t addr, uint64_t bytes, bool mapped) {
+        unsigned flags = hipHostRegisterPortable | (mapped ? hipHostRegisterMapped : 0u);
+        py::gil_scoped_release nogil;
+        check(hipHostRegister(as_ptr<void>(addr), bytes, flags), "hipHostRegister");
+      },
+      py::arg("addr"), py::arg("bytes"), py::arg("mapped") = true);
+  m.def("host_unregister", [](uintptr_t addr) { check(hipHostUnregister(as_ptr<void>(addr)), "hipHostUnregister"); });
+  m.def("host_device_pointer", [](uintptr_t addr) {
+    void* d = nullptr;
+    check(hipHostGetDevicePointer(&d, as_ptr<void>(addr), 0), "hipHostGetDevicePointer");
+    return reinterpret_cast<uintptr_t>(d);
+  });
+  m.def("pointer_is_host_registered", [](uintptr_t addr) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, as_ptr<void>(addr)) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    return a.type == hipMemoryTypeHost;
+  });
+  m.def(
+      "memcpy_h2d",
+      [](uintptr_t dst, uintptr_t src, uint64_t bytes, uintptr_t stream) {
+        check(hipMemcpyAsync(as_ptr<void>(dst), as_ptr<const void>(src), bytes, hipMemcpyHostToDevice,
+                             as_stream(stream)),
+              "hipMemcpyAsync(H2D)");
+      },
+      py::arg("dst"), py::arg("src"), py::arg("bytes"), py::arg("stream"));
+  m.def(
+      "memcpy_d2h",
+      [](uintptr_t dst, uintptr_t src, uint64_t bytes, uintptr_t stream) {
+        check(hipMemcpyAsync(as_ptr<void>(dst), as_ptr<const void>(src), bytes, hipMemcpyDeviceToHost,
+                             as_stream(stream)),
+              "hipMemcpyAsync(D2H)");
+      },
+      py::arg("dst"), py::arg("src"), py::arg("bytes"), py::arg("stream"));
+  m.def(
+      "memcpy_d2d",
+      [](uintptr_t dst, uintptr_t src, uint64_t bytes, uintptr_t stream) {
+        check(hipMemcpyAsync(as_ptr<void>(dst), as_ptr<const void>(src), bytes, hipMemcpyDeviceToDevice,
+                             as_stream(stream)),
+              "hipMemcpyAsync(D2D)");
+      },
+      py::arg("dst"), py::arg("src"), py::arg("bytes"), py::arg("stream"));
+  m.def(
+      "enqueue_release",
+      [](uintptr_t state_word, uint32_t value, uintptr_t stream) {
+        auto* r = new ReleaseReq{as_ptr<std::atomic<uint32_t>>(state_word), value};
+        hipError_t e = hipLaunchHostFunc(as_stream(stream), release_cb, r);
+        if (e != hipSuccess) {
+          delete r;
+          check(e, "hipLaunchHostFunc");
+        }
+      },
+      py::arg("state_word"), py::arg("value"), py::arg("stream"),
+      "Store `value` into the shm slot state word (+ futex wake) once the stream reaches this point.");
+
+  // --------------------------------------------------------------- kernels
+  m.def(
+      "gather_rows",
+      [](uintptr_t dst, int out_dt, uintptr_t src, int in_dt, int64_t n_rows, int64_t row_elems, int mode,
+         uintptr_t idx, int64_t base, std::vector<uint64_t> keys, uint64_t n_domain, uint32_t half_bits,
+         std::vector<float> scale, std::vector<float> bias, int64_t plane, bool scatter, uintptr_t stream) {
+        const ddl::RowIndex ri = make_index(mode, idx, base, keys, n_domain, half_bits);
+        const ddl::Affine aff = make_affine(scale, bias, plane);
+        check_rc(ddl::gather_rows(as_ptr<void>(dst), out_dt, as_ptr<const void>(src), in_dt, n_rows, row_elems, ri,
+                                  aff, scatter ? 1 : 0, as_stream(stream)),
+                 "gather_rows");
+      },
+      py::arg("dst"), py::arg("out_dt"), py::arg("src"), py::arg("in_dt"), py::arg("n_rows"), py::arg("row_elems"),
+      py::arg("mode"), py::arg("idx"), py::arg("base"), py::arg("keys"), py::arg("n_domain"), py::arg("half_bits"),
+      py::arg("scale"), py::arg("bias"), py::arg("plane"), py::arg("scatter"), py::arg("stream"));
+  m.def(
+      "feistel_indices",
+      [](uintptr_t out, int64_t count, int64_t base, std::vector<uint64_t> keys, uint64_t n_domain,
+         uint32_t half_bits, uintptr_t stream) {
+        check_rc(ddl::feistel_indices(as_ptr<int64_t>(out), count, base, make_keys(keys, n_domain, half_bits),
+                                      as_stream(stream)),
+                 "feistel_indices");
+      },
+      py::arg("out"), py::arg("count"), py::arg("base"), py::arg("keys"), py::arg("n_domain"), py::arg("half_bits"),
+      py::arg("stream"));
+  m.def(
+      "collate_hwc_to_chw",
+      [](uintptr_t dst, int out_dt, uintptr_t src, int in_dt, int64_t batch, int64_t pixels, int channels, int mode,
+         uintptr_t idx, int64_t base, std::vector<uint64_t> keys, uint64_t n_domain, uint32_t half_bits,
+         std::vector<float> scale, std::vector<float> bias, uintptr_t stream) {
+        const ddl::RowIndex ri = make_index(mode, idx, base, keys, n_domain, half_bits);
+        const ddl::Affine aff = make_affine(scale, bias, pixels);
+        check_rc(ddl::collate_hwc_to_chw(as_ptr<void>(dst), out_dt, as_ptr<const void>(src), in_dt, batch, pixels,
+                                         channels, ri, aff, as_stream(stream)),
+                 "collate_hwc_to_chw");
+      },
+      py::arg("dst"), py::arg("out_dt"), py::arg("src"), py::arg("in_dt"), py::arg("batch"), py::arg("pixels"),
+      py::arg("channels"), py::arg("mode"), py::arg("idx"), py::arg("base"), py::arg("keys"), py::arg("n_domain"),
+      py::arg("half_bits"), py::arg("scale"), py::arg("bias"), py::arg("stream"));
+  m.def(
+      "split_columns",
+      [](std::vector<uintptr_t> dsts, std::vector<int> widths, int out_dt, uintptr_t src, int in_dt, int64_t n_rows,
+         int64_t n_values, int mode, uintptr_t idx, int64_t base, std::vector<uint64_t> keys, uint64_t n_domain,
+         uint32_t half_bits, uintptr_t stream) {
+        if (dsts.size() != widths.size() || dsts.empty() || dsts.size() > 8)
+          throw std::invalid_argument("split_columns: 1..8 groups");
+        ddl::SplitSpec sp{};
+        int64_t tot = 0;
+        for (size_t i = 0; i < dsts.size(); ++i) {
+          sp.dst[i] = as_ptr<void>(dsts[i]);
+          sp.width[i] = widths[i];
+          tot += widths[i];
+        }
+        if (tot != n_values) throw std::invalid_argument("split_columns: widths must sum to n_values");
+        sp.n_groups = static_cast<int32_t>(dsts.size());
+        sp.out_dt = out_dt;
+        const ddl::RowIndex ri = make_index(mode, idx, base, keys, n_domain, half_bits);
+        check_rc(ddl::split_columns(sp, as_ptr<const void>(src), in_dt, n_rows, n_values, ri, as_stream(stream)),
+                 "split_columns");
+      },
+      py::arg("dsts"), py::arg("widths"), py::arg("out_dt"), py::arg("src"), py::arg("in_dt"), py::arg("n_rows"),
+      py::arg("n_values"), py::arg("mode"), py::arg("idx"), py::arg("base"), py::arg("keys"), py::arg("n_domain"),
+      py::arg("half_bits"), py::arg("stream"));
+  m.def(
+      "pad_pack_tokens",
+      [](uintptr_t tokens, uintptr_t offsets, uintptr_t row_start, uintptr_t row_end, uintptr_t seg_offsets,
+         int64_t n_seg, uintptr_t out_tokens, uintptr_t attn_mask, uintptr_t position_ids, bool pos_is_i64,
+         uintptr_t segment_ids, int64_t rows, int64_t seq_len, int pad_id, int mode, uintptr_t stream) {
+        ddl::TokenSpec sp{};
+        sp.tokens = as_ptr<const int32_t>(tokens);
+        sp.offsets = as_ptr<const int64_t>(offsets);
+        sp.row_start = as_ptr<const int64_t>(row_start);
+        sp.row_end = as_ptr<const int64_t>(row_end);
+        sp.seg_offsets = as_ptr<const int64_t>(seg_offsets);
+        sp.n_seg = n_seg;
+        sp.out_tokens = as_ptr<int32_t>(out_tokens);
+        sp.attn_mask = as_ptr<uint8_t>(attn_mask);
+        sp.position_ids = as_ptr<void>(position_ids);
+        sp.pos_is_i64 = pos_is_i64 ? 1 : 0;
+        sp.segment_ids = as_ptr<int32_t>(segment_ids);
+        sp.rows = rows;
+        sp.seq_len = seq_len;
+        sp.pad_id = pad_id;
+        sp.mode = mode;
+        check_rc(ddl::pad_pack_tokens(sp, as_stream(stream)), "pad_pack_tokens");
+      },
+      py::arg("tokens"), py::arg("offsets"), py::arg("row_start"), py::arg("row_end"), py::arg("seg_offsets"),
+      py::arg("n_seg"), py::arg("out_tokens"), py::arg("attn_mask"), py::arg("position_ids"), py::arg("pos_is_i64"),
+      py::arg("segment_ids"), py::arg("rows"), py::arg("seq_len"), py::arg("pad_id"), py::arg("mode"),
+      py::arg("stream"));
+  m.def(
+      "checksum_words",
+      [](uintptr_t ptr, int64_t bytes, uintptr_t out, uintptr_t stream) {
+        check_rc(ddl::checksum_words(as_ptr<const void>(ptr), bytes, as_ptr<uint64_t>(out), as_stream(stream)),
+                 "checksum_words");
+      },
+      py::arg("ptr"), py::arg("bytes"), py::arg("out"), py::arg("stream"));
+  m.def(
+      "column_stats",
+      [](uintptr_t src, int64_t n, int64_t cols, uintptr_t sum, uintptr_t sumsq, uintptr_t mn, uintptr_t mx,
+         uintptr_t stream) {
+        check_rc(ddl::column_stats(as_ptr<const float>(src), n, cols, as_ptr<float>(sum), as_ptr<float>(sumsq),
+                                   as_ptr<float>(mn), as_ptr<float>(mx), as_stream(stream)),
+                 "column_stats");
+      },
+      py::arg("src"), py::arg("n"), py::arg("cols"), py::arg("sum"), py::arg("sumsq"), py::arg("min"), py::arg("max"),
+      py::arg("stream"));
+}

@@ -1,0 +1,190 @@
+// Collate kernels.
+//
+// collate_hwc_to_chw: decoded images usually arrive pixel-interleaved (HWC,
+// uint8); models want planar NCHW bf16, normalised per channel. The kernel
+// stages a 2048-pixel tile in LDS with coalesced 16 B loads, then every lane
+// de-interleaves 8 consecutive pixels and writes one 16 B bf16 vector per
+// channel plane -- both the global read and the global write are fully
+// vectorised and coalesced; LDS absorbs the stride-C shuffle.
+//
+// split_columns: the reference hands the consumer a tuple of strided views of
+// one [B, nValues] row block (ddl/mpi_dataloader.py:193-196). For device
+// batches we emit the column groups as contiguous tensors in one pass fused
+// with the permutation gather and the dtype cast.
+#include "common.h"
+#include "launch.h"
+
+namespace ddl {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kPix = 2048;  // pixels per tile: 8 per lane
+
+template <typename T>
+struct Px;
+template <>
+struct Px<uint8_t> {
+  static __device__ __forceinline__ float get(const uint8_t* s, int i) { return static_cast<float>(s[i]); }
+};
+template <>
+struct Px<float> {
+  static __device__ __forceinline__ float get(const float* s, int i) { return s[i]; }
+};
+template <>
+struct Px<uint16_t> {  // bf16 bits
+  static __device__ __forceinline__ float get(const uint16_t* s, int i) { return bf16_bits_to_f32(s[i]); }
+};
+
+template <int OUT_BF16>
+struct Out8 {
+  static __device__ __forceinline__ void store(void* dst, int64_t off, const float (&f)[8]) {
+    if constexpr (OUT_BF16) {
+      uint4 v;
+      v.x = pack_bf16x2(f[0], f[1]);
+      v.y = pack_bf16x2(f[2], f[3]);
+      v.z = pack_bf16x2(f[4], f[5]);
+      v.w = pack_bf16x2(f[6], f[7]);
+      *reinterpret_cast<uint4*>(static_cast<uint16_t*>(dst) + off) = v;
+    } else {
+      float* d = static_cast<float*>(dst) + off;
+      *reinterpret_cast<float4*>(d) = make_float4(f[0], f[1], f[2], f[3]);
+      *reinterpret_cast<float4*>(d + 4) = make_float4(f[4], f[5], f[6], f[7]);
+    }
+  }
+  static __device__ __forceinline__ void store1(void* dst, int64_t off, float f) {
+    if constexpr (OUT_BF16)
+      static_cast<uint16_t*>(dst)[off] = f32_to_bf16_bits(f);
+    else
+      static_cast<float*>(dst)[off] = f;
+  }
+};
+
+// grid: (tiles_per_image * batch); LDS: kPix * C * sizeof(Tin) bytes.
+template <typename Tin, int OUT_BF16>
+__global__ void __launch_bounds__(kThreads) hwc_to_chw_kernel(void* __restrict__ dst, const Tin* __restrict__ src,
+                                                              int64_t pixels, int32_t channels, int64_t tiles,
+                                                              RowIndex ri, Affine aff) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
+  Tin* tile = reinterpret_cast<Tin*>(lds_raw);
+  const int64_t img = blockIdx.x / tiles;
+  const int64_t t = blockIdx.x % tiles;
+  const int64_t p0 = t * kPix;
+  const int npx = static_cast<int>(pixels - p0 < kPix ? pixels - p0 : kPix);
+  const int64_t srow = source_row(ri, img);
+  const Tin* s = src + (srow * pixels + p0) * channels;
+  const int elems = npx * channels;
+  const int bytes = elems * static_cast<int>(sizeof(Tin));
+  // Stage: 16 B per lane when the span is 16 B aligned, element-wise otherwise.
+  if ((reinterpret_cast<uintptr_t>(s) & 15u) == 0 && (bytes & 15) == 0) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(s);
+    uint4* l4 = reinterpret_cast<uint4*>(tile);
+    for (int i = threadIdx.x; i < bytes / 16; i += kThreads) l4[i] = s4[i];
+  } else {
+    for (int i = threadIdx.x; i < elems; i += kThreads) tile[i] = s[i];
+  }
+  __syncthreads();
+  const int px = threadIdx.x * 8;
+  const int64_t out_img = img * channels * pixels;
+  for (int c = 0; c < channels; ++c) {
+    const float sc = aff.enabled ? aff.scale[c] : 1.f;
+    const float bi = aff.enabled ? aff.bias[c] : 0.f;
+    const int64_t obase = out_img + c * pixels + p0;
+    if (px + 8 <= npx && ((obase + px) & 7) == 0) {
+      float f[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) f[k] = fmaf(Px<Tin>::get(tile, (px + k) * channels + c), sc, bi);
+      Out8<OUT_BF16>::store(dst, obase + px, f);
+    } else {
+      for (int k = 0; k < 8 && px + k < npx; ++k)
+        Out8<OUT_BF16>::store1(dst, obase + px + k, fmaf(Px<Tin>::get(tile, (px + k) * channels + c), sc, bi));
+    }
+  }
+}
+
+template <typename Tin>
+int launch_hwc(void* dst, int32_t out_dt, const void* src, int64_t batch, int64_t pixels, int32_t channels,
+               const RowIndex& ri, const Affine& aff, hipStream_t st) {
+  const int64_t tiles = (pixels + kPix - 1) / kPix;
+  const size_t lds = static_cast<size_t>(kPix) * channels * sizeof(Tin);
+  const dim3 grid(static_cast<uint32_t>(batch * tiles));
+  if (out_dt == kBF16)
+    hipLaunchKernelGGL((hwc_to_chw_kernel<Tin, 1>), grid, dim3(kThreads), lds, st, dst, static_cast<const Tin*>(src),
+                       pixels, channels, tiles, ri, aff);
+  else if (out_dt == kF32)
+    hipLaunchKernelGGL((hwc_to_chw_kernel<Tin, 0>), grid, dim3(kThreads), lds, st, dst, static_cast<const Tin*>(src),
+                       pixels, channels, tiles, ri, aff);
+  else
+    return -1;
+  return static_cast<int>(hipGetLastError());
+}
+
+// ------------------------------------------------------------------ split ---
+template <typename Tin, int OUT>
+__global__ void __launch_bounds__(kThreads) split_columns_kernel(SplitSpec spec, const Tin* __restrict__ src,
+                                                                 int64_t n_rows, int64_t n_values, RowIndex ri) {
+  // One lane per (row, column): rows are short (the reference's CI rows are
+  // 9 floats); consecutive lanes cover consecutive columns of consecutive
+  // rows, so both the read and the per-group writes stay coalesced.
+  const int64_t total = n_rows * n_values;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  for (int64_t e = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; e < total; e += stride) {
+    const int64_t row = e / n_values;
+    int col = static_cast<int>(e - row * n_values);
+    const float v = Px<Tin>::get(src + source_row(ri, row) * n_values, col);
+    int g = 0;
+    while (g < spec.n_groups - 1 && col >= spec.width[g]) {
+      col -= spec.width[g];
+      ++g;
+    }
+    const int64_t off = row * spec.width[g] + col;
+    if constexpr (OUT == kBF16)
+      static_cast<uint16_t*>(spec.dst[g])[off] = f32_to_bf16_bits(v);
+    else
+      static_cast<float*>(spec.dst[g])[off] = v;
+  }
+}
+
+}  // namespace
+
+int collate_hwc_to_chw(void* dst, int32_t out_dt, const void* src, int32_t in_dt, int64_t batch, int64_t pixels,
+                       int32_t channels, const RowIndex& ri, const Affine& aff, hipStream_t st) {
+  if (batch <= 0 || pixels <= 0) return 0;
+  if (channels <= 0 || channels > 8) return -2;
+  switch (in_dt) {
+    case kU8: return launch_hwc<uint8_t>(dst, out_dt, src, batch, pixels, channels, ri, aff, st);
+    case kF32: return launch_hwc<float>(dst, out_dt, src, batch, pixels, channels, ri, aff, st);
+    case kBF16: return launch_hwc<uint16_t>(dst, out_dt, src, batch, pixels, channels, ri, aff, st);
+  }
+  return -1;
+}
+
+int split_columns(const SplitSpec& spec, const void* src, int32_t in_dt, int64_t n_rows, int64_t n_values,
+                  const RowIndex& ri, hipStream_t st) {
+  if (n_rows <= 0) return 0;
+  if (spec.n_groups < 1 || spec.n_groups > 8) return -2;
+  const int64_t total = n_rows * n_values;
+  int64_t blocks = (total + kThreads - 1) / kThreads;
+  if (blocks > 8192) blocks = 8192;
+  const dim3 grid(static_cast<uint32_t>(blocks));
+#define DDL_SPLIT(TIN)                                                                                             \
+  do {                                                                                                             \
+    if (spec.out_dt == kBF16)                                                                                      \
+      hipLaunchKernelGGL((split_columns_kernel<TIN, kBF16>), grid, dim3(kThreads), 0, st, spec,                   \
+                         static_cast<const TIN*>(src), n_rows, n_values, ri);                                      \
+    else if (spec.out_dt == kF32)                                                                                  \
+      hipLaunchKernelGGL((split_columns_kernel<TIN, kF32>), grid, dim3(kThreads), 0, st, spec,                    \
+                         static_cast<const TIN*>(src), n_rows, n_values, ri);                                      \
+    else                                                                                                           \
+      return -1;                                                                                                   \
+  } while (0)
+  switch (in_dt) {
+    case kF32: DDL_SPLIT(float); break;
+    case kBF16: DDL_SPLIT(uint16_t); break;
+    case kU8: DDL_SPLIT(uint8_t); break;
+    default: return -1;
+  }
+#undef DDL_SPLIT
+  return static_cast<int>(hipGetLastError());
+}
+
+}  // namespace ddl

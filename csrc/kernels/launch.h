@@ -1,0 +1,74 @@
+// Host-side launchers of the ddl_amd gfx950 kernels. Every launcher enqueues on
+// the given stream, never synchronises, never allocates (graph-capturable,
+// guide G9) and returns 0 or a hipError_t / negative argument error.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "common.h"
+
+namespace ddl {
+
+// permute.hip ---------------------------------------------------------------
+// dst[r, :] = cast(src[source_row(ri, r), :]) (scatter=0)
+// dst[source_row(ri, r), :] = src[r, :]       (scatter=1, same dtype only)
+int gather_rows(void* dst, int32_t out_dt, const void* src, int32_t in_dt, int64_t n_rows, int64_t row_elems,
+                const RowIndex& ri, const Affine& aff, int scatter, hipStream_t st);
+// out[i] = feistel_perm(base + i), i < count
+int feistel_indices(int64_t* out, int64_t count, int64_t base, const FeistelKeys& keys, hipStream_t st);
+
+// collate.hip ---------------------------------------------------------------
+// Image collate: src [B, H*W, C] (HWC, u8 / f32 / bf16) -> dst [B, C, H*W]
+// bf16 / f32 with out = x * scale[c] + bias[c]; rows gathered through ri.
+int collate_hwc_to_chw(void* dst, int32_t out_dt, const void* src, int32_t in_dt, int64_t batch, int64_t pixels,
+                       int32_t channels, const RowIndex& ri, const Affine& aff, hipStream_t st);
+// Column-group split of a [n, nValues] row batch into up to 8 contiguous
+// outputs dst_k [n, width_k] (reference tuple-of-splits batches,
+// ddl/mpi_dataloader.py:195-196, made contiguous), with fused gather + cast.
+struct SplitSpec {
+  void* dst[8];
+  int32_t width[8];
+  int32_t n_groups;
+  int32_t out_dt;
+};
+int split_columns(const SplitSpec& spec, const void* src, int32_t in_dt, int64_t n_rows, int64_t n_values,
+                  const RowIndex& ri, hipStream_t st);
+
+// tokens.hip ----------------------------------------------------------------
+// Pad: row b takes tokens[offsets[b] : offsets[b+1]] (truncated to seq_len);
+// writes out_tokens [B, S] (pad_id fill), attn_mask [B, S] (u8 or null) and
+// position_ids [B, S] (i32/i64 or null).
+// Pack: row r holds the token span [row_start[r], row_end[r]) of the flat
+// stream; seg_offsets (sorted sequence starts, n_seg+1 entries) drive the
+// per-token position id (reset at every sequence start) and segment id.
+struct TokenSpec {
+  const int32_t* tokens;
+  const int64_t* offsets;      // pad mode: [B+1]
+  const int64_t* row_start;    // pack mode: [R]
+  const int64_t* row_end;      // pack mode: [R]
+  const int64_t* seg_offsets;  // pack mode: [n_seg+1]
+  int64_t n_seg;
+  int32_t* out_tokens;
+  uint8_t* attn_mask;
+  void* position_ids;
+  int32_t* segment_ids;        // pack mode only (or null)
+  int64_t rows;
+  int64_t seq_len;
+  int32_t pad_id;
+  int32_t pos_is_i64;
+  int32_t mode;  // 0 pad, 1 pack
+  int32_t pad;
+};
+int pad_pack_tokens(const TokenSpec& spec, hipStream_t st);
+
+// misc.hip ------------------------------------------------------------------
+// Sum of the 32-bit words of [ptr, ptr+bytes) into *out (u64, accumulated --
+// zero it first). Debug batch checksums and the bench consumer step.
+int checksum_words(const void* ptr, int64_t bytes, uint64_t* out, hipStream_t st);
+// Per-column sum / sum of squares / min / max of an [n, cols] f32 matrix
+// (reference harness normalisation stats, tests/run_ddl.py:45-77).
+int column_stats(const float* src, int64_t n, int64_t cols, float* out_sum, float* out_sumsq, float* out_min,
+                 float* out_max, hipStream_t st);
+
+}  // namespace ddl

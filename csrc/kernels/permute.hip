@@ -1,0 +1,293 @@
+// Row gather / permute / scatter kernels with fused dtype cast and per-channel
+// normalisation.
+//
+// One kernel family serves every "move rows by index" need of the loader:
+//   * the global-shuffle permutation of a window resident in HBM (the
+//     reference's rng.shuffle of the producer window, tests/run_ddl.py:167,
+//     now an out-of-place device gather -- each row read once, written once),
+//   * gather/scatter of the rows exchanged between GPUs over RCCL
+//     (reference ddl/shuffle.py:92-108),
+//   * zero-copy gathers straight out of pinned, device-mapped host memory.
+// The source row of output row r comes from RowIndex: identity, an explicit
+// index vector, or the counter-based Feistel permutation computed inline.
+//
+// Memory-bound: every lane moves 16 B per access (guide G13), 4 independent
+// accesses in flight per lane, one row chunk per workgroup so a 301 KB image
+// row becomes ~19 workgroups (thousands of workgroups per batch >> 256 CUs).
+#include "common.h"
+#include "launch.h"
+
+namespace ddl {
+namespace {
+
+constexpr int kThreads = 256;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kUnroll = 4;
+
+// ------------------------------ raw byte moves ------------------------------
+template <typename U>
+__global__ void __launch_bounds__(kThreads) move_rows_chunked(uint8_t* __restrict__ dst,
+                                                              const uint8_t* __restrict__ src,
+                                                              int64_t units_per_row, int64_t chunks_per_row,
+                                                              RowIndex ri, int scatter) {
+  const int64_t row = blockIdx.x / chunks_per_row;
+  const int64_t chunk = blockIdx.x % chunks_per_row;
+  const int64_t mapped = source_row(ri, row);
+  const int64_t srow = scatter ? row : mapped;
+  const int64_t drow = scatter ? mapped : row;
+  const U* s = reinterpret_cast<const U*>(src) + srow * units_per_row;
+  U* d = reinterpret_cast<U*>(dst) + drow * units_per_row;
+  const int64_t u0 = chunk * (kThreads * kUnroll) + threadIdx.x;
+  U v[kUnroll];
+#pragma unroll
+  for (int k = 0; k < kUnroll; ++k) {
+    const int64_t u = u0 + k * kThreads;
+    if (u < units_per_row) v[k] = s[u];
+  }
+#pragma unroll
+  for (int k = 0; k < kUnroll; ++k) {
+    const int64_t u = u0 + k * kThreads;
+    if (u < units_per_row) d[u] = v[k];
+  }
+}
+
+template <typename U>
+__global__ void __launch_bounds__(kThreads) move_rows_flat(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
+                                                           int64_t units_per_row, int64_t total_units, RowIndex ri,
+                                                           int scatter) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  for (int64_t u = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; u < total_units; u += stride) {
+    const int64_t row = u / units_per_row;
+    const int64_t col = u - row * units_per_row;
+    const int64_t mapped = source_row(ri, row);
+    const int64_t srow = scatter ? row : mapped;
+    const int64_t drow = scatter ? mapped : row;
+    reinterpret_cast<U*>(dst)[drow * units_per_row + col] =
+        reinterpret_cast<const U*>(src)[srow * units_per_row + col];
+  }
+}
+
+// ------------------------------ converting moves ----------------------------
+template <typename T>
+struct Elem;
+template <>
+struct Elem<uint8_t> {
+  static __device__ __forceinline__ void load8(const uint8_t* p, float (&f)[8]) {
+    const uint2 v = *reinterpret_cast<const uint2*>(p);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f[i] = static_cast<float>((v.x >> (8 * i)) & 0xffu);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f[4 + i] = static_cast<float>((v.y >> (8 * i)) & 0xffu);
+  }
+  static __device__ __forceinline__ float load1(const uint8_t* p) { return static_cast<float>(*p); }
+};
+template <>
+struct Elem<float> {
+  static __device__ __forceinline__ void load8(const float* p, float (&f)[8]) {
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    const float4 b = *reinterpret_cast<const float4*>(p + 4);
+    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
+    f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+  }
+  static __device__ __forceinline__ void store8(float* p, const float (&f)[8]) {
+    *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(f[4], f[5], f[6], f[7]);
+  }
+  static __device__ __forceinline__ float load1(const float* p) { return *p; }
+  static __device__ __forceinline__ void store1(float* p, float f) { *p = f; }
+};
+// 2-byte storage tags (sizeof must equal the element size for pointer math).
+struct BF16Tag { uint16_t bits; };
+struct F16Tag { uint16_t bits; };
+static_assert(sizeof(BF16Tag) == 2 && sizeof(F16Tag) == 2, "tag size");
+template <>
+struct Elem<BF16Tag> {
+  static __device__ __forceinline__ void load8(const BF16Tag* p, float (&f)[8]) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f[2 * i] = bf16_bits_to_f32(static_cast<uint16_t>(w[i] & 0xffffu));
+      f[2 * i + 1] = bf16_bits_to_f32(static_cast<uint16_t>(w[i] >> 16));
+    }
+  }
+  static __device__ __forceinline__ void store8(BF16Tag* p, const float (&f)[8]) {
+    uint4 v;
+    v.x = pack_bf16x2(f[0], f[1]);
+    v.y = pack_bf16x2(f[2], f[3]);
+    v.z = pack_bf16x2(f[4], f[5]);
+    v.w = pack_bf16x2(f[6], f[7]);
+    *reinterpret_cast<uint4*>(p) = v;
+  }
+  static __device__ __forceinline__ float load1(const BF16Tag* p) {
+    return bf16_bits_to_f32(*reinterpret_cast<const uint16_t*>(p));
+  }
+  static __device__ __forceinline__ void store1(BF16Tag* p, float f) {
+    *reinterpret_cast<uint16_t*>(p) = f32_to_bf16_bits(f);
+  }
+};
+template <>
+struct Elem<F16Tag> {
+  static __device__ __forceinline__ void load8(const F16Tag* p, float (&f)[8]) {
+    const _Float16* h = reinterpret_cast<const _Float16*>(p);
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    const h8 v = *reinterpret_cast<const h8*>(h);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = static_cast<float>(v[i]);
+  }
+  static __device__ __forceinline__ void store8(F16Tag* p, const float (&f)[8]) {
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    h8 v;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = static_cast<_Float16>(f[i]);
+    *reinterpret_cast<h8*>(p) = v;
+  }
+  static __device__ __forceinline__ float load1(const F16Tag* p) {
+    return static_cast<float>(*reinterpret_cast<const _Float16*>(p));
+  }
+  static __device__ __forceinline__ void store1(F16Tag* p, float f) {
+    *reinterpret_cast<_Float16*>(p) = static_cast<_Float16>(f);
+  }
+};
+
+__device__ __forceinline__ void apply_affine(const Affine& a, int64_t elem, float (&f)[8]) {
+  if (!a.enabled) return;
+  // 8 consecutive elements share a channel when plane % 8 == 0 (checked on host).
+  const int ch = static_cast<int>((elem / a.plane) % a.channels);
+  const float s = a.scale[ch], b = a.bias[ch];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = fmaf(f[i], s, b);
+}
+
+template <typename Tin, typename Tout>
+__global__ void __launch_bounds__(kThreads) convert_rows_chunked(Tout* __restrict__ dst, const Tin* __restrict__ src,
+                                                                 int64_t row_elems, int64_t chunks_per_row, RowIndex ri,
+                                                                 Affine aff) {
+  const int64_t row = blockIdx.x / chunks_per_row;
+  const int64_t chunk = blockIdx.x % chunks_per_row;
+  const int64_t srow = source_row(ri, row);
+  const Tin* s = src + srow * row_elems;
+  Tout* d = dst + row * row_elems;
+  const int64_t e0 = (chunk * (kThreads * kUnroll) + threadIdx.x) * 8;
+  float f[kUnroll][8];
+#pragma unroll
+  for (int k = 0; k < kUnroll; ++k) {
+    const int64_t e = e0 + static_cast<int64_t>(k) * kThreads * 8;
+    if (e < row_elems) Elem<Tin>::load8(s + e, f[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < kUnroll; ++k) {
+    const int64_t e = e0 + static_cast<int64_t>(k) * kThreads * 8;
+    if (e < row_elems) {
+      apply_affine(aff, e, f[k]);
+      Elem<Tout>::store8(d + e, f[k]);
+    }
+  }
+}
+
+template <typename Tin, typename Tout>
+__global__ void __launch_bounds__(kThreads) convert_rows_flat(Tout* __restrict__ dst, const Tin* __restrict__ src,
+                                                              int64_t row_elems, int64_t total, RowIndex ri, Affine aff) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  for (int64_t e = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; e < total; e += stride) {
+    const int64_t row = e / row_elems;
+    const int64_t col = e - row * row_elems;
+    float v = Elem<Tin>::load1(src + source_row(ri, row) * row_elems + col);
+    if (aff.enabled) {
+      const int ch = static_cast<int>((col / aff.plane) % aff.channels);
+      v = fmaf(v, aff.scale[ch], aff.bias[ch]);
+    }
+    Elem<Tout>::store1(dst + e, v);
+  }
+}
+
+int flat_grid(int64_t work) {
+  const int64_t blocks = (work + kThreads - 1) / kThreads;
+  return static_cast<int>(blocks < 4096 ? (blocks < 1 ? 1 : blocks) : 4096);
+}
+
+template <typename U>
+void launch_move(void* dst, const void* src, int64_t n_rows, int64_t row_bytes, const RowIndex& ri, int scatter,
+                 hipStream_t st) {
+  const int64_t units = row_bytes / static_cast<int64_t>(sizeof(U));
+  if (units >= kThreads) {
+    const int64_t chunks = (units + kThreads * kUnroll - 1) / (kThreads * kUnroll);
+    hipLaunchKernelGGL(move_rows_chunked<U>, dim3(static_cast<uint32_t>(n_rows * chunks)), dim3(kThreads), 0, st,
+                       static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), units, chunks, ri, scatter);
+  } else {
+    hipLaunchKernelGGL(move_rows_flat<U>, dim3(flat_grid(n_rows * units)), dim3(kThreads), 0, st,
+                       static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), units, n_rows * units, ri,
+                       scatter);
+  }
+}
+
+template <typename Tin, typename Tout>
+void launch_convert(void* dst, const void* src, int64_t n_rows, int64_t row_elems, const RowIndex& ri, const Affine& aff,
+                    bool vec_ok, hipStream_t st) {
+  if (vec_ok && row_elems >= kThreads * 8) {
+    const int64_t chunks = (row_elems + kThreads * kUnroll * 8 - 1) / (kThreads * kUnroll * 8);
+    hipLaunchKernelGGL((convert_rows_chunked<Tin, Tout>), dim3(static_cast<uint32_t>(n_rows * chunks)), dim3(kThreads),
+                       0, st, static_cast<Tout*>(dst), static_cast<const Tin*>(src), row_elems, chunks, ri, aff);
+  } else {
+    hipLaunchKernelGGL((convert_rows_flat<Tin, Tout>), dim3(flat_grid(n_rows * row_elems)), dim3(kThreads), 0, st,
+                       static_cast<Tout*>(dst), static_cast<const Tin*>(src), row_elems, n_rows * row_elems, ri, aff);
+  }
+}
+
+template <typename Tin>
+int dispatch_out(int32_t out_dt, void* dst, const void* src, int64_t n_rows, int64_t row_elems, const RowIndex& ri,
+                 const Affine& aff, bool vec_ok, hipStream_t st) {
+  switch (out_dt) {
+    case kBF16: launch_convert<Tin, BF16Tag>(dst, src, n_rows, row_elems, ri, aff, vec_ok, st); return 0;
+    case kF16: launch_convert<Tin, F16Tag>(dst, src, n_rows, row_elems, ri, aff, vec_ok, st); return 0;
+    case kF32: launch_convert<Tin, float>(dst, src, n_rows, row_elems, ri, aff, vec_ok, st); return 0;
+  }
+  return -1;
+}
+
+__global__ void __launch_bounds__(kThreads) feistel_fill(int64_t* __restrict__ out, int64_t count, int64_t base,
+                                                         FeistelKeys keys) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < count; i += stride)
+    out[i] = static_cast<int64_t>(feistel_perm(static_cast<uint64_t>(base + i), keys));
+}
+
+}  // namespace
+
+int gather_rows(void* dst, int32_t out_dt, const void* src, int32_t in_dt, int64_t n_rows, int64_t row_elems,
+                const RowIndex& ri, const Affine& aff, int scatter, hipStream_t st) {
+  if (n_rows <= 0 || row_elems <= 0) return 0;
+  const bool same = (out_dt == in_dt) && !aff.enabled;
+  if (same) {
+    const int64_t row_bytes = row_elems * dtype_size(in_dt);
+    const uintptr_t align = reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src);
+    if (row_bytes % 16 == 0 && align % 16 == 0)
+      launch_move<u32x4>(dst, src, n_rows, row_bytes, ri, scatter, st);
+    else if (row_bytes % 4 == 0 && align % 4 == 0)
+      launch_move<uint32_t>(dst, src, n_rows, row_bytes, ri, scatter, st);
+    else
+      launch_move<uint8_t>(dst, src, n_rows, row_bytes, ri, scatter, st);
+    return static_cast<int>(hipGetLastError());
+  }
+  if (scatter) return -2;  // converting scatters are not needed by the loader
+  const uintptr_t align = reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src);
+  bool vec_ok = (row_elems % 8 == 0) && (align % 16 == 0);
+  if (aff.enabled && (aff.plane % 8 != 0)) vec_ok = false;
+  int rc = -1;
+  switch (in_dt) {
+    case kU8: rc = dispatch_out<uint8_t>(out_dt, dst, src, n_rows, row_elems, ri, aff, vec_ok, st); break;
+    case kF32: rc = dispatch_out<float>(out_dt, dst, src, n_rows, row_elems, ri, aff, vec_ok, st); break;
+    case kBF16: rc = dispatch_out<BF16Tag>(out_dt, dst, src, n_rows, row_elems, ri, aff, vec_ok, st); break;
+    case kF16: rc = dispatch_out<F16Tag>(out_dt, dst, src, n_rows, row_elems, ri, aff, vec_ok, st); break;
+  }
+  if (rc != 0) return -3;
+  return static_cast<int>(hipGetLastError());
+}
+
+int feistel_indices(int64_t* out, int64_t count, int64_t base, const FeistelKeys& keys, hipStream_t st) {
+  if (count <= 0) return 0;
+  hipLaunchKernelGGL(feistel_fill, dim3(flat_grid(count)), dim3(kThreads), 0, st, out, count, base, keys);
+  return static_cast<int>(hipGetLastError());
+}
+
+}  // namespace ddl

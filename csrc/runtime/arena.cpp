@@ -1,0 +1,387 @@
+// Implementation of the shared-memory slot arena (see arena.h).
+#include "arena.h"
+
+#include <errno.h>
+#include <fcntl.h>
+#include <linux/futex.h>
+#include <signal.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <sys/syscall.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <stdexcept>
+#include <thread>
+
+namespace ddl {
+
+namespace {
+
+uint64_t align_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
+
+std::runtime_error sys_error(const std::string& what) {
+  return std::runtime_error(what + ": " + std::strerror(errno));
+}
+
+int futex_wait(std::atomic<uint32_t>* word, uint32_t expected, int64_t timeout_ns) {
+  struct timespec ts;
+  ts.tv_sec = timeout_ns / 1000000000ll;
+  ts.tv_nsec = timeout_ns % 1000000000ll;
+  // Shared (non-private) futex: the word lives in a MAP_SHARED mapping.
+  return static_cast<int>(syscall(SYS_futex, reinterpret_cast<uint32_t*>(word), FUTEX_WAIT,
+                                  expected, &ts, nullptr, 0));
+}
+
+inline void cpu_relax() { __builtin_ia32_pause(); }
+
+}  // namespace
+
+uint64_t now_ns() {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return static_cast<uint64_t>(ts.tv_sec) * 1000000000ull + static_cast<uint64_t>(ts.tv_nsec);
+}
+
+void futex_wake_all(std::atomic<uint32_t>* word) {
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(word), FUTEX_WAKE, INT32_MAX, nullptr, nullptr,
+          0);
+}
+
+bool pid_alive(int32_t pid) {
+  if (pid <= 0) return true;
+  if (kill(pid, 0) != 0 && errno == ESRCH) return false;
+  // A crashed child that has not been reaped yet is a zombie: kill() still
+  // succeeds. Read the state letter from /proc/<pid>/stat.
+  char path[64];
+  std::snprintf(path, sizeof(path), "/proc/%d/stat", pid);
+  FILE* f = std::fopen(path, "r");
+  if (!f) return false;
+  char buf[512];
+  size_t n = std::fread(buf, 1, sizeof(buf) - 1, f);
+  std::fclose(f);
+  buf[n] = 0;
+  const char* rp = std::strrchr(buf, ')');  // comm may contain spaces
+  if (!rp || rp[1] == 0 || rp[2] == 0) return true;
+  char st = rp[2];
+  return !(st == 'Z' || st == 'X');
+}
+
+Arena* Arena::create(const std::string& name, const std::vector<uint64_t>& capacities,
+                     uint32_t n_slots) {
+  if (capacities.empty()) throw std::invalid_argument("arena needs at least one producer");
+  if (n_slots == 0) throw std::invalid_argument("arena needs at least one slot per producer");
+  const uint32_t n_prod = static_cast<uint32_t>(capacities.size());
+  const uint64_t meta = align_up(sizeof(ArenaHeader), 4096) +
+                        align_up(sizeof(ProducerRecord) * n_prod, 4096) +
+                        align_up(sizeof(SlotHeader) * n_prod * n_slots, 4096);
+  const uint64_t data_off = align_up(meta, kDataAlign);
+  uint64_t total = data_off;
+  for (uint64_t c : capacities) total += align_up(std::max<uint64_t>(c, 1), kDataAlign) * n_slots;
+
+  int fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+  if (fd < 0) throw sys_error("shm_open(create " + name + ")");
+  if (ftruncate(fd, static_cast<off_t>(total)) != 0) {
+    int e = errno;
+    close(fd);
+    shm_unlink(name.c_str());
+    errno = e;
+    throw sys_error("ftruncate(" + std::to_string(total) + ")");
+  }
+  void* p = mmap(nullptr, total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  if (p == MAP_FAILED) {
+    int e = errno;
+    close(fd);
+    shm_unlink(name.c_str());
+    errno = e;
+    throw sys_error("mmap");
+  }
+  auto* a = new Arena();
+  a->name_ = name;
+  a->fd_ = fd;
+  a->base_ = static_cast<uint8_t*>(p);
+  a->map_bytes_ = total;
+  a->owner_ = true;
+  a->hdr_ = reinterpret_cast<ArenaHeader*>(a->base_);
+
+  std::memset(a->base_, 0, meta);  // data pages stay untouched (lazy)
+  ArenaHeader* h = a->hdr_;
+  new (&h->shutdown) std::atomic<uint32_t>(0);
+  new (&h->failed_producer) std::atomic<uint32_t>(0);
+  new (&h->attached) std::atomic<uint32_t>(0);
+  h->version = kArenaVersion;
+  h->n_producers = n_prod;
+  h->n_slots = n_slots;
+  h->total_bytes = total;
+  h->data_offset = data_off;
+  h->creator_pid = getpid();
+
+  uint64_t off = data_off;
+  for (uint32_t pi = 0; pi < n_prod; ++pi) {
+    const uint64_t cap = align_up(std::max<uint64_t>(capacities[pi], 1), kDataAlign);
+    for (uint32_t si = 0; si < n_slots; ++si) {
+      SlotHeader* s = a->slot(pi, si);
+      new (&s->state) std::atomic<uint32_t>(kEmpty);
+      s->offset = off;
+      s->capacity = capacities[pi];
+      off += cap;
+    }
+  }
+  std::atomic_thread_fence(std::memory_order_release);
+  // Magic last: an attacher that sees it sees a fully initialised header.
+  reinterpret_cast<std::atomic<uint64_t>*>(&h->magic)->store(kArenaMagic,
+                                                             std::memory_order_release);
+  return a;
+}
+
+Arena* Arena::attach(const std::string& name) {
+  int fd = shm_open(name.c_str(), O_RDWR, 0600);
+  if (fd < 0) throw sys_error("shm_open(attach " + name + ")");
+  struct stat st;
+  if (fstat(fd, &st) != 0) {
+    close(fd);
+    throw sys_error("fstat");
+  }
+  const uint64_t total = static_cast<uint64_t>(st.st_size);
+  if (total < sizeof(ArenaHeader)) {
+    close(fd);
+    throw std::runtime_error("arena " + name + " is truncated");
+  }
+  void* p = mmap(nullptr, total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  if (p == MAP_FAILED) {
+    close(fd);
+    throw sys_error("mmap");
+  }
+  auto* a = new Arena();
+  a->name_ = name;
+  a->fd_ = fd;
+  a->base_ = static_cast<uint8_t*>(p);
+  a->map_bytes_ = total;
+  a->hdr_ = reinterpret_cast<ArenaHeader*>(a->base_);
+  const uint64_t magic =
+      reinterpret_cast<std::atomic<uint64_t>*>(&a->hdr_->magic)->load(std::memory_order_acquire);
+  if (magic != kArenaMagic || a->hdr_->version != kArenaVersion || a->hdr_->total_bytes != total) {
+    delete a;
+    throw std::runtime_error("arena " + name + " has a bad header (magic/version/size)");
+  }
+  a->hdr_->attached.fetch_add(1, std::memory_order_acq_rel);
+  return a;
+}
+
+Arena::~Arena() {
+  if (base_) munmap(base_, map_bytes_);
+  if (fd_ >= 0) close(fd_);
+}
+
+void Arena::unlink() {
+  if (!name_.empty()) shm_unlink(name_.c_str());
+}
+
+SlotHeader* Arena::slot(uint32_t p, uint32_t s) const {
+  if (p >= hdr_->n_producers || s >= hdr_->n_slots) throw std::out_of_range("slot index");
+  const uint64_t off = align_up(sizeof(ArenaHeader), 4096) +
+                       align_up(sizeof(ProducerRecord) * hdr_->n_producers, 4096);
+  auto* first = reinterpret_cast<SlotHeader*>(base_ + off);
+  return first + (static_cast<uint64_t>(p) * hdr_->n_slots + s);
+}
+
+ProducerRecord* Arena::producer(uint32_t p) const {
+  if (p >= hdr_->n_producers) throw std::out_of_range("producer index");
+  auto* first = reinterpret_cast<ProducerRecord*>(base_ + align_up(sizeof(ArenaHeader), 4096));
+  return first + p;
+}
+
+WaitResult Arena::wait_state(uint32_t p, uint32_t s, uint32_t expected, int64_t timeout_ms,
+                             int32_t peer_pid, int32_t producer_index) const {
+  SlotHeader* sh = slot(p, s);
+  // Fast path: short spin covers back-to-back hand-offs without a syscall.
+  for (int i = 0; i < 256; ++i) {
+    if (sh->state.load(std::memory_order_acquire) == expected) return kOk;
+    cpu_relax();
+  }
+  const uint64_t start = now_ns();
+  const uint64_t deadline =
+      timeout_ms < 0 ? UINT64_MAX : start + static_cast<uint64_t>(timeout_ms) * 1000000ull;
+  const int64_t slice_ns = 20ll * 1000000ll;  // re-check liveness every 20 ms
+  for (;;) {
+    const uint32_t v = sh->state.load(std::memory_order_acquire);
+    if (v == expected) return kOk;
+    if (hdr_->shutdown.load(std::memory_order_acquire)) return kShutdown;
+    if (producer_index >= 0) {
+      const uint32_t st = producer(static_cast<uint32_t>(producer_index))
+                              ->status.load(std::memory_order_acquire);
+      if (st == kStatusFailed) return kPeerFailed;
+    }
+    if (peer_pid > 0 && !pid_alive(peer_pid)) {
+      // Re-check once: the peer may have published right before exiting.
+      if (sh->state.load(std::memory_order_acquire) == expected) return kOk;
+      return kPeerDead;
+    }
+    const uint64_t t = now_ns();
+    if (t >= deadline) return kTimeout;
+    const int64_t left = static_cast<int64_t>(deadline - t);
+    futex_wait(&sh->state, v, std::min(left, slice_ns));
+  }
+}
+
+void Arena::set_state(uint32_t p, uint32_t s, uint32_t value) const {
+  SlotHeader* sh = slot(p, s);
+  sh->state.store(value, std::memory_order_release);
+  futex_wake_all(&sh->state);
+}
+
+bool Arena::cas_state(uint32_t p, uint32_t s, uint32_t expected, uint32_t value) const {
+  SlotHeader* sh = slot(p, s);
+  uint32_t e = expected;
+  const bool ok = sh->state.compare_exchange_strong(e, value, std::memory_order_acq_rel);
+  if (ok) futex_wake_all(&sh->state);
+  return ok;
+}
+
+uint32_t Arena::get_state(uint32_t p, uint32_t s) const {
+  return slot(p, s)->state.load(std::memory_order_acquire);
+}
+
+void Arena::request_shutdown() const {
+  hdr_->shutdown.store(1, std::memory_order_release);
+  for (uint32_t p = 0; p < hdr_->n_producers; ++p)
+    for (uint32_t s = 0; s < hdr_->n_slots; ++s) futex_wake_all(&slot(p, s)->state);
+}
+
+bool Arena::shutdown_requested() const {
+  return hdr_->shutdown.load(std::memory_order_acquire) != 0;
+}
+
+void Arena::mark_failed(uint32_t p) const {
+  producer(p)->status.store(kStatusFailed, std::memory_order_release);
+  uint32_t none = 0;
+  hdr_->failed_producer.compare_exchange_strong(none, p + 1, std::memory_order_acq_rel);
+  for (uint32_t s = 0; s < hdr_->n_slots; ++s) futex_wake_all(&slot(p, s)->state);
+}
+
+int32_t Arena::failed_producer() const {
+  return static_cast<int32_t>(hdr_->failed_producer.load(std::memory_order_acquire)) - 1;
+}
+
+// ----------------------------------------------------------------------------
+// Host worker pool for gathers / copies.
+namespace {
+
+class Pool {
+ public:
+  static Pool& get() {
+    static Pool pool;
+    return pool;
+  }
+  // Run fn(i) for i in [0, n) on up to `threads` workers (caller included).
+  void run(int n, int threads, const std::function<void(int)>& fn) {
+    if (n <= 0) return;
+    threads = std::max(1, std::min(threads, n));
+    if (threads == 1) {
+      for (int i = 0; i < n; ++i) fn(i);
+      return;
+    }
+    ensure(threads - 1);
+    std::unique_lock<std::mutex> lk(mu_);
+    job_ = &fn;
+    next_ = 0;
+    total_ = n;
+    active_ = threads - 1;
+    pending_ = threads - 1;
+    ++gen_;
+    cv_.notify_all();
+    lk.unlock();
+    work();
+    lk.lock();
+    done_cv_.wait(lk, [&] { return pending_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  Pool() = default;
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+      cv_.notify_all();
+    }
+    for (auto& t : workers_) t.detach();  // process exit: do not block
+  }
+  void ensure(int n) {
+    std::lock_guard<std::mutex> lk(mu_);
+    while (static_cast<int>(workers_.size()) < n) {
+      const int id = static_cast<int>(workers_.size());
+      workers_.emplace_back([this, id] { loop(id); });
+    }
+  }
+  void work() {
+    for (;;) {
+      const int i = next_.fetch_add(1);
+      if (i >= total_) break;
+      (*job_)(i);
+    }
+  }
+  void loop(int id) {
+    uint64_t seen = 0;
+    for (;;) {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return stop_ || (gen_ != seen && id < active_); });
+      if (stop_) return;
+      seen = gen_;
+      lk.unlock();
+      work();
+      lk.lock();
+      if (--pending_ == 0) done_cv_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<std::thread> workers_;
+  const std::function<void(int)>* job_ = nullptr;
+  std::atomic<int> next_{0};
+  int total_ = 0, active_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+std::mutex g_pool_call_mu;  // one parallel job at a time per process
+
+}  // namespace
+
+void gather_rows(uint8_t* dst, const uint8_t* src, uint64_t row_bytes, const int64_t* idx,
+                 uint64_t n, uint64_t src_rows, int n_threads) {
+  for (uint64_t i = 0; i < n; ++i)
+    if (idx[i] < 0 || static_cast<uint64_t>(idx[i]) >= src_rows)
+      throw std::out_of_range("gather_rows: index " + std::to_string(idx[i]) + " out of range " +
+                              std::to_string(src_rows));
+  // Chunk so that every task moves >= ~1 MiB (amortises dispatch) while
+  // leaving enough tasks to balance threads.
+  const uint64_t rows_per_task = std::max<uint64_t>(1, (1ull << 20) / std::max<uint64_t>(row_bytes, 1));
+  const int tasks = static_cast<int>((n + rows_per_task - 1) / rows_per_task);
+  std::lock_guard<std::mutex> lk(g_pool_call_mu);
+  Pool::get().run(tasks, n_threads, [&](int t) {
+    const uint64_t b = static_cast<uint64_t>(t) * rows_per_task;
+    const uint64_t e = std::min(n, b + rows_per_task);
+    for (uint64_t i = b; i < e; ++i)
+      std::memcpy(dst + i * row_bytes, src + static_cast<uint64_t>(idx[i]) * row_bytes, row_bytes);
+  });
+}
+
+void parallel_copy(uint8_t* dst, const uint8_t* src, uint64_t bytes, int n_threads) {
+  const uint64_t chunk = 8ull << 20;
+  const int tasks = static_cast<int>((bytes + chunk - 1) / chunk);
+  std::lock_guard<std::mutex> lk(g_pool_call_mu);
+  Pool::get().run(tasks, n_threads, [&](int t) {
+    const uint64_t b = static_cast<uint64_t>(t) * chunk;
+    const uint64_t e = std::min(bytes, b + chunk);
+    std::memcpy(dst + b, src + b, e - b);
+  });
+}
+
+}  // namespace ddl

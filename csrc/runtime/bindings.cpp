@@ -1,0 +1,177 @@
+// pybind11 bindings for the host runtime: module ddl_amd._ddl_runtime.
+// No torch / HIP dependency: this module works on CPU-only hosts (the
+// producer worker processes never touch the GPU).
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <memory>
+#include <new>
+
+#include "arena.h"
+
+namespace py = pybind11;
+using ddl::Arena;
+
+namespace {
+
+py::dict slot_info(const Arena& a, uint32_t p, uint32_t s) {
+  ddl::SlotHeader* sh = a.slot(p, s);
+  py::dict d;
+  d["state"] = sh->state.load();
+  d["offset"] = sh->offset;
+  d["capacity"] = sh->capacity;
+  d["seq"] = sh->seq.load();
+  d["used_bytes"] = sh->used_bytes.load();
+  d["epoch"] = sh->epoch.load();
+  d["publish_ns"] = sh->publish_ns.load();
+  py::list tags;
+  for (auto& t : sh->tag) tags.append(t.load());
+  d["tag"] = tags;
+  return d;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_ddl_runtime, m) {
+  m.doc() = "ddl_amd native host runtime: shm slot arena, futex hand-off, host gather";
+
+  py::enum_<ddl::WaitResult>(m, "WaitResult")
+      .value("OK", ddl::kOk)
+      .value("SHUTDOWN", ddl::kShutdown)
+      .value("TIMEOUT", ddl::kTimeout)
+      .value("PEER_DEAD", ddl::kPeerDead)
+      .value("PEER_FAILED", ddl::kPeerFailed);
+
+  m.attr("EMPTY") = static_cast<uint32_t>(ddl::kEmpty);
+  m.attr("READY") = static_cast<uint32_t>(ddl::kReady);
+  m.attr("HELD") = static_cast<uint32_t>(ddl::kHeld);
+  m.attr("STATUS_INIT") = static_cast<uint32_t>(ddl::kStatusInit);
+  m.attr("STATUS_RUNNING") = static_cast<uint32_t>(ddl::kStatusRunning);
+  m.attr("STATUS_DONE") = static_cast<uint32_t>(ddl::kStatusDone);
+  m.attr("STATUS_FAILED") = static_cast<uint32_t>(ddl::kStatusFailed);
+  m.attr("DATA_ALIGN") = ddl::kDataAlign;
+
+  m.def("now_ns", &ddl::now_ns);
+  m.def("pid_alive", &ddl::pid_alive, py::arg("pid"));
+
+  py::class_<Arena, std::unique_ptr<Arena>>(m, "Arena")
+      .def_static(
+          "create",
+          [](const std::string& name, const std::vector<uint64_t>& caps, uint32_t n_slots) {
+            return std::unique_ptr<Arena>(Arena::create(name, caps, n_slots));
+          },
+          py::arg("name"), py::arg("capacities"), py::arg("n_slots"))
+      .def_static(
+          "attach", [](const std::string& name) { return std::unique_ptr<Arena>(Arena::attach(name)); },
+          py::arg("name"))
+      .def("unlink", &Arena::unlink)
+      .def_property_readonly("name", &Arena::name)
+      .def_property_readonly("base_address",
+                             [](const Arena& a) { return reinterpret_cast<uintptr_t>(a.base()); })
+      .def_property_readonly("total_bytes", &Arena::total_bytes)
+      .def_property_readonly("data_offset", &Arena::data_offset)
+      .def_property_readonly("n_producers", &Arena::n_producers)
+      .def_property_readonly("n_slots", &Arena::n_slots)
+      .def("slot_address",
+           [](const Arena& a, uint32_t p, uint32_t s) {
+             return reinterpret_cast<uintptr_t>(a.slot_data(p, s));
+           })
+      .def("state_address",
+           [](const Arena& a, uint32_t p, uint32_t s) {
+             return reinterpret_cast<uintptr_t>(&a.slot(p, s)->state);
+           })
+      .def("slot_capacity", [](const Arena& a, uint32_t p, uint32_t s) { return a.slot(p, s)->capacity; })
+      .def(
+          "slot_view",
+          [](const Arena& a, uint32_t p, uint32_t s) {
+            ddl::SlotHeader* sh = a.slot(p, s);
+            return py::memoryview::from_memory(a.base() + sh->offset,
+                                               static_cast<py::ssize_t>(sh->capacity), false);
+          },
+          py::arg("producer"), py::arg("slot"))
+      .def("slot_info", [](const Arena& a, uint32_t p, uint32_t s) { return slot_info(a, p, s); })
+      .def(
+          "wait_state",
+          [](const Arena& a, uint32_t p, uint32_t s, uint32_t expected, int64_t timeout_ms,
+             int32_t peer_pid, int32_t producer_index) {
+            py::gil_scoped_release nogil;
+            return a.wait_state(p, s, expected, timeout_ms, peer_pid, producer_index);
+          },
+          py::arg("producer"), py::arg("slot"), py::arg("expected"), py::arg("timeout_ms") = -1,
+          py::arg("peer_pid") = 0, py::arg("producer_index") = -1)
+      .def("set_state", &Arena::set_state)
+      .def("cas_state", &Arena::cas_state)
+      .def("get_state", &Arena::get_state)
+      .def(
+          "publish",
+          [](const Arena& a, uint32_t p, uint32_t s, uint64_t seq, uint64_t used, uint64_t epoch,
+             std::vector<int64_t> tags) {
+            ddl::SlotHeader* sh = a.slot(p, s);
+            if (used > sh->capacity) throw std::out_of_range("publish: used_bytes > capacity");
+            sh->seq.store(seq, std::memory_order_relaxed);
+            sh->used_bytes.store(used, std::memory_order_relaxed);
+            sh->epoch.store(epoch, std::memory_order_relaxed);
+            for (size_t i = 0; i < tags.size() && i < 4; ++i)
+              sh->tag[i].store(tags[i], std::memory_order_relaxed);
+            sh->publish_ns.store(ddl::now_ns(), std::memory_order_relaxed);
+            a.set_state(p, s, ddl::kReady);  // release: orders every store above
+          },
+          py::arg("producer"), py::arg("slot"), py::arg("seq"), py::arg("used_bytes"),
+          py::arg("epoch") = 0, py::arg("tags") = std::vector<int64_t>{})
+      .def("request_shutdown", &Arena::request_shutdown)
+      .def("shutdown_requested", &Arena::shutdown_requested)
+      .def("mark_failed", &Arena::mark_failed)
+      .def("failed_producer", &Arena::failed_producer)
+      .def("attached", [](const Arena& a) { return a.header()->attached.load(); })
+      .def("set_producer_pid",
+           [](const Arena& a, uint32_t p, int32_t pid) {
+             a.producer(p)->pid.store(pid);
+             a.producer(p)->status.store(ddl::kStatusRunning, std::memory_order_release);
+           })
+      .def("set_producer_status",
+           [](const Arena& a, uint32_t p, uint32_t st) {
+             a.producer(p)->status.store(st, std::memory_order_release);
+           })
+      .def("heartbeat",
+           [](const Arena& a, uint32_t p, uint64_t fill_ns, uint64_t wait_ns) {
+             ddl::ProducerRecord* r = a.producer(p);
+             r->heartbeat_ns.store(ddl::now_ns(), std::memory_order_relaxed);
+             r->rounds.fetch_add(1, std::memory_order_relaxed);
+             r->fill_ns_total.fetch_add(fill_ns, std::memory_order_relaxed);
+             r->wait_ns_total.fetch_add(wait_ns, std::memory_order_relaxed);
+           })
+      .def("producer_info", [](const Arena& a, uint32_t p) {
+        ddl::ProducerRecord* r = a.producer(p);
+        py::dict d;
+        d["pid"] = r->pid.load();
+        d["status"] = r->status.load();
+        d["heartbeat_ns"] = r->heartbeat_ns.load();
+        d["rounds"] = r->rounds.load();
+        d["fill_ns_total"] = r->fill_ns_total.load();
+        d["wait_ns_total"] = r->wait_ns_total.load();
+        return d;
+      });
+
+  m.def(
+      "gather_rows",
+      [](uintptr_t dst, uintptr_t src, uint64_t row_bytes, py::array_t<int64_t, py::array::c_style> idx,
+         uint64_t src_rows, int n_threads) {
+        const int64_t* ip = idx.data();
+        const uint64_t n = static_cast<uint64_t>(idx.size());
+        py::gil_scoped_release nogil;
+        ddl::gather_rows(reinterpret_cast<uint8_t*>(dst), reinterpret_cast<const uint8_t*>(src),
+                         row_bytes, ip, n, src_rows, n_threads);
+      },
+      py::arg("dst"), py::arg("src"), py::arg("row_bytes"), py::arg("indices"), py::arg("src_rows"),
+      py::arg("n_threads") = 4,
+      "dst[i*row_bytes:(i+1)*row_bytes] = src[idx[i]*row_bytes:...] on a host worker pool");
+  m.def(
+      "parallel_copy",
+      [](uintptr_t dst, uintptr_t src, uint64_t bytes, int n_threads) {
+        py::gil_scoped_release nogil;
+        ddl::parallel_copy(reinterpret_cast<uint8_t*>(dst), reinterpret_cast<const uint8_t*>(src),
+                           bytes, n_threads);
+      },
+      py::arg("dst"), py::arg("src"), py::arg("bytes"), py::arg("n_threads") = 4);
+}

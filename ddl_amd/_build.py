@@ -1,0 +1,154 @@
+"""In-tree native build for ddl_amd (no setuptools / hipify involved).
+
+Two shared objects are produced next to this file:
+
+* ``_ddl_runtime``  -- host C++ runtime (shm arena, futex hand-off, host
+  gather pool). Built with g++; no torch / HIP dependency so producer worker
+  processes and CPU-only hosts can load it.
+* ``_ddl_hip``      -- hand-written CDNA4 (gfx950) HIP kernels + torch
+  bindings. Kernels are compiled with ``hipcc --offload-arch=gfx950``; the
+  module links against the HIP runtime bundled in torch/lib so a single HIP
+  runtime lives in the process.
+
+Usage: ``python -m ddl_amd._build [--only runtime|hip] [--force] [-j N]``.
+"""
+
+from __future__ import annotations
+
+import argparse
+import glob
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(REPO, "csrc")
+BUILD = os.path.join(REPO, "build", "native")
+EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+ARCH = os.environ.get("DDL_AMD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (set HIPCC)")
+
+
+def _py_includes() -> list[str]:
+    import pybind11
+
+    return [sysconfig.get_paths()["include"], pybind11.get_include()]
+
+
+def _torch_paths() -> tuple[str, list[str]]:
+    import torch
+
+    root = os.path.dirname(torch.__file__)
+    inc = [os.path.join(root, "include"), os.path.join(root, "include", "torch", "csrc", "api", "include")]
+    return os.path.join(root, "lib"), inc
+
+
+def _newer(target: str, deps: list[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd: list[str]) -> None:
+    proc = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if proc.returncode != 0:
+        sys.stderr.write(proc.stdout)
+        raise RuntimeError(f"native build failed ({proc.returncode}): {' '.join(cmd[:4])} ...")
+    if os.environ.get("DDL_AMD_BUILD_VERBOSE"):
+        sys.stderr.write(proc.stdout)
+
+
+def runtime_target() -> str:
+    return os.path.join(PKG_DIR, "_ddl_runtime" + EXT_SUFFIX)
+
+
+def hip_target() -> str:
+    return os.path.join(PKG_DIR, "_ddl_hip" + EXT_SUFFIX)
+
+
+def build_runtime(force: bool = False, extra_flags: list[str] | None = None) -> str:
+    srcs = [os.path.join(CSRC, "runtime", f) for f in ("arena.cpp", "bindings.cpp")]
+    deps = srcs + [os.path.join(CSRC, "runtime", "arena.h")]
+    out = runtime_target()
+    if not force and not _newer(out, deps):
+        return out
+    cxx = os.environ.get("CXX", "g++")
+    cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wno-unused-function"]
+    cmd += [f"-I{p}" for p in _py_includes()]
+    cmd += list(extra_flags or [])
+    cmd += srcs + ["-o", out + ".tmp", "-lpthread", "-lrt"]
+    _run(cmd)
+    os.replace(out + ".tmp", out)
+    return out
+
+
+def _kernel_sources() -> list[str]:
+    return sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+
+
+def build_hip(force: bool = False, jobs: int = 8) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    hipcc = _hipcc()
+    torch_lib, _ = _torch_paths()
+    headers = glob.glob(os.path.join(CSRC, "kernels", "*.h"))
+    out = hip_target()
+    kernel_srcs = _kernel_sources()
+    binding = os.path.join(CSRC, "kernels", "bindings.cpp")
+
+    jobs_list: list[tuple[list[str], str]] = []
+    objs: list[str] = []
+    common = ["-O3", "-std=c++17", "-fPIC", f"-I{os.path.join(CSRC, 'runtime')}", f"-I{os.path.join(CSRC, 'kernels')}"]
+    for src in kernel_srcs:
+        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        objs.append(obj)
+        if force or _newer(obj, [src] + headers):
+            cmd = [hipcc, f"--offload-arch={ARCH}", "-c", src, "-o", obj, "-munsafe-fp-atomics"] + common
+            jobs_list.append((cmd, obj))
+    bobj = os.path.join(BUILD, "bindings.cpp.o")
+    objs.append(bobj)
+    if force or _newer(bobj, [binding] + headers):
+        cmd = [hipcc, "-c", binding, "-o", bobj] + common
+        cmd += [f"-I{p}" for p in _py_includes()] + ["-fvisibility=hidden"]
+        jobs_list.append((cmd, bobj))
+
+    if jobs_list:
+        with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+            list(ex.map(lambda j: _run(j[0]), jobs_list))
+    if force or jobs_list or _newer(out, objs):
+        cmd = [hipcc, "-shared", "-fPIC", *objs, "-o", out + ".tmp", f"-L{torch_lib}", f"-Wl,-rpath,{torch_lib}",
+               "-l:libamdhip64.so", "-lpthread", "-lrt"]
+        _run(cmd)
+        os.replace(out + ".tmp", out)
+    return out
+
+
+def build_all(force: bool = False, jobs: int = 8) -> None:
+    build_runtime(force=force)
+    build_hip(force=force, jobs=jobs)
+
+
+def main(argv: list[str] | None = None) -> None:
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--only", choices=["runtime", "hip"], default=None)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=8)
+    a = ap.parse_args(argv)
+    if a.only in (None, "runtime"):
+        print(build_runtime(force=a.force))
+    if a.only in (None, "hip"):
+        print(build_hip(force=a.force, jobs=a.jobs))
+
+
+if __name__ == "__main__":
+    main()

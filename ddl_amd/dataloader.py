@@ -1,0 +1,465 @@
+"""Consumer: ``DistributedDataLoader`` (reference ddl/mpi_dataloader.py:31-249).
+
+Drop-in API of the reference -- constructor arguments, ``len()`` = batches of
+the current epoch, ``__getitem__`` returning a tuple of column-group tensors,
+``mark(Marker.END_OF_BATCH / END_OF_EPOCH)`` driving the window state machine,
+round-robin over the producers' windows, shutdown after ``n_epochs`` -- on the
+MI355X-native data path:
+
+    producer windows (pinned shm arena)
+      --hipMemcpyAsync, prefetch stream, depth-2 HBM ring (staging.py)-->
+    HBM window  --global-shuffle exchange over RCCL/xGMI (parallel/shuffle.py)-->
+    per-batch fused gfx950 kernel on the compute stream: Feistel permutation
+    gather + dtype cast + per-channel normalise / HWC->CHW collate / contiguous
+    column split (ops/) --> device tensors.
+
+On a CPU-only host the batches are zero-copy views of the shm windows, as in
+the reference (reference ddl/mpi_dataloader.py:190-196).
+
+Additions over the reference: ``__iter__`` (optionally auto-marking, i.e. a
+torch DataLoader drop-in), ``set_epoch``, ``state_dict``/``load_state_dict``
+(epoch/window/batch cursor + seed), device output dtype/normalisation, the
+device-side permutation, prefetch depth, bounded waits with typed errors.
+
+Window schedule: window ``w`` (0, 1, 2, ... over the whole run) comes from
+producer ``w % P``, which fills its rounds into slots ``round % n_slots``, so
+window ``w`` is producer round ``w // P`` in slot ``(w // P) % n_slots``.
+An epoch is ``windows_per_epoch`` consecutive windows: 1 (reference default
+"do_not_split_along_epoch", ddl/mpi_dataloader.py:149-157), P
+("split_along_epoch") or the producer-announced count (indexed producers,
+where one window is one global batch).
+"""
+
+from __future__ import annotations
+
+import math
+import time
+from typing import Any, Iterator, Sequence
+
+import torch
+
+from . import ops
+from .connection import Connection
+from .datasetwrapper import ProducerFunctionSkeleton
+from .exceptions import ShapeMismatchError
+from .ops import _dtypes
+from .permutation import FeistelPermutation
+from .types import DDLEnv, Marker, MetaData_Consumer_To_Producer, MetaData_Producer_To_Consumer
+from .utils.logging import for_all_methods, logger, with_logging
+from .utils.tracing import LoaderMetrics, trace_range
+
+STATE_VERSION = 1
+MODES = ("do_not_split_along_epoch", "split_along_epoch", "window", "indexed")
+
+
+@for_all_methods(with_logging, exclude=["__getitem__", "__len__", "__iter__", "mark", "_on_batch_end",
+                                        "_window", "_batch_from_window", "_schedule"])
+class DistributedDataLoader:
+    def __init__(
+        self,
+        producer_function: ProducerFunctionSkeleton,
+        batch_size: int,
+        connection: Connection | None,
+        n_epochs: int,
+        fraction_exchange: float = 0.0,
+        exchange_method: str = "alltoall",
+        instance_idx: int = 0,
+        n_instances: int = 1,
+        *,
+        device: str | torch.device | None = None,
+        out_dtype: Any = None,
+        shuffle: str = "none",
+        seed: int = 0,
+        n_slots: int = 1,
+        prefetch_depth: int = 2,
+        mode: str = "window",
+        normalize: dict | None = None,
+        contiguous: bool = False,
+        env: DDLEnv | None = None,
+        auto_mark: bool = False,
+        resume_state: dict | None = None,
+        timeout_s: float | None = None,
+        host_threads: int = 4,
+        debug_checksum: bool = False,
+    ):
+        if mode not in MODES:
+            raise ValueError(f"unknown mode {mode!r}; one of {MODES}")
+        if shuffle not in ("none", "device"):
+            raise ValueError("shuffle must be 'none' or 'device'")
+        self.batch_size = int(batch_size)
+        self.connection = connection
+        self.n_epochs = int(n_epochs)
+        self.fraction_exchange = float(fraction_exchange)
+        self.exchange_method = exchange_method
+        self.instance_idx = instance_idx
+        self.n_instances = n_instances
+        self.shuffle = shuffle
+        self.seed = int(seed)
+        self.n_slots = int(n_slots)
+        self.prefetch_depth = int(prefetch_depth)
+        self.mode = "do_not_split_along_epoch" if mode == "window" else mode
+        self.normalize = normalize
+        self.contiguous = contiguous
+        self.env = env
+        self.auto_mark = auto_mark
+        self.debug_checksum = debug_checksum
+        self.metrics = LoaderMetrics()
+        self.timeout_s = timeout_s if timeout_s is not None else (connection.timeout_s if connection else 600.0)
+        self.checksums: list[int] = []
+
+        # cursor
+        self.epoch = 0
+        self.batch = 0          # batches consumed in the current window
+        self.epoch_batch = 0    # batches consumed in the current epoch
+        self.window = 0         # global window index
+        self.window_in_epoch = 0
+        if resume_state is not None:
+            self._apply_state(resume_state)
+        self.target_rank = 1    # reference-compatible: producer of the current window, 1-based
+
+        if device is None:
+            device = "cuda" if torch.cuda.is_available() else "cpu"
+        self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.out_dtype = _dtypes.to_torch_dtype(out_dtype) if out_dtype is not None else None
+
+        self._finalized = False
+        self._stager = None
+        self._host_window: int | None = None  # host path: window currently held
+        self._cur = None                      # device path: StagedWindow of the current window
+
+        if connection is None or connection.n_producers == 0:
+            # Reference behaviour for a single-rank run: nothing to iterate (ddl/mpi_dataloader.py:173-174).
+            self._len = 0
+            self.metadata_from_producer = []
+            return
+
+        P = connection.n_producers
+        rounds0 = [self._first_round(p, P, self.window) for p in range(P)]
+        base_meta = MetaData_Consumer_To_Producer(
+            producer_function=producer_function,
+            global_shuffle_fraction_exchange=self.fraction_exchange,
+            global_shuffle_exchange_method=exchange_method,
+            batch_size=self.batch_size,
+            rank=env.rank if env else instance_idx,
+            world_size=env.world_size if env else n_instances,
+            n_slots=self.n_slots,
+            seed=self.seed,
+            host_threads=host_threads,
+        )
+        # per-producer start round (resume mid-run)
+        import copy
+
+        for i, pipe in enumerate(connection.pipes):
+            m = copy.copy(base_meta)
+            m.producer_index, m.n_producers, m.start_round = i, P, rounds0[i]
+            pipe.send("meta", m)
+        self.metadata_from_producer: list[MetaData_Producer_To_Consumer] = connection.recv_metadata_as_consumer()
+        md = self.metadata_from_producer
+        self.splits = [tuple(x.splits) for x in md]
+        self.batches_per_window = [int(x.batches_per_window) for x in md]
+        self.shapes = [tuple(x.shape) for x in md]
+        self.dtypes = [_dtypes.to_torch_dtype(x.dtype) for x in md]
+        if len(set(self.splits)) != 1 or len({s[1:] for s in self.shapes}) != 1 or len(set(self.dtypes)) != 1:
+            raise ShapeMismatchError(md, "producers disagree on sample shape / splits / dtype")
+        if self.mode == "indexed":
+            wpe = {int(x.extra.get("batches_per_epoch", 0)) for x in md}
+            if len(wpe) != 1 or 0 in wpe:
+                raise ShapeMismatchError(md, "indexed producers must announce one batches_per_epoch")
+            self.windows_per_epoch = wpe.pop()
+        elif self.mode == "split_along_epoch":
+            self.windows_per_epoch = P
+        else:
+            self.windows_per_epoch = 1
+        self.sample_shape = self.shapes[0][1:]
+        self.window_dtype = self.dtypes[0]
+
+        views = connection.init_windows(self.shapes, self.dtypes, self.n_slots,
+                                        pin=self.device.type == "cuda")
+        self.arys = views  # reference name: zero-copy window views
+        connection.Barrier()
+        self.total_windows = self.n_epochs * self.windows_per_epoch - self.window
+        self._setup_exchange()
+        if self.device.type == "cuda":
+            from .staging import WindowStager
+
+            max_bytes = max(math.prod(s) * _dtypes.itemsize(d) for s, d in zip(self.shapes, self.dtypes))
+            self._stager = WindowStager(connection, self._schedule, self.total_windows, self.prefetch_depth,
+                                        self.device, max_bytes, post_copy=self._exchange_fn,
+                                        timeout_s=self.timeout_s, first_window=self.window)
+        self._update_len()
+
+    # --------------------------------------------------------------- schedule
+    def _schedule(self, w: int) -> tuple[int, int]:
+        P = self.connection.n_producers
+        return w % P, (w // P) % self.n_slots
+
+    @staticmethod
+    def _first_round(p: int, P: int, first_window: int = 0) -> int:
+        """Number of windows of producer ``p`` before ``first_window`` (= its first round on resume)."""
+        return max(0, -(-(first_window - p) // P))
+
+    def _update_len(self) -> None:
+        if self.mode == "do_not_split_along_epoch":
+            p, _ = self._schedule(self.window)
+            self._len = self.batches_per_window[p]
+        else:
+            first = self.window - self.window_in_epoch
+            self._len = sum(self.batches_per_window[self._schedule(first + k)[0]]
+                            for k in range(self.windows_per_epoch))
+
+    def __len__(self) -> int:
+        return self._len
+
+    # --------------------------------------------------------------- exchange
+    def _setup_exchange(self) -> None:
+        self._exchange_fn = None
+        world = self.env.world_size if self.env else 1
+        if self.fraction_exchange <= 0 or world <= 1 or self.env is None or self.env.process_group is None:
+            return
+        from .parallel.shuffle import make_exchange
+
+        n_min = min(x.nData for x in self.metadata_from_producer)
+        self._exchange_fn = make_exchange(self.env, self.exchange_method, self.fraction_exchange, n_min,
+                                          self.sample_shape, self.window_dtype, self.seed,
+                                          device=self.device, shuffle=self.shuffle)
+
+    # ----------------------------------------------------------------- access
+    def _window(self):
+        """Make the current window available (device: staged; host: acquired)."""
+        if self._stager is not None:
+            if self._cur is None or self._cur.index != self.window:
+                t0 = time.perf_counter()
+                with trace_range("ddl.consumer.wait_window"):
+                    self._cur = self._stager.get(self.window)
+                self.metrics.consumer_wait_s += time.perf_counter() - t0
+                self.metrics.windows += 1
+            return self._cur
+        if self._host_window != self.window:
+            p, s = self._schedule(self.window)
+            t0 = time.perf_counter()
+            info = self.connection.acquire(p, s, self.timeout_s)
+            self.metrics.consumer_wait_s += time.perf_counter() - t0
+            self.metrics.windows += 1
+            if self._exchange_fn is not None:
+                _, t = self.arys[p][s]
+                self._exchange_fn(t.view(-1).view(torch.uint8), self.window, info)
+            self._host_window = self.window
+            self._host_seq = int(info["seq"])
+        return None
+
+    def __getitem__(self, idx: int):
+        if idx < 0:
+            raise ValueError(f"negative batch index {idx}")
+        if idx >= self._len:
+            raise IndexError(idx)
+        # map the epoch-level index to the current window
+        p, s = self._schedule(self.window)
+        bpw = self.batches_per_window[p]
+        first_in_window = self.epoch_batch - self.batch
+        local = idx - first_in_window
+        if not 0 <= local < bpw:
+            raise IndexError(f"batch {idx} is not in the current window (sequential access only across windows)")
+        sw = self._window()
+        out = self._batch_from_window(sw, p, s, local)
+        self.metrics.on_batch(self.batch_size)
+        if self.debug_checksum:
+            self.checksums.append(int(ops.checksum(out[0] if isinstance(out, tuple) else out).item()))
+        return out
+
+    def _perm_for(self, p: int, seq: int) -> FeistelPermutation | None:
+        if self.shuffle != "device":
+            return None
+        # key = (seed, producer, round): every window visit gets a fresh order.
+        return FeistelPermutation(self.metadata_from_producer[p].nData, self.seed,
+                                  (seq << 8) | (p & 0xFF))
+
+    def _batch_from_window(self, sw, p: int, s: int, local: int):
+        B = self.batch_size
+        n_data = self.shapes[p][0]
+        wdt = self.window_dtype
+        if sw is None:  # host path: zero-copy views of the shm window
+            _, win = self.arys[p][s]
+            seq = self._host_seq
+        else:
+            win = sw.data.view(wdt).view((n_data,) + self.sample_shape)
+            seq = sw.seq
+        perm = self._perm_for(p, seq)
+        out_dtype = self.out_dtype or wdt
+        splits = list(self.splits[p])
+        norm = self.normalize
+        with trace_range("ddl.consumer.batch"):
+            if norm is not None and norm.get("layout", "chw") == "hwc":
+                x = ops.collate_hwc_to_chw(win, perm=perm, base=local * B, n_rows=B, out_dtype=out_dtype,
+                                           mean=norm.get("mean"), std=norm.get("std"))
+                return (x,)
+            if self.contiguous and len(splits) > 1 and len(self.sample_shape) == 1:
+                return ops.split_columns(win, splits, perm=perm, base=local * B, n_rows=B, out_dtype=out_dtype)
+            if perm is None and out_dtype == wdt and norm is None:
+                x = win[local * B:(local + 1) * B]  # zero-copy view (reference semantics)
+            else:
+                kw = {}
+                if norm is not None:
+                    plane = int(math.prod(self.sample_shape[1:])) if len(self.sample_shape) > 1 else 1
+                    c = self.sample_shape[0] if len(self.sample_shape) > 1 else len(norm.get("mean", [0]))
+                    sc, bi = ops.kernels._norm_affine(c, norm.get("mean"), norm.get("std"), norm.get("scale"),
+                                                      norm.get("bias"))
+                    kw = dict(scale=sc, bias=bi, plane=plane)
+                x = ops.gather_rows(win, perm=perm, base=local * B, n_rows=B, out_dtype=out_dtype, **kw)
+        if len(splits) == 1:
+            return (x,)
+        flat = x.reshape(B, -1)
+        return tuple(torch.split(flat, splits, dim=1))
+
+    def __iter__(self) -> Iterator:
+        n = self._len
+        for i in range(n):
+            item = self[i]
+            yield item
+            if self.auto_mark:
+                self.mark(Marker.END_OF_BATCH)
+        if self.auto_mark:
+            self.mark(Marker.END_OF_EPOCH)
+
+    # ---------------------------------------------------------- state machine
+    def mark(self, mark: Marker) -> None:
+        if mark == Marker.END_OF_BATCH:
+            self._on_batch_end()
+        elif mark == Marker.END_OF_EPOCH:
+            self._on_epoch_end()
+        else:
+            raise ValueError(f"Unknown mark {mark}")
+
+    def _release_window(self) -> None:
+        if self._stager is not None:
+            self._stager.release(self.window)
+            self._cur = None
+        elif self._host_window == self.window:
+            p, s = self._schedule(self.window)
+            self.connection.release(p, s)
+            self._host_window = None
+
+    def _advance_window(self) -> None:
+        self._release_window()
+        self.window += 1
+        self.window_in_epoch += 1
+        self.batch = 0
+        P = self.connection.n_producers
+        self.target_rank = self.window % P + 1
+
+    def _on_batch_end(self) -> None:
+        if self._finalized:
+            return
+        self.batch += 1
+        self.epoch_batch += 1
+        p, _ = self._schedule(self.window)
+        if self.batch >= self.batches_per_window[p]:
+            if self.window_in_epoch + 1 < self.windows_per_epoch:
+                self._advance_window()
+            else:
+                # last window of the epoch: hand it back now (the reference releases at
+                # the window's last END_OF_BATCH too, ddl/mpi_dataloader.py:223-227)
+                self._release_window()
+
+    def _on_epoch_end(self) -> None:
+        if self._finalized or self.connection is None or self.connection.n_producers == 0:
+            self.epoch += 1
+            return
+        self._release_window()
+        last = self.epoch + 1 >= self.n_epochs
+        # a partial epoch still consumes its remaining windows, in order, so the
+        # producers' round-robin stays aligned (skipped entirely when finishing)
+        while self.window_in_epoch + 1 < self.windows_per_epoch:
+            self.window += 1
+            self.window_in_epoch += 1
+            if not last:
+                self._window()
+                self._release_window()
+        self.window += 1
+        self.window_in_epoch = 0
+        self.batch = 0
+        self.epoch_batch = 0
+        self.epoch += 1
+        self.target_rank = self.window % self.connection.n_producers + 1
+        if self.epoch >= self.n_epochs:
+            self._finalize()
+        else:
+            self._update_len()
+
+    def set_epoch(self, epoch: int) -> None:
+        """torch-style hook; the order is driven by the internal cursor, so this only checks it."""
+        if epoch != self.epoch:
+            logger.warning("set_epoch(%d) while the loader cursor is at epoch %d", epoch, self.epoch)
+
+    def _can_continue(self) -> bool:
+        return self.epoch < self.n_epochs
+
+    # ------------------------------------------------------------ checkpoint
+    def state_dict(self) -> dict:
+        return {
+            "version": STATE_VERSION,
+            "kind": "window",
+            "mode": self.mode,
+            "seed": self.seed,
+            "epoch": self.epoch,
+            "window": self.window,
+            "window_in_epoch": self.window_in_epoch,
+            "batch": self.batch,
+            "epoch_batch": self.epoch_batch,
+            "batch_size": self.batch_size,
+            "n_producers": self.connection.n_producers if self.connection else 0,
+            "n_slots": self.n_slots,
+            "shuffle": self.shuffle,
+            "fraction_exchange": self.fraction_exchange,
+            "world_size": self.env.world_size if self.env else self.n_instances,
+            "dtype": str(self.out_dtype or getattr(self, "window_dtype", torch.float32)).replace("torch.", ""),
+        }
+
+    def _apply_state(self, sd: dict) -> None:
+        if sd.get("version") != STATE_VERSION:
+            raise ValueError(f"unsupported loader state version {sd.get('version')}")
+        if sd.get("batch", 0) != 0:
+            logger.warning("resuming mid-window: the partially consumed window is skipped")
+        self.epoch = int(sd["epoch"])
+        self.window = int(sd["window"]) + (1 if sd.get("batch", 0) else 0)
+        self.window_in_epoch = int(sd["window_in_epoch"]) + (1 if sd.get("batch", 0) else 0)
+        self.batch = 0
+        self.epoch_batch = int(sd.get("epoch_batch", 0))
+        if sd.get("seed") is not None:
+            self.seed = int(sd["seed"])
+
+    def load_state_dict(self, sd: dict) -> None:
+        raise RuntimeError("pass the state as DistributedDataLoader(..., resume_state=sd): producers are started "
+                           "at construction and must begin at the checkpointed round")
+
+    # --------------------------------------------------------------- teardown
+    def _finalize(self) -> None:
+        if self._finalized:
+            return
+        self._finalized = True
+        if self.connection is not None:
+            self.connection.shutdown_operation()
+        if self._stager is not None:
+            self.metrics.bytes_h2d = self._stager.bytes_h2d
+            self._stager.close()
+        if self.connection is not None:
+            self.connection.finalize()
+
+    def close(self) -> None:
+        self._finalize()
+
+    def stats(self) -> dict:
+        d = self.metrics.as_dict()
+        if self._stager is not None:
+            d.update(self._stager.stats())
+        if self.connection is not None:
+            d["producers"] = self.connection.producer_stats()
+        return d
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            if not getattr(self, "_finalized", True):
+                self._finalize()
+        except Exception:
+            pass

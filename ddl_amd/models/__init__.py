@@ -1,0 +1,23 @@
+"""Dataset / producer families and the synthetic train steps used by the benches."""
+
+from .datasets import (
+    DummyDataset,
+    NpyMemmapSource,
+    PointWiseData,
+    SharedArraySource,
+    SyntheticTokens,
+    synthetic_images,
+)
+from .producers import ImageWindowProducer, IndexedProducer, PointwiseProducer
+
+__all__ = [
+    "DummyDataset",
+    "NpyMemmapSource",
+    "PointWiseData",
+    "SharedArraySource",
+    "SyntheticTokens",
+    "synthetic_images",
+    "ImageWindowProducer",
+    "IndexedProducer",
+    "PointwiseProducer",
+]

@@ -1,0 +1,228 @@
+"""Synthetic datasets and shared sample sources ("model families" of a data loader).
+
+* ``PointWiseData`` / ``DummyDataset``: the reference harness's tabular
+  point-cloud data with min-max / standard normalisation (reference
+  tests/run_ddl.py:20-104), used by the reference-parity tests and configs.
+* ``SyntheticImages``: ImageNet-shape samples (BASELINE configs 2/3/5).
+* ``SyntheticTokens``: ragged token sequences (BASELINE config 4).
+* ``SharedArraySource``: a node-wide dataset in POSIX shared memory, created
+  once and mapped by every producer of every rank on the node; picklable by
+  name. Producers gather samples out of it with the native multi-threaded
+  gather (``_ddl_runtime.gather_rows``).
+* ``NpyMemmapSource``: an ``.npy`` file mapped read-only (page cache shared).
+"""
+
+from __future__ import annotations
+
+import math
+import os
+from multiprocessing import shared_memory
+
+import numpy as np
+import torch
+
+from ..ops import _dtypes
+
+
+class PointWiseData:
+    """Column groups [parameter | x | u | (sample weight)] (reference tests/run_ddl.py:20-77)."""
+
+    def __init__(self, parameter_data, x_data, u_data, sample_weight=None):
+        parts = [parameter_data, x_data, u_data] + ([sample_weight] if sample_weight is not None else [])
+        self.data_raw = np.hstack(parts)
+        self.data = None
+        self.sample_weight = None
+        self.n_p = parameter_data.shape[-1]
+        self.n_x = x_data.shape[-1]
+        self.n_o = u_data.shape[-1]
+
+    @property
+    def parameter(self):
+        return self.data[:, : self.n_p]
+
+    @property
+    def x(self):
+        return self.data[:, self.n_p : self.n_p + self.n_x]
+
+    @property
+    def u(self):
+        return self.data[:, self.n_p + self.n_x : self.n_p + self.n_x + self.n_o]
+
+    @staticmethod
+    def standard_normalize(raw, area_weighted=False):
+        mean = raw.mean(axis=0)
+        std = raw.std(axis=0)
+        if area_weighted:
+            mean[-1] = 0.0
+            std[-1] = np.mean(raw[:, -1])
+            out = (raw - mean) / std
+            return out[:, :-1], mean, std, out[:, -1]
+        return (raw - mean) / std, mean, std
+
+    @staticmethod
+    def minmax_normalize(raw, n_para, n_x, n_target, area_weighted=False):
+        mean = raw.mean(axis=0)
+        std = raw.std(axis=0)
+        lo, hi = raw.min(axis=0), raw.max(axis=0)
+        k = n_para + n_x
+        mean[:k] = 0.5 * (lo[:k] + hi[:k])
+        std[:k] = 0.5 * (hi[:k] - lo[:k])
+        std[k:k + n_target] = np.abs(raw[:, k:k + n_target]).max(axis=0)
+        if area_weighted:
+            mean[-1] = 0.0
+            std[-1] = np.mean(raw[:, -1])
+            out = (raw - mean) / std
+            return out[:, :-1], mean, std, out[:, -1]
+        return (raw - mean) / std, mean, std
+
+
+class DummyDataset(PointWiseData):
+    """Random (n x 10) f32 table split into groups (1, 2, 5, weight) (reference tests/run_ddl.py:80-104)."""
+
+    ROWS_PER_TIMESTEP = 10052
+
+    def __init__(self, nTimesteps: int, idx: int, n_instances: int, seed: int | None = None):  # noqa: N803
+        n_data = nTimesteps * self.ROWS_PER_TIMESTEP
+        start = -(idx + 1) * n_data // n_instances - 1
+        end = -idx * n_data // n_instances - 1
+        rng = np.random.default_rng(seed)
+        data = rng.random((end - start, 10), dtype=np.float32)
+        super().__init__(data[:, [0]], data[:, [2, 3]], data[:, [4, 5, 6, 7, 8]], data[:, [-1]])
+        self.data, self.mean, self.std, self.sample_weight = self.minmax_normalize(
+            self.data_raw, n_para=self.n_p, n_x=self.n_x, n_target=self.n_o, area_weighted=True)
+
+
+def synthetic_images(n: int, shape=(3, 224, 224), dtype=torch.bfloat16, seed: int = 0, start: int = 0) -> torch.Tensor:
+    """Deterministic synthetic images: sample i depends only on (seed, start + i)."""
+    g = torch.Generator().manual_seed(seed * 1_000_003 + start)
+    if dtype == torch.uint8:
+        return torch.randint(0, 256, (n, *shape), generator=g, dtype=torch.uint8)
+    return torch.rand((n, *shape), generator=g, dtype=torch.float32).to(dtype)
+
+
+class SharedArraySource:
+    """A node-wide [N, *sample_shape] array in POSIX shm (created once, mapped by name)."""
+
+    def __init__(self, name: str, n: int, sample_shape: tuple[int, ...], dtype, create: bool = False):
+        self.name = name
+        self.n = int(n)
+        self.sample_shape = tuple(sample_shape)
+        self.dtype = _dtypes.to_torch_dtype(dtype)
+        self.row_bytes = int(math.prod(self.sample_shape)) * _dtypes.itemsize(self.dtype)
+        self._shm: shared_memory.SharedMemory | None = None
+        self._owner = create
+        if create:
+            self._shm = shared_memory.SharedMemory(name=name, create=True, size=max(1, self.n * self.row_bytes))
+
+    @classmethod
+    def create(cls, name: str, data: torch.Tensor) -> "SharedArraySource":
+        src = cls(name, data.shape[0], tuple(data.shape[1:]), data.dtype, create=True)
+        src.tensor().copy_(data)
+        return src
+
+    def __getstate__(self):
+        return {"name": self.name, "n": self.n, "sample_shape": self.sample_shape, "dtype": self.dtype}
+
+    def __setstate__(self, st):
+        self.__init__(st["name"], st["n"], st["sample_shape"], st["dtype"], create=False)
+
+    def _map(self) -> shared_memory.SharedMemory:
+        if self._shm is None:
+            # track=False-equivalent: do not let the resource tracker unlink the owner's segment
+            self._shm = shared_memory.SharedMemory(name=self.name, create=False)
+            try:
+                from multiprocessing import resource_tracker
+
+                resource_tracker.unregister(self._shm._name, "shared_memory")  # type: ignore[attr-defined]
+            except Exception:
+                pass
+        return self._shm
+
+    @property
+    def address(self) -> int:
+        import ctypes
+
+        buf = self._map().buf
+        return ctypes.addressof(ctypes.c_char.from_buffer(buf))
+
+    def tensor(self) -> torch.Tensor:
+        shm = self._map()
+        t = torch.frombuffer(shm.buf, dtype=torch.uint8, count=self.n * self.row_bytes)
+        return t.view(self.dtype).view((self.n,) + self.sample_shape)
+
+    def gather(self, indices: np.ndarray, dst_address: int, n_threads: int = 4) -> None:
+        from .. import _native
+
+        _native.runtime().gather_rows(dst_address, self.address, self.row_bytes,
+                                      np.ascontiguousarray(indices, dtype=np.int64), self.n, n_threads)
+
+    def close(self, unlink: bool | None = None) -> None:
+        if self._shm is None:
+            return
+        unlink = self._owner if unlink is None else unlink
+        try:
+            self._shm.close()
+        except BufferError:
+            pass
+        if unlink:
+            try:
+                self._shm.unlink()
+            except FileNotFoundError:
+                pass
+        self._shm = None
+
+
+class NpyMemmapSource:
+    """Read-only memory-mapped ``.npy`` dataset [N, ...] (page cache shared across processes)."""
+
+    def __init__(self, path: str):
+        self.path = os.path.abspath(path)
+        arr = np.load(self.path, mmap_mode="r")
+        self.n = arr.shape[0]
+        self.sample_shape = tuple(arr.shape[1:])
+        self.dtype = _dtypes.to_torch_dtype(arr.dtype)
+        self.row_bytes = int(math.prod(self.sample_shape)) * arr.dtype.itemsize
+        self._arr = None
+
+    def __getstate__(self):
+        return {"path": self.path}
+
+    def __setstate__(self, st):
+        self.__init__(st["path"])
+
+    def _a(self) -> np.ndarray:
+        if self._arr is None:
+            self._arr = np.load(self.path, mmap_mode="r")
+        return self._arr
+
+    def gather(self, indices: np.ndarray, dst_address: int, n_threads: int = 4) -> None:
+        import ctypes
+
+        from .. import _native
+
+        a = self._a()
+        addr = a.ctypes.data if a.flags["C_CONTIGUOUS"] else None
+        if addr is None:  # pragma: no cover
+            raise ValueError("memmap must be C-contiguous")
+        _native.runtime().gather_rows(dst_address, addr, self.row_bytes, np.ascontiguousarray(indices, np.int64),
+                                      self.n, n_threads)
+        del ctypes
+
+
+class SyntheticTokens:
+    """Deterministic ragged token sequences: sequence i has length in [min_len, max_len]."""
+
+    def __init__(self, n: int, min_len: int = 128, max_len: int = 4096, vocab: int = 50257, seed: int = 0):
+        self.n, self.min_len, self.max_len, self.vocab, self.seed = n, min_len, max_len, vocab, seed
+        rng = np.random.default_rng(seed)
+        self.lengths = rng.integers(min_len, max_len + 1, size=n).astype(np.int64)
+        self.offsets = np.concatenate([[0], np.cumsum(self.lengths)]).astype(np.int64)
+
+    def sequence(self, i: int) -> np.ndarray:
+        rng = np.random.default_rng([self.seed, i])
+        return rng.integers(0, self.vocab, size=int(self.lengths[i]), dtype=np.int32)
+
+    def batch(self, indices) -> tuple[np.ndarray, np.ndarray]:
+        seqs = [self.sequence(int(i)) for i in indices]
+        offs = np.concatenate([[0], np.cumsum([len(s) for s in seqs])]).astype(np.int64)
+        return (np.concatenate(seqs) if seqs else np.zeros(0, np.int32)), offs

@@ -1,0 +1,144 @@
+"""Built-in producer functions (``ProducerFunctionSkeleton`` subclasses).
+
+* ``PointwiseProducer``  -- the reference harness's producer (reference
+  tests/run_ddl.py:107-167): tabular shard, column groups (3, 5, 1), optional
+  host-side in-place row shuffle per round. Round-deterministic RNG (seeded by
+  (seed, rank, producer, round)) so a resumed run reproduces the windows.
+* ``ImageWindowProducer`` -- a window of synthetic 3x224x224 images (bf16 or
+  uint8, CHW or HWC). ``execute_function`` stamps the round into every sample
+  (a cheap refill that makes each window visit distinct) or regenerates it.
+* ``IndexedProducer``    -- world-size-invariant global order: window = one
+  rank-local batch of the global batch ``g`` of the ``EpochOrder``; the
+  producer gathers the samples out of a node-shared source with the native
+  multi-threaded gather straight into its pinned slot.
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Any
+
+import numpy as np
+import torch
+
+from ..datapusher import DataProducerOnInitReturn
+from ..datasetwrapper import ProducerFunctionSkeleton
+from ..ops import _dtypes
+from ..permutation import EpochOrder
+from .datasets import DummyDataset, synthetic_images
+
+
+class PointwiseProducer(ProducerFunctionSkeleton):
+    def __init__(self, n_timesteps: int = 10, idx: int = 0, n_instances: int = 1, host_shuffle: bool = True,
+                 seed: int = 0, rows_per_timestep: int | None = None):
+        super().__init__()
+        self.n_timesteps = n_timesteps
+        self.idx = idx
+        self.n_instances = n_instances
+        self.host_shuffle = host_shuffle
+        self.seed = seed
+        self.rows_per_timestep = rows_per_timestep
+        self.nData = None
+        self._groups = None
+
+    def on_init(self, *args, **kwargs):
+        super().on_init(*args, **kwargs)
+        if self.rows_per_timestep is not None:
+            DummyDataset.ROWS_PER_TIMESTEP = self.rows_per_timestep
+        ds = DummyDataset(self.n_timesteps, self.idx, self.n_instances,
+                          seed=[self.seed, self.rank_global or 0, self.producer_index or 0])
+        data, w = ds.data, ds.sample_weight
+        self._groups = (data[:, :3], data[:, 3:8], w.reshape(-1, 1))
+        self.nData = data.shape[0]
+        splits = tuple(g.shape[1] for g in self._groups)
+        return DataProducerOnInitReturn(self.nData, sum(splits), (self.nData, sum(splits)), splits, "float32")
+
+    def post_init(self, *args, **kwargs):
+        super().post_init(*args, **kwargs)
+        self.my_ary[...] = np.concatenate([g.astype(np.float32) for g in self._groups], axis=1)
+        self._groups = None
+
+    def execute_function(self, *args, **kwargs):
+        if not self.host_shuffle:
+            return
+        rng = np.random.default_rng([self.seed, self.rank_global or 0, self.producer_index or 0,
+                                     int(kwargs.get("round", 0))])
+        rng.shuffle(self.my_ary)
+
+
+class ImageWindowProducer(ProducerFunctionSkeleton):
+    def __init__(self, n_samples: int, shape=(3, 224, 224), dtype: Any = "bfloat16", seed: int = 0,
+                 refill: str = "stamp"):
+        super().__init__()
+        if refill not in ("stamp", "none", "regenerate"):
+            raise ValueError("refill must be 'stamp', 'none' or 'regenerate'")
+        self.n_samples = int(n_samples)
+        self.shape = tuple(shape)
+        self.dtype = dtype
+        self.seed = seed
+        self.refill = refill
+
+    def on_init(self, *args, **kwargs):
+        super().on_init(*args, **kwargs)
+        nv = int(math.prod(self.shape))
+        return DataProducerOnInitReturn(self.n_samples, nv, (self.n_samples, *self.shape), (nv,), self.dtype)
+
+    def _fill(self, t: torch.Tensor, rnd: int) -> None:
+        dt = _dtypes.to_torch_dtype(self.dtype)
+        s = self.seed * 7919 + (self.rank_global or 0) * 131 + (self.producer_index or 0)
+        chunk = 256
+        for i in range(0, self.n_samples, chunk):
+            n = min(chunk, self.n_samples - i)
+            t[i:i + n].copy_(synthetic_images(n, self.shape, dt, seed=s, start=i + rnd * self.n_samples))
+
+    def post_init(self, *args, **kwargs):
+        super().post_init(*args, **kwargs)
+        self._fill(self.my_tensor, 0)
+
+    def execute_function(self, *args, **kwargs):
+        rnd = int(kwargs.get("round", 0))
+        t = kwargs.get("my_tensor", self.my_tensor)
+        if self.refill == "stamp":
+            flat = t.view(self.n_samples, -1)
+            flat[:, 0] = float(rnd % 251) if t.dtype != torch.uint8 else rnd % 251
+        elif self.refill == "regenerate":
+            self._fill(t, rnd)
+
+
+class IndexedProducer(ProducerFunctionSkeleton):
+    """Producer of the world-size-invariant global order (one window = one local batch)."""
+
+    def __init__(self, source, global_batch: int, seed: int = 0, drop_last: bool = True, host_threads: int = 4):
+        super().__init__()
+        self.source = source
+        self.global_batch = int(global_batch)
+        self.seed = int(seed)
+        self.drop_last = drop_last
+        self.host_threads = host_threads
+        self.world_size = 1
+        self.order: EpochOrder | None = None
+
+    def on_init(self, *args, **kwargs):
+        super().on_init(*args, **kwargs)
+        self.world_size = int(kwargs.get("world_size", 1))
+        self.order = EpochOrder(self.source.n, self.global_batch, self.seed, self.drop_last)
+        lb = self.order.local_batch(self.world_size)
+        nv = int(math.prod(self.source.sample_shape)) if self.source.sample_shape else 1
+        return DataProducerOnInitReturn(lb, nv, (lb, *self.source.sample_shape), (nv,), self.source.dtype,
+                                        extra={"batches_per_epoch": self.order.batches_per_epoch,
+                                               "global_batch": self.global_batch, "n_samples": self.source.n})
+
+    def post_init(self, *args, **kwargs):
+        super().post_init(*args, **kwargs)
+
+    def batch_indices(self, rnd: int) -> np.ndarray:
+        assert self.order is not None
+        g_total = rnd * (self.n_producers or 1) + (self.producer_index or 0)
+        epoch, g = divmod(g_total, self.order.batches_per_epoch)
+        return self.order.indices(epoch, g, self.rank_global or 0, self.world_size)
+
+    def execute_function(self, *args, **kwargs):
+        rnd = int(kwargs.get("round", 0))
+        t: torch.Tensor = kwargs.get("my_tensor", self.my_tensor)
+        idx = self.batch_indices(rnd)
+        self.source.gather(idx, t.data_ptr(), self.host_threads)

@@ -1,0 +1,473 @@
+"""Python front-end of the hand-written gfx950 kernels (csrc/kernels/*.hip).
+
+Every op dispatches to the HIP kernel when its tensors live on the GPU and to
+a plain-PyTorch reference (``ref_*``) when they live on the CPU. There is no
+silent fallback on GPU: if the extension is missing on a GPU host the call
+raises ``NativeExtensionError`` (see ``ddl_amd._native``). Tests compare each
+kernel against its ``ref_*`` (an fp32 PyTorch reference of the same op).
+
+Row-indexing convention shared by the gather-style ops (``RowIndex`` in
+csrc/kernels/common.h): output row ``r`` reads source row
+  * ``index[r]``                      if ``index`` is given,
+  * ``perm(base + r)``                if ``perm`` (a FeistelPermutation) is given,
+  * ``base + r``                      otherwise.
+"""
+
+from __future__ import annotations
+
+import dataclasses
+import math
+from typing import Sequence
+
+import numpy as np
+import torch
+
+from .. import _native
+from ..permutation import FeistelPermutation
+from . import _dtypes
+
+
+@dataclasses.dataclass
+class HostRows:
+    """Rows living in pinned, device-mapped host memory (zero-copy source).
+
+    ``cpu`` is a CPU tensor view of the memory ([N, *row_shape]); ``device_ptr``
+    is the address the GPU uses for it (``hipHostGetDevicePointer``).
+    """
+
+    cpu: torch.Tensor
+    device_ptr: int
+
+    @property
+    def shape(self):
+        return self.cpu.shape
+
+    @property
+    def dtype(self):
+        return self.cpu.dtype
+
+    @property
+    def device(self):
+        return torch.device("cuda", torch.cuda.current_device())
+
+
+def _stream_handle(stream) -> int:
+    if stream is None:
+        return torch.cuda.current_stream().cuda_stream
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+def _is_gpu(t) -> bool:
+    return isinstance(t, HostRows) or (isinstance(t, torch.Tensor) and t.is_cuda)
+
+
+def _src_addr(src) -> int:
+    return src.device_ptr if isinstance(src, HostRows) else src.data_ptr()
+
+
+def _index_kw(index: torch.Tensor | None, perm: FeistelPermutation | None, base: int) -> dict:
+    if index is not None and perm is not None:
+        raise ValueError("give either index or perm, not both")
+    if index is not None:
+        if index.dtype != torch.int64:
+            raise TypeError("index must be int64")
+        if not index.is_cuda:
+            raise ValueError("index must live on the GPU for a GPU gather")
+        return dict(mode=1, idx=index.data_ptr(), base=0, keys=[0] * 6, n_domain=1, half_bits=1)
+    if perm is not None:
+        return dict(mode=2, idx=0, base=int(base), **perm.device_args())
+    return dict(mode=0, idx=0, base=int(base), keys=[0] * 6, n_domain=1, half_bits=1)
+
+
+def _ref_rows(n_src: int, n_rows: int, index, perm, base) -> torch.Tensor:
+    if index is not None:
+        return index.to("cpu", torch.int64)
+    pos = np.arange(base, base + n_rows, dtype=np.int64)
+    if perm is not None:
+        return torch.from_numpy(perm(pos))
+    if pos.size and pos.max() >= n_src:
+        raise IndexError("identity rows out of range")
+    return torch.from_numpy(pos)
+
+
+def _affine_lists(scale, bias) -> tuple[list[float], list[float]]:
+    if scale is None and bias is None:
+        return [], []
+    if scale is None:
+        scale = [1.0] * len(bias)
+    if bias is None:
+        bias = [0.0] * len(scale)
+    scale, bias = [float(s) for s in scale], [float(b) for b in bias]
+    if len(scale) != len(bias) or not 1 <= len(scale) <= 8:
+        raise ValueError("scale/bias: 1..8 channels of equal length")
+    return scale, bias
+
+
+def _check_rows(src, index, perm, base, n_rows) -> int:
+    n_src = src.shape[0]
+    if n_rows is None:
+        if index is not None:
+            n_rows = index.numel()
+        elif perm is not None:
+            n_rows = perm.n - base
+        else:
+            n_rows = n_src - base
+    if n_rows < 0:
+        raise ValueError("negative row count")
+    if perm is not None and (base < 0 or base + n_rows > perm.n):
+        raise IndexError("perm positions out of range")
+    if perm is not None and perm.n > n_src:
+        raise IndexError("permutation domain larger than the source")
+    if index is None and perm is None and base + n_rows > n_src:
+        raise IndexError("identity rows out of range")
+    return int(n_rows)
+
+
+# --------------------------------------------------------------------- gather
+def ref_gather_rows(src, index=None, perm=None, base=0, n_rows=None, out_dtype=None, scale=None, bias=None,
+                    plane=None) -> torch.Tensor:
+    x = src.cpu if isinstance(src, HostRows) else src
+    n_rows = _check_rows(x, index, perm, base, n_rows)
+    rows = x.index_select(0, _ref_rows(x.shape[0], n_rows, index, perm, base).to(x.device))
+    out_dtype = out_dtype or x.dtype
+    sc, bi = _affine_lists(scale, bias)
+    if sc:
+        flat = rows.reshape(n_rows, -1).double()
+        ch = (torch.arange(flat.shape[1], device=flat.device) // int(plane)) % len(sc)
+        s = torch.tensor(sc, dtype=torch.float64, device=flat.device)[ch]
+        b = torch.tensor(bi, dtype=torch.float64, device=flat.device)[ch]
+        rows = (flat * s + b).float().reshape(rows.shape)
+    elif out_dtype != x.dtype:
+        rows = rows.float()
+    return rows.to(out_dtype)
+
+
+def gather_rows(src, index: torch.Tensor | None = None, *, perm: FeistelPermutation | None = None, base: int = 0,
+                n_rows: int | None = None, out: torch.Tensor | None = None, out_dtype=None, scale=None, bias=None,
+                plane: int | None = None, stream=None) -> torch.Tensor:
+    """out[r] = cast(affine(src[row(r)])): fused permute + cast + per-channel normalise."""
+    out_dtype = _dtypes.to_torch_dtype(out_dtype) if out_dtype is not None else src.dtype
+    if not _is_gpu(src):
+        res = ref_gather_rows(src, index, perm, base, n_rows, out_dtype, scale, bias, plane)
+        if out is not None:
+            out.copy_(res)
+            return out
+        return res
+    n_rows = _check_rows(src, index, perm, base, n_rows)
+    row_shape = tuple(src.shape[1:])
+    row_elems = int(math.prod(row_shape)) if row_shape else 1
+    if isinstance(src, torch.Tensor) and not src.is_contiguous():
+        raise ValueError("gather_rows: source must be contiguous")
+    if out is None:
+        out = torch.empty((n_rows,) + row_shape, dtype=out_dtype, device=src.device)
+    elif not out.is_contiguous() or out.dtype != out_dtype or out.numel() != n_rows * row_elems:
+        raise ValueError("gather_rows: bad out tensor")
+    sc, bi = _affine_lists(scale, bias)
+    if sc and plane is None:
+        raise ValueError("plane (elements per channel) is required with scale/bias")
+    if sc and (out_dtype in (torch.uint8, torch.int32, torch.int64)):
+        raise TypeError("normalisation needs a floating output dtype")
+    if out_dtype != src.dtype and out_dtype not in (torch.bfloat16, torch.float16, torch.float32):
+        raise TypeError(f"cannot cast {src.dtype} -> {out_dtype} in the gather")
+    _native.hip().gather_rows(
+        dst=out.data_ptr(), out_dt=_dtypes.code(out_dtype), src=_src_addr(src), in_dt=_dtypes.code(src.dtype),
+        n_rows=n_rows, row_elems=row_elems, scale=sc, bias=bi, plane=int(plane or 0), scatter=False,
+        stream=_stream_handle(stream), **_index_kw(index, perm, base))
+    return out
+
+
+def scatter_rows(dst: torch.Tensor, src: torch.Tensor, index: torch.Tensor, *, stream=None) -> torch.Tensor:
+    """dst[index[r]] = src[r] (same dtype). Used to put exchanged rows back."""
+    if dst.dtype != src.dtype or dst.shape[1:] != src.shape[1:]:
+        raise ValueError("scatter_rows: dst/src row mismatch")
+    if index.numel() != src.shape[0]:
+        raise ValueError("scatter_rows: one index per source row")
+    if not dst.is_cuda:
+        dst.index_copy_(0, index.to(torch.int64), src)
+        return dst
+    row_elems = int(math.prod(src.shape[1:])) if src.dim() > 1 else 1
+    _native.hip().gather_rows(
+        dst=dst.data_ptr(), out_dt=_dtypes.code(dst.dtype), src=src.data_ptr(), in_dt=_dtypes.code(src.dtype),
+        n_rows=src.shape[0], row_elems=row_elems, scale=[], bias=[], plane=0, scatter=True,
+        stream=_stream_handle(stream), **_index_kw(index, None, 0))
+    return dst
+
+
+def feistel_indices(perm: FeistelPermutation, base: int, count: int, device=None, stream=None) -> torch.Tensor:
+    """Materialise perm(base .. base+count-1) (int64) on ``device``."""
+    device = torch.device(device) if device is not None else torch.device("cpu")
+    if base < 0 or base + count > perm.n:
+        raise IndexError("positions out of range")
+    if device.type != "cuda":
+        return torch.from_numpy(perm(np.arange(base, base + count, dtype=np.int64)))
+    out = torch.empty(count, dtype=torch.int64, device=device)
+    _native.hip().feistel_indices(out=out.data_ptr(), count=count, base=base, stream=_stream_handle(stream),
+                                  **perm.device_args())
+    return out
+
+
+def cast(x: torch.Tensor, dtype, *, scale=None, bias=None, plane=None, stream=None) -> torch.Tensor:
+    """Vectorised dtype cast (RNE to bf16) with optional per-channel affine."""
+    dtype = _dtypes.to_torch_dtype(dtype)
+    rows = x.reshape(x.shape[0], -1) if x.dim() > 1 else x.reshape(1, -1)
+    out = gather_rows(rows, out_dtype=dtype, scale=scale, bias=bias, plane=plane, stream=stream)
+    return out.reshape(x.shape)
+
+
+# -------------------------------------------------------------------- collate
+def ref_collate_hwc_to_chw(src, index=None, perm=None, base=0, n_rows=None, out_dtype=torch.bfloat16, mean=None,
+                           std=None, scale=None, bias=None) -> torch.Tensor:
+    x = src.cpu if isinstance(src, HostRows) else src
+    n_rows = _check_rows(x, index, perm, base, n_rows)
+    rows = x.index_select(0, _ref_rows(x.shape[0], n_rows, index, perm, base).to(x.device))
+    c = rows.shape[-1]
+    sc, bi = _norm_affine(c, mean, std, scale, bias)
+    y = rows.double().movedim(-1, 1)  # [B, C, H, W]
+    if sc:
+        s = torch.tensor(sc, dtype=torch.float64, device=y.device).view(1, c, *([1] * (y.dim() - 2)))
+        b = torch.tensor(bi, dtype=torch.float64, device=y.device).view(1, c, *([1] * (y.dim() - 2)))
+        y = y * s + b
+    return y.float().to(out_dtype).contiguous()
+
+
+def _norm_affine(c, mean, std, scale, bias):
+    """(x/255 - mean)/std  ==  x*scale + bias  with scale=1/(255*std), bias=-mean/std."""
+    if mean is not None or std is not None:
+        mean = list(mean) if mean is not None else [0.0] * c
+        std = list(std) if std is not None else [1.0] * c
+        if len(mean) != c or len(std) != c:
+            raise ValueError("mean/std must have one entry per channel")
+        return [1.0 / (255.0 * s) for s in std], [-m / s for m, s in zip(mean, std)]
+    return _affine_lists(scale, bias)
+
+
+def collate_hwc_to_chw(src, index: torch.Tensor | None = None, *, perm: FeistelPermutation | None = None,
+                       base: int = 0, n_rows: int | None = None, out_dtype=torch.bfloat16, mean=None, std=None,
+                       scale=None, bias=None, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """[N, H, W, C] (u8/f32/bf16, HWC) rows -> [B, C, H, W] normalised bf16/f32 (LDS-staged de-interleave).
+
+    ``mean``/``std`` follow the torchvision convention on [0, 1] pixels
+    (``(x/255 - mean)/std``); alternatively pass a raw ``scale``/``bias``.
+    """
+    out_dtype = _dtypes.to_torch_dtype(out_dtype)
+    if src.dim() < 3:
+        raise ValueError("collate_hwc_to_chw expects [N, ..., C]")
+    c = src.shape[-1]
+    if not _is_gpu(src):
+        res = ref_collate_hwc_to_chw(src, index, perm, base, n_rows, out_dtype, mean, std, scale, bias)
+        if out is not None:
+            out.copy_(res)
+            return out
+        return res
+    n_rows = _check_rows(src, index, perm, base, n_rows)
+    spatial = tuple(src.shape[1:-1])
+    pixels = int(math.prod(spatial))
+    sc, bi = _norm_affine(c, mean, std, scale, bias)
+    if out is None:
+        out = torch.empty((n_rows, c) + spatial, dtype=out_dtype, device=src.device)
+    _native.hip().collate_hwc_to_chw(
+        dst=out.data_ptr(), out_dt=_dtypes.code(out_dtype), src=_src_addr(src), in_dt=_dtypes.code(src.dtype),
+        batch=n_rows, pixels=pixels, channels=c, scale=sc, bias=bi, stream=_stream_handle(stream),
+        **_index_kw(index, perm, base))
+    return out
+
+
+def ref_split_columns(src, splits, index=None, perm=None, base=0, n_rows=None, out_dtype=None):
+    x = src.cpu if isinstance(src, HostRows) else src
+    n_rows = _check_rows(x, index, perm, base, n_rows)
+    rows = x.index_select(0, _ref_rows(x.shape[0], n_rows, index, perm, base).to(x.device))
+    out_dtype = out_dtype or x.dtype
+    return tuple(p.float().to(out_dtype).contiguous() for p in torch.split(rows, list(splits), dim=1))
+
+
+def split_columns(src, splits: Sequence[int], index: torch.Tensor | None = None, *,
+                  perm: FeistelPermutation | None = None, base: int = 0, n_rows: int | None = None, out_dtype=None,
+                  stream=None) -> tuple[torch.Tensor, ...]:
+    """[N, nValues] rows -> tuple of contiguous [B, w_k] column groups (fused gather + cast)."""
+    out_dtype = _dtypes.to_torch_dtype(out_dtype) if out_dtype is not None else src.dtype
+    if src.dim() != 2:
+        raise ValueError("split_columns expects [N, nValues]")
+    if sum(splits) != src.shape[1]:
+        raise ValueError("splits must sum to nValues")
+    if not _is_gpu(src):
+        return ref_split_columns(src, splits, index, perm, base, n_rows, out_dtype)
+    if out_dtype not in (torch.bfloat16, torch.float32):
+        raise TypeError("split_columns outputs bf16 or f32")
+    n_rows = _check_rows(src, index, perm, base, n_rows)
+    outs = tuple(torch.empty((n_rows, w), dtype=out_dtype, device=src.device) for w in splits)
+    _native.hip().split_columns(
+        dsts=[o.data_ptr() for o in outs], widths=[int(w) for w in splits], out_dt=_dtypes.code(out_dtype),
+        src=_src_addr(src), in_dt=_dtypes.code(src.dtype), n_rows=n_rows, n_values=src.shape[1],
+        stream=_stream_handle(stream), **_index_kw(index, perm, base))
+    return outs
+
+
+# --------------------------------------------------------------------- tokens
+def ref_pad_tokens(tokens: torch.Tensor, offsets: torch.Tensor, seq_len: int, pad_id: int = 0,
+                   position_dtype=torch.int64):
+    offs = offsets.to("cpu", torch.int64).tolist()
+    b = len(offs) - 1
+    t = tokens.to("cpu", torch.int32)
+    out = torch.full((b, seq_len), pad_id, dtype=torch.int32)
+    mask = torch.zeros((b, seq_len), dtype=torch.uint8)
+    pos = torch.zeros((b, seq_len), dtype=position_dtype)
+    for i in range(b):
+        n = min(offs[i + 1] - offs[i], seq_len)
+        if n > 0:
+            out[i, :n] = t[offs[i]:offs[i] + n]
+            mask[i, :n] = 1
+            pos[i, :n] = torch.arange(n, dtype=position_dtype)
+    return out, mask, pos
+
+
+def pad_tokens(tokens: torch.Tensor, offsets: torch.Tensor, seq_len: int, pad_id: int = 0,
+               position_dtype=torch.int64, stream=None):
+    """Ragged int32 token stream + [B+1] int64 offsets -> (tokens [B,S], mask u8 [B,S], position ids [B,S])."""
+    if tokens.dtype != torch.int32 or offsets.dtype != torch.int64:
+        raise TypeError("tokens must be int32 and offsets int64")
+    if not tokens.is_cuda:
+        return ref_pad_tokens(tokens, offsets, seq_len, pad_id, position_dtype)
+    b = offsets.numel() - 1
+    dev = tokens.device
+    out = torch.empty((b, seq_len), dtype=torch.int32, device=dev)
+    mask = torch.empty((b, seq_len), dtype=torch.uint8, device=dev)
+    pos = torch.empty((b, seq_len), dtype=position_dtype, device=dev)
+    _native.hip().pad_pack_tokens(
+        tokens=tokens.data_ptr(), offsets=offsets.data_ptr(), row_start=0, row_end=0, seg_offsets=0, n_seg=0,
+        out_tokens=out.data_ptr(), attn_mask=mask.data_ptr(), position_ids=pos.data_ptr(),
+        pos_is_i64=position_dtype == torch.int64, segment_ids=0, rows=b, seq_len=seq_len, pad_id=pad_id, mode=0,
+        stream=_stream_handle(stream))
+    return out, mask, pos
+
+
+def pack_plan(seq_offsets: np.ndarray, seq_len: int, max_rows: int | None = None):
+    """Greedy in-order packing of sequences into rows of ``seq_len`` tokens.
+
+    Sequences longer than ``seq_len`` are split into ``seq_len`` chunks (each
+    chunk restarts its position ids). Returns (row_start, row_end, seg_offsets)
+    int64 arrays: row r holds flat tokens [row_start[r], row_end[r]);
+    seg_offsets are the (split) sequence starts plus the end.
+    """
+    offs = np.asarray(seq_offsets, dtype=np.int64)
+    segs = []
+    for i in range(len(offs) - 1):
+        s, e = int(offs[i]), int(offs[i + 1])
+        while e - s > seq_len:
+            segs.append((s, s + seq_len))
+            s += seq_len
+        if e > s:
+            segs.append((s, e))
+    row_start, row_end = [], []
+    cur_s, cur_e = None, None
+    for s, e in segs:
+        if cur_s is None:
+            cur_s, cur_e = s, e
+        elif e - cur_s <= seq_len and s == cur_e:
+            cur_e = e
+        else:
+            row_start.append(cur_s)
+            row_end.append(cur_e)
+            cur_s, cur_e = s, e
+        if max_rows is not None and len(row_start) >= max_rows:
+            break
+    if cur_s is not None and (max_rows is None or len(row_start) < max_rows):
+        row_start.append(cur_s)
+        row_end.append(cur_e)
+    seg_offsets = np.array([s for s, _ in segs] + ([segs[-1][1]] if segs else [0]), dtype=np.int64)
+    return np.array(row_start, dtype=np.int64), np.array(row_end, dtype=np.int64), seg_offsets
+
+
+def ref_pack_tokens(tokens, row_start, row_end, seg_offsets, seq_len, pad_id=0, position_dtype=torch.int64):
+    t = tokens.to("cpu", torch.int32)
+    rs, re_, so = (np.asarray(a) for a in (row_start, row_end, seg_offsets))
+    r = len(rs)
+    out = torch.full((r, seq_len), pad_id, dtype=torch.int32)
+    mask = torch.zeros((r, seq_len), dtype=torch.uint8)
+    pos = torch.zeros((r, seq_len), dtype=position_dtype)
+    seg = torch.full((r, seq_len), -1, dtype=torch.int32)
+    for i in range(r):
+        n = min(int(re_[i] - rs[i]), seq_len)
+        g = np.arange(rs[i], rs[i] + n)
+        sidx = np.searchsorted(so, g, side="right") - 1
+        out[i, :n] = t[rs[i]:rs[i] + n]
+        mask[i, :n] = 1
+        pos[i, :n] = torch.from_numpy(g - so[sidx]).to(position_dtype)
+        seg[i, :n] = torch.from_numpy(sidx.astype(np.int32))
+    return out, mask, pos, seg
+
+
+def pack_tokens(tokens: torch.Tensor, seq_offsets, seq_len: int, pad_id: int = 0, position_dtype=torch.int64,
+                stream=None):
+    """Pack a ragged token stream into rows of ``seq_len`` (varlen-attention layout).
+
+    Returns (tokens [R,S] i32, mask [R,S] u8, position_ids [R,S], segment_ids [R,S] i32 (-1 = pad),
+    cu_seqlens [n_seg+1] i64).
+    """
+    rs, re_, so = pack_plan(np.asarray(seq_offsets.cpu() if torch.is_tensor(seq_offsets) else seq_offsets),
+                            seq_len)
+    cu = torch.from_numpy(so)
+    if not tokens.is_cuda:
+        return (*ref_pack_tokens(tokens, rs, re_, so, seq_len, pad_id, position_dtype), cu)
+    dev = tokens.device
+    rs_d, re_d, so_d = (torch.from_numpy(a).to(dev, non_blocking=False) for a in (rs, re_, so))
+    r = len(rs)
+    out = torch.empty((r, seq_len), dtype=torch.int32, device=dev)
+    mask = torch.empty((r, seq_len), dtype=torch.uint8, device=dev)
+    pos = torch.empty((r, seq_len), dtype=position_dtype, device=dev)
+    seg = torch.empty((r, seq_len), dtype=torch.int32, device=dev)
+    _native.hip().pad_pack_tokens(
+        tokens=tokens.data_ptr(), offsets=0, row_start=rs_d.data_ptr(), row_end=re_d.data_ptr(),
+        seg_offsets=so_d.data_ptr(), n_seg=len(so) - 1, out_tokens=out.data_ptr(), attn_mask=mask.data_ptr(),
+        position_ids=pos.data_ptr(), pos_is_i64=position_dtype == torch.int64, segment_ids=seg.data_ptr(), rows=r,
+        seq_len=seq_len, pad_id=pad_id, mode=1, stream=_stream_handle(stream))
+    return out, mask, pos, seg, cu.to(dev)
+
+
+# ----------------------------------------------------------------- reductions
+def ref_checksum(x: torch.Tensor) -> int:
+    b = x.detach().contiguous().reshape(-1).view(torch.uint8).cpu().numpy()
+    n = b.size // 4 * 4
+    return int(b[:n].view(np.uint32).astype(np.uint64).sum()) & ((1 << 64) - 1)
+
+
+def checksum(x: torch.Tensor, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """Sum of the 32-bit words of ``x`` (u64 wrap-around) as a 1-element int64 tensor (accumulates into ``out``)."""
+    if not x.is_contiguous():
+        raise ValueError("checksum needs a contiguous tensor")
+    nbytes = x.numel() * x.element_size()
+    if not x.is_cuda:
+        v = ref_checksum(x)
+        v = v - (1 << 64) if v >= (1 << 63) else v
+        res = torch.tensor([v], dtype=torch.int64)
+        if out is not None:
+            out += res
+            return out
+        return res
+    if out is None:
+        out = torch.zeros(1, dtype=torch.int64, device=x.device)
+    _native.hip().checksum_words(ptr=x.data_ptr(), bytes=nbytes - nbytes % 4, out=out.data_ptr(),
+                                 stream=_stream_handle(stream))
+    return out
+
+
+def column_stats(x: torch.Tensor, stream=None) -> dict[str, torch.Tensor]:
+    """Per-column sum / sumsq / min / max / mean / std of an [N, C] f32 matrix."""
+    if x.dim() != 2 or x.dtype != torch.float32:
+        raise TypeError("column_stats expects [N, C] float32")
+    n, c = x.shape
+    if not x.is_cuda:
+        s, q = x.double().sum(0).float(), (x.double() ** 2).sum(0).float()
+        mn, mx = x.min(0).values, x.max(0).values
+    else:
+        x = x.contiguous()
+        s = torch.zeros(c, dtype=torch.float32, device=x.device)
+        q = torch.zeros_like(s)
+        mn = torch.full_like(s, float("inf"))
+        mx = torch.full_like(s, float("-inf"))
+        _native.hip().column_stats(src=x.data_ptr(), n=n, cols=c, sum=s.data_ptr(), sumsq=q.data_ptr(),
+                                   min=mn.data_ptr(), max=mx.data_ptr(), stream=_stream_handle(stream))
+    mean = s / n
+    var = (q / n - mean * mean).clamp_min(0)
+    return {"sum": s, "sumsq": q, "min": mn, "max": mx, "mean": mean, "std": var.sqrt()}

@@ -1,0 +1,134 @@
+"""Topology / process-environment bootstrap (reference ddl/ddl_env.py:12-97).
+
+The reference derives its layout from ``mpirun`` ranks: contiguous blocks of
+``size/n_instances`` ranks per GPU, four communicator splits, and an
+``Abort(1)`` when the sizes do not divide (reference ddl/ddl_env.py:12-97).
+
+Here one process per MI355X is the DP rank (torchrun / srun task); its
+producers are child processes, so there is nothing to split. The rank math
+comes from the environment (torchrun ``RANK/WORLD_SIZE/LOCAL_RANK/
+LOCAL_WORLD_SIZE``, falling back to SLURM ``SLURM_PROCID/SLURM_NTASKS/
+SLURM_LOCALID``), the DP group is a torch.distributed group -- RCCL (backend
+"nccl") on GPUs, gloo on CPU -- plus a gloo *control* group for host-side
+metadata, and the node-locality check of the reference's
+``Split_type(COMM_TYPE_SHARED)`` becomes a hostname all-gather.
+"""
+
+from __future__ import annotations
+
+import os
+import socket
+from datetime import timedelta
+
+from ..exceptions import TopologyError
+from ..types import DDLEnv
+from ..utils.logging import logger
+
+DEFAULT_PRODUCERS = 3  # the reference's CI layout: mpirun -np 4 = 1 consumer + 3 producers
+
+
+def _int_env(*names: str, default: int | None = None) -> int | None:
+    for n in names:
+        v = os.environ.get(n)
+        if v not in (None, ""):
+            try:
+                return int(v.split("(")[0].split(",")[0])
+            except ValueError:
+                raise TopologyError(v, f"environment variable {n}={v!r} is not an integer") from None
+    return default
+
+
+def read_env(n_producers: int | None = None) -> DDLEnv:
+    """Compute the rank layout from the environment (no GPU, no communication)."""
+    rank = _int_env("RANK", "SLURM_PROCID", default=0)
+    world = _int_env("WORLD_SIZE", "SLURM_NTASKS", default=1)
+    local_rank = _int_env("LOCAL_RANK", "SLURM_LOCALID", default=0)
+    local_world = _int_env("LOCAL_WORLD_SIZE", "SLURM_NTASKS_PER_NODE", default=None)
+    if local_world is None:
+        local_world = world if _int_env("SLURM_NNODES", default=1) == 1 else 1
+    assert rank is not None and world is not None and local_rank is not None
+    if world < 1 or not 0 <= rank < world:
+        raise TopologyError((rank, world), f"invalid rank {rank} for world size {world}")
+    if not 0 <= local_rank < max(local_world, 1):
+        raise TopologyError((local_rank, local_world), f"invalid local rank {local_rank} of {local_world}")
+    if world % max(local_world, 1) != 0:
+        raise TopologyError((world, local_world),
+                            f"world size {world} is not a multiple of the ranks per node {local_world}")
+    if n_producers is None:
+        n_producers = _int_env("DDL_PRODUCERS_PER_RANK", default=DEFAULT_PRODUCERS)
+    assert n_producers is not None
+    if n_producers < 0:
+        raise TopologyError(n_producers, "number of producers must be >= 0")
+    return DDLEnv(
+        rank=rank,
+        world_size=world,
+        local_rank=local_rank,
+        local_world_size=local_world,
+        node_rank=rank // max(local_world, 1),
+        n_producers=n_producers,
+        hostname=socket.gethostname(),
+    )
+
+
+def init_distributed(env: DDLEnv, backend: str | None = None, timeout_s: float = 600.0) -> DDLEnv:
+    """Create the DP (RCCL or gloo) group and a gloo control group; set the device.
+
+    Touches the GPU: call it only after producer workers have been spawned.
+    """
+    import torch
+    import torch.distributed as dist
+
+    use_gpu = torch.cuda.is_available()
+    if use_gpu:
+        n_dev = torch.cuda.device_count()
+        dev_index = env.local_rank % max(n_dev, 1)
+        torch.cuda.set_device(dev_index)
+        env.device = f"cuda:{dev_index}"
+    else:
+        env.device = "cpu"
+    if env.world_size == 1:
+        env.backend = None
+        return env
+    backend = backend or ("nccl" if use_gpu else "gloo")
+    env.backend = backend
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29500")
+    if not dist.is_initialized():
+        kwargs = dict(backend=backend, rank=env.rank, world_size=env.world_size, timeout=timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kwargs["device_id"] = torch.device(env.device)
+        dist.init_process_group(**kwargs)
+    env.process_group = dist.group.WORLD
+    env.control_group = dist.new_group(backend="gloo") if backend != "gloo" else dist.group.WORLD
+    check_node_locality(env)
+    return env
+
+
+def check_node_locality(env: DDLEnv) -> None:
+    """Hostname all-gather: ranks sharing a host must be exactly its local ranks.
+
+    The reference raises ``DoesNotMatchError`` when a GPU group spans nodes
+    (reference ddl/ddl_env.py:72-73).
+    """
+    import torch.distributed as dist
+
+    if env.world_size == 1 or env.control_group is None:
+        return
+    infos: list = [None] * env.world_size
+    dist.all_gather_object(infos, (env.hostname, env.local_rank, env.local_world_size), group=env.control_group)
+    mine = [i for i in infos if i[0] == env.hostname]
+    local_ranks = sorted(i[1] for i in mine)
+    if local_ranks != list(range(len(mine))) or len(mine) != env.local_world_size:
+        raise TopologyError(infos, f"ranks on host {env.hostname} have local ranks {local_ranks}, "
+                                   f"expected 0..{env.local_world_size - 1}")
+    logger.debug("node locality ok: %s", infos)
+
+
+def destroy_distributed() -> None:
+    import torch.distributed as dist
+
+    if dist.is_initialized():
+        try:
+            dist.destroy_process_group()
+        except Exception:  # pragma: no cover - best effort at teardown
+            pass

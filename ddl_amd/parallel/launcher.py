@@ -1,0 +1,97 @@
+"""Launcher / role dispatcher: ``@distributed_dataloader`` (reference ddl/ddl_env.py:100-128).
+
+Reference: every MPI rank enters the decorator; local rank 0 of each GPU
+group runs the user function, the other local ranks become ``DataPusher``s,
+and kwargs given to the user function are dropped (reference
+ddl/ddl_env.py:115-116).
+
+Here one process per GPU (torchrun / srun task) enters the decorator; it
+spawns its ``P`` producer workers as child processes (``spawn`` start method,
+*before* anything touches the GPU), then creates the DP process groups (RCCL
+on GPUs), then calls ``func(*args, env, conn, **kwargs)`` (kwargs forwarded).
+On exit the producers are shut down and joined, and all ranks meet at a final
+barrier (reference ddl/ddl_env.py:126).
+"""
+
+from __future__ import annotations
+
+import contextlib
+import functools
+import multiprocessing as mp
+import os
+from typing import Any, Callable, Iterator
+
+from ..connection import DEFAULT_TIMEOUT_S, Connection
+from ..types import DDLEnv
+from ..utils.logging import configure, logger
+from .env import destroy_distributed, init_distributed, read_env
+
+
+def spawn_producers(env: DDLEnv, timeout_s: float = DEFAULT_TIMEOUT_S, env_overrides: dict | None = None) -> Connection:
+    """Start ``env.n_producers`` producer worker processes; return the consumer Connection."""
+    from ..datapusher import producer_main
+
+    ctx = mp.get_context("spawn")
+    pipes, procs = [], []
+    for i in range(env.n_producers):
+        parent, child = ctx.Pipe(duplex=True)
+        proc = ctx.Process(target=producer_main, name=f"ddl-producer-{env.rank}.{i}",
+                           args=(child, i, os.getpid(), env.rank, env.world_size, timeout_s, env_overrides),
+                           daemon=True)
+        proc.start()
+        child.close()
+        pipes.append(parent)
+        procs.append(proc)
+    logger.debug("spawned %d producers: %s", len(procs), [p.pid for p in procs])
+    return Connection(pipes, procs, timeout_s=timeout_s, rank=env.rank)
+
+
+@contextlib.contextmanager
+def start(n_producers: int | None = None, init_dist: bool = True, backend: str | None = None,
+          timeout_s: float = DEFAULT_TIMEOUT_S, env_overrides: dict | None = None) -> Iterator[tuple[DDLEnv, Connection | None]]:
+    """Context-manager form of the launcher: ``with start() as (env, conn): ...``."""
+    configure()
+    env = read_env(n_producers)
+    conn = spawn_producers(env, timeout_s, env_overrides) if env.n_producers > 0 else None
+    created_pg = False
+    try:
+        if init_dist:
+            import torch.distributed as dist
+
+            was = dist.is_available() and dist.is_initialized()
+            init_distributed(env, backend)
+            created_pg = not was and env.world_size > 1
+        yield env, conn
+    finally:
+        if conn is not None:
+            conn.finalize()
+        if created_pg:
+            import torch.distributed as dist
+
+            try:
+                dist.barrier(group=env.control_group)
+            except Exception as e:  # pragma: no cover
+                logger.warning("final barrier failed: %s", e)
+            destroy_distributed()
+
+
+def distributed_dataloader(func: Callable | None = None, *, n_producers: int | None = None, init_dist: bool = True,
+                           backend: str | None = None, timeout_s: float = DEFAULT_TIMEOUT_S):
+    """Decorator: run ``func(*args, env, conn, **kwargs)`` as this rank's consumer with its producers.
+
+    Usable bare (``@distributed_dataloader``) or with options
+    (``@distributed_dataloader(n_producers=4)``). The number of producers per
+    rank defaults to ``$DDL_PRODUCERS_PER_RANK`` or 3.
+    """
+
+    def deco(f: Callable) -> Callable:
+        @functools.wraps(f)
+        def wrapper(*args: Any, **kwargs: Any) -> Any:
+            with start(n_producers, init_dist, backend, timeout_s) as (env, conn):
+                return f(*args, env, conn, **kwargs)
+
+        return wrapper
+
+    if func is not None:
+        return deco(func)
+    return deco

@@ -1,0 +1,187 @@
+"""Cross-GPU global shuffle (reference ddl/shuffle.py).
+
+Reference: the k-th producers of all GPUs swap ``fraction x nData`` rows per
+window iteration with ``Sendrecv_replace`` -- first half to ``send_to``,
+second half to ``recv_from``, partners from a seeded derangement without
+2-cycles (reference ddl/shuffle.py:32-108). It never runs: the callback
+dispatcher only calls ``callbacks[0]`` (reference ddl/utils.py:22).
+
+Here the exchange really runs, on the consumer side, on the window *after* it
+has been staged into HBM, on the prefetch stream, over RCCL/xGMI:
+
+1. a per-window exchange permutation ``Px = Feistel(n, seed', window)`` picks
+   the ``n_ex`` rows to trade (``Px(0..n_ex-1)``: a uniformly random subset,
+   identical formula on every rank, nothing communicated);
+2. the ``gather_rows`` HIP kernel packs them contiguously (Px evaluated
+   inline, no index table);
+3. ``all_to_all_single`` on a dedicated loader process group (RCCL): an
+   8-GPU MI355X node is fully connected by xGMI, and an all-to-all drives all 7
+   links of every GPU at once, where the reference's 2-partner exchange
+   drives 2 (SURVEY §5 "MI355X-native communication design");
+   ``exchange_method="sendrecv_replace"`` keeps the reference's 2-partner
+   pattern (grouped ``isend``/``irecv``);
+4. ``scatter_rows`` puts the received rows back at the same positions.
+
+Deterministic: partners and rows depend only on (seed, window index).
+"""
+
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..ops import _dtypes
+from ..permutation import FeistelPermutation
+from ..types import DDLEnv
+from ..utils.logging import logger
+
+_EXCHANGE_SALT = 0x5EED_C0DE
+
+
+def derangement_partners(n: int, rank: int, rng: np.random.Generator, max_tries: int = 1000) -> tuple[int, int]:
+    """(send_to, recv_from) of ``rank`` under a random permutation with no fixed
+    points and no 2-cycles (reference semantics, ddl/shuffle.py:32-79)."""
+    if n == 1:
+        return 0, 0
+    if n == 2:
+        return (1, 1) if rank == 0 else (0, 0)
+    idx = np.arange(n)
+    for _ in range(max_tries):
+        col = rng.permutation(n)
+        if np.any(col == idx):
+            continue
+        if np.any(col[col] == idx):  # 2-cycle: send_to == recv_from for someone
+            continue
+        send_to = int(col[rank])
+        recv_from = int(np.nonzero(col == rank)[0][0])
+        return send_to, recv_from
+    raise RuntimeError(f"no valid communication pattern after {max_tries} tries")
+
+
+class GlobalShuffler:
+    """Base: owns the loader process group and the row-selection permutation."""
+
+    def __init__(self, env: DDLEnv, fraction: float, n_rows: int, sample_shape: tuple[int, ...], dtype: torch.dtype,
+                 seed: int, device: torch.device, group=None):
+        import torch.distributed as dist
+
+        self.env = env
+        self.world = env.world_size
+        self.rank = env.rank
+        self.fraction = fraction
+        self.n_rows = n_rows
+        self.sample_shape = tuple(sample_shape)
+        self.dtype = dtype
+        self.seed = seed
+        self.device = torch.device(device)
+        backend = "nccl" if self.device.type == "cuda" else "gloo"
+        # dedicated communicator: loader traffic never interleaves with the model's collectives
+        self.group = group if group is not None else dist.new_group(backend=backend)
+        if env.control_group is not None:
+            # every rank must trade the same number of rows: agree on the smallest window
+            t = torch.tensor([n_rows], dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=env.control_group)
+            n_rows = self.n_rows = int(t.item())
+        self.row_elems = int(math.prod(self.sample_shape)) if self.sample_shape else 1
+        self.n_exchange = self._n_exchange()
+        self.calls = 0
+        self.bytes_sent = 0
+
+    def _n_exchange(self) -> int:
+        return int(self.n_rows * self.fraction)
+
+    def rows_perm(self, window: int) -> FeistelPermutation:
+        return FeistelPermutation(self.n_rows, self.seed ^ _EXCHANGE_SALT, window)
+
+    def _rows(self, win_bytes: torch.Tensor) -> torch.Tensor:
+        return win_bytes.view(self.dtype).view((-1,) + self.sample_shape)[: self.n_rows]
+
+    def __call__(self, win_bytes: torch.Tensor, window: int, info: dict | None = None) -> None:
+        self.global_shuffle(win_bytes, window)
+
+    def global_shuffle(self, win_bytes: torch.Tensor, window: int) -> None:  # pragma: no cover - abstract
+        raise NotImplementedError
+
+
+class AllToAllGlobalShuffler(GlobalShuffler):
+    """Fraction-exchange as one all-to-all over every peer (all xGMI links)."""
+
+    def _n_exchange(self) -> int:
+        n = int(self.n_rows * self.fraction)
+        return n // self.world * self.world
+
+    def global_shuffle(self, win_bytes: torch.Tensor, window: int) -> None:
+        import torch.distributed as dist
+
+        n_ex = self.n_exchange
+        if n_ex == 0:
+            return
+        rows = self._rows(win_bytes)
+        px = self.rows_perm(window)
+        send = ops.gather_rows(rows, perm=px, base=0, n_rows=n_ex)
+        recv = torch.empty_like(send)
+        dist.all_to_all_single(recv.view(-1).view(torch.uint8), send.view(-1).view(torch.uint8), group=self.group)
+        idx = ops.feistel_indices(px, 0, n_ex, device=rows.device)
+        ops.scatter_rows(rows, recv, idx)
+        self.calls += 1
+        self.bytes_sent += send.numel() * send.element_size() * (self.world - 1) // self.world
+
+
+class SendRecvReplaceGlobalShuffler(GlobalShuffler):
+    """Reference pattern: half the rows to ``send_to``, half to ``recv_from`` (ddl/shuffle.py:82-108)."""
+
+    def _n_exchange(self) -> int:
+        return int(self.n_rows * self.fraction) // 2 * 2
+
+    def partners(self, window: int) -> tuple[int, int]:
+        rng = np.random.default_rng([self.seed & 0xFFFFFFFF, window])
+        return derangement_partners(self.world, self.rank, rng)
+
+    def global_shuffle(self, win_bytes: torch.Tensor, window: int) -> None:
+        import torch.distributed as dist
+
+        n_ex = self.n_exchange
+        if n_ex == 0:
+            return
+        rows = self._rows(win_bytes)
+        px = self.rows_perm(window)
+        send = ops.gather_rows(rows, perm=px, base=0, n_rows=n_ex)
+        recv = torch.empty_like(send)
+        half = n_ex // 2
+        send_to, recv_from = self.partners(window)
+        sb = send.view(n_ex, -1)
+        rb = recv.view(n_ex, -1)
+        p2p = [
+            dist.P2POp(dist.isend, sb[:half].contiguous(), send_to, group=self.group),
+            dist.P2POp(dist.irecv, rb[:half], recv_from, group=self.group),
+            dist.P2POp(dist.isend, sb[half:].contiguous(), recv_from, group=self.group),
+            dist.P2POp(dist.irecv, rb[half:], send_to, group=self.group),
+        ]
+        for req in dist.batch_isend_irecv(p2p):
+            req.wait()
+        idx = ops.feistel_indices(px, 0, n_ex, device=rows.device)
+        ops.scatter_rows(rows, recv, idx)
+        self.calls += 1
+        self.bytes_sent += send.numel() * send.element_size()
+
+
+_METHODS = {
+    "alltoall": AllToAllGlobalShuffler,
+    "all_to_all": AllToAllGlobalShuffler,
+    "sendrecv_replace": SendRecvReplaceGlobalShuffler,
+}
+
+
+def make_exchange(env: DDLEnv, method: str, fraction: float, n_rows: int, sample_shape, dtype, seed: int, device,
+                  shuffle: str = "none") -> GlobalShuffler:
+    try:
+        cls = _METHODS[method]
+    except KeyError:
+        raise NotImplementedError(f"exchange method {method!r} is not implemented; one of {sorted(_METHODS)}") from None
+    dtype = _dtypes.to_torch_dtype(dtype)
+    sh = cls(env, fraction, n_rows, tuple(sample_shape), dtype, seed, device)
+    logger.debug("global shuffle: %s, %d rows/window", cls.__name__, sh.n_exchange)
+    return sh
