@@ -1,0 +1,200 @@
+#!/usr/bin/env python3
+"""Headline benchmark: samples/s fed to the GPU + GPU idle %, synthetic 3x224x224 bf16.
+
+Metric and config from BASELINE.json ("samples/sec fed to GPU + GPU idle%,
+synthetic 3x224x224 bf16 at 1/2/4/8 ranks"). One process per GPU (torchrun),
+each rank = one consumer with its own producer worker processes:
+
+  producers (host, pinned shm windows of synthetic bf16 images, refreshed every
+  round) --hipMemcpyAsync on the prefetch stream--> HBM window ring
+  --[global-shuffle all-to-all over RCCL when --exchange > 0]-->
+  per-batch fused gfx950 Feistel-permutation gather --> bf16 [B,3,224,224]
+  on the compute stream --> consumer step.
+
+Phase 1 (the reported ``value``): the consumer step is a checksum kernel that
+reads every delivered byte, so the number is the loader's feed rate. Every
+sample crosses PCIe in every step (each window is re-copied H2D each visit;
+no caching). W warmup steps, then EXACTLY K timed steps bracketed by
+barrier + synchronize; max time over ranks; value = total samples/s of the job.
+Phase 2 (``gpu_idle_pct``): a fixed-cost bf16 train step (PatchMLP fwd+bwd+SGD)
+consumes the batches; the compute stream's idle fraction is measured with HIP
+events (idle = 1 - busy/wall).
+
+vs_baseline = value / (28,500 samples/s x N): BASELINE.md's reference
+ceiling for this shape (P=3 host producers, f32, no H2D) scaled linearly.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REF_SAMPLES_PER_S_PER_GPU = 28_500.0
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--window", type=int, default=1024, help="samples per producer window")
+    ap.add_argument("--producers", type=int, default=3)
+    ap.add_argument("--slots", type=int, default=1, help="windows per producer")
+    ap.add_argument("--depth", type=int, default=2, help="HBM prefetch depth (windows)")
+    ap.add_argument("--source-dtype", default="bfloat16", choices=["bfloat16", "uint8", "float32"])
+    ap.add_argument("--shuffle", default="device", choices=["device", "none"])
+    ap.add_argument("--exchange", type=float, default=0.0, help="global-shuffle fraction per window (N>1)")
+    ap.add_argument("--exchange-method", default="alltoall")
+    ap.add_argument("--idle-steps", type=int, default=-1, help="phase-2 steps (default: = --steps; 0 disables)")
+    ap.add_argument("--model-dim", type=int, default=384)
+    ap.add_argument("--model-depth", type=int, default=4)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args(argv)
+
+
+def main(argv=None) -> int:
+    args = parse(argv)
+    import torch
+    import torch.distributed as dist
+
+    import ddl_amd
+    from ddl_amd import Marker, ops
+    from ddl_amd.models.producers import ImageWindowProducer
+    from ddl_amd.utils.tracing import ComputeIdleMeter
+
+    n_world = int(os.environ.get("WORLD_SIZE", "1"))
+    if n_world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={n_world}", file=sys.stderr)
+    idle_steps = args.steps if args.idle_steps < 0 else args.idle_steps
+    total_steps = args.warmup + args.steps + (args.warmup // 2 + idle_steps if idle_steps else 0)
+    bpw = args.window // args.batch
+    if bpw < 1:
+        raise SystemExit("--window must hold at least one --batch")
+    n_epochs = math.ceil(total_steps / bpw) + 1
+    shape = (3, 224, 224)
+
+    with ddl_amd.start(n_producers=args.producers) as (env, conn):
+        dev = torch.device(env.device)
+        producer = ImageWindowProducer(args.window, shape, args.source_dtype, seed=args.seed, refill="stamp")
+        norm = None
+        if args.source_dtype == "uint8":
+            norm = {"mean": [0.485, 0.456, 0.406], "std": [0.229, 0.224, 0.225], "layout": "chw"}
+        dl = ddl_amd.DistributedDataLoader(
+            producer, args.batch, conn, n_epochs, args.exchange, args.exchange_method, env.rank, env.world_size,
+            env=env, device=dev, out_dtype=torch.bfloat16, shuffle=args.shuffle, seed=args.seed,
+            n_slots=args.slots, prefetch_depth=args.depth, normalize=norm)
+        acc = torch.zeros(1, dtype=torch.int64, device=dev)
+
+        def batches():
+            while True:
+                for i in range(len(dl)):
+                    yield dl[i]
+                    dl.mark(Marker.END_OF_BATCH)
+                dl.mark(Marker.END_OF_EPOCH)
+
+        it = batches()
+
+        def barrier():
+            if env.world_size > 1:
+                dist.barrier(group=env.control_group)
+            torch.cuda.synchronize(dev)
+
+        # ---------------- phase 1: feed rate
+        for _ in range(args.warmup):
+            (x,) = next(it)
+            ops.checksum(x, out=acc)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            (x,) = next(it)
+            ops.checksum(x, out=acc)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        barrier()
+        elapsed = t1 - t0
+        if env.world_size > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=env.control_group)
+            elapsed = float(t.item())
+        samples = args.batch * args.steps * env.world_size
+        value = samples / elapsed
+        stats = dl.stats()
+
+        # ---------------- phase 2: GPU idle % behind a fixed-cost train step
+        idle = {}
+        if idle_steps:
+            from ddl_amd.models.trainstep import TrainStep
+
+            step = TrainStep(dev, dim=args.model_dim, depth=args.model_depth)
+            for _ in range(args.warmup // 2):
+                (x,) = next(it)
+                step(x)
+            meter = ComputeIdleMeter()
+            barrier()
+            t2 = time.perf_counter()
+            for _ in range(idle_steps):
+                (x,) = next(it)
+                meter.step_begin()
+                step(x)
+                meter.step_end()
+            torch.cuda.synchronize(dev)
+            t3 = time.perf_counter()
+            idle = meter.result()
+            idle["train_samples_per_s"] = args.batch * idle_steps * env.world_size / (t3 - t2)
+            if env.world_size > 1:
+                t = torch.tensor([idle["gpu_idle_pct"]], dtype=torch.float64)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=env.control_group)
+                idle["gpu_idle_pct"] = float(t.item())
+        dl.close()
+
+        if env.rank == 0:
+            out = {
+                "metric": "samples/sec fed to GPU (synthetic 3x224x224 bf16)",
+                "value": round(value, 1),
+                "unit": "samples/s",
+                "n_gpus": env.world_size,
+                "steps": args.steps,
+                "warmup": args.warmup,
+                "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
+                "higher_is_better": True,
+                "scaling": "weak",
+                "vs_baseline": round(value / (REF_SAMPLES_PER_S_PER_GPU * env.world_size), 3),
+                "dtype": "bf16",
+                "data": f"synthetic (random {args.source_dtype} images, refreshed every producer round)",
+                "config": {
+                    "model": "ddl_amd loader: ImageNet-shape 3x224x224 bf16, pinned H2D prefetch stream",
+                    "global_batch": args.batch * env.world_size,
+                    "seq_len": None,
+                    "parallelism": f"dp{env.world_size}",
+                    "producers_per_gpu": args.producers,
+                    "window_samples": args.window,
+                    "prefetch_depth": args.depth,
+                    "shuffle": args.shuffle,
+                    "exchange_fraction": args.exchange,
+                    "source_dtype": args.source_dtype,
+                },
+                "gpu_idle_pct": None if not idle else round(idle["gpu_idle_pct"], 3),
+                "train_step": None if not idle else {
+                    "model": f"PatchMLP dim={args.model_dim} depth={args.model_depth} fwd+bwd+SGD bf16",
+                    "samples_per_s": round(idle["train_samples_per_s"], 1),
+                    "busy_ms": round(idle["busy_ms"], 3), "wall_ms": round(idle["wall_ms"], 3)},
+                "loader": {"consumer_wait_s": round(stats["consumer_wait_s"], 4),
+                           "stager_wait_producer_s": round(stats.get("stager_wait_producer_s", 0.0), 4),
+                           "windows_staged": stats.get("windows_staged")},
+            }
+            line = json.dumps(out)
+            print(line, flush=True)
+            if args.json_out:
+                with open(args.json_out, "w") as f:
+                    f.write(line + "\n")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,54 @@
+"""Fixed-cost synthetic train steps used to measure GPU idle % behind the loader.
+
+``PatchMLP`` is a ViT-shaped GEMM model (patch embedding + pre-norm MLP
+blocks + mean pool + classifier) so its cost is hipBLASLt GEMMs -- no MIOpen
+convolution tuning on first use -- and scales with ``dim``/``depth``. A step
+is forward + backward + SGD update in bf16 on the compute stream.
+"""
+
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class PatchMLP(nn.Module):
+    def __init__(self, in_ch: int = 3, image: int = 224, patch: int = 16, dim: int = 384, depth: int = 4,
+                 mlp_ratio: int = 4, n_classes: int = 1000):
+        super().__init__()
+        self.patch = patch
+        self.embed = nn.Linear(in_ch * patch * patch, dim)
+        self.blocks = nn.ModuleList(
+            nn.Sequential(nn.LayerNorm(dim), nn.Linear(dim, dim * mlp_ratio), nn.GELU(), nn.Linear(dim * mlp_ratio, dim))
+            for _ in range(depth))
+        self.norm = nn.LayerNorm(dim)
+        self.head = nn.Linear(dim, n_classes)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        b, c, h, w = x.shape
+        p = self.patch
+        x = x.reshape(b, c, h // p, p, w // p, p).permute(0, 2, 4, 1, 3, 5).reshape(b, (h // p) * (w // p), c * p * p)
+        x = self.embed(x)
+        for blk in self.blocks:
+            x = x + blk(x)
+        return self.head(self.norm(x).mean(dim=1))
+
+
+class TrainStep:
+    """forward + backward + SGD on one [B, 3, H, W] batch (labels synthetic)."""
+
+    def __init__(self, device, dim: int = 384, depth: int = 4, lr: float = 1e-3, dtype=torch.bfloat16):
+        self.model = PatchMLP(dim=dim, depth=depth).to(device=device, dtype=dtype)
+        self.opt = torch.optim.SGD(self.model.parameters(), lr=lr)
+        self.device = device
+        self.dtype = dtype
+
+    def __call__(self, images: torch.Tensor) -> torch.Tensor:
+        x = images.to(self.dtype)
+        labels = torch.zeros(x.shape[0], dtype=torch.long, device=x.device)
+        loss = F.cross_entropy(self.model(x).float(), labels)
+        self.opt.zero_grad(set_to_none=True)
+        loss.backward()
+        self.opt.step()
+        return loss.detach()

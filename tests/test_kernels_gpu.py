@@ -1,0 +1,218 @@
+"""gfx950 kernels vs plain-PyTorch fp32 references (SURVEY §4.4 level 3)."""
+
+import numpy as np
+import pytest
+import torch
+
+from ddl_amd import ops
+from ddl_amd.permutation import FeistelPermutation
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _assert_bf16_close(a, b, max_ulp=1):
+    assert a.dtype == b.dtype == torch.bfloat16
+    ai = a.cpu().view(torch.int16).int()
+    bi = b.cpu().view(torch.int16).int()
+    diff = (ai - bi).abs().max().item() if a.numel() else 0
+    assert diff <= max_ulp, f"max ulp diff {diff}"
+
+
+def test_native_module_is_loaded():
+    from ddl_amd import _native
+
+    h = _native.hip()
+    assert h.device_count() >= 1
+    assert "gfx950" in h.arch_name(torch.cuda.current_device())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.uint8, torch.float16])
+@pytest.mark.parametrize("row_shape", [(9,), (3, 224, 224), (7,), (1024,)])
+@pytest.mark.parametrize("how", ["identity", "index", "perm"])
+def test_gather_rows_same_dtype_bitwise(dtype, row_shape, how):
+    n = 300
+    g = torch.Generator().manual_seed(1)
+    src = (torch.rand((n, *row_shape), generator=g) * 200).to(dtype)
+    d = src.to(_dev())
+    kw = {}
+    if how == "index":
+        idx = torch.randint(0, n, (77,), generator=g)
+        kw = dict(index=idx)
+        dk = dict(index=idx.to(_dev()))
+    elif how == "perm":
+        p = FeistelPermutation(n, seed=3, epoch=5)
+        kw = dict(perm=p, base=11, n_rows=64)
+        dk = kw
+    else:
+        kw = dict(base=5, n_rows=100)
+        dk = kw
+    ref = ops.ref_gather_rows(src, **kw)
+    out = ops.gather_rows(d, **dk)
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu(), ref)
+
+
+@pytest.mark.parametrize("src_dtype", [torch.float32, torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("row_shape", [(150528,), (9,), (40,)])
+def test_gather_cast_to_bf16_is_rne(src_dtype, row_shape):
+    n = 64
+    src = torch.randn((n, *row_shape)).to(src_dtype) * 3
+    p = FeistelPermutation(n, seed=9, epoch=1)
+    ref = ops.ref_gather_rows(src, perm=p, out_dtype=torch.bfloat16)
+    out = ops.gather_rows(src.to(_dev()), perm=p, out_dtype=torch.bfloat16)
+    assert torch.equal(out.cpu().view(torch.int16), ref.view(torch.int16))
+
+
+def test_gather_u8_normalise_chw():
+    n, c, h, w = 40, 3, 64, 64
+    src = torch.randint(0, 256, (n, c, h, w), dtype=torch.uint8)
+    mean, std = [0.485, 0.456, 0.406], [0.229, 0.224, 0.225]
+    sc = [1.0 / (255 * s) for s in std]
+    bi = [-m / s for m, s in zip(mean, std)]
+    p = FeistelPermutation(n, 1, 2)
+    ref = ops.ref_gather_rows(src, perm=p, out_dtype=torch.bfloat16, scale=sc, bias=bi, plane=h * w)
+    out = ops.gather_rows(src.to(_dev()), perm=p, out_dtype=torch.bfloat16, scale=sc, bias=bi, plane=h * w)
+    _assert_bf16_close(out, ref)
+    # and against the plain-PyTorch formula
+    direct = ((src.float() / 255 - torch.tensor(mean).view(1, 3, 1, 1)) / torch.tensor(std).view(1, 3, 1, 1))
+    direct = direct[torch.from_numpy(p.full())].to(torch.bfloat16)
+    _assert_bf16_close(out, direct, max_ulp=2)
+
+
+def test_scatter_rows():
+    n = 128
+    src_rows = torch.randn(32, 77)
+    dst = torch.zeros(n, 77)
+    idx = torch.randperm(n)[:32]
+    ref = dst.clone().index_copy_(0, idx, src_rows)
+    out = ops.scatter_rows(dst.to(_dev()), src_rows.to(_dev()), idx.to(_dev()))
+    assert torch.equal(out.cpu(), ref)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 1000, 65536 + 17, 1 << 20])
+def test_feistel_device_matches_host(n):
+    p = FeistelPermutation(n, seed=12345, epoch=7)
+    d = ops.feistel_indices(p, 0, n, device=_dev()).cpu().numpy()
+    h = p.full()
+    assert np.array_equal(d, h)
+    assert np.array_equal(np.sort(d), np.arange(n))
+
+
+@pytest.mark.parametrize("in_dtype", [torch.uint8, torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("hw", [(224, 224), (17, 13), (32, 32)])
+def test_collate_hwc_to_chw(in_dtype, hw):
+    n, c = 24, 3
+    src = (torch.rand((n, *hw, c)) * 255).to(in_dtype)
+    mean, std = [0.5, 0.4, 0.3], [0.2, 0.25, 0.3]
+    p = FeistelPermutation(n, 4, 4)
+    ref = ops.ref_collate_hwc_to_chw(src, perm=p, out_dtype=torch.bfloat16, mean=mean, std=std)
+    out = ops.collate_hwc_to_chw(src.to(_dev()), perm=p, out_dtype=torch.bfloat16, mean=mean, std=std)
+    assert out.shape == (n, c, *hw)
+    _assert_bf16_close(out, ref)
+    out32 = ops.collate_hwc_to_chw(src.to(_dev()), perm=p, out_dtype=torch.float32, mean=mean, std=std)
+    ref32 = ops.ref_collate_hwc_to_chw(src, perm=p, out_dtype=torch.float32, mean=mean, std=std)
+    torch.testing.assert_close(out32.cpu(), ref32, rtol=1e-6, atol=1e-5)
+
+
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+def test_split_columns(out_dtype):
+    src = torch.randn(4096 * 3, 9)
+    p = FeistelPermutation(src.shape[0], 0, 3)
+    ref = ops.ref_split_columns(src, (3, 5, 1), perm=p, base=4096, n_rows=4096, out_dtype=out_dtype)
+    out = ops.split_columns(src.to(_dev()), (3, 5, 1), perm=p, base=4096, n_rows=4096, out_dtype=out_dtype)
+    for a, b in zip(out, ref):
+        assert a.is_contiguous()
+        assert torch.equal(a.cpu(), b)
+
+
+@pytest.mark.parametrize("seq_len", [4096, 130])
+def test_pad_tokens(seq_len):
+    rng = np.random.default_rng(0)
+    lens = rng.integers(0, 2 * seq_len, size=33)
+    offs = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64))
+    toks = torch.from_numpy(rng.integers(0, 50000, size=int(offs[-1])).astype(np.int32))
+    ref = ops.ref_pad_tokens(toks, offs, seq_len, pad_id=7)
+    out = ops.pad_tokens(toks.to(_dev()), offs.to(_dev()), seq_len, pad_id=7)
+    for a, b in zip(out, ref):
+        assert torch.equal(a.cpu(), b)
+
+
+@pytest.mark.parametrize("seq_len", [4096, 100])
+def test_pack_tokens(seq_len):
+    rng = np.random.default_rng(1)
+    lens = rng.integers(1, int(1.5 * seq_len), size=40)
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    toks = torch.from_numpy(rng.integers(0, 50000, size=int(offs[-1])).astype(np.int32))
+    rs, re_, so = ops.pack_plan(offs, seq_len)
+    ref = ops.ref_pack_tokens(toks, rs, re_, so, seq_len, pad_id=0)
+    out = ops.pack_tokens(toks.to(_dev()), offs, seq_len, pad_id=0)
+    for a, b in zip(out[:4], ref):
+        assert torch.equal(a.cpu(), b)
+    # every token appears exactly once, in order
+    mask = ref[1].bool()
+    assert torch.equal(ref[0][mask], toks)
+
+
+@pytest.mark.parametrize("nbytes", [4, 1000, 4096 * 77 + 12, 256 * 3 * 224 * 224 * 2])
+def test_checksum(nbytes):
+    x = torch.randint(0, 256, (nbytes,), dtype=torch.uint8)
+    ref = ops.ref_checksum(x)
+    out = ops.checksum(x.to(_dev())).item() & ((1 << 64) - 1)
+    assert out == ref
+
+
+def test_column_stats():
+    x = torch.randn(100_003, 10) * torch.arange(1, 11)
+    s = ops.column_stats(x.to(_dev()))
+    torch.testing.assert_close(s["min"].cpu(), x.min(0).values)
+    torch.testing.assert_close(s["max"].cpu(), x.max(0).values)
+    torch.testing.assert_close(s["mean"].cpu(), x.double().mean(0).float(), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(s["std"].cpu(), x.double().std(0, unbiased=False).float(), rtol=1e-3, atol=1e-3)
+
+
+def test_zero_copy_gather_from_registered_host_memory():
+    from ddl_amd import _native
+
+    h = _native.hip()
+    n, row = 64, 3 * 32 * 32
+    host = torch.empty((n, row), dtype=torch.uint8)
+    host.copy_(torch.randint(0, 256, (n, row), dtype=torch.uint8))
+    h.host_register(host.data_ptr(), host.numel(), True)
+    try:
+        dptr = h.host_device_pointer(host.data_ptr())
+        src = ops.HostRows(host, dptr)
+        p = FeistelPermutation(n, 2, 2)
+        out = ops.gather_rows(src, perm=p, out_dtype=torch.bfloat16)
+        torch.cuda.synchronize()
+        ref = ops.ref_gather_rows(host, perm=p, out_dtype=torch.bfloat16)
+        assert torch.equal(out.cpu().view(torch.int16), ref.view(torch.int16))
+    finally:
+        h.host_unregister(host.data_ptr())
+
+
+def test_h2d_and_release_callback():
+    """memcpy_h2d from registered memory + hipLaunchHostFunc slot release."""
+    from ddl_amd import _native
+
+    rt, h = _native.runtime(), _native.hip()
+    a = rt.Arena.create("/ddl_amd.test.h2d", [1 << 20], 1)
+    a.unlink()
+    try:
+        h.host_register(a.base_address, a.total_bytes, True)
+        v = torch.frombuffer(a.slot_view(0, 0), dtype=torch.uint8)
+        v.copy_(torch.arange(v.numel(), dtype=torch.int64).remainder(251).to(torch.uint8))
+        a.set_state(0, 0, rt.HELD)
+        dst = torch.empty(1 << 20, dtype=torch.uint8, device=_dev())
+        s = torch.cuda.Stream()
+        h.memcpy_h2d(dst.data_ptr(), a.slot_address(0, 0), 1 << 20, s.cuda_stream)
+        h.enqueue_release(a.state_address(0, 0), rt.EMPTY, s.cuda_stream)
+        assert a.wait_state(0, 0, rt.EMPTY, 10_000) == rt.WaitResult.OK
+        s.synchronize()
+        assert torch.equal(dst.cpu(), v)
+        h.host_unregister(a.base_address)
+    finally:
+        del a
