@@ -260,11 +260,14 @@ PYBIND11_MODULE(_ddl_hip, m) {
       py::arg("stream"));
   m.def(
       "checksum_words",
-      [](uintptr_t ptr, int64_t bytes, uintptr_t out, uintptr_t stream) {
-        check_rc(ddl::checksum_words(as_ptr<const void>(ptr), bytes, as_ptr<uint64_t>(out), as_stream(stream)),
+      [](uintptr_t ptr, int64_t bytes, uintptr_t out, uintptr_t scratch, int64_t scratch_len, uintptr_t stream) {
+        check_rc(ddl::checksum_words(as_ptr<const void>(ptr), bytes, as_ptr<uint64_t>(out), as_ptr<uint64_t>(scratch),
+                                     scratch_len, as_stream(stream)),
                  "checksum_words");
       },
-      py::arg("ptr"), py::arg("bytes"), py::arg("out"), py::arg("stream"));
+      py::arg("ptr"), py::arg("bytes"), py::arg("out"), py::arg("scratch"), py::arg("scratch_len"),
+      py::arg("stream"));
+  m.attr("CHECKSUM_MAX_BLOCKS") = ddl::kChecksumMaxBlocks;
   m.def(
       "column_stats",
       [](uintptr_t src, int64_t n, int64_t cols, uintptr_t sum, uintptr_t sumsq, uintptr_t mn, uintptr_t mx,

@@ -63,9 +63,12 @@ struct TokenSpec {
 int pad_pack_tokens(const TokenSpec& spec, hipStream_t st);
 
 // misc.hip ------------------------------------------------------------------
-// Sum of the 32-bit words of [ptr, ptr+bytes) into *out (u64, accumulated --
-// zero it first). Debug batch checksums and the bench consumer step.
-int checksum_words(const void* ptr, int64_t bytes, uint64_t* out, hipStream_t st);
+// Sum of the 32-bit words of [ptr, ptr+bytes) added into *out (u64). Two
+// stages through `scratch` (>= kChecksumMaxBlocks u64). Debug batch checksums
+// and the bench consumer step.
+constexpr int64_t kChecksumMaxBlocks = 1024;
+int checksum_words(const void* ptr, int64_t bytes, uint64_t* out, uint64_t* scratch, int64_t scratch_len,
+                   hipStream_t st);
 // Per-column sum / sum of squares / min / max of an [n, cols] f32 matrix
 // (reference harness normalisation stats, tests/run_ddl.py:45-77).
 int column_stats(const float* src, int64_t n, int64_t cols, float* out_sum, float* out_sumsq, float* out_min,

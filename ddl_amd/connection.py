@@ -71,8 +71,8 @@ class _Pipe:
             if self.conn.poll(0.05):
                 try:
                     tag, payload = self.conn.recv()
-                except EOFError:
-                    raise PeerDeathError(f"{self.name}: connection closed while waiting for {expect!r}") from None
+                except (EOFError, OSError) as e:
+                    raise PeerDeathError(f"{self.name}: connection lost while waiting for {expect!r} ({e!r})") from None
                 if tag == "error":
                     raise PeerDeathError(f"{self.name} failed:\n{payload}")
                 if tag != expect:
@@ -82,8 +82,8 @@ class _Pipe:
                 # drain a final error message if the peer managed to send one
                 if self.conn.poll(0):
                     continue
-                raise PeerDeathError(f"{self.name} died (exit code {self.peer.exitcode}) while we waited for "
-                                     f"{expect!r}", pid=self.peer.pid)
+                raise PeerDeathError(f"{self.name} died (exit code {getattr(self.peer, 'exitcode', None)}) while we "
+                                     f"waited for {expect!r}", pid=getattr(self.peer, "pid", None))
             if time.monotonic() > deadline:
                 raise DDLTimeoutError(f"{self.name}: timed out after {timeout_s:.0f}s waiting for {expect!r}")
 
@@ -139,7 +139,8 @@ class Connection:
 
     @property
     def producer_pids(self) -> list[int]:
-        return [p.pid if p is not None else 0 for p in self.processes]
+        # producer threads (thread mode) share our pid: liveness = thread liveness via the pipe
+        return [getattr(p, "pid", 0) or 0 for p in self.processes]
 
     # ------------------------------------------------------------- windows
     def init_windows(self, shapes: list[tuple[int, ...]], dtypes: list[torch.dtype], n_slots: int = 1,
@@ -241,7 +242,7 @@ class Connection:
             except (BrokenPipeError, OSError):
                 pass
 
-    def finalize(self, join_timeout_s: float = 30.0) -> None:
+    def finalize(self, join_timeout_s: float = 10.0) -> None:
         if self._closed:
             return
         self._closed = True
@@ -250,7 +251,7 @@ class Connection:
             if proc is None:
                 continue
             proc.join(join_timeout_s)
-            if proc.is_alive():
+            if proc.is_alive() and hasattr(proc, "terminate"):
                 logger.warning("producer pid %s did not exit; terminating", proc.pid)
                 proc.terminate()
                 proc.join(5)

@@ -81,6 +81,7 @@ class DistributedDataLoader:
         timeout_s: float | None = None,
         host_threads: int = 4,
         debug_checksum: bool = False,
+        copy_batches: bool | None = None,
     ):
         if mode not in MODES:
             raise ValueError(f"unknown mode {mode!r}; one of {MODES}")
@@ -102,10 +103,15 @@ class DistributedDataLoader:
         self.contiguous = contiguous
         self.env = env
         self.auto_mark = auto_mark
+        # Zero-copy views alias the window and die when it is released (reference
+        # semantics, ddl/mpi_dataloader.py:193). With auto_mark the caller does not
+        # control the release, so batches are owned copies by default.
+        self.copy_batches = auto_mark if copy_batches is None else bool(copy_batches)
         self.debug_checksum = debug_checksum
         self.metrics = LoaderMetrics()
         self.timeout_s = timeout_s if timeout_s is not None else (connection.timeout_s if connection else 600.0)
         self.checksums: list[int] = []
+        self._pending = False
 
         # cursor
         self.epoch = 0
@@ -168,6 +174,15 @@ class DistributedDataLoader:
             if len(wpe) != 1 or 0 in wpe:
                 raise ShapeMismatchError(md, "indexed producers must announce one batches_per_epoch")
             self.windows_per_epoch = wpe.pop()
+            chk = getattr(self, "_resume_check", None)
+            if chk is not None:
+                ex = md[0].extra
+                for key in ("global_batch", "n_samples", "order_seed"):
+                    if chk.get(key) is not None and ex.get(key) is not None and chk[key] != ex[key]:
+                        raise ShapeMismatchError((key, chk[key], ex[key]),
+                                                 f"checkpoint {key}={chk[key]} does not match the producers' {ex[key]}")
+                if int(chk["batches_per_epoch"]) != self.windows_per_epoch:
+                    raise ShapeMismatchError(chk, "checkpoint batches_per_epoch does not match")
         elif self.mode == "split_along_epoch":
             self.windows_per_epoch = P
         else:
@@ -294,9 +309,9 @@ class DistributedDataLoader:
                 x = ops.collate_hwc_to_chw(win, perm=perm, base=local * B, n_rows=B, out_dtype=out_dtype,
                                            mean=norm.get("mean"), std=norm.get("std"))
                 return (x,)
-            if self.contiguous and len(splits) > 1 and len(self.sample_shape) == 1:
+            if (self.contiguous or self.copy_batches) and len(splits) > 1 and len(self.sample_shape) == 1:
                 return ops.split_columns(win, splits, perm=perm, base=local * B, n_rows=B, out_dtype=out_dtype)
-            if perm is None and out_dtype == wdt and norm is None:
+            if perm is None and out_dtype == wdt and norm is None and not self.copy_batches:
                 x = win[local * B:(local + 1) * B]  # zero-copy view (reference semantics)
             else:
                 kw = {}
@@ -314,9 +329,12 @@ class DistributedDataLoader:
 
     def __iter__(self) -> Iterator:
         n = self._len
-        for i in range(n):
+        start = self.epoch_batch if self.auto_mark else 0  # resumed mid-epoch: continue at the cursor
+        for i in range(start, n):
             item = self[i]
+            self._pending = self.auto_mark  # yielded, not yet marked: counts as consumed in state_dict
             yield item
+            self._pending = False
             if self.auto_mark:
                 self.mark(Marker.END_OF_BATCH)
         if self.auto_mark:
@@ -397,37 +415,72 @@ class DistributedDataLoader:
 
     # ------------------------------------------------------------ checkpoint
     def state_dict(self) -> dict:
-        return {
+        """Checkpointable cursor. A batch already handed out by the auto-marking
+        iterator counts as consumed (resume continues with the next one).
+
+        ``kind="indexed"`` (world-size-invariant order): ``(seed, epoch,
+        global_batch_cursor)`` + the order's geometry -- resumable at ANY world
+        size with the same global batch. ``kind="window"``: epoch / window /
+        batch cursor of the producer-window schedule (same layout required).
+        """
+        consumed = self.epoch_batch + (1 if self._pending else 0)
+        base = {
             "version": STATE_VERSION,
-            "kind": "window",
-            "mode": self.mode,
             "seed": self.seed,
             "epoch": self.epoch,
-            "window": self.window,
-            "window_in_epoch": self.window_in_epoch,
-            "batch": self.batch,
-            "epoch_batch": self.epoch_batch,
             "batch_size": self.batch_size,
-            "n_producers": self.connection.n_producers if self.connection else 0,
-            "n_slots": self.n_slots,
-            "shuffle": self.shuffle,
-            "fraction_exchange": self.fraction_exchange,
             "world_size": self.env.world_size if self.env else self.n_instances,
             "dtype": str(self.out_dtype or getattr(self, "window_dtype", torch.float32)).replace("torch.", ""),
+            "shuffle": self.shuffle,
+            "fraction_exchange": self.fraction_exchange,
         }
+        if self.mode == "indexed":
+            extra = self.metadata_from_producer[0].extra if self.metadata_from_producer else {}
+            base.update({
+                "kind": "indexed",
+                "global_batch_cursor": consumed,
+                "batches_per_epoch": self.windows_per_epoch,
+                "global_batch": extra.get("global_batch"),
+                "n_samples": extra.get("n_samples"),
+                "order_seed": extra.get("order_seed"),
+            })
+            return base
+        base.update({
+            "kind": "window",
+            "mode": self.mode,
+            "window": self.window,
+            "window_in_epoch": self.window_in_epoch,
+            "batch": self.batch + (1 if self._pending else 0),
+            "epoch_batch": consumed,
+            "n_producers": self.connection.n_producers if self.connection else 0,
+            "n_slots": self.n_slots,
+        })
+        return base
 
     def _apply_state(self, sd: dict) -> None:
         if sd.get("version") != STATE_VERSION:
             raise ValueError(f"unsupported loader state version {sd.get('version')}")
-        if sd.get("batch", 0) != 0:
-            logger.warning("resuming mid-window: the partially consumed window is skipped")
         self.epoch = int(sd["epoch"])
-        self.window = int(sd["window"]) + (1 if sd.get("batch", 0) else 0)
-        self.window_in_epoch = int(sd["window_in_epoch"]) + (1 if sd.get("batch", 0) else 0)
-        self.batch = 0
-        self.epoch_batch = int(sd.get("epoch_batch", 0))
         if sd.get("seed") is not None:
             self.seed = int(sd["seed"])
+        if sd.get("kind") == "indexed":
+            bpe = int(sd["batches_per_epoch"])
+            cur = int(sd["global_batch_cursor"])
+            if cur >= bpe:
+                self.epoch, cur = self.epoch + 1, 0
+            self.window = self.epoch * bpe + cur
+            self.window_in_epoch = cur
+            self.epoch_batch = cur
+            self.batch = 0
+            self._resume_check = sd
+            return
+        if sd.get("batch", 0):
+            logger.warning("resuming mid-window: the partially consumed window is skipped")
+        skip = 1 if sd.get("batch", 0) else 0
+        self.window = int(sd["window"]) + skip
+        self.window_in_epoch = int(sd["window_in_epoch"]) + skip
+        self.batch = 0
+        self.epoch_batch = int(sd.get("epoch_batch", 0))
 
     def load_state_dict(self, sd: dict) -> None:
         raise RuntimeError("pass the state as DistributedDataLoader(..., resume_state=sd): producers are started "

@@ -157,13 +157,14 @@ class DataPusher:
 
 
 def producer_main(pipe, producer_index: int, consumer_pid: int, rank: int, world_size: int,
-                  timeout_s: float, env_overrides: dict | None = None) -> None:
-    """Entry point of a spawned producer worker process."""
-    if env_overrides:
-        os.environ.update(env_overrides)
-    # Producers are host-only: make sure nothing in them can grab the GPU.
-    os.environ["HIP_VISIBLE_DEVICES"] = os.environ.get("DDL_PRODUCER_VISIBLE_DEVICES", "-1")
-    torch.set_num_threads(max(1, int(os.environ.get("DDL_PRODUCER_TORCH_THREADS", "1"))))
+                  timeout_s: float, env_overrides: dict | None = None, in_thread: bool = False) -> None:
+    """Entry point of a producer worker (spawned process, or thread of the consumer)."""
+    if not in_thread:
+        if env_overrides:
+            os.environ.update(env_overrides)
+        # Producers are host-only: make sure nothing in them can grab the GPU.
+        os.environ["HIP_VISIBLE_DEVICES"] = os.environ.get("DDL_PRODUCER_VISIBLE_DEVICES", "-1")
+        torch.set_num_threads(max(1, int(os.environ.get("DDL_PRODUCER_TORCH_THREADS", "1"))))
     set_role("producer", producer_index)
     from .utils.logging import configure
 
@@ -175,4 +176,5 @@ def producer_main(pipe, producer_index: int, consumer_pid: int, rank: int, world
     except BaseException as e:  # report, then exit non-zero
         logger.error("producer %d failed: %r", producer_index, e)
         conn.report_error(e)
-        raise SystemExit(1)
+        if not in_thread:
+            raise SystemExit(1)

@@ -104,7 +104,7 @@ class SharedArraySource:
     """A node-wide [N, *sample_shape] array in POSIX shm (created once, mapped by name)."""
 
     def __init__(self, name: str, n: int, sample_shape: tuple[int, ...], dtype, create: bool = False):
-        self.name = name
+        self.name = name.lstrip("/")
         self.n = int(n)
         self.sample_shape = tuple(sample_shape)
         self.dtype = _dtypes.to_torch_dtype(dtype)
@@ -112,7 +112,7 @@ class SharedArraySource:
         self._shm: shared_memory.SharedMemory | None = None
         self._owner = create
         if create:
-            self._shm = shared_memory.SharedMemory(name=name, create=True, size=max(1, self.n * self.row_bytes))
+            self._shm = shared_memory.SharedMemory(name=self.name, create=True, size=max(1, self.n * self.row_bytes))
 
     @classmethod
     def create(cls, name: str, data: torch.Tensor) -> "SharedArraySource":
@@ -128,14 +128,16 @@ class SharedArraySource:
 
     def _map(self) -> shared_memory.SharedMemory:
         if self._shm is None:
-            # track=False-equivalent: do not let the resource tracker unlink the owner's segment
-            self._shm = shared_memory.SharedMemory(name=self.name, create=False)
-            try:
-                from multiprocessing import resource_tracker
+            # attach without registering with the resource tracker (python < 3.13 has no
+            # track=False): only the creator owns -- and unlinks -- the segment
+            from multiprocessing import resource_tracker
 
-                resource_tracker.unregister(self._shm._name, "shared_memory")  # type: ignore[attr-defined]
-            except Exception:
-                pass
+            orig = resource_tracker.register
+            resource_tracker.register = lambda *a, **k: None
+            try:
+                self._shm = shared_memory.SharedMemory(name=self.name, create=False)
+            finally:
+                resource_tracker.register = orig
         return self._shm
 
     @property

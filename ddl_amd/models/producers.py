@@ -108,11 +108,12 @@ class ImageWindowProducer(ProducerFunctionSkeleton):
 class IndexedProducer(ProducerFunctionSkeleton):
     """Producer of the world-size-invariant global order (one window = one local batch)."""
 
-    def __init__(self, source, global_batch: int, seed: int = 0, drop_last: bool = True, host_threads: int = 4):
+    def __init__(self, source, global_batch: int, seed: int | None = None, drop_last: bool = True,
+                 host_threads: int = 4):
         super().__init__()
         self.source = source
         self.global_batch = int(global_batch)
-        self.seed = int(seed)
+        self.seed = seed  # None: use the loader's seed
         self.drop_last = drop_last
         self.host_threads = host_threads
         self.world_size = 1
@@ -121,12 +122,15 @@ class IndexedProducer(ProducerFunctionSkeleton):
     def on_init(self, *args, **kwargs):
         super().on_init(*args, **kwargs)
         self.world_size = int(kwargs.get("world_size", 1))
-        self.order = EpochOrder(self.source.n, self.global_batch, self.seed, self.drop_last)
+        if self.seed is None:
+            self.seed = int(kwargs.get("seed", 0))
+        self.order = EpochOrder(self.source.n, self.global_batch, int(self.seed), self.drop_last)
         lb = self.order.local_batch(self.world_size)
         nv = int(math.prod(self.source.sample_shape)) if self.source.sample_shape else 1
         return DataProducerOnInitReturn(lb, nv, (lb, *self.source.sample_shape), (nv,), self.source.dtype,
                                         extra={"batches_per_epoch": self.order.batches_per_epoch,
-                                               "global_batch": self.global_batch, "n_samples": self.source.n})
+                                               "global_batch": self.global_batch, "n_samples": self.source.n,
+                                               "order_seed": int(self.seed)})
 
     def post_init(self, *args, **kwargs):
         super().post_init(*args, **kwargs)

@@ -447,8 +447,10 @@ def checksum(x: torch.Tensor, out: torch.Tensor | None = None, stream=None) -> t
         return res
     if out is None:
         out = torch.zeros(1, dtype=torch.int64, device=x.device)
-    _native.hip().checksum_words(ptr=x.data_ptr(), bytes=nbytes - nbytes % 4, out=out.data_ptr(),
-                                 stream=_stream_handle(stream))
+    h = _native.hip()
+    scratch = torch.empty(h.CHECKSUM_MAX_BLOCKS, dtype=torch.int64, device=x.device)
+    h.checksum_words(ptr=x.data_ptr(), bytes=nbytes - nbytes % 4, out=out.data_ptr(), scratch=scratch.data_ptr(),
+                     scratch_len=scratch.numel(), stream=_stream_handle(stream))
     return out
 
 

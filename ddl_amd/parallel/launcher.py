@@ -27,22 +27,40 @@ from ..utils.logging import configure, logger
 from .env import destroy_distributed, init_distributed, read_env
 
 
-def spawn_producers(env: DDLEnv, timeout_s: float = DEFAULT_TIMEOUT_S, env_overrides: dict | None = None) -> Connection:
-    """Start ``env.n_producers`` producer worker processes; return the consumer Connection."""
+def spawn_producers(env: DDLEnv, timeout_s: float = DEFAULT_TIMEOUT_S, env_overrides: dict | None = None,
+                    mode: str | None = None) -> Connection:
+    """Start ``env.n_producers`` producer workers; return the consumer Connection.
+
+    ``mode`` (default ``$DDL_PRODUCER_MODE`` or ``"process"``): ``"process"``
+    spawns one host process per producer (the production layout: user hooks
+    run truly in parallel, a crash is contained); ``"thread"`` runs them as
+    threads of the consumer (debugging, and profiling under ``rocprofv3``,
+    whose preloaded library may initialise the GPU before ``main`` -- a
+    process spawned after that would be forked from a GPU-initialised parent).
+    """
+    import threading
+
     from ..datapusher import producer_main
 
+    mode = mode or os.environ.get("DDL_PRODUCER_MODE", "process")
+    if mode not in ("process", "thread"):
+        raise ValueError(f"producer mode must be 'process' or 'thread', got {mode!r}")
     ctx = mp.get_context("spawn")
     pipes, procs = [], []
     for i in range(env.n_producers):
         parent, child = ctx.Pipe(duplex=True)
-        proc = ctx.Process(target=producer_main, name=f"ddl-producer-{env.rank}.{i}",
-                           args=(child, i, os.getpid(), env.rank, env.world_size, timeout_s, env_overrides),
-                           daemon=True)
-        proc.start()
-        child.close()
+        args = (child, i, os.getpid(), env.rank, env.world_size, timeout_s, env_overrides)
+        if mode == "process":
+            proc = ctx.Process(target=producer_main, name=f"ddl-producer-{env.rank}.{i}", args=args, daemon=True)
+            proc.start()
+            child.close()
+        else:
+            proc = threading.Thread(target=producer_main, name=f"ddl-producer-{env.rank}.{i}", args=args,
+                                    kwargs={"in_thread": True}, daemon=True)
+            proc.start()
         pipes.append(parent)
         procs.append(proc)
-    logger.debug("spawned %d producers: %s", len(procs), [p.pid for p in procs])
+    logger.debug("spawned %d producers: %s", len(procs), [getattr(p, "pid", None) for p in procs])
     return Connection(pipes, procs, timeout_s=timeout_s, rank=env.rank)
 
 
@@ -52,6 +70,9 @@ def start(n_producers: int | None = None, init_dist: bool = True, backend: str |
     """Context-manager form of the launcher: ``with start() as (env, conn): ...``."""
     configure()
     env = read_env(n_producers)
+    from ..utils.numa import bind_to_gpu_numa
+
+    bind_to_gpu_numa(env.local_rank)  # before spawning: producers inherit the affinity
     conn = spawn_producers(env, timeout_s, env_overrides) if env.n_producers > 0 else None
     created_pg = False
     try:

@@ -65,7 +65,12 @@ class WindowStager:
         self.post_copy = post_copy
         self.timeout_s = timeout_s
         self.first = first_window
-        self.stream = torch.cuda.Stream(device=self.device)
+        # H2D copies run on the copy stream; post-copy device work (the RCCL
+        # exchange) on a second stream, so window w's exchange overlaps window
+        # w+1's DMA instead of idling the copy engine.
+        self.copy_stream = torch.cuda.Stream(device=self.device)
+        self.stream = torch.cuda.Stream(device=self.device) if post_copy is not None else self.copy_stream
+        self._copy_done = [torch.cuda.Event() for _ in range(depth)]
         self.buffers = [torch.empty(max_window_bytes, dtype=torch.uint8, device=self.device) for _ in range(depth)]
         self.ready_events = [torch.cuda.Event() for _ in range(depth)]
         self.free_events: list[torch.cuda.Event | None] = [None] * depth
@@ -85,7 +90,7 @@ class WindowStager:
     def _run(self) -> None:
         try:
             torch.cuda.set_device(self.device)
-            handle = self.stream.cuda_stream
+            handle = self.copy_stream.cuda_stream
             for w in range(self.first, self.first + self.total):
                 b = (w - self.first) % self.depth
                 with self._cv:
@@ -95,7 +100,7 @@ class WindowStager:
                         return
                     free_ev = self.free_events[b]
                 if free_ev is not None:
-                    self.stream.wait_event(free_ev)
+                    self.copy_stream.wait_event(free_ev)
                 p, s = self.schedule(w)
                 t0 = time.perf_counter()
                 with trace_range("ddl.stage.wait_producer"):
@@ -110,6 +115,8 @@ class WindowStager:
                 self.conn.release_on_stream(p, s, handle)
                 view = buf[:nbytes]
                 if self.post_copy is not None:
+                    self._copy_done[b].record(self.copy_stream)
+                    self.stream.wait_event(self._copy_done[b])
                     with torch.cuda.stream(self.stream), trace_range("ddl.stage.post_copy"):
                         self.post_copy(view, w, info)
                 self.ready_events[b].record(self.stream)
@@ -162,6 +169,7 @@ class WindowStager:
         self._thread.join(timeout=30)
         if self._thread.is_alive():  # pragma: no cover
             logger.warning("staging thread did not exit")
+        self.copy_stream.synchronize()
         self.stream.synchronize()
 
     def stats(self) -> dict:

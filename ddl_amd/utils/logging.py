@@ -11,26 +11,26 @@ from __future__ import annotations
 import functools
 import logging
 import os
+import threading
 from typing import Any, Callable, TypeVar
 
 F = TypeVar("F", bound=Callable[..., Any])
 
 logger = logging.getLogger("ddl_amd")
 
-_ROLE = {"role": "consumer", "index": 0}
+_ROLE = threading.local()
 
 
 def set_role(role: str, index: int = 0) -> None:
-    """Record the calling process's role for log prefixes."""
-    _ROLE["role"] = role
-    _ROLE["index"] = index
+    """Record the calling thread's role (consumer / producer k) for log prefixes."""
+    _ROLE.role = role
+    _ROLE.index = index
 
 
 def rank_prefix() -> str:
     rank = int(os.environ.get("RANK", os.environ.get("SLURM_PROCID", "0")) or 0)
-    role = _ROLE["role"]
-    if role == "producer":
-        return f"[{rank:03d}.p{_ROLE['index']}]"
+    if getattr(_ROLE, "role", "consumer") == "producer":
+        return f"[{rank:03d}.p{_ROLE.index}]"
     return f"[{rank:03d}]"
 
 

@@ -1,0 +1,50 @@
+"""Run a function on W torch.distributed ranks (gloo, 127.0.0.1) as separate processes.
+
+Each rank process is non-daemonic so it can spawn its own producer workers
+(the production layout). Results come back through a Queue; a rank that
+raises reports its traceback and the harness re-raises it in the test.
+"""
+
+import multiprocessing as mp
+import os
+import socket
+import traceback
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_main(fn, rank, world, port, q, args, env):
+    os.environ.update(env)
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    try:
+        q.put((rank, "ok", fn(rank, world, *args)))
+    except BaseException:
+        q.put((rank, "err", traceback.format_exc()))
+
+
+def run_ranks(fn, world: int, *args, timeout: float = 180.0, env: dict | None = None):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_rank_main, args=(fn, r, world, port, q, args, env or {})) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in range(world):
+            rank, status, payload = q.get(timeout=timeout)
+            if status == "err":
+                raise AssertionError(f"rank {rank} failed:\n{payload}")
+            results[rank] = payload
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+                p.join()
+    return [results[r] for r in range(world)]

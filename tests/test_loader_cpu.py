@@ -1,0 +1,202 @@
+"""Consumer/producer engine on CPU with real producer processes (SURVEY §4.4 level 2).
+
+Replaces the reference's only test (``mpirun -np 4 python3 run_ddl.py``,
+reference tests/test_ddl.py:8-28, which checks no data) with assertions on
+shapes, window round-robin, exactly-once delivery, determinism, resume and
+failure handling.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+import ddl_amd
+from ddl_amd import Marker
+from ddl_amd.exceptions import DDLTimeoutError, PeerDeathError, ShapeMismatchError
+from ddl_amd.models import PointwiseProducer
+from tests.helpers import FailingProducer, IdProducer
+
+
+def _epochs(dl, n_epochs, collect=True):
+    out = []
+    for _ in range(n_epochs):
+        rows = []
+        for i, batch in enumerate(dl):
+            if collect:
+                rows.append(torch.cat([b.reshape(b.shape[0], -1) for b in batch], 1).clone())
+            dl.mark(Marker.END_OF_BATCH)
+        dl.mark(Marker.END_OF_EPOCH)
+        out.append(torch.cat(rows) if rows else None)
+    return out
+
+
+def test_reference_harness_config_parity():
+    """BASELINE config 1 layout: 1 consumer + 3 producers, nData=10 timesteps, batch 4096, splits (3,5,1)."""
+    with ddl_amd.start(n_producers=3) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(PointwiseProducer(n_timesteps=10), 4096, conn, 3, 0.5,
+                                           "sendrecv_replace", 0, 1, env=env)
+        assert dl.device.type == "cpu"
+        assert len(dl) == 24  # 100,520 // 4096
+        windows = []
+        for epoch in range(3):
+            n = 0
+            for i, (pos, target, w) in enumerate(dl):
+                assert pos.shape == (4096, 3) and target.shape == (4096, 5) and w.shape == (4096, 1)
+                assert pos.dtype == torch.float32
+                n += 1
+                dl.mark(Marker.END_OF_BATCH)
+            windows.append(dl.target_rank)
+            assert n == 24
+            dl.mark(Marker.END_OF_EPOCH)
+        assert dl._finalized
+
+
+def test_round_robin_windows_and_exactly_once():
+    with ddl_amd.start(n_producers=3) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(IdProducer(48, 6), 8, conn, 7, env=env)
+        eps = _epochs(dl, 7)
+    for e, rows in enumerate(eps):
+        assert rows.shape == (48, 6)
+        assert rows[:, 1].unique().tolist() == [e % 3]          # window order 1,2,3,1,2,3,1 (reference §3.4)
+        assert rows[:, 3].unique().tolist() == [e // 3]         # producer round
+        assert rows[:, 2].tolist() == list(range(48))           # exactly once, window order
+        assert torch.equal(rows[:, 4], rows[:, 2] * 7 + 4)
+
+
+def test_zero_copy_views_alias_the_window():
+    with ddl_amd.start(n_producers=2) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(IdProducer(16, 4), 4, conn, 1, env=env)
+        a, b = dl[0]
+        _, win = dl.arys[0][0]
+        assert a.data_ptr() == win.data_ptr()  # reference semantics: views of the shared window
+        for i in range(len(dl)):
+            dl.mark(Marker.END_OF_BATCH)
+        dl.mark(Marker.END_OF_EPOCH)
+
+
+def test_split_along_epoch_mode():
+    with ddl_amd.start(n_producers=3) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(IdProducer(32, 4), 8, conn, 2, env=env, mode="split_along_epoch",
+                                           copy_batches=True)
+        assert len(dl) == 12
+        eps = _epochs(dl, 2)
+    for e, rows in enumerate(eps):
+        assert rows.shape == (96, 4)
+        assert rows[:, 1].tolist() == [0] * 32 + [1] * 32 + [2] * 32
+        assert rows[:, 3].unique().tolist() == [e]
+
+
+def test_auto_mark_dataloader_dropin_with_slots():
+    with ddl_amd.start(n_producers=2) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(IdProducer(20, 4), 5, conn, 4, env=env, auto_mark=True, n_slots=2)
+        seen = []
+        for epoch in range(4):
+            seen.append(torch.cat([torch.cat(b, 1) for b in dl]))
+    for e, rows in enumerate(seen):
+        assert rows[:, 2].tolist() == list(range(20))
+        assert rows[:, 1].unique().tolist() == [e % 2]
+
+
+def test_host_device_shuffle_uses_feistel_order():
+    from ddl_amd.permutation import FeistelPermutation
+
+    with ddl_amd.start(n_producers=2) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(IdProducer(40, 4), 8, conn, 2, env=env, shuffle="device", seed=3)
+        eps = _epochs(dl, 2)
+    for e, rows in enumerate(eps):
+        perm = FeistelPermutation(40, 3, (0 << 8) | e).full()
+        assert np.array_equal(rows[:, 2].numpy(), perm)
+
+
+def test_single_rank_without_producers_has_len_zero():
+    with ddl_amd.start(n_producers=0) as (env, conn):
+        assert conn is None
+        dl = ddl_amd.DistributedDataLoader(IdProducer(), 4, conn, 2)
+        assert len(dl) == 0
+        assert list(dl) == []
+
+
+def test_decorator_forwards_kwargs_and_runs_producers():
+    @ddl_amd.distributed_dataloader(n_producers=2)
+    def main(cfg, env, conn, *, extra=None):
+        dl = ddl_amd.DistributedDataLoader(IdProducer(16, 4), cfg, conn, 2, env=env)
+        n = sum(1 for _ in _epochs(dl, 2, collect=False))
+        return env.n_producers, extra, n
+
+    assert main(4, extra="kw") == (2, "kw", 2)  # reference drops kwargs (ddl/ddl_env.py:116)
+
+
+def test_thread_mode_producers(monkeypatch):
+    monkeypatch.setenv("DDL_PRODUCER_MODE", "thread")
+    with ddl_amd.start(n_producers=2) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(IdProducer(16, 4), 4, conn, 3, env=env, copy_batches=True)
+        eps = _epochs(dl, 3)
+    assert [r[:, 1].unique().item() for r in eps] == [0, 1, 0]
+
+
+def test_resume_from_state_dict():
+    with ddl_amd.start(n_producers=3) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(IdProducer(16, 4), 4, conn, 5, env=env, copy_batches=True)
+        first = _epochs(dl, 2)
+        sd = dl.state_dict()
+        dl.close()
+    assert sd["epoch"] == 2 and sd["window"] == 2 and sd["batch"] == 0
+    with ddl_amd.start(n_producers=3) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(IdProducer(16, 4), 4, conn, 5, env=env, copy_batches=True,
+                                           resume_state=sd)
+        rest = _epochs(dl, 3)
+    with ddl_amd.start(n_producers=3) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(IdProducer(16, 4), 4, conn, 5, env=env, copy_batches=True)
+        full = _epochs(dl, 5)
+    for a, b in zip(first + rest, full):
+        assert torch.equal(a, b)  # the resumed run continues bit-identically
+
+
+def test_producer_on_init_failure_is_reported():
+    with pytest.raises(PeerDeathError, match="boom in on_init"):
+        with ddl_amd.start(n_producers=2) as (env, conn):
+            ddl_amd.DistributedDataLoader(FailingProducer(), 4, conn, 1, env=env)
+
+
+def test_producer_crash_midrun_is_detected(monkeypatch):
+    monkeypatch.setenv("DDL_FAULT_PRODUCER", "1:1:exit")
+    with pytest.raises(PeerDeathError):
+        with ddl_amd.start(n_producers=2, timeout_s=60) as (env, conn):
+            dl = ddl_amd.DistributedDataLoader(IdProducer(8, 4), 4, conn, 10, env=env)
+            _epochs(dl, 10, collect=False)
+
+
+def test_producer_exception_midrun_is_reported(monkeypatch):
+    monkeypatch.setenv("DDL_FAULT_PRODUCER", "0:1:raise")
+    with pytest.raises(PeerDeathError):
+        with ddl_amd.start(n_producers=2, timeout_s=60) as (env, conn):
+            dl = ddl_amd.DistributedDataLoader(IdProducer(8, 4), 4, conn, 10, env=env)
+            _epochs(dl, 10, collect=False)
+
+
+def test_hung_producer_times_out(monkeypatch):
+    monkeypatch.setenv("DDL_FAULT_PRODUCER", "0:1:hang")
+    with pytest.raises(DDLTimeoutError):
+        with ddl_amd.start(n_producers=1, timeout_s=3) as (env, conn):
+            dl = ddl_amd.DistributedDataLoader(IdProducer(8, 4), 4, conn, 5, env=env)
+            _epochs(dl, 5, collect=False)
+
+
+def test_window_smaller_than_batch_rejected():
+    with pytest.raises(PeerDeathError, match="holds no batch"):
+        with ddl_amd.start(n_producers=1) as (env, conn):
+            ddl_amd.DistributedDataLoader(IdProducer(3, 4), 4, conn, 1, env=env)
+
+
+def test_mismatched_producers_rejected():
+    with pytest.raises(ShapeMismatchError):
+        with ddl_amd.start(n_producers=2, env_overrides=None) as (env, conn):
+            ddl_amd.DistributedDataLoader(_OddProducer(16, 4), 4, conn, 1, env=env)
+
+
+class _OddProducer(IdProducer):
+    def on_init(self, *a, **k):
+        r = super().on_init(*a, **k)
+        if self.producer_index == 1:
+            r.splits = (1, self.width - 1)
+        return r

@@ -1,0 +1,113 @@
+"""Multi-rank (DP) behaviour over gloo on CPU: world-size-invariant order, global
+shuffle exchange, resume at a different world size (SURVEY §4.4 level 2)."""
+
+import numpy as np
+import pytest
+import torch
+
+from tests.mp_harness import run_ranks
+
+
+def _indexed_rank(rank, world, n, gb, epochs, name, resume=None, stop_after=None):
+    import ddl_amd
+    from ddl_amd.models import IndexedProducer, SharedArraySource
+
+    src = SharedArraySource(name, n, (2,), "int64")
+    out = []
+    with ddl_amd.start(n_producers=2) as (env, conn):
+        assert env.world_size == world and env.rank == rank
+        dl = ddl_amd.DistributedDataLoader(IndexedProducer(src, gb, seed=7), gb // world, conn, epochs,
+                                           mode="indexed", env=env, auto_mark=True, resume_state=resume)
+        for e in range(dl.epoch, epochs):
+            rows = []
+            for i, (b,) in enumerate(dl):
+                rows.append(b[:, 0].clone())
+                if stop_after is not None and e == stop_after[0] and i + 1 == stop_after[1]:
+                    sd = dl.state_dict()
+                    dl.close()
+                    return out, sd
+            out.append(torch.cat(rows).numpy())
+    return out, None
+
+
+@pytest.fixture
+def shared_source():
+    from ddl_amd.models import SharedArraySource
+
+    n = 1000
+    data = torch.stack([torch.arange(n), torch.arange(n) * 10], 1)
+    src = SharedArraySource.create(f"ddl_amd_src_{np.random.randint(1 << 30)}", data)
+    yield src
+    src.close()
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_indexed_order_is_world_size_invariant(shared_source, world):
+    from ddl_amd.permutation import EpochOrder
+
+    n, gb, epochs = shared_source.n, 64, 2
+    res = run_ranks(_indexed_rank, world, n, gb, epochs, shared_source.name)
+    order = EpochOrder(n, gb, seed=7)
+    for e in range(epochs):
+        ref = order.perm(e).full()[: order.batches_per_epoch * gb].reshape(-1, gb)
+        per_rank = [r[0][e].reshape(-1, gb // world) for r in res]
+        merged = np.concatenate(per_rank, axis=1)  # global batch g = concat of rank slices
+        assert np.array_equal(merged, ref)
+
+
+def test_indexed_resume_at_different_world_size(shared_source):
+    n, gb = shared_source.n, 64
+    # run on 2 ranks, stop after epoch 0 batch 5 (global batch cursor = 5)
+    res = run_ranks(_indexed_rank, 2, n, gb, 2, shared_source.name, None, (0, 5))
+    sd = res[0][1]
+    assert sd["kind"] == "indexed" and sd["global_batch_cursor"] == 5
+    # resume on 1 rank
+    (out, _), = run_ranks(_indexed_rank, 1, n, gb, 2, shared_source.name, sd)
+    from ddl_amd.permutation import EpochOrder
+
+    order = EpochOrder(n, gb, seed=7)
+    ref0 = order.perm(0).full()[5 * gb: order.batches_per_epoch * gb]
+    assert np.array_equal(out[0], ref0)
+    ref1 = order.perm(1).full()[: order.batches_per_epoch * gb]
+    assert np.array_equal(out[1], ref1)
+
+
+def _exchange_rank(rank, world, method, fraction):
+    import ddl_amd
+    from ddl_amd import Marker
+    from tests.helpers import IdProducer
+
+    eps = []
+    with ddl_amd.start(n_producers=2) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(IdProducer(40, 6), 8, conn, 3, fraction, method, env=env,
+                                           copy_batches=True, seed=1)
+        assert dl._exchange_fn is not None
+        for e in range(3):
+            rows = []
+            for i, (a, b) in enumerate(dl):
+                rows.append(torch.cat([a, b], 1))
+                dl.mark(Marker.END_OF_BATCH)
+            dl.mark(Marker.END_OF_EPOCH)
+            eps.append(torch.cat(rows).numpy())
+        n_ex = dl._exchange_fn.n_exchange
+    return eps, n_ex
+
+
+@pytest.mark.parametrize("method,world", [("alltoall", 2), ("alltoall", 4), ("sendrecv_replace", 2),
+                                          ("sendrecv_replace", 3)])
+def test_global_shuffle_exchange_conserves_rows(method, world):
+    res = run_ranks(_exchange_rank, world, method, 0.5)
+    n_ex = res[0][1]
+    assert n_ex > 0
+    for e in range(3):
+        all_rows = np.concatenate([r[0][e] for r in res])
+        # every rank's window rows (rank, producer, i) are still delivered exactly once overall
+        keys = {tuple(x) for x in all_rows[:, :3].tolist()}
+        assert len(keys) == len(all_rows) == world * 40
+        for r in range(world):
+            mine = res[r][0][e]
+            foreign = (mine[:, 0] != r).sum()
+            if method == "alltoall":
+                assert foreign == n_ex - n_ex // world  # chunk for self stays
+            else:
+                assert foreign == n_ex

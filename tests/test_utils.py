@@ -1,0 +1,167 @@
+"""Cross-cutting layer: hook dispatch, lazy logging, typed errors, env parsing, NUMA."""
+
+import logging
+
+import pytest
+
+from ddl_amd.exceptions import DoesNotMatchError, TopologyError
+from ddl_amd.parallel.env import read_env
+from ddl_amd.parallel.shuffle import derangement_partners
+from ddl_amd.utils.callbacks import execute_callbacks
+from ddl_amd.utils.logging import for_all_methods, with_logging
+
+
+class _A:
+    def __init__(self, log):
+        self.log = log
+
+    def on_init(self, **kw):
+        self.log.append(("A", kw["x"]))
+        return "from-A"
+
+    def global_shuffle(self, **kw):
+        self.log.append("A-shuffle")
+
+
+class _B:
+    def __init__(self, log):
+        self.log = log
+
+    def on_init(self, **kw):
+        self.log.append(("B", kw["x"]))
+        return "from-B"
+
+    def global_shuffle(self, **kw):
+        self.log.append("B-shuffle")
+
+
+def test_every_callback_runs_in_order():
+    log = []
+    ret = execute_callbacks("on_init", [_A(log), _B(log)], x=1)
+    assert log == [("A", 1), ("B", 1)]  # reference runs only callbacks[0] (ddl/utils.py:22)
+    assert ret == "from-A"
+    execute_callbacks("global_shuffle", [_A(log), object(), _B(log)])
+    assert log[-2:] == ["A-shuffle", "B-shuffle"]
+    assert execute_callbacks("missing_hook", [_A(log)]) is None
+
+
+class _Loud:
+    def __init__(self):
+        self.n = 0
+
+    def __repr__(self):
+        self.n += 1
+        return "loud"
+
+
+def test_with_logging_is_lazy(caplog):
+    @with_logging
+    def f(a):
+        return 3
+
+    loud = _Loud()
+    logging.getLogger("ddl_amd").setLevel(logging.INFO)
+    assert f(loud) == 3
+    assert loud.n == 0  # reference builds repr() eagerly on every call (ddl/utils.py:28-30)
+    logging.getLogger("ddl_amd").setLevel(logging.DEBUG)
+    with caplog.at_level(logging.DEBUG, logger="ddl_amd"):
+        f(loud)
+    assert loud.n == 1 and "loud" in caplog.text
+    logging.getLogger("ddl_amd").setLevel(logging.WARNING)
+
+
+def test_with_logging_reraises(caplog):
+    @with_logging
+    def g():
+        raise KeyError("x")
+
+    with pytest.raises(KeyError):
+        g()
+    assert "exception raised" in caplog.text
+
+
+def test_for_all_methods_no_double_wrap():
+    calls = []
+
+    def deco(fn):
+        calls.append(fn.__name__)
+        return fn
+
+    @for_all_methods(deco, exclude="skip")
+    class C:
+        def a(self):
+            pass
+
+        def skip(self):
+            pass
+
+        @staticmethod
+        def s():
+            pass
+
+        @property
+        def p(self):
+            return 1
+
+    assert sorted(calls) == ["__init__"] or sorted(calls) == ["a"]
+
+
+def test_does_not_match_error_constructor():
+    e = DoesNotMatchError((1, 2), "mismatch")  # reference typo __init (ddl/exceptions.py:2)
+    assert e.value == (1, 2) and e.message == "mismatch" and str(e) == "mismatch"
+
+
+def test_read_env_torchrun(monkeypatch):
+    for k in ("SLURM_PROCID", "SLURM_NTASKS", "SLURM_LOCALID", "SLURM_NTASKS_PER_NODE", "SLURM_NNODES"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("RANK", "5")
+    monkeypatch.setenv("WORLD_SIZE", "8")
+    monkeypatch.setenv("LOCAL_RANK", "1")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
+    env = read_env(2)
+    assert (env.rank, env.world_size, env.local_rank, env.local_world_size, env.node_rank) == (5, 8, 1, 4, 1)
+    assert env.n_instances == 8 and env.n_producers == 2
+
+
+def test_read_env_slurm_fallback(monkeypatch):
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("SLURM_PROCID", "3")
+    monkeypatch.setenv("SLURM_NTASKS", "4")
+    monkeypatch.setenv("SLURM_LOCALID", "3")
+    monkeypatch.setenv("SLURM_NNODES", "1")
+    monkeypatch.setenv("DDL_PRODUCERS_PER_RANK", "5")
+    env = read_env()
+    assert (env.rank, env.world_size, env.local_rank, env.local_world_size, env.n_producers) == (3, 4, 3, 4, 5)
+
+
+@pytest.mark.parametrize("bad", [{"RANK": "4", "WORLD_SIZE": "4"}, {"RANK": "0", "WORLD_SIZE": "6", "LOCAL_WORLD_SIZE": "4"},
+                                 {"RANK": "x"}])
+def test_read_env_errors(monkeypatch, bad):
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in bad.items():
+        monkeypatch.setenv(k, v)
+    with pytest.raises(TopologyError):
+        read_env(1)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 8])
+def test_derangement_partners_consistent(n):
+    import numpy as np
+
+    pairs = [derangement_partners(n, r, np.random.default_rng([0, 4])) for r in range(n)]
+    send = [p[0] for p in pairs]
+    recv = [p[1] for p in pairs]
+    for r in range(n):
+        assert recv[send[r]] == r  # my receiver receives from me
+        if n > 2:
+            assert send[r] != r and send[r] != recv[r]  # no self, no 2-cycle
+
+
+def test_numa_helpers_do_not_fail():
+    from ddl_amd.utils import numa
+
+    numa.visible_gpu_render_minors()
+    assert numa.node_cpus(0) or True
+    assert numa.bind_to_gpu_numa(0) in (None, 0, 1, 2, 3, 4, 5, 6, 7)
