@@ -1,0 +1,110 @@
+#!/usr/bin/env python3
+"""BASELINE config 4: token sequences, seq_len=4096, ragged H2D + on-device pad/pack collate.
+
+Synthetic corpus (random token ids, lengths uniform in [min_len, 4096]) in node
+shm; producers gather sequences in the world-size-invariant global order into
+pinned windows (ragged: only real tokens cross PCIe); the consumer expands
+them with the gfx950 pad_pack_tokens kernel. Reports tokens/s fed to the GPU
+(real tokens, padding excluded) and batches/s. torchrun-compatible.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=64, help="sequences per rank per step")
+    ap.add_argument("--seq-len", type=int, default=4096)
+    ap.add_argument("--min-len", type=int, default=256)
+    ap.add_argument("--n-seqs", type=int, default=8192)
+    ap.add_argument("--producers", type=int, default=4)
+    ap.add_argument("--mode", default="pack", choices=["pad", "pack"])
+    a = ap.parse_args(argv)
+
+    import torch
+    import torch.distributed as dist
+
+    import ddl_amd
+    from ddl_amd import ops
+    from ddl_amd.models.tokens import SharedTokenSource, TokenBatchProducer
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    name = f"ddl_amd_benchtok_{os.environ.get('MASTER_PORT', '0')}"
+    src = None
+    if int(os.environ.get("LOCAL_RANK", "0")) == 0:
+        src = SharedTokenSource.synthetic(name, a.n_seqs, a.min_len, a.seq_len, seed=1)
+    gb = a.batch * world
+    try:
+        with ddl_amd.start(n_producers=a.producers) as (env, conn):
+            if env.world_size > 1:
+                dist.barrier(group=env.control_group)
+            if src is None:
+                from ddl_amd.models.datasets import SharedArraySource
+
+                t = SharedArraySource(name + "_tok", 0, (1,), "int32")
+                o = SharedArraySource(name + "_off", a.n_seqs + 1, (1,), "int64")
+                offs = o.tensor().view(-1).numpy()
+                t.n = int(offs[-1])
+                source = SharedTokenSource(t, o, int(np.diff(offs).max()))
+            else:
+                source = src
+            n_epochs = (a.warmup + a.steps) // (a.n_seqs // gb) + 2
+            dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(source, gb, a.seq_len, a.mode), a.batch, conn,
+                                               n_epochs, mode="indexed", env=env, collate="tokens", auto_mark=True)
+            dev = torch.device(env.device)
+            acc = torch.zeros(1, dtype=torch.int64, device=dev)
+
+            def gen():
+                while True:
+                    yield from dl
+
+            it = gen()
+            real = 0
+            for _ in range(a.warmup):
+                b = next(it)
+                ops.checksum(b["input_ids"], out=acc)
+            torch.cuda.synchronize()
+            if env.world_size > 1:
+                dist.barrier(group=env.control_group)
+            t0 = time.perf_counter()
+            rows = 0
+            for _ in range(a.steps):
+                b = next(it)
+                ops.checksum(b["input_ids"], out=acc)
+                rows += b["input_ids"].shape[0]
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            st = dl.stats()
+            if env.world_size > 1:
+                t = torch.tensor([dt], dtype=torch.float64)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=env.control_group)
+                dt = float(t.item())
+            toks = source.offsets.tensor().view(-1).numpy()
+            mean_len = float(np.diff(toks).mean())
+            real_tokens = a.steps * a.batch * mean_len * env.world_size
+            dl.close()
+            if env.rank == 0:
+                print(json.dumps({
+                    "metric": "tokens/s fed to GPU (seq_len 4096, on-device pad/pack)", "mode": a.mode,
+                    "value": round(real_tokens / dt, 1), "unit": "tokens/s (real, est. from mean length)",
+                    "sequences_per_s": round(a.steps * a.batch * env.world_size / dt, 1),
+                    "packed_rows_per_step": round(rows / a.steps, 2), "n_gpus": env.world_size,
+                    "steps": a.steps, "ms_per_step": round(1000 * dt / a.steps, 3), "batch_seqs": a.batch,
+                    "producers": a.producers, "mean_len": round(mean_len, 1),
+                    "consumer_wait_s": round(st["consumer_wait_s"], 3)}), flush=True)
+    finally:
+        if src is not None:
+            src.close()
+
+
+if __name__ == "__main__":
+    sys.exit(main())

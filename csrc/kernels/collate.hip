@@ -144,6 +144,25 @@ __global__ void __launch_bounds__(kThreads) split_columns_kernel(SplitSpec spec,
   }
 }
 
+// Same-dtype split: raw element copies (any 1/2/4/8-byte dtype, no rounding).
+template <typename T>
+__global__ void __launch_bounds__(kThreads) split_columns_raw_kernel(SplitSpec spec, const T* __restrict__ src,
+                                                                     int64_t n_rows, int64_t n_values, RowIndex ri) {
+  const int64_t total = n_rows * n_values;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  for (int64_t e = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; e < total; e += stride) {
+    const int64_t row = e / n_values;
+    int col = static_cast<int>(e - row * n_values);
+    const T v = src[source_row(ri, row) * n_values + col];
+    int g = 0;
+    while (g < spec.n_groups - 1 && col >= spec.width[g]) {
+      col -= spec.width[g];
+      ++g;
+    }
+    static_cast<T*>(spec.dst[g])[row * spec.width[g] + col] = v;
+  }
+}
+
 }  // namespace
 
 int collate_hwc_to_chw(void* dst, int32_t out_dt, const void* src, int32_t in_dt, int64_t batch, int64_t pixels,
@@ -166,6 +185,20 @@ int split_columns(const SplitSpec& spec, const void* src, int32_t in_dt, int64_t
   int64_t blocks = (total + kThreads - 1) / kThreads;
   if (blocks > 8192) blocks = 8192;
   const dim3 grid(static_cast<uint32_t>(blocks));
+  if (spec.out_dt == in_dt) {
+    switch (dtype_size(in_dt)) {
+      case 1: hipLaunchKernelGGL(split_columns_raw_kernel<uint8_t>, grid, dim3(kThreads), 0, st, spec,
+                                 static_cast<const uint8_t*>(src), n_rows, n_values, ri); break;
+      case 2: hipLaunchKernelGGL(split_columns_raw_kernel<uint16_t>, grid, dim3(kThreads), 0, st, spec,
+                                 static_cast<const uint16_t*>(src), n_rows, n_values, ri); break;
+      case 4: hipLaunchKernelGGL(split_columns_raw_kernel<uint32_t>, grid, dim3(kThreads), 0, st, spec,
+                                 static_cast<const uint32_t*>(src), n_rows, n_values, ri); break;
+      case 8: hipLaunchKernelGGL(split_columns_raw_kernel<uint64_t>, grid, dim3(kThreads), 0, st, spec,
+                                 static_cast<const uint64_t*>(src), n_rows, n_values, ri); break;
+      default: return -1;
+    }
+    return static_cast<int>(hipGetLastError());
+  }
 #define DDL_SPLIT(TIN)                                                                                             \
   do {                                                                                                             \
     if (spec.out_dt == kBF16)                                                                                      \

@@ -82,6 +82,8 @@ class DistributedDataLoader:
         host_threads: int = 4,
         debug_checksum: bool = False,
         copy_batches: bool | None = None,
+        collate: str | None = None,
+        pad_id: int = 0,
     ):
         if mode not in MODES:
             raise ValueError(f"unknown mode {mode!r}; one of {MODES}")
@@ -107,6 +109,10 @@ class DistributedDataLoader:
         # semantics, ddl/mpi_dataloader.py:193). With auto_mark the caller does not
         # control the release, so batches are owned copies by default.
         self.copy_batches = auto_mark if copy_batches is None else bool(copy_batches)
+        if collate not in (None, "tokens"):
+            raise ValueError("collate must be None or 'tokens'")
+        self.collate = collate
+        self.pad_id = pad_id
         self.debug_checksum = debug_checksum
         self.metrics = LoaderMetrics()
         self.timeout_s = timeout_s if timeout_s is not None else (connection.timeout_s if connection else 600.0)
@@ -231,8 +237,10 @@ class DistributedDataLoader:
     def _setup_exchange(self) -> None:
         self._exchange_fn = None
         world = self.env.world_size if self.env else 1
-        if self.fraction_exchange <= 0 or world <= 1 or self.env is None or self.env.process_group is None:
+        if self.fraction_exchange <= 0 or self.env is None or self.env.process_group is None:
             return
+        if world <= 1 and self.env.backend is None:
+            return  # single rank without a process group: nothing to exchange with
         from .parallel.shuffle import make_exchange
 
         n_min = min(x.nData for x in self.metadata_from_producer)
@@ -262,6 +270,7 @@ class DistributedDataLoader:
                 self._exchange_fn(t.view(-1).view(torch.uint8), self.window, info)
             self._host_window = self.window
             self._host_seq = int(info["seq"])
+            self._host_tags = tuple(info["tag"])
         return None
 
     def __getitem__(self, idx: int):
@@ -296,10 +305,17 @@ class DistributedDataLoader:
         wdt = self.window_dtype
         if sw is None:  # host path: zero-copy views of the shm window
             _, win = self.arys[p][s]
-            seq = self._host_seq
+            seq, tags = self._host_seq, self._host_tags
         else:
-            win = sw.data.view(wdt).view((n_data,) + self.sample_shape)
-            seq = sw.seq
+            win = sw.data.view(wdt).view((n_data,) + self.sample_shape) if self.collate is None else sw.data
+            seq, tags = sw.seq, sw.tags
+        if self.collate == "tokens":
+            from .models.tokens import TokenWindowLayout, collate_token_window
+
+            ex = self.metadata_from_producer[p].extra
+            with trace_range("ddl.consumer.tokens"):
+                return collate_token_window(win.reshape(-1), TokenWindowLayout(**ex["token_layout"]),
+                                            ex["token_mode"], tags, self.pad_id)
         perm = self._perm_for(p, seq)
         out_dtype = self.out_dtype or wdt
         splits = list(self.splits[p])

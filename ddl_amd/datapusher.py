@@ -26,6 +26,7 @@ import os
 import time
 from typing import Any
 
+import numpy as np
 import torch
 
 from .connection import ProducerConnection
@@ -129,7 +130,14 @@ class DataPusher:
         self._set_user_window(my_ary, my_tensor)
         kw = dict(my_ary=my_ary, my_tensor=my_tensor, round=rnd, slot=slot, producer_index=self.index)
         execute_callbacks("global_shuffle", self.callbacks, **kw)
-        execute_callbacks("execute_function", self.callbacks, **kw)
+        ret = execute_callbacks("execute_function", self.callbacks, **kw)
+        # optional publish metadata: a list of <=4 ints (slot tags) or
+        # {"tags": [...], "used_bytes": n} (ship only the first n bytes H2D)
+        if isinstance(ret, dict):
+            return list(ret.get("tags", [])), int(ret.get("used_bytes", self.window_bytes))
+        if isinstance(ret, (list, tuple)) and all(isinstance(x, (int, np.integer)) for x in ret):
+            return [int(x) for x in ret], self.window_bytes
+        return [], self.window_bytes
 
     def push_data(self) -> None:
         """Hot loop (reference ddl/datapusher.py:147-170)."""
@@ -144,9 +152,9 @@ class DataPusher:
                 break
             t1 = time.perf_counter_ns()
             faults.maybe_fail_producer(self.index, rnd)
-            self._fill_round(slot, rnd)
+            tags, used = self._fill_round(slot, rnd)
             t2 = time.perf_counter_ns()
-            if conn.Iend_access_epoch(slot, seq=rnd, used_bytes=self.window_bytes, epoch=rnd) is WorkerInfo.STOP:
+            if conn.Iend_access_epoch(slot, seq=rnd, used_bytes=used, epoch=rnd, tags=tags) is WorkerInfo.STOP:
                 break
             conn.arena.heartbeat(self.index, t2 - t1, t1 - t0)
             execute_callbacks("on_shuffle_end", self.callbacks, round=rnd, slot=slot)

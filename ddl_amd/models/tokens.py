@@ -1,0 +1,194 @@
+"""Token-sequence family (BASELINE config 4: seq_len = 4096, on-device pad/pack).
+
+The producer ships the batch RAGGED -- flat int32 tokens + int64 offsets (+ the
+pack plan) -- so PCIe carries only real tokens (a padded [B, 4096] batch of
+sequences averaging 2k tokens would double the bytes); the consumer expands it
+on the GPU with the ``pad_pack_tokens`` gfx950 kernel into
+``tokens [R, S]``, ``attention_mask [R, S]``, ``position_ids [R, S]`` (+
+``segment_ids`` / ``cu_seqlens`` in pack mode).
+
+Sequence order is the world-size-invariant ``EpochOrder`` over sequences, so
+token batches share the indexed-mode checkpoint format.
+"""
+
+from __future__ import annotations
+
+import dataclasses
+import math
+
+import numpy as np
+import torch
+
+from ..datapusher import DataProducerOnInitReturn
+from ..datasetwrapper import ProducerFunctionSkeleton
+from ..ops.kernels import pack_plan
+from ..permutation import EpochOrder
+from .datasets import SharedArraySource
+
+
+@dataclasses.dataclass(frozen=True)
+class TokenWindowLayout:
+    """Byte layout of one token window (all regions 8-byte aligned)."""
+
+    batch: int      # sequences per (local) batch
+    seq_len: int    # S
+    max_len: int    # longest sequence in the corpus
+
+    @property
+    def max_segments(self) -> int:
+        return self.batch * max(1, -(-self.max_len // self.seq_len))
+
+    def regions(self) -> dict[str, tuple[int, int]]:
+        """name -> (byte offset, element count)."""
+        out, off = {}, 0
+        for name, count, size in (("offsets", self.batch + 1, 8), ("row_start", self.max_segments, 8),
+                                  ("row_end", self.max_segments, 8), ("seg_offsets", self.max_segments + 1, 8),
+                                  ("tokens", self.batch * self.max_len, 4)):
+            out[name] = (off, count)
+            off += -(-count * size // 8) * 8
+        out["_total"] = (off, 0)
+        return out
+
+    @property
+    def nbytes(self) -> int:
+        return self.regions()["_total"][0]
+
+    @property
+    def row_bytes(self) -> int:
+        return -(-self.nbytes // self.batch // 16) * 16
+
+    def views(self, buf: torch.Tensor) -> dict[str, torch.Tensor]:
+        """Typed views of a uint8 window buffer (host or device)."""
+        v = {}
+        for name, (off, count) in self.regions().items():
+            if name == "_total":
+                continue
+            dt = torch.int32 if name == "tokens" else torch.int64
+            size = 4 if name == "tokens" else 8
+            v[name] = buf[off:off + count * size].view(dt)
+        return v
+
+
+class SharedTokenSource:
+    """A tokenised corpus in node-wide shm: flat int32 tokens + int64 sequence offsets."""
+
+    def __init__(self, tokens: SharedArraySource, offsets: SharedArraySource, max_len: int):
+        self.tokens, self.offsets, self.max_len = tokens, offsets, int(max_len)
+        self.n = offsets.n - 1
+
+    @classmethod
+    def create(cls, name: str, tokens: np.ndarray, offsets: np.ndarray) -> "SharedTokenSource":
+        t = SharedArraySource.create(name + "_tok", torch.from_numpy(np.ascontiguousarray(tokens, np.int32)).view(-1, 1))
+        o = SharedArraySource.create(name + "_off", torch.from_numpy(np.ascontiguousarray(offsets, np.int64)).view(-1, 1))
+        return cls(t, o, int(np.diff(offsets).max()) if len(offsets) > 1 else 0)
+
+    @classmethod
+    def synthetic(cls, name: str, n: int, min_len: int = 128, max_len: int = 4096, vocab: int = 50257,
+                  seed: int = 0) -> "SharedTokenSource":
+        rng = np.random.default_rng(seed)
+        lens = rng.integers(min_len, max_len + 1, size=n).astype(np.int64)
+        offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        toks = rng.integers(0, vocab, size=int(offs[-1]), dtype=np.int32)
+        return cls.create(name, toks, offs)
+
+    def close(self) -> None:
+        self.tokens.close()
+        self.offsets.close()
+
+
+class TokenBatchProducer(ProducerFunctionSkeleton):
+    """One window = this rank's slice of a global batch of sequences, shipped ragged."""
+
+    def __init__(self, source: SharedTokenSource, global_batch: int, seq_len: int = 4096, mode: str = "pad",
+                 seed: int | None = None):
+        super().__init__()
+        if mode not in ("pad", "pack"):
+            raise ValueError("mode must be 'pad' or 'pack'")
+        self.source, self.global_batch, self.seq_len, self.mode, self.seed = source, global_batch, seq_len, mode, seed
+        self.order = None
+        self.layout = None
+
+    def on_init(self, *args, **kwargs):
+        super().on_init(*args, **kwargs)
+        self.world_size = int(kwargs.get("world_size", 1))
+        if self.seed is None:
+            self.seed = int(kwargs.get("seed", 0))
+        self.order = EpochOrder(self.source.n, self.global_batch, int(self.seed))
+        lb = self.order.local_batch(self.world_size)
+        self.layout = TokenWindowLayout(lb, self.seq_len, self.source.max_len)
+        rb = self.layout.row_bytes
+        return DataProducerOnInitReturn(lb, rb, (lb, rb), (rb,), "uint8", extra={
+            "batches_per_epoch": self.order.batches_per_epoch, "global_batch": self.global_batch,
+            "n_samples": self.source.n, "order_seed": int(self.seed), "token_layout": dataclasses.asdict(self.layout),
+            "token_mode": self.mode})
+
+    def execute_function(self, *args, **kwargs):
+        rnd = int(kwargs.get("round", 0))
+        g_total = rnd * (self.n_producers or 1) + (self.producer_index or 0)
+        epoch, g = divmod(g_total, self.order.batches_per_epoch)
+        idx = self.order.indices(epoch, g, self.rank_global or 0, self.world_size)
+        buf: torch.Tensor = kwargs["my_tensor"].view(-1)
+        v = self.layout.views(buf)
+        toks = self.source.tokens.tensor().view(-1)
+        offs = self.source.offsets.tensor().view(-1)
+        starts, ends = offs[idx], offs[idx + 1]
+        lens = ends - starts
+        o = v["offsets"]
+        o[0] = 0
+        torch.cumsum(lens, 0, out=o[1:])
+        dst = v["tokens"]
+        for i in range(len(idx)):  # one contiguous memcpy per sequence
+            dst[int(o[i]):int(o[i + 1])].copy_(toks[int(starts[i]):int(ends[i])])
+        n_tokens = int(o[-1])
+        n_rows = n_seg = 0
+        if self.mode == "pack":
+            rs, re_, so = pack_plan(o.numpy(), self.seq_len)
+            n_rows, n_seg = len(rs), len(so) - 1
+            v["row_start"][:n_rows] = torch.from_numpy(rs)
+            v["row_end"][:n_rows] = torch.from_numpy(re_)
+            v["seg_offsets"][: n_seg + 1] = torch.from_numpy(so)
+        tok_off = self.layout.regions()["tokens"][0]
+        return {"tags": [n_tokens, n_rows, n_seg], "used_bytes": tok_off + 4 * n_tokens}
+
+
+def collate_token_window(buf: torch.Tensor, layout: TokenWindowLayout, mode: str, tags, pad_id: int = 0):
+    """Expand one (device or host) token window into model inputs."""
+    from .. import ops
+
+    v = layout.views(buf.view(-1))
+    n_tokens, n_rows, n_seg = (int(x) for x in tags[:3])
+    tokens = v["tokens"][:n_tokens]
+    if mode == "pad":
+        ids, mask, pos = ops.pad_tokens(tokens, v["offsets"], layout.seq_len, pad_id)
+        return {"input_ids": ids, "attention_mask": mask, "position_ids": pos}
+    if not tokens.is_cuda:
+        ids, mask, pos, seg = ops.ref_pack_tokens(tokens, v["row_start"][:n_rows].numpy(),
+                                                  v["row_end"][:n_rows].numpy(), v["seg_offsets"][: n_seg + 1].numpy(),
+                                                  layout.seq_len, pad_id)
+        return {"input_ids": ids, "attention_mask": mask, "position_ids": pos, "segment_ids": seg,
+                "cu_seqlens": v["seg_offsets"][: n_seg + 1].clone()}
+    dev = tokens.device
+    s = layout.seq_len
+    ids = torch.empty((n_rows, s), dtype=torch.int32, device=dev)
+    mask = torch.empty((n_rows, s), dtype=torch.uint8, device=dev)
+    pos = torch.empty((n_rows, s), dtype=torch.int64, device=dev)
+    seg = torch.empty((n_rows, s), dtype=torch.int32, device=dev)
+    from .. import _native
+    from ..ops.kernels import _stream_handle
+
+    _native.hip().pad_pack_tokens(
+        tokens=tokens.data_ptr(), offsets=0, row_start=v["row_start"].data_ptr(), row_end=v["row_end"].data_ptr(),
+        seg_offsets=v["seg_offsets"].data_ptr(), n_seg=n_seg, out_tokens=ids.data_ptr(), attn_mask=mask.data_ptr(),
+        position_ids=pos.data_ptr(), pos_is_i64=True, segment_ids=seg.data_ptr(), rows=n_rows, seq_len=s,
+        pad_id=pad_id, mode=1, stream=_stream_handle(None))
+    return {"input_ids": ids, "attention_mask": mask, "position_ids": pos, "segment_ids": seg,
+            "cu_seqlens": v["seg_offsets"][: n_seg + 1]}
+
+
+def expected_tokens(source: SharedTokenSource, idx) -> list[np.ndarray]:
+    toks = source.tokens.tensor().view(-1).numpy()
+    offs = source.offsets.tensor().view(-1).numpy()
+    return [toks[offs[i]:offs[i + 1]] for i in idx]
+
+
+_ = math  # keep import (layout arithmetic helpers)

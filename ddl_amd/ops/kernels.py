@@ -279,6 +279,8 @@ def ref_split_columns(src, splits, index=None, perm=None, base=0, n_rows=None, o
     n_rows = _check_rows(x, index, perm, base, n_rows)
     rows = x.index_select(0, _ref_rows(x.shape[0], n_rows, index, perm, base).to(x.device))
     out_dtype = out_dtype or x.dtype
+    if out_dtype == x.dtype:
+        return tuple(p.contiguous() for p in torch.split(rows, list(splits), dim=1))
     return tuple(p.float().to(out_dtype).contiguous() for p in torch.split(rows, list(splits), dim=1))
 
 
@@ -293,8 +295,8 @@ def split_columns(src, splits: Sequence[int], index: torch.Tensor | None = None,
         raise ValueError("splits must sum to nValues")
     if not _is_gpu(src):
         return ref_split_columns(src, splits, index, perm, base, n_rows, out_dtype)
-    if out_dtype not in (torch.bfloat16, torch.float32):
-        raise TypeError("split_columns outputs bf16 or f32")
+    if out_dtype != src.dtype and out_dtype not in (torch.bfloat16, torch.float32):
+        raise TypeError("split_columns casts to bf16 or f32 only (same-dtype splits are raw copies)")
     n_rows = _check_rows(src, index, perm, base, n_rows)
     outs = tuple(torch.empty((n_rows, w), dtype=out_dtype, device=src.device) for w in splits)
     _native.hip().split_columns(

@@ -1,0 +1,296 @@
+"""HBM-resident sharded dataset with an exact, world-size-invariant global shuffle.
+
+BASELINE configs 3 and 5 ("datapusher scatter on RCCL over xGMI"; "global
+shuffle across 8 ranks (on-device permute kernel) + prefetch-depth sweep at
+288 GB HBM"). The reference can only trade a fraction of rows between the
+k-th producers of two GPUs per window (reference ddl/shuffle.py:82-108), and
+that code never runs. With 288 GB of HBM per MI355X a dataset
+shard usually fits on the GPU, so here:
+
+* the dataset (N samples) is sharded once across the W ranks -- rank r keeps
+  rows [r*S, (r+1)*S) resident in HBM (S = ceil(N/W)), loaded through pinned
+  bounce buffers on a copy stream;
+* every epoch visits ``perm_e`` (the counter-based Feistel permutation of
+  ``EpochOrder``): global batch g = perm_e(g*GB .. (g+1)*GB), rank r takes the
+  slice [r*LB, (r+1)*LB) -- identical union for any W, so any rank may need
+  any sample;
+* batch assembly per step, on a prep stream, ``depth`` steps ahead:
+  1. every rank knows the whole global batch (pure function of (seed, e, g)),
+     so it knows which of ITS resident rows each peer needs -- no metadata is
+     exchanged, only rows;
+  2. the gfx950 ``gather_rows`` kernel packs the rows to send, grouped by
+     destination;
+  3. one RCCL ``all_to_all_single`` with per-peer split sizes over xGMI (all
+     7 links of every GPU at once);
+  4. a second ``gather_rows`` puts the received rows into batch order fused
+     with the dtype cast and per-channel normalisation.
+  With W = 1 step 4 alone runs, straight out of the resident shard, with the
+  permutation evaluated inside the kernel.
+
+Checkpoint: the same ``kind="indexed"`` record as the loader
+(seed, epoch, global_batch_cursor) -- resumable at any world size.
+"""
+
+from __future__ import annotations
+
+import collections
+import math
+import time
+from typing import Any, Iterator
+
+import numpy as np
+import torch
+
+from . import _native, ops
+from .ops import _dtypes
+from .permutation import EpochOrder
+from .types import DDLEnv
+from .utils.logging import logger
+from .utils.tracing import trace_range
+
+STATE_VERSION = 1
+
+
+def _source_address(source) -> tuple[int, int]:
+    """(host address, rows) of a source: SharedArraySource / NpyMemmapSource / CPU tensor."""
+    if isinstance(source, torch.Tensor):
+        if source.is_cuda or not source.is_contiguous():
+            raise ValueError("tensor sources must be contiguous CPU tensors")
+        return source.data_ptr(), source.shape[0]
+    if hasattr(source, "address"):
+        return int(source.address), int(source.n)
+    if hasattr(source, "_a"):
+        a = source._a()
+        return int(a.ctypes.data), int(source.n)
+    raise TypeError(f"unsupported source {type(source).__name__}")
+
+
+def _source_geometry(source) -> tuple[tuple[int, ...], torch.dtype]:
+    if isinstance(source, torch.Tensor):
+        return tuple(source.shape[1:]), source.dtype
+    return tuple(source.sample_shape), _dtypes.to_torch_dtype(source.dtype)
+
+
+class ResidentGlobalLoader:
+    def __init__(self, source, global_batch: int, env: DDLEnv | None = None, *, seed: int = 0,
+                 drop_last: bool = True, out_dtype: Any = None, normalize: dict | None = None, depth: int = 2,
+                 device: str | torch.device | None = None, n_epochs: int | None = None,
+                 resume_state: dict | None = None, chunk_bytes: int = 256 << 20, host_threads: int = 8):
+        import torch.distributed as dist
+
+        self.env = env or DDLEnv()
+        self.W, self.rank = self.env.world_size, self.env.rank
+        self.sample_shape, self.src_dtype = _source_geometry(source)
+        self.row_elems = int(math.prod(self.sample_shape)) if self.sample_shape else 1
+        self.row_bytes = self.row_elems * _dtypes.itemsize(self.src_dtype)
+        src_addr, n = _source_address(source)
+        self.N = n
+        self.order = EpochOrder(n, global_batch, seed, drop_last)
+        self.GB = int(global_batch)
+        self.LB = self.order.local_batch(self.W)
+        self.seed = int(seed)
+        self.S = -(-n // self.W)
+        self.lo = self.rank * self.S
+        self.hi = min(n, self.lo + self.S)
+        if device is None:
+            device = self.env.device if self.env.device != "cpu" or not torch.cuda.is_available() else "cuda"
+        self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.out_dtype = _dtypes.to_torch_dtype(out_dtype) if out_dtype is not None else self.src_dtype
+        self.normalize = normalize
+        self.depth = max(1, int(depth))
+        self.n_epochs = n_epochs
+        self.epoch, self.cursor = 0, 0
+        if resume_state is not None:
+            self._apply_state(resume_state)
+        self._pending = False
+        self.group = None
+        if self.W > 1:
+            backend = "nccl" if self.device.type == "cuda" else "gloo"
+            self.group = dist.new_group(backend=backend)
+        self.bytes_exchanged = 0
+        self.batches = 0
+        t0 = time.perf_counter()
+        self.shard = self._load_shard(src_addr, chunk_bytes, host_threads)
+        self.load_s = time.perf_counter() - t0
+        self.prep_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        self._queue: collections.deque = collections.deque()
+        self._next_t = None
+
+    # ----------------------------------------------------------------- load
+    def _load_shard(self, src_addr: int, chunk_bytes: int, host_threads: int) -> torch.Tensor:
+        rows = self.hi - self.lo
+        shard = torch.empty((rows,) + self.sample_shape, dtype=self.src_dtype, device=self.device)
+        if rows == 0:
+            return shard
+        base = src_addr + self.lo * self.row_bytes
+        total = rows * self.row_bytes
+        rt = _native.runtime()
+        dst_bytes = shard.view(-1).view(torch.uint8)
+        if self.device.type != "cuda":
+            rt.parallel_copy(dst_bytes.data_ptr(), base, total, host_threads)
+            return shard
+        # double-buffered pinned bounce buffers: host parallel memcpy || SDMA H2D
+        hip = _native.hip()
+        chunk = max(self.row_bytes, min(chunk_bytes, total))
+        bufs = [torch.empty(chunk, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+        evs = [torch.cuda.Event(), torch.cuda.Event()]
+        used = [False, False]
+        s = torch.cuda.Stream(self.device)
+        off, i = 0, 0
+        with trace_range("ddl.resident.load"):
+            while off < total:
+                n = min(chunk, total - off)
+                b = i % 2
+                if used[b]:
+                    evs[b].synchronize()
+                rt.parallel_copy(bufs[b].data_ptr(), base + off, n, host_threads)
+                hip.memcpy_h2d(dst_bytes.data_ptr() + off, bufs[b].data_ptr(), n, s.cuda_stream)
+                evs[b].record(s)
+                used[b] = True
+                off += n
+                i += 1
+            s.synchronize()
+        return shard
+
+    # ------------------------------------------------------------- assembly
+    def __len__(self) -> int:
+        """Batches left in the current epoch."""
+        return self.order.batches_per_epoch - self.cursor
+
+    @property
+    def batches_per_epoch(self) -> int:
+        return self.order.batches_per_epoch
+
+    def _norm_kw(self) -> dict:
+        norm = self.normalize
+        if norm is None:
+            return {}
+        c = self.sample_shape[0] if len(self.sample_shape) > 1 else len(norm.get("mean", [0]))
+        plane = int(math.prod(self.sample_shape[1:])) if len(self.sample_shape) > 1 else 1
+        sc, bi = ops.kernels._norm_affine(c, norm.get("mean"), norm.get("std"), norm.get("scale"), norm.get("bias"))
+        return dict(scale=sc, bias=bi, plane=plane)
+
+    def _to_dev(self, a: np.ndarray) -> torch.Tensor:
+        t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.int64))
+        if self.device.type == "cuda":
+            return t.pin_memory().to(self.device, non_blocking=True)
+        return t
+
+    def _assemble(self, t: int) -> tuple[torch.Tensor, Any]:
+        """Enqueue the assembly of global step t = epoch*bpe + g; returns (batch, ready event)."""
+        import torch.distributed as dist
+
+        e, g = divmod(t, self.order.batches_per_epoch)
+        perm = self.order.perm(e)
+        kw = self._norm_kw()
+        ctx = torch.cuda.stream(self.prep_stream) if self.prep_stream is not None else _nullctx()
+        with ctx, trace_range("ddl.resident.assemble"):
+            if self.W == 1:
+                batch = ops.gather_rows(self.shard, perm=perm, base=g * self.GB, n_rows=self.LB,
+                                        out_dtype=self.out_dtype, **kw)
+            else:
+                pos = np.arange(g * self.GB, (g + 1) * self.GB, dtype=np.int64)
+                idx_all = perm(pos)
+                owner = idx_all // self.S
+                send_mask = owner == self.rank
+                send_rows = idx_all[send_mask] - self.lo
+                dest = (np.nonzero(send_mask)[0] // self.LB)
+                send_counts = np.bincount(dest, minlength=self.W).tolist()
+                mine = owner[self.rank * self.LB:(self.rank + 1) * self.LB]
+                order_k = np.argsort(mine, kind="stable")
+                recv_counts = np.bincount(mine, minlength=self.W).tolist()
+                inv = np.empty(self.LB, dtype=np.int64)
+                inv[order_k] = np.arange(self.LB)
+                send = ops.gather_rows(self.shard, index=self._to_dev(send_rows)) if len(send_rows) else \
+                    torch.empty((0,) + self.sample_shape, dtype=self.src_dtype, device=self.device)
+                recv = torch.empty((self.LB,) + self.sample_shape, dtype=self.src_dtype, device=self.device)
+                dist.all_to_all_single(recv.view(self.LB, -1), send.view(send.shape[0], -1), recv_counts,
+                                       send_counts, group=self.group)
+                self.bytes_exchanged += (len(send_rows) - send_counts[self.rank]) * self.row_bytes
+                batch = ops.gather_rows(recv, index=self._to_dev(inv), out_dtype=self.out_dtype, **kw)
+            ev = None
+            if self.prep_stream is not None:
+                ev = torch.cuda.Event()
+                ev.record(self.prep_stream)
+        return batch, ev
+
+    def _total_steps(self) -> int | None:
+        return None if self.n_epochs is None else self.n_epochs * self.order.batches_per_epoch
+
+    def _fill(self, upto: int) -> None:
+        total = self._total_steps()
+        while self._next_t < upto and (total is None or self._next_t < total):
+            self._queue.append((self._next_t,) + self._assemble(self._next_t))
+            self._next_t += 1
+
+    def __iter__(self) -> Iterator[torch.Tensor]:
+        """One epoch of batches ([LB, *sample_shape] in ``out_dtype``)."""
+        bpe = self.order.batches_per_epoch
+        if self.n_epochs is not None and self.epoch >= self.n_epochs:
+            return
+        t0 = self.epoch * bpe + self.cursor
+        if self._next_t is None:
+            self._next_t = t0
+        for t in range(t0, (self.epoch + 1) * bpe):
+            self._fill(t + self.depth)
+            tq, batch, ev = self._queue.popleft()
+            assert tq == t, (tq, t)
+            if ev is not None:
+                cur = torch.cuda.current_stream(self.device)
+                cur.wait_event(ev)
+                batch.record_stream(cur)
+            self.cursor = t - self.epoch * bpe
+            self._pending = True
+            self.batches += 1
+            yield batch
+            self._pending = False
+            self.cursor += 1
+        self.epoch += 1
+        self.cursor = 0
+
+    # ----------------------------------------------------------- checkpoint
+    def state_dict(self) -> dict:
+        return {
+            "version": STATE_VERSION,
+            "kind": "indexed",
+            "seed": self.seed,
+            "order_seed": self.seed,
+            "epoch": self.epoch,
+            "global_batch_cursor": self.cursor + (1 if self._pending else 0),
+            "batches_per_epoch": self.order.batches_per_epoch,
+            "global_batch": self.GB,
+            "n_samples": self.N,
+            "world_size": self.W,
+            "dtype": str(self.out_dtype).replace("torch.", ""),
+        }
+
+    def _apply_state(self, sd: dict) -> None:
+        if sd.get("kind") != "indexed" or sd.get("version") != STATE_VERSION:
+            raise ValueError("not an indexed loader state")
+        for key, mine in (("global_batch", self.GB), ("n_samples", self.N), ("order_seed", self.seed)):
+            if sd.get(key) is not None and sd[key] != mine:
+                raise ValueError(f"checkpoint {key}={sd[key]} does not match {mine}")
+        self.epoch = int(sd["epoch"])
+        self.cursor = int(sd["global_batch_cursor"])
+        if self.cursor >= self.order.batches_per_epoch:
+            self.epoch, self.cursor = self.epoch + 1, 0
+
+    def stats(self) -> dict:
+        return {"batches": self.batches, "bytes_exchanged": self.bytes_exchanged, "shard_rows": self.hi - self.lo,
+                "shard_bytes": (self.hi - self.lo) * self.row_bytes, "load_s": self.load_s}
+
+    def close(self) -> None:
+        if self.prep_stream is not None:
+            self.prep_stream.synchronize()
+        self._queue.clear()
+        logger.debug("resident loader closed: %s", self.stats())
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

@@ -49,6 +49,7 @@ class StagedWindow:
     nbytes: int
     data: torch.Tensor  # uint8 view [nbytes] of the HBM buffer
     t_ready_host: float
+    tags: tuple = ()
 
 
 class WindowStager:
@@ -123,7 +124,8 @@ class WindowStager:
                 self.bytes_h2d += nbytes
                 self.windows_staged += 1
                 with self._cv:
-                    self._staged[w] = StagedWindow(w, b, p, s, int(info["seq"]), nbytes, view, time.perf_counter())
+                    self._staged[w] = StagedWindow(w, b, p, s, int(info["seq"]), nbytes, view, time.perf_counter(),
+                                                   tuple(info["tag"]))
                     self._cv.notify_all()
         except ShutdownError:
             pass

@@ -119,9 +119,11 @@ def test_collate_hwc_to_chw(in_dtype, hw):
     torch.testing.assert_close(out32.cpu(), ref32, rtol=1e-6, atol=1e-5)
 
 
-@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
-def test_split_columns(out_dtype):
-    src = torch.randn(4096 * 3, 9)
+@pytest.mark.parametrize("src_dtype,out_dtype", [(torch.float32, torch.float32), (torch.float32, torch.bfloat16),
+                                                 (torch.int32, torch.int32), (torch.int64, torch.int64),
+                                                 (torch.uint8, torch.uint8), (torch.bfloat16, torch.bfloat16)])
+def test_split_columns(src_dtype, out_dtype):
+    src = (torch.randn(4096 * 3, 9) * 100).to(src_dtype)
     p = FeistelPermutation(src.shape[0], 0, 3)
     ref = ops.ref_split_columns(src, (3, 5, 1), perm=p, base=4096, n_rows=4096, out_dtype=out_dtype)
     out = ops.split_columns(src.to(_dev()), (3, 5, 1), perm=p, base=4096, n_rows=4096, out_dtype=out_dtype)

@@ -62,3 +62,55 @@ def test_gpu_multi_slot_deep_prefetch():
     for e, rows in enumerate(seen):
         assert set(rows[:, 1].tolist()) == {e % 2}
         assert set(rows[:, 3].tolist()) == {e // 2}
+
+
+def test_gpu_indexed_mode_world_size_invariant_order():
+    import numpy as np
+
+    from ddl_amd.models import IndexedProducer, SharedArraySource
+    from ddl_amd.permutation import EpochOrder
+
+    n, gb = 2000, 128
+    data = torch.stack([torch.arange(n), torch.arange(n) * 3], 1)
+    src = SharedArraySource.create(f"ddl_amd_gsrc_{np.random.randint(1 << 30)}", data)
+    try:
+        with ddl_amd.start(n_producers=3) as (env, conn):
+            dl = ddl_amd.DistributedDataLoader(IndexedProducer(src, gb), gb, conn, 2, mode="indexed", env=env,
+                                               auto_mark=True, seed=9)
+            order = EpochOrder(n, gb, 9)
+            for e in range(2):
+                got = torch.cat([b[0][:, 0].cpu() for b in dl]).numpy()
+                assert np.array_equal(got, order.perm(e).full()[: order.batches_per_epoch * gb])
+    finally:
+        src.close()
+
+
+def test_gpu_uint8_normalised_and_hwc_collate():
+    from ddl_amd.models.producers import ImageWindowProducer
+
+    mean, std = [0.485, 0.456, 0.406], [0.229, 0.224, 0.225]
+    with ddl_amd.start(n_producers=2) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(ImageWindowProducer(32, (3, 24, 24), "uint8", refill="none"), 8, conn,
+                                           2, env=env, out_dtype=torch.bfloat16, shuffle="none",
+                                           normalize={"mean": mean, "std": std})
+        (x,) = dl[0]
+        _, win = dl.arys[0][0]
+        ref = ((win[:8].float() / 255 - torch.tensor(mean).view(1, 3, 1, 1)) / torch.tensor(std).view(1, 3, 1, 1))
+        torch.testing.assert_close(x.float().cpu(), ref, rtol=1e-2, atol=1e-2)
+        for i in range(len(dl)):
+            dl.mark(Marker.END_OF_BATCH)
+        dl.mark(Marker.END_OF_EPOCH)
+        for i in range(len(dl)):
+            dl.mark(Marker.END_OF_BATCH)
+        dl.mark(Marker.END_OF_EPOCH)
+    with ddl_amd.start(n_producers=1) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(ImageWindowProducer(16, (20, 20, 3), "uint8", refill="none"), 4, conn,
+                                           1, env=env, normalize={"mean": mean, "std": std, "layout": "hwc"})
+        (x,) = dl[1]
+        _, win = dl.arys[0][0]
+        ref = ((win[4:8].float() / 255 - torch.tensor(mean)) / torch.tensor(std)).permute(0, 3, 1, 2)
+        assert x.shape == (4, 3, 20, 20)
+        torch.testing.assert_close(x.float().cpu(), ref, rtol=1e-2, atol=1e-2)
+        for i in range(len(dl)):
+            dl.mark(Marker.END_OF_BATCH)
+        dl.mark(Marker.END_OF_EPOCH)

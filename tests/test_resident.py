@@ -1,0 +1,70 @@
+"""HBM-resident sharded loader with exact global shuffle (BASELINE configs 3/5), gloo on CPU."""
+
+import numpy as np
+import pytest
+import torch
+
+from tests.mp_harness import run_ranks
+
+
+def _resident_rank(rank, world, name, n, gb, epochs, depth, resume=None, stop=None):
+    import ddl_amd
+    from ddl_amd.models import SharedArraySource
+    from ddl_amd.resident import ResidentGlobalLoader
+
+    src = SharedArraySource(name, n, (3,), "int64")
+    with ddl_amd.start(n_producers=0) as (env, _):
+        dl = ResidentGlobalLoader(src, gb, env, seed=11, depth=depth, n_epochs=epochs, resume_state=resume)
+        assert dl.shard.shape[0] == dl.hi - dl.lo
+        out = []
+        while dl.epoch < epochs:
+            e = dl.epoch
+            rows = []
+            for i, b in enumerate(dl):
+                assert b.shape == (gb // world, 3)
+                rows.append(b[:, 0].clone())
+                if stop is not None and (e, i) == stop:
+                    sd = dl.state_dict()
+                    return out, sd, dl.stats()
+            out.append(torch.cat(rows).numpy())
+        return out, None, dl.stats()
+
+
+@pytest.fixture
+def src():
+    from ddl_amd.models import SharedArraySource
+
+    n = 777
+    data = torch.stack([torch.arange(n), -torch.arange(n), torch.arange(n) * 2], 1)
+    s = SharedArraySource.create(f"ddl_amd_res_{np.random.randint(1 << 30)}", data)
+    yield s
+    s.close()
+
+
+@pytest.mark.parametrize("world,depth", [(1, 1), (2, 2), (3, 3), (4, 2)])
+def test_resident_exact_global_order(src, world, depth):
+    from ddl_amd.permutation import EpochOrder
+
+    gb = 48
+    res = run_ranks(_resident_rank, world, src.name, src.n, gb, 2, depth)
+    order = EpochOrder(src.n, gb, 11)
+    bpe = order.batches_per_epoch
+    for e in range(2):
+        ref = order.perm(e).full()[: bpe * gb].reshape(bpe, gb)
+        merged = np.concatenate([r[0][e].reshape(bpe, gb // world) for r in res], axis=1)
+        assert np.array_equal(merged, ref)
+    if world > 1:
+        assert sum(r[2]["bytes_exchanged"] for r in res) > 0
+
+
+def test_resident_resume_across_world_sizes(src):
+    from ddl_amd.permutation import EpochOrder
+
+    gb = 48
+    (_, sd, _), _ = run_ranks(_resident_rank, 2, src.name, src.n, gb, 2, 2, None, (0, 3))
+    assert sd["global_batch_cursor"] == 4
+    (out, _, _), = run_ranks(_resident_rank, 1, src.name, src.n, gb, 2, 1, sd)
+    order = EpochOrder(src.n, gb, 11)
+    bpe = order.batches_per_epoch
+    assert np.array_equal(out[0], order.perm(0).full()[4 * gb: bpe * gb])
+    assert np.array_equal(out[1], order.perm(1).full()[: bpe * gb])

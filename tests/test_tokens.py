@@ -1,0 +1,67 @@
+"""Token family (BASELINE config 4): ragged windows, pad / pack collate, exactly-once sequences."""
+
+import numpy as np
+import pytest
+import torch
+
+import ddl_amd
+from ddl_amd.models.tokens import SharedTokenSource, TokenBatchProducer, expected_tokens
+from ddl_amd.permutation import EpochOrder
+
+
+@pytest.fixture
+def corpus():
+    src = SharedTokenSource.synthetic(f"ddl_amd_tok_{np.random.randint(1 << 30)}", 200, 5, 300, seed=3)
+    yield src
+    src.close()
+
+
+def _check_pad(batch, source, idx, seq_len):
+    ids, mask, pos = batch["input_ids"].cpu(), batch["attention_mask"].cpu(), batch["position_ids"].cpu()
+    for r, seq in enumerate(expected_tokens(source, idx)):
+        n = min(len(seq), seq_len)
+        assert torch.equal(ids[r, :n], torch.from_numpy(seq[:n]))
+        assert mask[r, :n].all() and not mask[r, n:].any()
+        assert torch.equal(pos[r, :n], torch.arange(n))
+
+
+@pytest.mark.parametrize("mode", ["pad", "pack"])
+def test_token_batches_cpu(corpus, mode):
+    seq_len, gb = 256, 16
+    order = EpochOrder(corpus.n, gb, 4)
+    with ddl_amd.start(n_producers=2) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(corpus, gb, seq_len, mode), gb, conn, 2,
+                                           mode="indexed", env=env, auto_mark=True, collate="tokens", seed=4)
+        for e in range(2):
+            for g, batch in enumerate(dl):
+                idx = order.indices(e, g)
+                if mode == "pad":
+                    assert batch["input_ids"].shape == (gb, seq_len)
+                    _check_pad(batch, corpus, idx, seq_len)
+                else:
+                    m = batch["attention_mask"].bool()
+                    flat = batch["input_ids"][m]
+                    ref = np.concatenate(expected_tokens(corpus, idx))
+                    assert np.array_equal(flat.numpy(), ref)  # every token exactly once, in order
+                    assert batch["input_ids"].shape[1] == seq_len
+                    cu = batch["cu_seqlens"]
+                    assert int(cu[-1]) == len(ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["pad", "pack"])
+def test_token_batches_gpu(corpus, mode):
+    seq_len, gb = 256, 16
+    order = EpochOrder(corpus.n, gb, 4)
+    with ddl_amd.start(n_producers=2) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(corpus, gb, seq_len, mode), gb, conn, 1,
+                                           mode="indexed", env=env, auto_mark=True, collate="tokens", seed=4)
+        for g, batch in enumerate(dl):
+            assert batch["input_ids"].is_cuda
+            idx = order.indices(0, g)
+            if mode == "pad":
+                _check_pad(batch, corpus, idx, seq_len)
+            else:
+                m = batch["attention_mask"].bool().cpu()
+                flat = batch["input_ids"].cpu()[m]
+                assert np.array_equal(flat.numpy(), np.concatenate(expected_tokens(corpus, idx)))
