@@ -11,6 +11,10 @@ each rank = one consumer with its own producer worker processes:
   per-batch fused gfx950 Feistel-permutation gather --> bf16 [B,3,224,224]
   on the compute stream --> consumer step.
 
+With N > 1 every window also goes through the global-shuffle exchange: half of
+its rows are traded with all peers in one RCCL all-to-all over xGMI (BASELINE
+config 3), overlapped with the next window's DMA.
+
 Phase 1 (the reported ``value``): the consumer step is a checksum kernel that
 reads every delivered byte, so the number is the loader's feed rate. Every
 sample crosses PCIe in every step (each window is re-copied H2D each visit;
@@ -48,7 +52,9 @@ def parse(argv=None):
     ap.add_argument("--depth", type=int, default=2, help="HBM prefetch depth (windows)")
     ap.add_argument("--source-dtype", default="bfloat16", choices=["bfloat16", "uint8", "float32"])
     ap.add_argument("--shuffle", default="device", choices=["device", "none"])
-    ap.add_argument("--exchange", type=float, default=0.0, help="global-shuffle fraction per window (N>1)")
+    ap.add_argument("--exchange", type=float, default=None,
+                    help="global-shuffle fraction per window over RCCL (default 0.5 when N>1, as the reference "
+                         "harness's fraction_exchange; 0 disables)")
     ap.add_argument("--exchange-method", default="alltoall")
     ap.add_argument("--idle-steps", type=int, default=-1, help="phase-2 steps (default: = --steps; 0 disables)")
     ap.add_argument("--model-dim", type=int, default=384)
@@ -72,6 +78,8 @@ def main(argv=None) -> int:
     if n_world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={n_world}", file=sys.stderr)
     idle_steps = args.steps if args.idle_steps < 0 else args.idle_steps
+    if args.exchange is None:
+        args.exchange = 0.5 if n_world > 1 else 0.0
     total_steps = args.warmup + args.steps + (args.warmup // 2 + idle_steps if idle_steps else 0)
     bpw = args.window // args.batch
     if bpw < 1:
@@ -100,10 +108,14 @@ def main(argv=None) -> int:
 
         it = batches()
 
+        def sync():
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+
         def barrier():
             if env.world_size > 1:
                 dist.barrier(group=env.control_group)
-            torch.cuda.synchronize(dev)
+            sync()
 
         # ---------------- phase 1: feed rate
         for _ in range(args.warmup):
@@ -114,7 +126,7 @@ def main(argv=None) -> int:
         for _ in range(args.steps):
             (x,) = next(it)
             ops.checksum(x, out=acc)
-        torch.cuda.synchronize(dev)
+        sync()
         t1 = time.perf_counter()
         barrier()
         elapsed = t1 - t0
@@ -135,17 +147,19 @@ def main(argv=None) -> int:
             for _ in range(args.warmup // 2):
                 (x,) = next(it)
                 step(x)
-            meter = ComputeIdleMeter()
+            meter = ComputeIdleMeter() if dev.type == "cuda" else None
             barrier()
             t2 = time.perf_counter()
             for _ in range(idle_steps):
                 (x,) = next(it)
-                meter.step_begin()
+                if meter:
+                    meter.step_begin()
                 step(x)
-                meter.step_end()
-            torch.cuda.synchronize(dev)
+                if meter:
+                    meter.step_end()
+            sync()
             t3 = time.perf_counter()
-            idle = meter.result()
+            idle = meter.result() if meter else {"gpu_idle_pct": float("nan"), "busy_ms": 0.0, "wall_ms": 0.0}
             idle["train_samples_per_s"] = args.batch * idle_steps * env.world_size / (t3 - t2)
             if env.world_size > 1:
                 t = torch.tensor([idle["gpu_idle_pct"]], dtype=torch.float64)

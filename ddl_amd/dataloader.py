@@ -317,7 +317,7 @@ class DistributedDataLoader:
                 return collate_token_window(win.reshape(-1), TokenWindowLayout(**ex["token_layout"]),
                                             ex["token_mode"], tags, self.pad_id)
         perm = self._perm_for(p, seq)
-        out_dtype = self.out_dtype or wdt
+        out_dtype = self.out_dtype or (torch.float32 if self.normalize is not None else wdt)
         splits = list(self.splits[p])
         norm = self.normalize
         with trace_range("ddl.consumer.batch"):

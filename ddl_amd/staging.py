@@ -12,8 +12,12 @@ ddl/connection.py:89-92). This is the MI355X-native replacement of that gap
   (``hipLaunchHostFunc``) the hand-back of the slot to its producer, so the
   producer refills it the moment the DMA retires -- the consumer thread is
   never involved;
-* optional post-copy device work on the same stream (the cross-GPU global
-  shuffle exchange over RCCL, ``parallel/shuffle.py``);
+* optional post-copy device work (the cross-GPU global shuffle exchange over
+  RCCL, ``parallel/shuffle.py``) on a second stream. Collectives must be
+  issued in the same order and number on every rank, so they are NOT issued
+  by the staging thread (whose progress depends on producer timing): the
+  consumer thread issues window w+1's exchange when it starts window w
+  (``get``), i.e. one window ahead, deterministically;
 * a ``ready`` event per buffer; the compute stream waits on it *on the device*
   (``hipStreamWaitEvent``) -- the host never blocks on a copy;
 * a buffer is recycled only after a ``free`` event recorded on the compute
@@ -77,6 +81,8 @@ class WindowStager:
         self.free_events: list[torch.cuda.Event | None] = [None] * depth
         self._cv = threading.Condition()
         self._staged: dict[int, StagedWindow] = {}
+        self._infos: dict[int, dict] = {}
+        self._posted: set[int] = set()
         self._released_upto = first_window  # windows < this are released by the consumer
         self._stop = False
         self._error: BaseException | None = None
@@ -116,16 +122,15 @@ class WindowStager:
                 self.conn.release_on_stream(p, s, handle)
                 view = buf[:nbytes]
                 if self.post_copy is not None:
-                    self._copy_done[b].record(self.copy_stream)
-                    self.stream.wait_event(self._copy_done[b])
-                    with torch.cuda.stream(self.stream), trace_range("ddl.stage.post_copy"):
-                        self.post_copy(view, w, info)
-                self.ready_events[b].record(self.stream)
+                    self._copy_done[b].record(self.copy_stream)  # post_copy runs later, from get()
+                else:
+                    self.ready_events[b].record(self.copy_stream)
                 self.bytes_h2d += nbytes
                 self.windows_staged += 1
                 with self._cv:
                     self._staged[w] = StagedWindow(w, b, p, s, int(info["seq"]), nbytes, view, time.perf_counter(),
                                                    tuple(info["tag"]))
+                    self._infos[w] = info
                     self._cv.notify_all()
         except ShutdownError:
             pass
@@ -138,6 +143,27 @@ class WindowStager:
     # -------------------------------------------------------------- consumer
     def get(self, w: int) -> StagedWindow:
         """Window ``w`` staged in HBM; the current stream is made to wait for it (device-side)."""
+        if self.post_copy is not None:
+            self._post(w)
+            if self.depth >= 2 and w + 1 < self.first + self.total:
+                self._post(w + 1)  # one window ahead, in lockstep on every rank
+        sw = self._wait_staged(w)
+        torch.cuda.current_stream(self.device).wait_event(self.ready_events[sw.buffer])
+        return sw
+
+    def _post(self, w: int) -> None:
+        if w in self._posted:
+            return
+        sw = self._wait_staged(w)
+        with self._cv:
+            info = self._infos.pop(w, {})
+        self.stream.wait_event(self._copy_done[sw.buffer])
+        with torch.cuda.stream(self.stream), trace_range("ddl.stage.post_copy"):
+            self.post_copy(sw.data, w, info)
+        self.ready_events[sw.buffer].record(self.stream)
+        self._posted.add(w)
+
+    def _wait_staged(self, w: int) -> StagedWindow:
         deadline = time.monotonic() + self.timeout_s
         with self._cv:
             while w not in self._staged:
@@ -148,9 +174,7 @@ class WindowStager:
                 if time.monotonic() > deadline:
                     raise DDLTimeoutError(f"window {w} was not staged within {self.timeout_s:.0f}s")
                 self._cv.wait(0.05)
-            sw = self._staged[w]
-        torch.cuda.current_stream(self.device).wait_event(self.ready_events[sw.buffer])
-        return sw
+            return self._staged[w]
 
     def release(self, w: int) -> None:
         """Consumer is done with window ``w`` (as of the current stream position)."""
@@ -158,6 +182,7 @@ class WindowStager:
             sw = self._staged.pop(w, None)
             if sw is None:
                 return
+            self._posted.discard(w)
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.device))
             self.free_events[sw.buffer] = ev
