@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""Per-kernel throughput of the gfx950 loader kernels at production shapes.
+
+Each kernel is timed with HIP events over many launches and reported as
+effective HBM GB/s (bytes read + written) against the ~6.3 TB/s achievable
+HBM3E roofline (MI355X_MICROARCH "HBM"). No child processes, no producers:
+safe to run under ``rocprofv3 --pmc``.
+"""
+
+import json
+import sys
+
+import numpy as np
+import torch
+
+from ddl_amd import ops
+from ddl_amd.permutation import FeistelPermutation
+
+
+def bench(fn, reps=50):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / reps * 1e-3
+
+
+def report(name, t, bytes_moved, **kw):
+    print(json.dumps({"kernel": name, "us": round(t * 1e6, 2), "GBps": round(bytes_moved / t / 1e9, 1),
+                      "pct_of_6300GBps": round(100 * bytes_moved / t / 6.3e12, 1), **kw}), flush=True)
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    B, C, H, W = 256, 3, 224, 224
+    n = 2048
+    win_bf16 = torch.randn(n, C, H, W, device=dev).to(torch.bfloat16)
+    win_u8 = torch.randint(0, 256, (n, C, H, W), dtype=torch.uint8, device=dev)
+    win_hwc = torch.randint(0, 256, (n, H, W, C), dtype=torch.uint8, device=dev)
+    p = FeistelPermutation(n, 1, 2)
+    out_bf16 = torch.empty(B, C, H, W, dtype=torch.bfloat16, device=dev)
+    img = C * H * W
+    mean, std = [0.485, 0.456, 0.406], [0.229, 0.224, 0.225]
+    sc = [1 / (255 * s_) for s_ in std]
+    bi = [-m / s_ for m, s_ in zip(mean, std)]
+
+    t = bench(lambda: ops.gather_rows(win_bf16, perm=p, base=0, n_rows=B, out=out_bf16))
+    report("permute_gather bf16->bf16", t, 2 * B * img * 2, rows=B, row_bytes=img * 2)
+    t = bench(lambda: ops.gather_rows(win_u8, perm=p, base=0, n_rows=B, out=out_bf16, scale=sc, bias=bi,
+                                      plane=H * W))
+    report("permute_gather u8->bf16 normalise", t, B * img * 3, rows=B)
+    t = bench(lambda: ops.collate_hwc_to_chw(win_hwc, perm=p, base=0, n_rows=B, out=out_bf16, mean=mean, std=std))
+    report("collate HWC u8 -> CHW bf16 normalise", t, B * img * 3, rows=B)
+    f32 = torch.randn(B, img, device=dev)
+    t = bench(lambda: ops.cast(f32, torch.bfloat16))
+    report("cast f32->bf16", t, B * img * 6)
+    idx = torch.from_numpy(p(np.arange(B))).to(dev)
+    t = bench(lambda: ops.scatter_rows(win_bf16.view(n, -1), out_bf16.view(B, -1), idx))
+    report("scatter_rows bf16", t, 2 * B * img * 2)
+    t = bench(lambda: ops.checksum(out_bf16))
+    report("checksum (reduce)", t, B * img * 2)
+    t = bench(lambda: ops.feistel_indices(FeistelPermutation(1 << 24, 3, 3), 0, 1 << 24, device=dev), reps=10)
+    report("feistel_indices 16M", t, (1 << 24) * 8)
+    # pointwise (reference CI shape): 100,520 x 9 f32 window, 4096-row batch split (3,5,1)
+    pw = torch.randn(100_520, 9, device=dev)
+    pp = FeistelPermutation(100_520, 5, 5)
+    t = bench(lambda: ops.split_columns(pw, (3, 5, 1), perm=pp, base=0, n_rows=4096))
+    report("split_columns 4096x(3,5,1) f32", t, 2 * 4096 * 36)
+    # tokens: 64 sequences, mean 2k, seq_len 4096 pack + pad
+    rng = np.random.default_rng(0)
+    lens = rng.integers(256, 4097, size=64)
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    toks = torch.from_numpy(rng.integers(0, 50000, size=int(offs[-1])).astype(np.int32)).to(dev)
+    offs_d = torch.from_numpy(offs).to(dev)
+    t = bench(lambda: ops.pad_tokens(toks, offs_d, 4096))
+    report("pad_tokens 64x4096", t, toks.numel() * 4 + 64 * 4096 * (4 + 1 + 8))
+    t = bench(lambda: ops.pack_tokens(toks, offs, 4096), reps=20)
+    report("pack_tokens 64 seqs (incl. host plan)", t, toks.numel() * (4 + 4 + 1 + 8 + 4))
+    x = torch.randn(1_000_000, 9, device=dev)
+    t = bench(lambda: ops.column_stats(x), reps=20)
+    report("column_stats 1Mx9", t, x.numel() * 4)
+
+
+if __name__ == "__main__":
+    sys.exit(main())
