@@ -101,12 +101,80 @@ __global__ void __launch_bounds__(kThreads) hwc_to_chw_kernel(void* __restrict__
   }
 }
 
+// Specialisation for the common case (uint8 RGB): each lane pulls its 8 pixels
+// (24 B) out of LDS with three conflict-free ds_read_b64 (lane stride 24 B ->
+// dword stride 6: the 32 lanes of a half-wave cover all 64 banks once) instead
+// of 24 single-byte reads, then de-interleaves in registers.
+template <int OUT_BF16>
+__global__ void __launch_bounds__(kThreads) hwc3_u8_to_chw_kernel(void* __restrict__ dst, const uint8_t* __restrict__ src,
+                                                                  int64_t pixels, int64_t tiles, RowIndex ri,
+                                                                  Affine aff) {
+  __shared__ __attribute__((aligned(16))) uint8_t tile[kPix * 3];
+  const int64_t img = blockIdx.x / tiles;
+  const int64_t t = blockIdx.x % tiles;
+  const int64_t p0 = t * kPix;
+  const int npx = static_cast<int>(pixels - p0 < kPix ? pixels - p0 : kPix);
+  const uint8_t* s = src + (source_row(ri, img) * pixels + p0) * 3;
+  const int bytes = npx * 3;
+  if ((reinterpret_cast<uintptr_t>(s) & 15u) == 0 && (bytes & 15) == 0) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(s);
+    uint4* l4 = reinterpret_cast<uint4*>(tile);
+    for (int i = threadIdx.x; i < bytes / 16; i += kThreads) l4[i] = s4[i];
+  } else {
+    for (int i = threadIdx.x; i < bytes; i += kThreads) tile[i] = s[i];
+  }
+  __syncthreads();
+  const int px = threadIdx.x * 8;
+  if (px >= npx) return;
+  const int64_t out_img = img * 3 * pixels;
+  if (px + 8 <= npx) {
+    const uint64_t* l8 = reinterpret_cast<const uint64_t*>(tile + px * 3);
+    const uint64_t w[3] = {l8[0], l8[1], l8[2]};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float sc = aff.enabled ? aff.scale[c] : 1.f;
+      const float bi = aff.enabled ? aff.bias[c] : 0.f;
+      float f[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int b = 3 * k + c;  // byte index inside the lane's 24 bytes
+        f[k] = fmaf(static_cast<float>((w[b >> 3] >> (8 * (b & 7))) & 0xffu), sc, bi);
+      }
+      const int64_t o = out_img + c * pixels + p0 + px;
+      if ((o & 7) == 0) {
+        Out8<OUT_BF16>::store(dst, o, f);
+      } else {
+        for (int k = 0; k < 8; ++k) Out8<OUT_BF16>::store1(dst, o + k, f[k]);
+      }
+    }
+  } else {
+    for (int c = 0; c < 3; ++c) {
+      const float sc = aff.enabled ? aff.scale[c] : 1.f;
+      const float bi = aff.enabled ? aff.bias[c] : 0.f;
+      for (int k = 0; k < 8 && px + k < npx; ++k)
+        Out8<OUT_BF16>::store1(dst, out_img + c * pixels + p0 + px + k,
+                               fmaf(static_cast<float>(tile[(px + k) * 3 + c]), sc, bi));
+    }
+  }
+}
+
 template <typename Tin>
 int launch_hwc(void* dst, int32_t out_dt, const void* src, int64_t batch, int64_t pixels, int32_t channels,
                const RowIndex& ri, const Affine& aff, hipStream_t st) {
   const int64_t tiles = (pixels + kPix - 1) / kPix;
   const size_t lds = static_cast<size_t>(kPix) * channels * sizeof(Tin);
   const dim3 grid(static_cast<uint32_t>(batch * tiles));
+  if constexpr (sizeof(Tin) == 1) {
+    if (channels == 3 && (out_dt == kBF16 || out_dt == kF32)) {
+      if (out_dt == kBF16)
+        hipLaunchKernelGGL(hwc3_u8_to_chw_kernel<1>, grid, dim3(kThreads), 0, st, dst,
+                           static_cast<const uint8_t*>(src), pixels, tiles, ri, aff);
+      else
+        hipLaunchKernelGGL(hwc3_u8_to_chw_kernel<0>, grid, dim3(kThreads), 0, st, dst,
+                           static_cast<const uint8_t*>(src), pixels, tiles, ri, aff);
+      return static_cast<int>(hipGetLastError());
+    }
+  }
   if (out_dt == kBF16)
     hipLaunchKernelGGL((hwc_to_chw_kernel<Tin, 1>), grid, dim3(kThreads), lds, st, dst, static_cast<const Tin*>(src),
                        pixels, channels, tiles, ri, aff);

@@ -73,10 +73,77 @@ __global__ void __launch_bounds__(kThreads) checksum_final_kernel(const uint64_t
   }
 }
 
-// One block per column tile of 64 columns x all rows slice; lanes stride rows.
-__global__ void __launch_bounds__(kThreads) column_stats_kernel(const float* __restrict__ src, int64_t n, int64_t cols,
-                                                                float* sum, float* sumsq, float* mn, float* mx,
-                                                                int64_t rows_per_block) {
+// Narrow matrices (cols <= 256): flat, coalesced grid-stride over elements
+// with a per-thread stride that is a multiple of `cols`, so every thread
+// always lands on the same column and accumulates it in registers (no idle
+// lanes, no strided loads). Per-column partials are then combined through LDS
+// and one atomic per (block, column).
+template <int kMaxCols>
+__global__ void __launch_bounds__(kThreads) column_stats_narrow_kernel(const float* __restrict__ src, int64_t total,
+                                                                       int cols, float* sum, float* sumsq, float* mn,
+                                                                       float* mx) {
+  __shared__ float ps[kMaxCols], pq[kMaxCols];
+  for (int c = threadIdx.x; c < cols; c += kThreads) {
+    ps[c] = 0.f;
+    pq[c] = 0.f;
+  }
+  __syncthreads();
+  const int active = (kThreads / cols) * cols;  // threads per block that take part
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * active;  // multiple of cols
+  float s = 0.f, q = 0.f, lo = INFINITY, hi = -INFINITY;
+  if (threadIdx.x < active) {
+    int64_t e = static_cast<int64_t>(blockIdx.x) * active + threadIdx.x;
+    for (; e + 3 * stride < total; e += 4 * stride) {  // 4 independent loads in flight per lane
+      const float v0 = src[e], v1 = src[e + stride], v2 = src[e + 2 * stride], v3 = src[e + 3 * stride];
+      s += (v0 + v1) + (v2 + v3);
+      q = fmaf(v0, v0, fmaf(v1, v1, fmaf(v2, v2, fmaf(v3, v3, q))));
+      lo = fminf(lo, fminf(fminf(v0, v1), fminf(v2, v3)));
+      hi = fmaxf(hi, fmaxf(fmaxf(v0, v1), fmaxf(v2, v3)));
+    }
+    for (; e < total; e += stride) {
+      const float v = src[e];
+      s += v;
+      q = fmaf(v, v, q);
+      lo = fminf(lo, v);
+      hi = fmaxf(hi, v);
+    }
+    const int c = static_cast<int>((static_cast<int64_t>(blockIdx.x) * active + threadIdx.x) % cols);
+    atomicAdd(&ps[c], s);  // LDS atomics: cheap, few threads per column
+    atomicAdd(&pq[c], q);
+  }
+  __syncthreads();
+  // min/max through a second LDS pass (float atomics on LDS for min/max are not native)
+  __shared__ float red_lo[kThreads], red_hi[kThreads];
+  red_lo[threadIdx.x] = threadIdx.x < active ? lo : INFINITY;
+  red_hi[threadIdx.x] = threadIdx.x < active ? hi : -INFINITY;
+  __syncthreads();
+  const int64_t b0 = static_cast<int64_t>(blockIdx.x) * active;
+  for (int c = threadIdx.x; c < cols; c += kThreads) {
+    float l = INFINITY, h = -INFINITY;
+    // threads t with (b0 + t) % cols == c
+    const int first = static_cast<int>(((c - b0 % cols) % cols + cols) % cols);
+    for (int t = first; t < active; t += cols) {
+      l = fminf(l, red_lo[t]);
+      h = fmaxf(h, red_hi[t]);
+    }
+    atomicAdd(sum + c, ps[c]);
+    atomicAdd(sumsq + c, pq[c]);
+    const int li = __float_as_int(l), hi_i = __float_as_int(h);
+    if (li >= 0)
+      atomicMin(reinterpret_cast<int*>(mn + c), li);
+    else
+      atomicMax(reinterpret_cast<unsigned int*>(mn + c), static_cast<unsigned int>(li));
+    if (hi_i >= 0)
+      atomicMax(reinterpret_cast<int*>(mx + c), hi_i);
+    else
+      atomicMin(reinterpret_cast<unsigned int*>(mx + c), static_cast<unsigned int>(hi_i));
+  }
+}
+
+// Wide matrices: one block per 64-column tile x row slice; lanes = columns.
+__global__ void __launch_bounds__(kThreads) column_stats_wide_kernel(const float* __restrict__ src, int64_t n,
+                                                                     int64_t cols, float* sum, float* sumsq, float* mn,
+                                                                     float* mx, int64_t rows_per_block) {
   const int64_t c = static_cast<int64_t>(blockIdx.y) * 64 + (threadIdx.x & 63);
   const int wave = threadIdx.x >> 6;
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
@@ -107,7 +174,6 @@ __global__ void __launch_bounds__(kThreads) column_stats_kernel(const float* __r
     }
     atomicAdd(sum + c, s);
     atomicAdd(sumsq + c, q);
-    // float min/max via ordered-int atomics
     const int lo_i = __float_as_int(lo), hi_i = __float_as_int(hi);
     if (lo_i >= 0)
       atomicMin(reinterpret_cast<int*>(mn + c), lo_i);
@@ -143,11 +209,21 @@ int checksum_words(const void* ptr, int64_t bytes, uint64_t* out, uint64_t* scra
 int column_stats(const float* src, int64_t n, int64_t cols, float* out_sum, float* out_sumsq, float* out_min,
                  float* out_max, hipStream_t st) {
   if (n <= 0 || cols <= 0) return 0;
+  if (cols <= 256) {
+    const int64_t total = n * cols;
+    // one block per CU: few enough same-address atomics (36 per block at 9 columns)
+    int64_t blocks = (total + kThreads * 16 - 1) / (kThreads * 16);
+    if (blocks > 256) blocks = 256;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(column_stats_narrow_kernel<256>, dim3(static_cast<uint32_t>(blocks)), dim3(kThreads), 0, st,
+                       src, total, static_cast<int>(cols), out_sum, out_sumsq, out_min, out_max);
+    return static_cast<int>(hipGetLastError());
+  }
   const int64_t col_tiles = (cols + 63) / 64;
   int64_t row_blocks = (n + 4095) / 4096;
   if (row_blocks > 1024) row_blocks = 1024;
   const int64_t rpb = (n + row_blocks - 1) / row_blocks;
-  hipLaunchKernelGGL(column_stats_kernel, dim3(static_cast<uint32_t>(row_blocks), static_cast<uint32_t>(col_tiles)),
+  hipLaunchKernelGGL(column_stats_wide_kernel, dim3(static_cast<uint32_t>(row_blocks), static_cast<uint32_t>(col_tiles)),
                      dim3(kThreads), 0, st, src, n, cols, out_sum, out_sumsq, out_min, out_max, rpb);
   return static_cast<int>(hipGetLastError());
 }

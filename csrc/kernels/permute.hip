@@ -79,6 +79,15 @@ struct Elem<uint8_t> {
 #pragma unroll
     for (int i = 0; i < 4; ++i) f[4 + i] = static_cast<float>((v.y >> (8 * i)) & 0xffu);
   }
+  // 16 bytes per lane (one dwordx4): the guide's 16 B/lane sweet spot (G13).
+  static __device__ __forceinline__ void load16(const uint8_t* p, float (&f)[8], float (&g)[8]) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = static_cast<float>((w[i >> 2] >> (8 * (i & 3))) & 0xffu);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) g[i] = static_cast<float>((w[2 + (i >> 2)] >> (8 * (i & 3))) & 0xffu);
+  }
   static __device__ __forceinline__ float load1(const uint8_t* p) { return static_cast<float>(*p); }
 };
 template <>
@@ -185,6 +194,36 @@ __global__ void __launch_bounds__(kThreads) convert_rows_chunked(Tout* __restric
   }
 }
 
+// uint8 sources: 16 elements per lane per access (16 B loads, 2 x 16 B bf16 stores).
+template <typename Tout>
+__global__ void __launch_bounds__(kThreads) convert_u8_rows_chunked(Tout* __restrict__ dst,
+                                                                    const uint8_t* __restrict__ src, int64_t row_elems,
+                                                                    int64_t chunks_per_row, RowIndex ri, Affine aff) {
+  constexpr int kU = 2;
+  const int64_t row = blockIdx.x / chunks_per_row;
+  const int64_t chunk = blockIdx.x % chunks_per_row;
+  const int64_t srow = source_row(ri, row);
+  const uint8_t* s = src + srow * row_elems;
+  Tout* d = dst + row * row_elems;
+  const int64_t e0 = (chunk * (kThreads * kU) + threadIdx.x) * 16;
+  float lo[kU][8], hi[kU][8];
+#pragma unroll
+  for (int k = 0; k < kU; ++k) {
+    const int64_t e = e0 + static_cast<int64_t>(k) * kThreads * 16;
+    if (e < row_elems) Elem<uint8_t>::load16(s + e, lo[k], hi[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < kU; ++k) {
+    const int64_t e = e0 + static_cast<int64_t>(k) * kThreads * 16;
+    if (e < row_elems) {
+      apply_affine(aff, e, lo[k]);
+      apply_affine(aff, e + 8, hi[k]);
+      Elem<Tout>::store8(d + e, lo[k]);
+      Elem<Tout>::store8(d + e + 8, hi[k]);
+    }
+  }
+}
+
 template <typename Tin, typename Tout>
 __global__ void __launch_bounds__(kThreads) convert_rows_flat(Tout* __restrict__ dst, const Tin* __restrict__ src,
                                                               int64_t row_elems, int64_t total, RowIndex ri, Affine aff) {
@@ -224,6 +263,15 @@ void launch_move(void* dst, const void* src, int64_t n_rows, int64_t row_bytes, 
 template <typename Tin, typename Tout>
 void launch_convert(void* dst, const void* src, int64_t n_rows, int64_t row_elems, const RowIndex& ri, const Affine& aff,
                     bool vec_ok, hipStream_t st) {
+  if constexpr (sizeof(Tin) == 1) {
+    if (vec_ok && row_elems % 16 == 0 && row_elems >= kThreads * 16) {
+      const int64_t chunks = (row_elems + kThreads * 2 * 16 - 1) / (kThreads * 2 * 16);
+      hipLaunchKernelGGL((convert_u8_rows_chunked<Tout>), dim3(static_cast<uint32_t>(n_rows * chunks)),
+                         dim3(kThreads), 0, st, static_cast<Tout*>(dst), static_cast<const uint8_t*>(src), row_elems,
+                         chunks, ri, aff);
+      return;
+    }
+  }
   if (vec_ok && row_elems >= kThreads * 8) {
     const int64_t chunks = (row_elems + kThreads * kUnroll * 8 - 1) / (kThreads * kUnroll * 8);
     hipLaunchKernelGGL((convert_rows_chunked<Tin, Tout>), dim3(static_cast<uint32_t>(n_rows * chunks)), dim3(kThreads),

@@ -148,7 +148,10 @@ def gather_rows(src, index: torch.Tensor | None = None, *, perm: FeistelPermutat
                 n_rows: int | None = None, out: torch.Tensor | None = None, out_dtype=None, scale=None, bias=None,
                 plane: int | None = None, stream=None) -> torch.Tensor:
     """out[r] = cast(affine(src[row(r)])): fused permute + cast + per-channel normalise."""
-    out_dtype = _dtypes.to_torch_dtype(out_dtype) if out_dtype is not None else src.dtype
+    if out_dtype is not None:
+        out_dtype = _dtypes.to_torch_dtype(out_dtype)
+    else:
+        out_dtype = out.dtype if out is not None else src.dtype
     if not _is_gpu(src):
         res = ref_gather_rows(src, index, perm, base, n_rows, out_dtype, scale, bias, plane)
         if out is not None:

@@ -168,8 +168,9 @@ def test_checksum(nbytes):
     assert out == ref
 
 
-def test_column_stats():
-    x = torch.randn(100_003, 10) * torch.arange(1, 11)
+@pytest.mark.parametrize("rows,cols", [(100_003, 10), (4096, 1), (7777, 9), (3000, 255), (2000, 256), (999, 300)])
+def test_column_stats(rows, cols):
+    x = torch.randn(rows, cols) * torch.arange(1, cols + 1) - 3
     s = ops.column_stats(x.to(_dev()))
     torch.testing.assert_close(s["min"].cpu(), x.min(0).values)
     torch.testing.assert_close(s["max"].cpu(), x.max(0).values)
