@@ -66,7 +66,8 @@ ddl::RowIndex make_index(int mode, uintptr_t idx, int64_t base, const std::vecto
 ddl::Affine make_affine(const std::vector<float>& scale, const std::vector<float>& bias, int64_t plane) {
   ddl::Affine a{};
   if (scale.empty()) return a;
-  if (scale.size() != bias.size() || scale.size() > 8) throw std::invalid_argument("affine: 1..8 channels");
+  if (scale.size() != bias.size() || scale.size() > static_cast<size_t>(ddl::kMaxAffineChannels))
+    throw std::invalid_argument("affine: 1..16 channels");
   if (plane <= 0) throw std::invalid_argument("affine: plane must be > 0");
   for (size_t i = 0; i < scale.size(); ++i) {
     a.scale[i] = scale[i];

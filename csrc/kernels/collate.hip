@@ -236,7 +236,7 @@ __global__ void __launch_bounds__(kThreads) split_columns_raw_kernel(SplitSpec s
 int collate_hwc_to_chw(void* dst, int32_t out_dt, const void* src, int32_t in_dt, int64_t batch, int64_t pixels,
                        int32_t channels, const RowIndex& ri, const Affine& aff, hipStream_t st) {
   if (batch <= 0 || pixels <= 0) return 0;
-  if (channels <= 0 || channels > 8) return -2;
+  if (channels <= 0 || channels > kMaxAffineChannels) return -2;
   switch (in_dt) {
     case kU8: return launch_hwc<uint8_t>(dst, out_dt, src, batch, pixels, channels, ri, aff, st);
     case kF32: return launch_hwc<float>(dst, out_dt, src, batch, pixels, channels, ri, aff, st);

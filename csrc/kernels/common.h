@@ -66,11 +66,12 @@ DDL_HD int64_t source_row(const RowIndex& ri, int64_t r) {
 
 // Per-channel affine epilogue (normalisation) fused into gathers / casts:
 // out = in * scale[ch] + bias[ch], ch = (element_in_row / plane) % channels.
+constexpr int kMaxAffineChannels = 16;
 struct Affine {
-  float scale[8];
-  float bias[8];
-  int64_t plane;    // elements per channel plane (H*W); 0 disables
-  int32_t channels; // <= 8
+  float scale[kMaxAffineChannels];
+  float bias[kMaxAffineChannels];
+  int64_t plane;    // elements per channel plane (H*W for images, 1 for per-column tables)
+  int32_t channels; // <= kMaxAffineChannels
   int32_t enabled;
 };
 

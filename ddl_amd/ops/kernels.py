@@ -100,8 +100,8 @@ def _affine_lists(scale, bias) -> tuple[list[float], list[float]]:
     if bias is None:
         bias = [0.0] * len(scale)
     scale, bias = [float(s) for s in scale], [float(b) for b in bias]
-    if len(scale) != len(bias) or not 1 <= len(scale) <= 8:
-        raise ValueError("scale/bias: 1..8 channels of equal length")
+    if len(scale) != len(bias) or not 1 <= len(scale) <= 16:
+        raise ValueError("scale/bias: 1..16 channels of equal length")
     return scale, bias
 
 
@@ -457,6 +457,36 @@ def checksum(x: torch.Tensor, out: torch.Tensor | None = None, stream=None) -> t
     h.checksum_words(ptr=x.data_ptr(), bytes=nbytes - nbytes % 4, out=out.data_ptr(), scratch=scratch.data_ptr(),
                      scratch_len=scratch.numel(), stream=_stream_handle(stream))
     return out
+
+
+def column_affine(stats: dict, mode: str = "standard", area_weighted: bool = False) -> tuple[list, list]:
+    """(scale, bias) per column so that x*scale + bias normalises like the reference harness.
+
+    ``standard``: (x - mean) / std. ``minmax``: (x - (max+min)/2) / ((max-min)/2).
+    ``area_weighted`` keeps the last column un-centred and scales it by its mean
+    (reference tests/run_ddl.py:45-77).
+    """
+    mean, std, mn, mx = (stats[k].double().cpu() for k in ("mean", "std", "min", "max"))
+    if mode == "standard":
+        centre, spread = mean.clone(), std.clone()
+    elif mode == "minmax":
+        centre, spread = 0.5 * (mx + mn), 0.5 * (mx - mn)
+    else:
+        raise ValueError("mode must be 'standard' or 'minmax'")
+    if area_weighted:
+        centre[-1], spread[-1] = 0.0, mean[-1]
+    spread = torch.where(spread == 0, torch.ones_like(spread), spread)
+    return (1.0 / spread).tolist(), (-centre / spread).tolist()
+
+
+def normalize_columns(x: torch.Tensor, mode: str = "standard", out_dtype=None, stats: dict | None = None,
+                      area_weighted: bool = False, stream=None) -> torch.Tensor:
+    """Per-column normalisation of an [N, C<=16] f32 table on the device (column_stats + fused affine gather)."""
+    if x.dim() != 2 or x.shape[1] > 16:
+        raise ValueError("normalize_columns expects [N, C] with C <= 16")
+    stats = stats or column_stats(x, stream=stream)
+    sc, bi = column_affine(stats, mode, area_weighted)
+    return gather_rows(x, out_dtype=out_dtype or torch.float32, scale=sc, bias=bi, plane=1, stream=stream)
 
 
 def column_stats(x: torch.Tensor, stream=None) -> dict[str, torch.Tensor]:

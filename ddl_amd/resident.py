@@ -75,15 +75,28 @@ class ResidentGlobalLoader:
     def __init__(self, source, global_batch: int, env: DDLEnv | None = None, *, seed: int = 0,
                  drop_last: bool = True, out_dtype: Any = None, normalize: dict | None = None, depth: int = 2,
                  device: str | torch.device | None = None, n_epochs: int | None = None,
-                 resume_state: dict | None = None, chunk_bytes: int = 256 << 20, host_threads: int = 8):
+                 resume_state: dict | None = None, chunk_bytes: int = 256 << 20, host_threads: int = 8,
+                 scatter_from: int | None = None):
         import torch.distributed as dist
 
         self.env = env or DDLEnv()
         self.W, self.rank = self.env.world_size, self.env.rank
-        self.sample_shape, self.src_dtype = _source_geometry(source)
+        self.scatter_from = scatter_from
+        if scatter_from is not None and self.W > 1:
+            # only `scatter_from` holds the dataset: broadcast its geometry (small metadata)
+            geom = [None]
+            if self.rank == scatter_from:
+                shp, dt = _source_geometry(source)
+                geom = [(shp, str(dt).replace("torch.", ""), _source_address(source)[1])]
+            dist.broadcast_object_list(geom, src=scatter_from, group=self.env.control_group)
+            shp, dt, n = geom[0]
+            self.sample_shape, self.src_dtype = tuple(shp), _dtypes.to_torch_dtype(dt)
+            src_addr = _source_address(source)[0] if self.rank == scatter_from else 0
+        else:
+            self.sample_shape, self.src_dtype = _source_geometry(source)
+            src_addr, n = _source_address(source)
         self.row_elems = int(math.prod(self.sample_shape)) if self.sample_shape else 1
         self.row_bytes = self.row_elems * _dtypes.itemsize(self.src_dtype)
-        src_addr, n = _source_address(source)
         self.N = n
         self.order = EpochOrder(n, global_batch, seed, drop_last)
         self.GB = int(global_batch)
@@ -112,7 +125,10 @@ class ResidentGlobalLoader:
         self.bytes_exchanged = 0
         self.batches = 0
         t0 = time.perf_counter()
-        self.shard = self._load_shard(src_addr, chunk_bytes, host_threads)
+        if scatter_from is not None and self.W > 1:
+            self.shard = self._scatter_shards(src_addr, chunk_bytes, host_threads, scatter_from)
+        else:
+            self.shard = self._load_shard(src_addr, chunk_bytes, host_threads)
         self.load_s = time.perf_counter() - t0
         self.prep_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
         self._queue: collections.deque = collections.deque()
@@ -152,6 +168,59 @@ class ResidentGlobalLoader:
                 off += n
                 i += 1
             s.synchronize()
+        return shard
+
+    def _scatter_shards(self, src_addr: int, chunk_bytes: int, host_threads: int, src_rank: int) -> torch.Tensor:
+        """Rank ``src_rank`` streams the dataset H2D chunk by chunk and sends every
+        peer the rows of its shard with grouped point-to-point ops (all peers at
+        once: on an xGMI-connected node every link carries one peer's slice);
+        the other ranks receive straight into their HBM shard."""
+        import torch.distributed as dist
+
+        rows = self.hi - self.lo
+        shard = torch.empty((rows,) + self.sample_shape, dtype=self.src_dtype, device=self.device)
+        # first op on the group must be collective (communicator bring-up on every rank)
+        probe = torch.zeros(1, device=self.device)
+        dist.all_reduce(probe, group=self.group)
+        rows_per_chunk = max(1, chunk_bytes // self.row_bytes)
+        bounds = [(q * self.S, min(self.N, (q + 1) * self.S)) for q in range(self.W)]
+        rt = _native.runtime()
+        staging = None
+        if self.rank == src_rank:
+            staging = torch.empty((rows_per_chunk,) + self.sample_shape, dtype=self.src_dtype, device=self.device)
+            bounce = torch.empty(rows_per_chunk * self.row_bytes, dtype=torch.uint8,
+                                 pin_memory=self.device.type == "cuda")
+        with trace_range("ddl.resident.scatter"):
+            for c0 in range(0, self.N, rows_per_chunk):
+                c1 = min(self.N, c0 + rows_per_chunk)
+                ops_ = []
+                if self.rank == src_rank:
+                    nbytes = (c1 - c0) * self.row_bytes
+                    rt.parallel_copy(bounce.data_ptr(), src_addr + c0 * self.row_bytes, nbytes, host_threads)
+                    stage = staging[: c1 - c0]
+                    stage.view(-1).view(torch.uint8)[:nbytes].copy_(bounce[:nbytes], non_blocking=True)
+                    for q, (lo, hi) in enumerate(bounds):
+                        o0, o1 = max(c0, lo), min(c1, hi)
+                        if o0 >= o1:
+                            continue
+                        piece = stage[o0 - c0:o1 - c0]
+                        if q == self.rank:
+                            shard[o0 - lo:o1 - lo].copy_(piece)
+                        else:
+                            ops_.append(dist.P2POp(dist.isend, piece.contiguous(), q, group=self.group))
+                    self.bytes_exchanged += sum(p.tensor.numel() * p.tensor.element_size() for p in ops_)
+                else:
+                    o0, o1 = max(c0, self.lo), min(c1, self.hi)
+                    if o0 < o1:
+                        ops_.append(dist.P2POp(dist.irecv, shard[o0 - self.lo:o1 - self.lo], src_rank,
+                                               group=self.group))
+                if ops_:
+                    for req in dist.batch_isend_irecv(ops_):
+                        req.wait()
+                if self.rank == src_rank and self.device.type == "cuda":
+                    torch.cuda.current_stream(self.device).synchronize()  # bounce/staging reuse
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
         return shard
 
     # ------------------------------------------------------------- assembly

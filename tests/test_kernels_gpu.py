@@ -220,3 +220,21 @@ def test_h2d_and_release_callback():
         h.host_unregister(a.base_address)
     finally:
         del a
+
+
+@pytest.mark.parametrize("mode", ["standard", "minmax"])
+def test_normalize_columns_matches_reference_harness(mode):
+    from ddl_amd.models.datasets import PointWiseData
+
+    raw = np.random.default_rng(0).random((50_000, 9)).astype(np.float32) * 5 - 1
+    x = torch.from_numpy(raw).to(_dev())
+    out = ops.normalize_columns(x, mode, area_weighted=True).cpu().numpy()
+    if mode == "standard":
+        ref = PointWiseData.standard_normalize(raw.astype(np.float64), area_weighted=True)
+        ref = np.concatenate([ref[0], ref[3][:, None]], 1)
+    else:
+        ref = PointWiseData.minmax_normalize(raw.astype(np.float64), 1, 2, 5, area_weighted=True)
+        ref = np.concatenate([ref[0], ref[3][:, None]], 1)
+        # the harness scales targets by max|x| instead of the half range: compare the parameter/x columns
+        out, ref = out[:, :3], ref[:, :3]
+    np.testing.assert_allclose(out, ref, rtol=2e-4, atol=2e-4)

@@ -68,3 +68,33 @@ def test_resident_resume_across_world_sizes(src):
     bpe = order.batches_per_epoch
     assert np.array_equal(out[0], order.perm(0).full()[4 * gb: bpe * gb])
     assert np.array_equal(out[1], order.perm(1).full()[: bpe * gb])
+
+
+def _scatter_rank(rank, world, name, n, gb):
+    import ddl_amd
+    from ddl_amd.models import SharedArraySource
+    from ddl_amd.resident import ResidentGlobalLoader
+
+    src = SharedArraySource(name, n, (3,), "int64") if rank == 0 else None
+    with ddl_amd.start(n_producers=0) as (env, _):
+        dl = ResidentGlobalLoader(src, gb, env, seed=11, n_epochs=1, scatter_from=0, chunk_bytes=24 * 50)
+        shard = dl.shard.clone()
+        rows = torch.cat([b[:, 0].clone() for b in dl]).numpy()
+        return shard.numpy(), rows, dl.lo, dl.hi, dl.stats()["bytes_exchanged"]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_resident_scatter_from_one_rank(src, world):
+    from ddl_amd.permutation import EpochOrder
+
+    gb = 48
+    res = run_ranks(_scatter_rank, world, src.name, src.n, gb)
+    full = src.tensor().numpy()
+    for shard, _, lo, hi, _ in res:
+        assert np.array_equal(shard, full[lo:hi])  # every rank received exactly its shard
+    order = EpochOrder(src.n, gb, 11)
+    bpe = order.batches_per_epoch
+    ref = order.perm(0).full()[: bpe * gb].reshape(bpe, gb)
+    merged = np.concatenate([r[1].reshape(bpe, gb // world) for r in res], axis=1)
+    assert np.array_equal(merged, ref)
+    assert res[0][4] > 0

@@ -165,3 +165,43 @@ def test_numa_helpers_do_not_fail():
     numa.visible_gpu_render_minors()
     assert numa.node_cpus(0) or True
     assert numa.bind_to_gpu_numa(0) in (None, 0, 1, 2, 3, 4, 5, 6, 7)
+
+
+def test_normalize_columns_cpu_reference():
+    import numpy as np
+    import torch
+
+    from ddl_amd import ops
+
+    x = torch.randn(1000, 5) * 3 + 2
+    y = ops.normalize_columns(x, "standard")
+    np.testing.assert_allclose(y.mean(0).numpy(), 0, atol=1e-5)
+    np.testing.assert_allclose(y.std(0, unbiased=False).numpy(), 1, atol=1e-4)
+    z = ops.normalize_columns(x, "minmax")
+    np.testing.assert_allclose(z.min(0).values.numpy(), -1, atol=1e-5)
+    np.testing.assert_allclose(z.max(0).values.numpy(), 1, atol=1e-5)
+
+
+def test_metrics_writer(tmp_path):
+    import json
+
+    import ddl_amd
+    from ddl_amd import Marker
+    from ddl_amd.utils.metrics import MetricsWriter
+    from tests.helpers import IdProducer
+
+    path = tmp_path / "m" / "metrics.jsonl"
+    with ddl_amd.start(n_producers=2) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(IdProducer(16, 4), 4, conn, 2, env=env)
+        mw = MetricsWriter(dl, str(path), interval_s=0.0)
+        for _ in range(2):
+            for i, _b in enumerate(dl):
+                dl.mark(Marker.END_OF_BATCH)
+                mw.step()
+            dl.mark(Marker.END_OF_EPOCH)
+        rec = mw.flush()
+    lines = path.read_text().splitlines()
+    assert len(lines) >= 8
+    last = json.loads(lines[-1])
+    assert last["batches"] == 8 and last["samples"] == 32 and "consumer_wait_s" in last
+    assert rec["producer_rounds"] and len(rec["producer_rounds"]) == 2
