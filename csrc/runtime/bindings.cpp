@@ -9,6 +9,7 @@
 #include <new>
 
 #include "arena.h"
+#include "feistel.h"
 
 namespace py = pybind11;
 using ddl::Arena;
@@ -166,6 +167,26 @@ PYBIND11_MODULE(_ddl_runtime, m) {
       py::arg("dst"), py::arg("src"), py::arg("row_bytes"), py::arg("indices"), py::arg("src_rows"),
       py::arg("n_threads") = 4,
       "dst[i*row_bytes:(i+1)*row_bytes] = src[idx[i]*row_bytes:...] on a host worker pool");
+  m.def(
+      "feistel",
+      [](std::vector<uint64_t> keys, uint32_t half_bits, uint64_t n, py::array_t<int64_t, py::array::c_style> pos) {
+        if (keys.size() != ddl::kHostFeistelRounds) throw std::invalid_argument("feistel: need 6 round keys");
+        auto out = py::array_t<int64_t>(pos.request().shape);
+        const int64_t* in = pos.data();
+        int64_t* o = out.mutable_data();
+        const py::ssize_t m = pos.size();
+        for (py::ssize_t i = 0; i < m; ++i) {
+          if (in[i] < 0 || static_cast<uint64_t>(in[i]) >= n) throw std::out_of_range("feistel: position out of range");
+        }
+        {
+          py::gil_scoped_release nogil;
+          for (py::ssize_t i = 0; i < m; ++i)
+            o[i] = static_cast<int64_t>(ddl::host_feistel_perm(static_cast<uint64_t>(in[i]), keys.data(), half_bits, n));
+        }
+        return out;
+      },
+      py::arg("keys"), py::arg("half_bits"), py::arg("n"), py::arg("positions"),
+      "perm(positions) of the 6-round Feistel permutation (bit-identical to the gfx950 kernels)");
   m.def(
       "parallel_copy",
       [](uintptr_t dst, uintptr_t src, uint64_t bytes, int n_threads) {

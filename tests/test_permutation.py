@@ -106,3 +106,10 @@ def test_epoch_order_validation():
         EpochOrder(10, 64)
     with pytest.raises(ValueError):
         EpochOrder(1000, 64).local_batch(3)
+
+
+@pytest.mark.parametrize("n", [1, 3, 1000, 1_281_167])
+def test_native_matches_numpy_network(n):
+    p = FeistelPermutation(n, seed=77, epoch=5)
+    pos = np.unique(np.random.default_rng(0).integers(0, n, size=min(n, 3000)))
+    assert np.array_equal(p(pos), p.numpy_eval(pos))
