@@ -34,7 +34,7 @@ from __future__ import annotations
 
 import math
 import time
-from typing import Any, Iterator, Sequence
+from typing import Any, Iterator
 
 import torch
 
@@ -334,8 +334,7 @@ class DistributedDataLoader:
                 if norm is not None:
                     plane = int(math.prod(self.sample_shape[1:])) if len(self.sample_shape) > 1 else 1
                     c = self.sample_shape[0] if len(self.sample_shape) > 1 else len(norm.get("mean", [0]))
-                    sc, bi = ops.kernels._norm_affine(c, norm.get("mean"), norm.get("std"), norm.get("scale"),
-                                                      norm.get("bias"))
+                    sc, bi = ops.norm_affine(c, norm.get("mean"), norm.get("std"), norm.get("scale"), norm.get("bias"))
                     kw = dict(scale=sc, bias=bi, plane=plane)
                 x = ops.gather_rows(win, perm=perm, base=local * B, n_rows=B, out_dtype=out_dtype, **kw)
         if len(splits) == 1:

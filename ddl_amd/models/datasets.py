@@ -197,18 +197,18 @@ class NpyMemmapSource:
             self._arr = np.load(self.path, mmap_mode="r")
         return self._arr
 
-    def gather(self, indices: np.ndarray, dst_address: int, n_threads: int = 4) -> None:
-        import ctypes
+    @property
+    def address(self) -> int:
+        a = self._a()
+        if not a.flags["C_CONTIGUOUS"]:  # pragma: no cover
+            raise ValueError("memmap must be C-contiguous")
+        return int(a.ctypes.data)
 
+    def gather(self, indices: np.ndarray, dst_address: int, n_threads: int = 4) -> None:
         from .. import _native
 
-        a = self._a()
-        addr = a.ctypes.data if a.flags["C_CONTIGUOUS"] else None
-        if addr is None:  # pragma: no cover
-            raise ValueError("memmap must be C-contiguous")
-        _native.runtime().gather_rows(dst_address, addr, self.row_bytes, np.ascontiguousarray(indices, np.int64),
-                                      self.n, n_threads)
-        del ctypes
+        _native.runtime().gather_rows(dst_address, self.address, self.row_bytes,
+                                      np.ascontiguousarray(indices, np.int64), self.n, n_threads)
 
 
 class SyntheticTokens:

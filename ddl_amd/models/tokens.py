@@ -14,7 +14,6 @@ token batches share the indexed-mode checkpoint format.
 from __future__ import annotations
 
 import dataclasses
-import math
 
 import numpy as np
 import torch
@@ -190,5 +189,3 @@ def expected_tokens(source: SharedTokenSource, idx) -> list[np.ndarray]:
     offs = source.offsets.tensor().view(-1).numpy()
     return [toks[offs[i]:offs[i + 1]] for i in idx]
 
-
-_ = math  # keep import (layout arithmetic helpers)

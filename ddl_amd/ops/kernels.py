@@ -226,7 +226,7 @@ def ref_collate_hwc_to_chw(src, index=None, perm=None, base=0, n_rows=None, out_
     n_rows = _check_rows(x, index, perm, base, n_rows)
     rows = x.index_select(0, _ref_rows(x.shape[0], n_rows, index, perm, base).to(x.device))
     c = rows.shape[-1]
-    sc, bi = _norm_affine(c, mean, std, scale, bias)
+    sc, bi = norm_affine(c, mean, std, scale, bias)
     y = rows.double().movedim(-1, 1)  # [B, C, H, W]
     if sc:
         s = torch.tensor(sc, dtype=torch.float64, device=y.device).view(1, c, *([1] * (y.dim() - 2)))
@@ -235,7 +235,7 @@ def ref_collate_hwc_to_chw(src, index=None, perm=None, base=0, n_rows=None, out_
     return y.float().to(out_dtype).contiguous()
 
 
-def _norm_affine(c, mean, std, scale, bias):
+def norm_affine(c, mean=None, std=None, scale=None, bias=None):
     """(x/255 - mean)/std  ==  x*scale + bias  with scale=1/(255*std), bias=-mean/std."""
     if mean is not None or std is not None:
         mean = list(mean) if mean is not None else [0.0] * c
@@ -267,7 +267,7 @@ def collate_hwc_to_chw(src, index: torch.Tensor | None = None, *, perm: FeistelP
     n_rows = _check_rows(src, index, perm, base, n_rows)
     spatial = tuple(src.shape[1:-1])
     pixels = int(math.prod(spatial))
-    sc, bi = _norm_affine(c, mean, std, scale, bias)
+    sc, bi = norm_affine(c, mean, std, scale, bias)
     if out is None:
         out = torch.empty((n_rows, c) + spatial, dtype=out_dtype, device=src.device)
     _native.hip().collate_hwc_to_chw(

@@ -34,6 +34,7 @@ Checkpoint: the same ``kind="indexed"`` record as the loader
 from __future__ import annotations
 
 import collections
+import contextlib
 import math
 import time
 from typing import Any, Iterator
@@ -238,7 +239,7 @@ class ResidentGlobalLoader:
             return {}
         c = self.sample_shape[0] if len(self.sample_shape) > 1 else len(norm.get("mean", [0]))
         plane = int(math.prod(self.sample_shape[1:])) if len(self.sample_shape) > 1 else 1
-        sc, bi = ops.kernels._norm_affine(c, norm.get("mean"), norm.get("std"), norm.get("scale"), norm.get("bias"))
+        sc, bi = ops.norm_affine(c, norm.get("mean"), norm.get("std"), norm.get("scale"), norm.get("bias"))
         return dict(scale=sc, bias=bi, plane=plane)
 
     def _to_dev(self, a: np.ndarray) -> torch.Tensor:
@@ -254,7 +255,7 @@ class ResidentGlobalLoader:
         e, g = divmod(t, self.order.batches_per_epoch)
         perm = self.order.perm(e)
         kw = self._norm_kw()
-        ctx = torch.cuda.stream(self.prep_stream) if self.prep_stream is not None else _nullctx()
+        ctx = torch.cuda.stream(self.prep_stream) if self.prep_stream is not None else contextlib.nullcontext()
         with ctx, trace_range("ddl.resident.assemble"):
             if self.W == 1:
                 batch = ops.gather_rows(self.shard, perm=perm, base=g * self.GB, n_rows=self.LB,
@@ -356,10 +357,3 @@ class ResidentGlobalLoader:
         self._queue.clear()
         logger.debug("resident loader closed: %s", self.stats())
 
-
-class _nullctx:
-    def __enter__(self):
-        return self
-
-    def __exit__(self, *a):
-        return False

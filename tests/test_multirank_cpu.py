@@ -111,3 +111,20 @@ def test_global_shuffle_exchange_conserves_rows(method, world):
                 assert foreign == n_ex - n_ex // world  # chunk for self stays
             else:
                 assert foreign == n_ex
+
+
+def test_npy_memmap_source_indexed(tmp_path):
+    import ddl_amd
+    from ddl_amd.models import IndexedProducer, NpyMemmapSource
+    from ddl_amd.permutation import EpochOrder
+
+    arr = np.stack([np.arange(500), np.arange(500) * 2], 1).astype(np.int32)
+    path = tmp_path / "data.npy"
+    np.save(path, arr)
+    src = NpyMemmapSource(str(path))
+    with ddl_amd.start(n_producers=2) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(IndexedProducer(src, 50, seed=2), 50, conn, 1, mode="indexed",
+                                           env=env, auto_mark=True)
+        got = torch.cat([b[0] for b in dl]).numpy()
+    ref = EpochOrder(500, 50, 2).perm(0).full()
+    assert np.array_equal(got[:, 0], ref) and np.array_equal(got[:, 1], ref * 2)
