@@ -13,8 +13,10 @@ namespace ddl {
 // permute.hip ---------------------------------------------------------------
 // dst[r, :] = cast(src[source_row(ri, r), :]) (scatter=0)
 // dst[source_row(ri, r), :] = src[r, :]       (scatter=1, same dtype only)
+// max_blocks > 0 caps the grid (grid-stride over tiles), e.g. to keep a
+// zero-copy gather out of pinned host memory on a few CUs.
 int gather_rows(void* dst, int32_t out_dt, const void* src, int32_t in_dt, int64_t n_rows, int64_t row_elems,
-                const RowIndex& ri, const Affine& aff, int scatter, hipStream_t st);
+                const RowIndex& ri, const Affine& aff, int scatter, int64_t max_blocks, hipStream_t st);
 // out[i] = feistel_perm(base + i), i < count
 int feistel_indices(int64_t* out, int64_t count, int64_t base, const FeistelKeys& keys, hipStream_t st);
 

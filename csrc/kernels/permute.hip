@@ -29,9 +29,12 @@ template <typename U>
 __global__ void __launch_bounds__(kThreads) move_rows_chunked(uint8_t* __restrict__ dst,
                                                               const uint8_t* __restrict__ src,
                                                               int64_t units_per_row, int64_t chunks_per_row,
-                                                              RowIndex ri, int scatter) {
-  const int64_t row = blockIdx.x / chunks_per_row;
-  const int64_t chunk = blockIdx.x % chunks_per_row;
+                                                              int64_t n_tiles, RowIndex ri, int scatter) {
+  // Grid-stride over (row, chunk) tiles: normally one tile per workgroup; a capped
+  // grid (zero-copy host gathers) keeps the PCIe-latency-bound kernel on few CUs.
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+  const int64_t row = tile / chunks_per_row;
+  const int64_t chunk = tile % chunks_per_row;
   const int64_t mapped = source_row(ri, row);
   const int64_t srow = scatter ? row : mapped;
   const int64_t drow = scatter ? mapped : row;
@@ -48,6 +51,7 @@ __global__ void __launch_bounds__(kThreads) move_rows_chunked(uint8_t* __restric
   for (int k = 0; k < kUnroll; ++k) {
     const int64_t u = u0 + k * kThreads;
     if (u < units_per_row) d[u] = v[k];
+  }
   }
 }
 
@@ -170,10 +174,11 @@ __device__ __forceinline__ void apply_affine(const Affine& a, int64_t elem, floa
 
 template <typename Tin, typename Tout>
 __global__ void __launch_bounds__(kThreads) convert_rows_chunked(Tout* __restrict__ dst, const Tin* __restrict__ src,
-                                                                 int64_t row_elems, int64_t chunks_per_row, RowIndex ri,
-                                                                 Affine aff) {
-  const int64_t row = blockIdx.x / chunks_per_row;
-  const int64_t chunk = blockIdx.x % chunks_per_row;
+                                                                 int64_t row_elems, int64_t chunks_per_row,
+                                                                 int64_t n_tiles, RowIndex ri, Affine aff) {
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+  const int64_t row = tile / chunks_per_row;
+  const int64_t chunk = tile % chunks_per_row;
   const int64_t srow = source_row(ri, row);
   const Tin* s = src + srow * row_elems;
   Tout* d = dst + row * row_elems;
@@ -192,16 +197,19 @@ __global__ void __launch_bounds__(kThreads) convert_rows_chunked(Tout* __restric
       Elem<Tout>::store8(d + e, f[k]);
     }
   }
+  }
 }
 
 // uint8 sources: 16 elements per lane per access (16 B loads, 2 x 16 B bf16 stores).
 template <typename Tout>
 __global__ void __launch_bounds__(kThreads) convert_u8_rows_chunked(Tout* __restrict__ dst,
                                                                     const uint8_t* __restrict__ src, int64_t row_elems,
-                                                                    int64_t chunks_per_row, RowIndex ri, Affine aff) {
+                                                                    int64_t chunks_per_row, int64_t n_tiles, RowIndex ri,
+                                                                    Affine aff) {
   constexpr int kU = 2;
-  const int64_t row = blockIdx.x / chunks_per_row;
-  const int64_t chunk = blockIdx.x % chunks_per_row;
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+  const int64_t row = tile / chunks_per_row;
+  const int64_t chunk = tile % chunks_per_row;
   const int64_t srow = source_row(ri, row);
   const uint8_t* s = src + srow * row_elems;
   Tout* d = dst + row * row_elems;
@@ -221,6 +229,7 @@ __global__ void __launch_bounds__(kThreads) convert_u8_rows_chunked(Tout* __rest
       Elem<Tout>::store8(d + e, lo[k]);
       Elem<Tout>::store8(d + e + 8, hi[k]);
     }
+  }
   }
 }
 
@@ -245,16 +254,27 @@ int flat_grid(int64_t work) {
   return static_cast<int>(blocks < 4096 ? (blocks < 1 ? 1 : blocks) : 4096);
 }
 
+dim3 tile_grid(int64_t n_tiles, int64_t max_blocks) {
+  const int64_t g = (max_blocks > 0 && max_blocks < n_tiles) ? max_blocks : n_tiles;
+  return dim3(static_cast<uint32_t>(g));
+}
+
+int flat_grid_capped(int64_t work, int64_t max_blocks) {
+  const int g = flat_grid(work);
+  return (max_blocks > 0 && max_blocks < g) ? static_cast<int>(max_blocks) : g;
+}
+
 template <typename U>
 void launch_move(void* dst, const void* src, int64_t n_rows, int64_t row_bytes, const RowIndex& ri, int scatter,
-                 hipStream_t st) {
+                 int64_t max_blocks, hipStream_t st) {
   const int64_t units = row_bytes / static_cast<int64_t>(sizeof(U));
   if (units >= kThreads) {
     const int64_t chunks = (units + kThreads * kUnroll - 1) / (kThreads * kUnroll);
-    hipLaunchKernelGGL(move_rows_chunked<U>, dim3(static_cast<uint32_t>(n_rows * chunks)), dim3(kThreads), 0, st,
-                       static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), units, chunks, ri, scatter);
+    hipLaunchKernelGGL(move_rows_chunked<U>, tile_grid(n_rows * chunks, max_blocks), dim3(kThreads), 0, st,
+                       static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), units, chunks, n_rows * chunks,
+                       ri, scatter);
   } else {
-    hipLaunchKernelGGL(move_rows_flat<U>, dim3(flat_grid(n_rows * units)), dim3(kThreads), 0, st,
+    hipLaunchKernelGGL(move_rows_flat<U>, dim3(flat_grid_capped(n_rows * units, max_blocks)), dim3(kThreads), 0, st,
                        static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), units, n_rows * units, ri,
                        scatter);
   }
@@ -262,33 +282,35 @@ void launch_move(void* dst, const void* src, int64_t n_rows, int64_t row_bytes, 
 
 template <typename Tin, typename Tout>
 void launch_convert(void* dst, const void* src, int64_t n_rows, int64_t row_elems, const RowIndex& ri, const Affine& aff,
-                    bool vec_ok, hipStream_t st) {
+                    bool vec_ok, int64_t max_blocks, hipStream_t st) {
   if constexpr (sizeof(Tin) == 1) {
     if (vec_ok && row_elems % 16 == 0 && row_elems >= kThreads * 16) {
       const int64_t chunks = (row_elems + kThreads * 2 * 16 - 1) / (kThreads * 2 * 16);
-      hipLaunchKernelGGL((convert_u8_rows_chunked<Tout>), dim3(static_cast<uint32_t>(n_rows * chunks)),
-                         dim3(kThreads), 0, st, static_cast<Tout*>(dst), static_cast<const uint8_t*>(src), row_elems,
-                         chunks, ri, aff);
+      hipLaunchKernelGGL((convert_u8_rows_chunked<Tout>), tile_grid(n_rows * chunks, max_blocks), dim3(kThreads), 0,
+                         st, static_cast<Tout*>(dst), static_cast<const uint8_t*>(src), row_elems, chunks,
+                         n_rows * chunks, ri, aff);
       return;
     }
   }
   if (vec_ok && row_elems >= kThreads * 8) {
     const int64_t chunks = (row_elems + kThreads * kUnroll * 8 - 1) / (kThreads * kUnroll * 8);
-    hipLaunchKernelGGL((convert_rows_chunked<Tin, Tout>), dim3(static_cast<uint32_t>(n_rows * chunks)), dim3(kThreads),
-                       0, st, static_cast<Tout*>(dst), static_cast<const Tin*>(src), row_elems, chunks, ri, aff);
+    hipLaunchKernelGGL((convert_rows_chunked<Tin, Tout>), tile_grid(n_rows * chunks, max_blocks), dim3(kThreads), 0,
+                       st, static_cast<Tout*>(dst), static_cast<const Tin*>(src), row_elems, chunks, n_rows * chunks,
+                       ri, aff);
   } else {
-    hipLaunchKernelGGL((convert_rows_flat<Tin, Tout>), dim3(flat_grid(n_rows * row_elems)), dim3(kThreads), 0, st,
+    hipLaunchKernelGGL((convert_rows_flat<Tin, Tout>), dim3(flat_grid_capped(n_rows * row_elems, max_blocks)),
+                       dim3(kThreads), 0, st,
                        static_cast<Tout*>(dst), static_cast<const Tin*>(src), row_elems, n_rows * row_elems, ri, aff);
   }
 }
 
 template <typename Tin>
 int dispatch_out(int32_t out_dt, void* dst, const void* src, int64_t n_rows, int64_t row_elems, const RowIndex& ri,
-                 const Affine& aff, bool vec_ok, hipStream_t st) {
+                 const Affine& aff, bool vec_ok, int64_t mb, hipStream_t st) {
   switch (out_dt) {
-    case kBF16: launch_convert<Tin, BF16Tag>(dst, src, n_rows, row_elems, ri, aff, vec_ok, st); return 0;
-    case kF16: launch_convert<Tin, F16Tag>(dst, src, n_rows, row_elems, ri, aff, vec_ok, st); return 0;
-    case kF32: launch_convert<Tin, float>(dst, src, n_rows, row_elems, ri, aff, vec_ok, st); return 0;
+    case kBF16: launch_convert<Tin, BF16Tag>(dst, src, n_rows, row_elems, ri, aff, vec_ok, mb, st); return 0;
+    case kF16: launch_convert<Tin, F16Tag>(dst, src, n_rows, row_elems, ri, aff, vec_ok, mb, st); return 0;
+    case kF32: launch_convert<Tin, float>(dst, src, n_rows, row_elems, ri, aff, vec_ok, mb, st); return 0;
   }
   return -1;
 }
@@ -303,18 +325,18 @@ __global__ void __launch_bounds__(kThreads) feistel_fill(int64_t* __restrict__ o
 }  // namespace
 
 int gather_rows(void* dst, int32_t out_dt, const void* src, int32_t in_dt, int64_t n_rows, int64_t row_elems,
-                const RowIndex& ri, const Affine& aff, int scatter, hipStream_t st) {
+                const RowIndex& ri, const Affine& aff, int scatter, int64_t max_blocks, hipStream_t st) {
   if (n_rows <= 0 || row_elems <= 0) return 0;
   const bool same = (out_dt == in_dt) && !aff.enabled;
   if (same) {
     const int64_t row_bytes = row_elems * dtype_size(in_dt);
     const uintptr_t align = reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src);
     if (row_bytes % 16 == 0 && align % 16 == 0)
-      launch_move<u32x4>(dst, src, n_rows, row_bytes, ri, scatter, st);
+      launch_move<u32x4>(dst, src, n_rows, row_bytes, ri, scatter, max_blocks, st);
     else if (row_bytes % 4 == 0 && align % 4 == 0)
-      launch_move<uint32_t>(dst, src, n_rows, row_bytes, ri, scatter, st);
+      launch_move<uint32_t>(dst, src, n_rows, row_bytes, ri, scatter, max_blocks, st);
     else
-      launch_move<uint8_t>(dst, src, n_rows, row_bytes, ri, scatter, st);
+      launch_move<uint8_t>(dst, src, n_rows, row_bytes, ri, scatter, max_blocks, st);
     return static_cast<int>(hipGetLastError());
   }
   if (scatter) return -2;  // converting scatters are not needed by the loader
@@ -323,10 +345,10 @@ int gather_rows(void* dst, int32_t out_dt, const void* src, int32_t in_dt, int64
   if (aff.enabled && (aff.plane % 8 != 0)) vec_ok = false;
   int rc = -1;
   switch (in_dt) {
-    case kU8: rc = dispatch_out<uint8_t>(out_dt, dst, src, n_rows, row_elems, ri, aff, vec_ok, st); break;
-    case kF32: rc = dispatch_out<float>(out_dt, dst, src, n_rows, row_elems, ri, aff, vec_ok, st); break;
-    case kBF16: rc = dispatch_out<BF16Tag>(out_dt, dst, src, n_rows, row_elems, ri, aff, vec_ok, st); break;
-    case kF16: rc = dispatch_out<F16Tag>(out_dt, dst, src, n_rows, row_elems, ri, aff, vec_ok, st); break;
+    case kU8: rc = dispatch_out<uint8_t>(out_dt, dst, src, n_rows, row_elems, ri, aff, vec_ok, max_blocks, st); break;
+    case kF32: rc = dispatch_out<float>(out_dt, dst, src, n_rows, row_elems, ri, aff, vec_ok, max_blocks, st); break;
+    case kBF16: rc = dispatch_out<BF16Tag>(out_dt, dst, src, n_rows, row_elems, ri, aff, vec_ok, max_blocks, st); break;
+    case kF16: rc = dispatch_out<F16Tag>(out_dt, dst, src, n_rows, row_elems, ri, aff, vec_ok, max_blocks, st); break;
   }
   if (rc != 0) return -3;
   return static_cast<int>(hipGetLastError());

@@ -146,8 +146,14 @@ def ref_gather_rows(src, index=None, perm=None, base=0, n_rows=None, out_dtype=N
 
 def gather_rows(src, index: torch.Tensor | None = None, *, perm: FeistelPermutation | None = None, base: int = 0,
                 n_rows: int | None = None, out: torch.Tensor | None = None, out_dtype=None, scale=None, bias=None,
-                plane: int | None = None, stream=None) -> torch.Tensor:
-    """out[r] = cast(affine(src[row(r)])): fused permute + cast + per-channel normalise."""
+                plane: int | None = None, stream=None, max_blocks: int = 0) -> torch.Tensor:
+    """out[r] = cast(affine(src[row(r)])): fused permute + cast + per-channel normalise.
+
+    ``max_blocks`` > 0 caps the grid (the kernel grid-strides over row tiles):
+    a zero-copy gather out of pinned host memory is PCIe-latency-bound and
+    saturates the link with a few dozen workgroups, leaving the other CUs to
+    the training step.
+    """
     if out_dtype is not None:
         out_dtype = _dtypes.to_torch_dtype(out_dtype)
     else:
@@ -177,7 +183,7 @@ def gather_rows(src, index: torch.Tensor | None = None, *, perm: FeistelPermutat
     _native.hip().gather_rows(
         dst=out.data_ptr(), out_dt=_dtypes.code(out_dtype), src=_src_addr(src), in_dt=_dtypes.code(src.dtype),
         n_rows=n_rows, row_elems=row_elems, scale=sc, bias=bi, plane=int(plane or 0), scatter=False,
-        stream=_stream_handle(stream), **_index_kw(index, perm, base))
+        stream=_stream_handle(stream), max_blocks=int(max_blocks), **_index_kw(index, perm, base))
     return out
 
 

@@ -72,7 +72,110 @@ def _source_geometry(source) -> tuple[tuple[int, ...], torch.dtype]:
     return tuple(source.sample_shape), _dtypes.to_torch_dtype(source.dtype)
 
 
-class ResidentGlobalLoader:
+class PrefetchedIndexedLoader:
+    """Shared machinery of the device-assembled indexed loaders.
+
+    Subclasses implement ``_assemble(t) -> (batch, ready_event)`` for global step
+    ``t = epoch * batches_per_epoch + g``; this class runs it ``depth`` steps ahead
+    (on the subclass's prep stream), hands each batch to the caller's stream with
+    ``wait_event`` + ``record_stream`` (no host sync) and owns the
+    ``kind="indexed"`` checkpoint cursor.
+    """
+
+    def _init_cursor(self, seed: int, depth: int, n_epochs: int | None, resume_state: dict | None) -> None:
+        self.seed = int(seed)
+        self.depth = max(1, int(depth))
+        self.n_epochs = n_epochs
+        self.epoch, self.cursor = 0, 0
+        if resume_state is not None:
+            self._apply_state(resume_state)
+        self._pending = False
+        self._queue: collections.deque = collections.deque()
+        self._next_t = None
+        self.batches = 0
+
+    def __len__(self) -> int:
+        """Batches left in the current epoch."""
+        return self.order.batches_per_epoch - self.cursor
+
+    @property
+    def batches_per_epoch(self) -> int:
+        return self.order.batches_per_epoch
+
+    def _norm_kw(self) -> dict:
+        norm = self.normalize
+        if norm is None:
+            return {}
+        c = self.sample_shape[0] if len(self.sample_shape) > 1 else len(norm.get("mean", [0]))
+        plane = int(math.prod(self.sample_shape[1:])) if len(self.sample_shape) > 1 else 1
+        sc, bi = ops.norm_affine(c, norm.get("mean"), norm.get("std"), norm.get("scale"), norm.get("bias"))
+        return dict(scale=sc, bias=bi, plane=plane)
+
+    def _total_steps(self) -> int | None:
+        return None if self.n_epochs is None else self.n_epochs * self.order.batches_per_epoch
+
+    def _fill(self, upto: int) -> None:
+        total = self._total_steps()
+        while self._next_t < upto and (total is None or self._next_t < total):
+            self._queue.append((self._next_t,) + self._assemble(self._next_t))
+            self._next_t += 1
+
+    def __iter__(self) -> Iterator[torch.Tensor]:
+        """One epoch of batches ([LB, *sample_shape] in ``out_dtype``)."""
+        bpe = self.order.batches_per_epoch
+        if self.n_epochs is not None and self.epoch >= self.n_epochs:
+            return
+        t0 = self.epoch * bpe + self.cursor
+        if self._next_t is None:
+            self._next_t = t0
+        for t in range(t0, (self.epoch + 1) * bpe):
+            self._fill(t + self.depth)
+            tq, batch, ev = self._queue.popleft()
+            assert tq == t, (tq, t)
+            if ev is not None:
+                cur = torch.cuda.current_stream(self.device)
+                cur.wait_event(ev)
+                batch.record_stream(cur)
+            self.cursor = t - self.epoch * bpe
+            self._pending = True
+            self.batches += 1
+            yield batch
+            self._pending = False
+            self.cursor += 1
+        self.epoch += 1
+        self.cursor = 0
+
+    # ----------------------------------------------------------- checkpoint
+    def state_dict(self) -> dict:
+        return {
+            "version": STATE_VERSION,
+            "kind": "indexed",
+            "seed": self.seed,
+            "order_seed": self.seed,
+            "epoch": self.epoch,
+            "global_batch_cursor": self.cursor + (1 if self._pending else 0),
+            "batches_per_epoch": self.order.batches_per_epoch,
+            "global_batch": self.order.global_batch,
+            "n_samples": self.order.n_samples,
+            "world_size": getattr(self, "W", 1),
+            "dtype": str(self.out_dtype).replace("torch.", ""),
+        }
+
+    def _apply_state(self, sd: dict) -> None:
+        if sd.get("kind") != "indexed" or sd.get("version") != STATE_VERSION:
+            raise ValueError("not an indexed loader state")
+        for key, mine in (("global_batch", self.order.global_batch), ("n_samples", self.order.n_samples),
+                          ("order_seed", self.seed)):
+            if sd.get(key) is not None and sd[key] != mine:
+                raise ValueError(f"checkpoint {key}={sd[key]} does not match {mine}")
+        self.epoch = int(sd["epoch"])
+        self.cursor = int(sd["global_batch_cursor"])
+        if self.cursor >= self.order.batches_per_epoch:
+            self.epoch, self.cursor = self.epoch + 1, 0
+
+
+
+class ResidentGlobalLoader(PrefetchedIndexedLoader):
     def __init__(self, source, global_batch: int, env: DDLEnv | None = None, *, seed: int = 0,
                  drop_last: bool = True, out_dtype: Any = None, normalize: dict | None = None, depth: int = 2,
                  device: str | torch.device | None = None, n_epochs: int | None = None,
@@ -102,7 +205,6 @@ class ResidentGlobalLoader:
         self.order = EpochOrder(n, global_batch, seed, drop_last)
         self.GB = int(global_batch)
         self.LB = self.order.local_batch(self.W)
-        self.seed = int(seed)
         self.S = -(-n // self.W)
         self.lo = self.rank * self.S
         self.hi = min(n, self.lo + self.S)
@@ -113,18 +215,12 @@ class ResidentGlobalLoader:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self.out_dtype = _dtypes.to_torch_dtype(out_dtype) if out_dtype is not None else self.src_dtype
         self.normalize = normalize
-        self.depth = max(1, int(depth))
-        self.n_epochs = n_epochs
-        self.epoch, self.cursor = 0, 0
-        if resume_state is not None:
-            self._apply_state(resume_state)
-        self._pending = False
+        self._init_cursor(seed, depth, n_epochs, resume_state)
         self.group = None
         if self.W > 1:
             backend = "nccl" if self.device.type == "cuda" else "gloo"
             self.group = dist.new_group(backend=backend)
         self.bytes_exchanged = 0
-        self.batches = 0
         t0 = time.perf_counter()
         if scatter_from is not None and self.W > 1:
             self.shard = self._scatter_shards(src_addr, chunk_bytes, host_threads, scatter_from)
@@ -132,8 +228,6 @@ class ResidentGlobalLoader:
             self.shard = self._load_shard(src_addr, chunk_bytes, host_threads)
         self.load_s = time.perf_counter() - t0
         self.prep_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
-        self._queue: collections.deque = collections.deque()
-        self._next_t = None
 
     # ----------------------------------------------------------------- load
     def _load_shard(self, src_addr: int, chunk_bytes: int, host_threads: int) -> torch.Tensor:
@@ -224,24 +318,6 @@ class ResidentGlobalLoader:
             torch.cuda.synchronize(self.device)
         return shard
 
-    # ------------------------------------------------------------- assembly
-    def __len__(self) -> int:
-        """Batches left in the current epoch."""
-        return self.order.batches_per_epoch - self.cursor
-
-    @property
-    def batches_per_epoch(self) -> int:
-        return self.order.batches_per_epoch
-
-    def _norm_kw(self) -> dict:
-        norm = self.normalize
-        if norm is None:
-            return {}
-        c = self.sample_shape[0] if len(self.sample_shape) > 1 else len(norm.get("mean", [0]))
-        plane = int(math.prod(self.sample_shape[1:])) if len(self.sample_shape) > 1 else 1
-        sc, bi = ops.norm_affine(c, norm.get("mean"), norm.get("std"), norm.get("scale"), norm.get("bias"))
-        return dict(scale=sc, bias=bi, plane=plane)
-
     def _to_dev(self, a: np.ndarray) -> torch.Tensor:
         t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.int64))
         if self.device.type == "cuda":
@@ -285,67 +361,6 @@ class ResidentGlobalLoader:
                 ev = torch.cuda.Event()
                 ev.record(self.prep_stream)
         return batch, ev
-
-    def _total_steps(self) -> int | None:
-        return None if self.n_epochs is None else self.n_epochs * self.order.batches_per_epoch
-
-    def _fill(self, upto: int) -> None:
-        total = self._total_steps()
-        while self._next_t < upto and (total is None or self._next_t < total):
-            self._queue.append((self._next_t,) + self._assemble(self._next_t))
-            self._next_t += 1
-
-    def __iter__(self) -> Iterator[torch.Tensor]:
-        """One epoch of batches ([LB, *sample_shape] in ``out_dtype``)."""
-        bpe = self.order.batches_per_epoch
-        if self.n_epochs is not None and self.epoch >= self.n_epochs:
-            return
-        t0 = self.epoch * bpe + self.cursor
-        if self._next_t is None:
-            self._next_t = t0
-        for t in range(t0, (self.epoch + 1) * bpe):
-            self._fill(t + self.depth)
-            tq, batch, ev = self._queue.popleft()
-            assert tq == t, (tq, t)
-            if ev is not None:
-                cur = torch.cuda.current_stream(self.device)
-                cur.wait_event(ev)
-                batch.record_stream(cur)
-            self.cursor = t - self.epoch * bpe
-            self._pending = True
-            self.batches += 1
-            yield batch
-            self._pending = False
-            self.cursor += 1
-        self.epoch += 1
-        self.cursor = 0
-
-    # ----------------------------------------------------------- checkpoint
-    def state_dict(self) -> dict:
-        return {
-            "version": STATE_VERSION,
-            "kind": "indexed",
-            "seed": self.seed,
-            "order_seed": self.seed,
-            "epoch": self.epoch,
-            "global_batch_cursor": self.cursor + (1 if self._pending else 0),
-            "batches_per_epoch": self.order.batches_per_epoch,
-            "global_batch": self.GB,
-            "n_samples": self.N,
-            "world_size": self.W,
-            "dtype": str(self.out_dtype).replace("torch.", ""),
-        }
-
-    def _apply_state(self, sd: dict) -> None:
-        if sd.get("kind") != "indexed" or sd.get("version") != STATE_VERSION:
-            raise ValueError("not an indexed loader state")
-        for key, mine in (("global_batch", self.GB), ("n_samples", self.N), ("order_seed", self.seed)):
-            if sd.get(key) is not None and sd[key] != mine:
-                raise ValueError(f"checkpoint {key}={sd[key]} does not match {mine}")
-        self.epoch = int(sd["epoch"])
-        self.cursor = int(sd["global_batch_cursor"])
-        if self.cursor >= self.order.batches_per_epoch:
-            self.epoch, self.cursor = self.epoch + 1, 0
 
     def stats(self) -> dict:
         return {"batches": self.batches, "bytes_exchanged": self.bytes_exchanged, "shard_rows": self.hi - self.lo,

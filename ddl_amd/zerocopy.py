@@ -1,0 +1,120 @@
+"""Producer-free zero-copy loader: a gfx950 kernel gathers each batch straight out
+of pinned, device-mapped host memory over PCIe.
+
+The window/indexed loaders move data host->HBM with SDMA copies of buffers
+that host producers assembled (a host memcpy per sample). For a dataset that
+already sits in host memory (node-shared shm, an ``.npy`` memmap in the page
+cache, a pinned tensor), there is a shorter MI355X path:
+
+* the whole source is registered once with ``hipHostRegister(..., Mapped)``;
+* per step, ONE ``gather_rows`` kernel evaluates the world-size-invariant
+  Feistel permutation inline, reads this rank's samples directly over PCIe
+  (16 B/lane loads of the mapped host pages) and writes the bf16 batch --
+  fused with the dtype cast / per-channel normalisation -- into HBM;
+* no producer processes, no host memcpy, no staging buffers, no per-sample
+  host work at all;
+* the kernel is PCIe-latency-bound, not CU-bound: ~2 us x ~55 GB/s is ~110 KB
+  in flight, i.e. a few dozen waves. ``max_blocks`` caps its grid
+  (grid-stride over row tiles) so it occupies a handful of CUs and the
+  training step keeps the rest; it runs ``depth`` steps ahead on its own
+  stream.
+
+Same order and checkpoint format as ``IndexedProducer`` / ``ResidentGlobalLoader``
+(``kind="indexed"``), so runs can switch between the three paths on resume.
+"""
+
+from __future__ import annotations
+
+from typing import Any
+
+import torch
+
+from . import _native, ops
+from .ops import _dtypes
+from .permutation import EpochOrder
+from .resident import PrefetchedIndexedLoader, _source_address, _source_geometry
+from .types import DDLEnv
+
+_PAGE = 4096
+
+
+def _cpu_view(source, n: int, shape, dtype) -> torch.Tensor:
+    if isinstance(source, torch.Tensor):
+        return source
+    if hasattr(source, "tensor"):
+        return source.tensor()
+    import numpy as np
+
+    a = source._a()
+    return torch.from_numpy(np.asarray(a)).view(dtype).view((n,) + tuple(shape))
+
+
+class ZeroCopyLoader(PrefetchedIndexedLoader):
+    def __init__(self, source, global_batch: int, env: DDLEnv | None = None, *, seed: int = 0,
+                 drop_last: bool = True, out_dtype: Any = None, normalize: dict | None = None, depth: int = 2,
+                 max_blocks: int = 64, device: str | torch.device | None = None, n_epochs: int | None = None,
+                 resume_state: dict | None = None):
+        self.env = env or DDLEnv()
+        self.W, self.rank = self.env.world_size, self.env.rank
+        self.sample_shape, self.src_dtype = _source_geometry(source)
+        addr, n = _source_address(source)
+        self.order = EpochOrder(n, global_batch, seed, drop_last)
+        self.GB, self.LB = int(global_batch), self.order.local_batch(self.W)
+        self.out_dtype = _dtypes.to_torch_dtype(out_dtype) if out_dtype is not None else self.src_dtype
+        self.normalize = normalize
+        self.max_blocks = int(max_blocks)
+        if device is None:
+            device = self.env.device if self.env.device != "cpu" or not torch.cuda.is_available() else "cuda"
+        self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self._init_cursor(seed, depth, n_epochs, resume_state)
+        self.cpu = _cpu_view(source, n, self.sample_shape, self.src_dtype)
+        self._source = source  # keep the mapping alive
+        row_bytes = self.cpu[0].numel() * self.cpu.element_size() if n else 0
+        self.nbytes = n * row_bytes
+        self._reg_base = None
+        self.prep_stream = None
+        if self.device.type == "cuda":
+            hip = _native.hip()
+            base = addr & ~(_PAGE - 1)
+            size = -(-(addr + self.nbytes - base) // _PAGE) * _PAGE
+            hip.host_register(base, size, True)
+            self._reg_base = base
+            dptr = hip.host_device_pointer(base) + (addr - base)
+            self.rows = ops.HostRows(self.cpu, dptr)
+            self.prep_stream = torch.cuda.Stream(self.device)
+        else:
+            self.rows = self.cpu
+
+    def _assemble(self, t: int):
+        e, g = divmod(t, self.order.batches_per_epoch)
+        kw = self._norm_kw()
+        base = g * self.GB + self.rank * self.LB
+        if self.prep_stream is None:
+            return ops.gather_rows(self.rows, perm=self.order.perm(e), base=base, n_rows=self.LB,
+                                   out_dtype=self.out_dtype, **kw), None
+        with torch.cuda.stream(self.prep_stream):
+            batch = ops.gather_rows(self.rows, perm=self.order.perm(e), base=base, n_rows=self.LB,
+                                    out_dtype=self.out_dtype, max_blocks=self.max_blocks, **kw)
+            ev = torch.cuda.Event()
+            ev.record(self.prep_stream)
+        return batch, ev
+
+    def stats(self) -> dict:
+        return {"batches": self.batches, "source_bytes": self.nbytes, "max_blocks": self.max_blocks}
+
+    def close(self) -> None:
+        if self.prep_stream is not None:
+            self.prep_stream.synchronize()
+        self._queue.clear()
+        if self._reg_base is not None:
+            torch.cuda.synchronize(self.device)
+            _native.hip().host_unregister(self._reg_base)
+            self._reg_base = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
