@@ -130,7 +130,10 @@ class DistributedDataLoader:
         self.target_rank = 1    # reference-compatible: producer of the current window, 1-based
 
         if device is None:
-            device = "cuda" if torch.cuda.is_available() else "cpu"
+            if env is not None and env.device:
+                device = env.device
+            else:
+                device = "cuda" if torch.cuda.is_available() else "cpu"
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())

@@ -70,15 +70,19 @@ def read_env(n_producers: int | None = None) -> DDLEnv:
     )
 
 
-def init_distributed(env: DDLEnv, backend: str | None = None, timeout_s: float = 600.0) -> DDLEnv:
+def init_distributed(env: DDLEnv, backend: str | None = None, timeout_s: float = 600.0,
+                     device: str | None = None) -> DDLEnv:
     """Create the DP (RCCL or gloo) group and a gloo control group; set the device.
 
-    Touches the GPU: call it only after producer workers have been spawned.
+    ``device="cpu"`` (or ``$DDL_DEVICE=cpu``) keeps the rank off the GPU even
+    when one is visible (CPU rehearsals of multi-rank runs). Touches the GPU
+    otherwise: call it only after producer workers have been spawned.
     """
     import torch
     import torch.distributed as dist
 
-    use_gpu = torch.cuda.is_available()
+    device = device or os.environ.get("DDL_DEVICE") or None
+    use_gpu = device != "cpu" and torch.cuda.is_available()
     if use_gpu:
         n_dev = torch.cuda.device_count()
         dev_index = env.local_rank % max(n_dev, 1)

@@ -66,7 +66,8 @@ def spawn_producers(env: DDLEnv, timeout_s: float = DEFAULT_TIMEOUT_S, env_overr
 
 @contextlib.contextmanager
 def start(n_producers: int | None = None, init_dist: bool = True, backend: str | None = None,
-          timeout_s: float = DEFAULT_TIMEOUT_S, env_overrides: dict | None = None) -> Iterator[tuple[DDLEnv, Connection | None]]:
+          timeout_s: float = DEFAULT_TIMEOUT_S, env_overrides: dict | None = None,
+          device: str | None = None) -> Iterator[tuple[DDLEnv, Connection | None]]:
     """Context-manager form of the launcher: ``with start() as (env, conn): ...``."""
     configure()
     env = read_env(n_producers)
@@ -80,7 +81,7 @@ def start(n_producers: int | None = None, init_dist: bool = True, backend: str |
             import torch.distributed as dist
 
             was = dist.is_available() and dist.is_initialized()
-            init_distributed(env, backend)
+            init_distributed(env, backend, device=device)
             created_pg = not was and env.world_size > 1
         yield env, conn
     finally:

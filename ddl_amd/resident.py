@@ -209,7 +209,7 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
         self.lo = self.rank * self.S
         self.hi = min(n, self.lo + self.S)
         if device is None:
-            device = self.env.device if self.env.device != "cpu" or not torch.cuda.is_available() else "cuda"
+            device = self.env.device or ("cuda" if torch.cuda.is_available() else "cpu")
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())

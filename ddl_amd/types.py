@@ -73,7 +73,7 @@ class DDLEnv:
     node_rank: int = 0
     n_producers: int = 0
     hostname: str = ""
-    device: str = "cpu"
+    device: str = ""  # set by init_distributed ("cuda:<i>" or "cpu"); "" = not chosen yet
     backend: str | None = None
     process_group: Any = None  # DP group (RCCL on GPU); None when world_size == 1
     control_group: Any = None  # gloo group for host-side control traffic

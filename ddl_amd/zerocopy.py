@@ -64,7 +64,7 @@ class ZeroCopyLoader(PrefetchedIndexedLoader):
         self.normalize = normalize
         self.max_blocks = int(max_blocks)
         if device is None:
-            device = self.env.device if self.env.device != "cpu" or not torch.cuda.is_available() else "cuda"
+            device = self.env.device or ("cuda" if torch.cuda.is_available() else "cpu")
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
@@ -77,11 +77,20 @@ class ZeroCopyLoader(PrefetchedIndexedLoader):
         self.prep_stream = None
         if self.device.type == "cuda":
             hip = _native.hip()
-            base = addr & ~(_PAGE - 1)
-            size = -(-(addr + self.nbytes - base) // _PAGE) * _PAGE
-            hip.host_register(base, size, True)
-            self._reg_base = base
-            dptr = hip.host_device_pointer(base) + (addr - base)
+            if isinstance(source, torch.Tensor):
+                # A heap tensor shares its edge pages with unrelated allocations: registering
+                # the page-rounded range would pin (and mark as registered) memory that other
+                # host buffers live in. Use a pinned copy instead (hipHostMalloc'd, mapped).
+                if not self.cpu.is_pinned():
+                    self.cpu = self.cpu.pin_memory()
+                dptr = hip.host_device_pointer(self.cpu.data_ptr())
+            else:
+                # shm segments / file mappings: the rounded range is the mapping itself
+                base = addr & ~(_PAGE - 1)
+                size = -(-(addr + self.nbytes - base) // _PAGE) * _PAGE
+                hip.host_register(base, size, True)
+                self._reg_base = base
+                dptr = hip.host_device_pointer(base) + (addr - base)
             self.rows = ops.HostRows(self.cpu, dptr)
             self.prep_stream = torch.cuda.Stream(self.device)
         else:

@@ -18,6 +18,8 @@ def free_port() -> int:
 
 
 def _rank_main(fn, rank, world, port, q, args, env):
+    # CPU multi-rank tests: several ranks on one box must not share (or fight over) a GPU
+    os.environ["DDL_DEVICE"] = "cpu"
     os.environ.update(env)
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
