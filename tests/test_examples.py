@@ -30,6 +30,7 @@ def test_example_single_rank():
 def test_example_two_ranks_torchrun():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
            "--master-port", str(free_port()), SCRIPT, "--epochs", "2", "--timesteps", "4"]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=_env())
+    # two ranks on one box: rehearse on CPU/gloo (RCCL refuses two ranks on one GPU)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=dict(_env(), DDL_DEVICE="cpu"))
     assert r.returncode == 0, r.stderr[-3000:]
     assert "epoch 2/2: 4 batches" in r.stdout  # 4*10052/2 rows per window // 4096
