@@ -17,6 +17,12 @@ from ddl_amd.models import PointwiseProducer
 from tests.helpers import FailingProducer, IdProducer
 
 
+@pytest.fixture(autouse=True)
+def _host_path(monkeypatch):
+    """These tests cover the host (CPU) data path even on a GPU box; the device path is test_loader_gpu.py."""
+    monkeypatch.setenv("DDL_DEVICE", "cpu")
+
+
 def _epochs(dl, n_epochs, collect=True):
     out = []
     for _ in range(n_epochs):
