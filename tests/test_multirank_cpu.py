@@ -125,6 +125,6 @@ def test_npy_memmap_source_indexed(tmp_path):
     with ddl_amd.start(n_producers=2) as (env, conn):
         dl = ddl_amd.DistributedDataLoader(IndexedProducer(src, 50, seed=2), 50, conn, 1, mode="indexed",
                                            env=env, auto_mark=True)
-        got = torch.cat([b[0] for b in dl]).numpy()
+        got = torch.cat([b[0].cpu() for b in dl]).numpy()
     ref = EpochOrder(500, 50, 2).perm(0).full()
     assert np.array_equal(got[:, 0], ref) and np.array_equal(got[:, 1], ref * 2)
