@@ -26,7 +26,8 @@ def _check_pad(batch, source, idx, seq_len):
 
 
 @pytest.mark.parametrize("mode", ["pad", "pack"])
-def test_token_batches_cpu(corpus, mode):
+def test_token_batches_cpu(corpus, mode, monkeypatch):
+    monkeypatch.setenv("DDL_DEVICE", "cpu")  # host collate path, even on a GPU box
     seq_len, gb = 256, 16
     order = EpochOrder(corpus.n, gb, 4)
     with ddl_amd.start(n_producers=2) as (env, conn):

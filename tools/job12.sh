@@ -1,2 +1,2 @@
 source tools/gpu_job.sh
-run 900 all_tests python -m pytest tests -q -x --deselect tests/test_sanitizers.py
+run 900 all_tests python -m pytest tests -q --deselect tests/test_sanitizers.py
