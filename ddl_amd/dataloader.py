@@ -141,6 +141,8 @@ class DistributedDataLoader:
 
         self._finalized = False
         self._stager = None
+        self._batch_stream = None
+        self._lookahead: dict = {}
         self._host_window: int | None = None  # host path: window currently held
         self._cur = None                      # device path: StagedWindow of the current window
 
@@ -212,6 +214,8 @@ class DistributedDataLoader:
             self._stager = WindowStager(connection, self._schedule, self.total_windows, self.prefetch_depth,
                                         self.device, max_bytes, post_copy=self._exchange_fn,
                                         timeout_s=self.timeout_s, first_window=self.window)
+            if self._produces_copy():
+                self._batch_stream = torch.cuda.Stream(self.device)
         self._update_len()
 
     # --------------------------------------------------------------- schedule
@@ -289,10 +293,44 @@ class DistributedDataLoader:
         if not 0 <= local < bpw:
             raise IndexError(f"batch {idx} is not in the current window (sequential access only across windows)")
         sw = self._window()
-        out = self._batch_from_window(sw, p, s, local)
+        if self._batch_stream is not None:
+            out = self._device_batch(sw, p, s, local, bpw)
+        else:
+            out = self._batch_from_window(sw, p, s, local)
         self.metrics.on_batch(self.batch_size)
         if self.debug_checksum:
             self.checksums.append(int(ops.checksum(out[0] if isinstance(out, tuple) else out).item()))
+        return out
+
+    # ---------------------------------------------------------- batch stream
+    def _produces_copy(self) -> bool:
+        """True when a batch is built by a kernel (not a zero-copy view of the window)."""
+        return (self.shuffle == "device" or self.out_dtype not in (None, self.window_dtype)
+                or self.normalize is not None or self.copy_batches or self.contiguous or self.collate is not None)
+
+    def _enqueue_batch(self, sw, p: int, s: int, local: int):
+        """Build batch ``local`` of window ``sw`` on the batch stream; returns (outputs, ready event)."""
+        bs = self._batch_stream
+        bs.wait_event(self._stager.ready_events[sw.buffer])
+        with torch.cuda.stream(bs):
+            out = self._batch_from_window(sw, p, s, local)
+            ev = torch.cuda.Event()
+            ev.record(bs)
+        return out, ev
+
+    def _device_batch(self, sw, p: int, s: int, local: int, bpw: int):
+        """Batch kernels run on their own stream one batch ahead of the consumer:
+        batch l+1's gather overlaps the training step on batch l, and the compute
+        stream only waits on an event (no host sync)."""
+        hit = self._lookahead.pop((self.window, local), None)
+        out, ev = hit if hit is not None else self._enqueue_batch(sw, p, s, local)
+        cur = torch.cuda.current_stream(self.device)
+        cur.wait_event(ev)
+        for t in (out.values() if isinstance(out, dict) else out):
+            if isinstance(t, torch.Tensor) and t.is_cuda:
+                t.record_stream(cur)
+        if local + 1 < bpw and (self.window, local + 1) not in self._lookahead:
+            self._lookahead[(self.window, local + 1)] = self._enqueue_batch(sw, p, s, local + 1)
         return out
 
     def _perm_for(self, p: int, seq: int) -> FeistelPermutation | None:
@@ -369,6 +407,11 @@ class DistributedDataLoader:
 
     def _release_window(self) -> None:
         if self._stager is not None:
+            if self._batch_stream is not None:
+                # batch kernels read the window too: the free event must follow them
+                for key in [k for k in self._lookahead if k[0] == self.window]:
+                    del self._lookahead[key]
+                torch.cuda.current_stream(self.device).wait_stream(self._batch_stream)
             self._stager.release(self.window)
             self._cur = None
         elif self._host_window == self.window:
@@ -509,6 +552,9 @@ class DistributedDataLoader:
         if self._finalized:
             return
         self._finalized = True
+        if self._batch_stream is not None:
+            self._lookahead.clear()
+            self._batch_stream.synchronize()
         if self.connection is not None:
             self.connection.shutdown_operation()
         if self._stager is not None:
