@@ -329,8 +329,15 @@ class DistributedDataLoader:
         for t in (out.values() if isinstance(out, dict) else out):
             if isinstance(t, torch.Tensor) and t.is_cuda:
                 t.record_stream(cur)
-        if local + 1 < bpw and (self.window, local + 1) not in self._lookahead:
-            self._lookahead[(self.window, local + 1)] = self._enqueue_batch(sw, p, s, local + 1)
+        if local + 1 < bpw:
+            if (self.window, local + 1) not in self._lookahead:
+                self._lookahead[(self.window, local + 1)] = self._enqueue_batch(sw, p, s, local + 1)
+        elif self.window_in_epoch + 1 < self.windows_per_epoch or self.epoch + 1 < self.n_epochs:
+            # last batch of this window: start the next window's first batch if it is already in HBM
+            nxt = self._stager.peek(self.window + 1)
+            if nxt is not None and (self.window + 1, 0) not in self._lookahead:
+                np_, ns = self._schedule(self.window + 1)
+                self._lookahead[(self.window + 1, 0)] = self._enqueue_batch(nxt, np_, ns, 0)
         return out
 
     def _perm_for(self, p: int, seq: int) -> FeistelPermutation | None:
@@ -409,7 +416,7 @@ class DistributedDataLoader:
         if self._stager is not None:
             if self._batch_stream is not None:
                 # batch kernels read the window too: the free event must follow them
-                for key in [k for k in self._lookahead if k[0] == self.window]:
+                for key in [k for k in self._lookahead if k[0] <= self.window]:
                     del self._lookahead[key]
                 torch.cuda.current_stream(self.device).wait_stream(self._batch_stream)
             self._stager.release(self.window)

@@ -151,6 +151,15 @@ class WindowStager:
         torch.cuda.current_stream(self.device).wait_event(self.ready_events[sw.buffer])
         return sw
 
+    def peek(self, w: int) -> StagedWindow | None:
+        """Window ``w`` if it is already staged AND its post-copy work (exchange) is
+        issued, else None -- never blocks, never issues collectives."""
+        with self._cv:
+            sw = self._staged.get(w)
+        if sw is None or (self.post_copy is not None and w not in self._posted):
+            return None
+        return sw
+
     def _post(self, w: int) -> None:
         if w in self._posted:
             return
