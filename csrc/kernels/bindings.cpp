@@ -235,6 +235,30 @@ PYBIND11_MODULE(_ddl_hip, m) {
       py::arg("n_values"), py::arg("mode"), py::arg("idx"), py::arg("base"), py::arg("keys"), py::arg("n_domain"),
       py::arg("half_bits"), py::arg("stream"));
   m.def(
+      "pack_columns",
+      [](std::vector<uintptr_t> srcs, std::vector<int> widths, int in_dt, uintptr_t dst, int out_dt, int64_t n_rows,
+         int64_t n_values, int mode, uintptr_t idx, int64_t base, std::vector<uint64_t> keys, uint64_t n_domain,
+         uint32_t half_bits, uintptr_t stream) {
+        if (srcs.size() != widths.size() || srcs.empty() || srcs.size() > 8)
+          throw std::invalid_argument("pack_columns: 1..8 groups");
+        ddl::SplitSpec sp{};
+        int64_t tot = 0;
+        for (size_t i = 0; i < srcs.size(); ++i) {
+          sp.dst[i] = as_ptr<void>(srcs[i]);
+          sp.width[i] = widths[i];
+          tot += widths[i];
+        }
+        if (tot != n_values) throw std::invalid_argument("pack_columns: widths must sum to n_values");
+        sp.n_groups = static_cast<int32_t>(srcs.size());
+        sp.out_dt = out_dt;
+        const ddl::RowIndex ri = make_index(mode, idx, base, keys, n_domain, half_bits);
+        check_rc(ddl::pack_columns(sp, as_ptr<void>(dst), in_dt, n_rows, n_values, ri, as_stream(stream)),
+                 "pack_columns");
+      },
+      py::arg("srcs"), py::arg("widths"), py::arg("in_dt"), py::arg("dst"), py::arg("out_dt"), py::arg("n_rows"),
+      py::arg("n_values"), py::arg("mode"), py::arg("idx"), py::arg("base"), py::arg("keys"), py::arg("n_domain"),
+      py::arg("half_bits"), py::arg("stream"));
+  m.def(
       "pad_pack_tokens",
       [](uintptr_t tokens, uintptr_t offsets, uintptr_t row_start, uintptr_t row_end, uintptr_t seg_offsets,
          int64_t n_seg, uintptr_t out_tokens, uintptr_t attn_mask, uintptr_t position_ids, bool pos_is_i64,

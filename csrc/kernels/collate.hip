@@ -231,6 +231,36 @@ __global__ void __launch_bounds__(kThreads) split_columns_raw_kernel(SplitSpec s
   }
 }
 
+// ------------------------------------------------------------------- pack ---
+// Inverse of split: k [n_src, w_g] groups -> one [n_rows, n_values] row block,
+// row r taking source row source_row(ri, r) of every group (gather + concat +
+// cast in one pass). Lane e covers output element e, so the (wide) output
+// write is coalesced; each group's reads are contiguous runs of w_g.
+template <typename Tin, int OUT>
+__global__ void __launch_bounds__(kThreads) pack_columns_kernel(SplitSpec spec, void* __restrict__ dst,
+                                                                int64_t n_rows, int64_t n_values, RowIndex ri) {
+  const int64_t total = n_rows * n_values;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  for (int64_t e = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; e < total; e += stride) {
+    const int64_t row = e / n_values;
+    int col = static_cast<int>(e - row * n_values);
+    int g = 0;
+    while (g < spec.n_groups - 1 && col >= spec.width[g]) {
+      col -= spec.width[g];
+      ++g;
+    }
+    const Tin* s = static_cast<const Tin*>(spec.dst[g]) + source_row(ri, row) * spec.width[g];
+    if constexpr (OUT == kBF16)
+      static_cast<uint16_t*>(dst)[e] = f32_to_bf16_bits(Px<Tin>::get(s, col));
+    else if constexpr (OUT == kF32)
+      static_cast<float*>(dst)[e] = Px<Tin>::get(s, col);
+    else
+      static_cast<Tin*>(dst)[e] = s[col];  // raw (same dtype)
+  }
+}
+
+constexpr int kRaw = -1;
+
 }  // namespace
 
 int collate_hwc_to_chw(void* dst, int32_t out_dt, const void* src, int32_t in_dt, int64_t batch, int64_t pixels,
@@ -285,6 +315,38 @@ int split_columns(const SplitSpec& spec, const void* src, int32_t in_dt, int64_t
     default: return -1;
   }
 #undef DDL_SPLIT
+  return static_cast<int>(hipGetLastError());
+}
+
+int pack_columns(const SplitSpec& spec, void* dst, int32_t in_dt, int64_t n_rows, int64_t n_values,
+                 const RowIndex& ri, hipStream_t st) {
+  if (n_rows <= 0) return 0;
+  if (spec.n_groups < 1 || spec.n_groups > 8) return -2;
+  const int64_t total = n_rows * n_values;
+  int64_t blocks = (total + kThreads - 1) / kThreads;
+  if (blocks > 8192) blocks = 8192;
+  const dim3 grid(static_cast<uint32_t>(blocks));
+#define DDL_PACK(TIN, OUT)                                                                                        \
+  hipLaunchKernelGGL((pack_columns_kernel<TIN, OUT>), grid, dim3(kThreads), 0, st, spec, dst, n_rows, n_values, ri)
+  if (spec.out_dt == in_dt) {
+    switch (dtype_size(in_dt)) {
+      case 1: DDL_PACK(uint8_t, kRaw); break;
+      case 2: DDL_PACK(uint16_t, kRaw); break;
+      case 4: DDL_PACK(uint32_t, kRaw); break;
+      case 8: DDL_PACK(uint64_t, kRaw); break;
+      default: return -1;
+    }
+    return static_cast<int>(hipGetLastError());
+  }
+  if (spec.out_dt != kBF16 && spec.out_dt != kF32) return -1;
+  const bool bf = spec.out_dt == kBF16;
+  switch (in_dt) {
+    case kF32: if (bf) DDL_PACK(float, kBF16); else DDL_PACK(float, kF32); break;
+    case kBF16: if (bf) DDL_PACK(uint16_t, kBF16); else DDL_PACK(uint16_t, kF32); break;
+    case kU8: if (bf) DDL_PACK(uint8_t, kBF16); else DDL_PACK(uint8_t, kF32); break;
+    default: return -1;
+  }
+#undef DDL_PACK
   return static_cast<int>(hipGetLastError());
 }
 

@@ -36,6 +36,10 @@ struct SplitSpec {
 };
 int split_columns(const SplitSpec& spec, const void* src, int32_t in_dt, int64_t n_rows, int64_t n_values,
                   const RowIndex& ri, hipStream_t st);
+// Inverse: spec.dst[g] are the SOURCE groups [*, width[g]] (dtype in_dt), dst is [n_rows, n_values] of
+// spec.out_dt; row r of dst is row source_row(ri, r) of every group.
+int pack_columns(const SplitSpec& spec, void* dst, int32_t in_dt, int64_t n_rows, int64_t n_values,
+                 const RowIndex& ri, hipStream_t st);
 
 // tokens.hip ----------------------------------------------------------------
 // Pad: row b takes tokens[offsets[b] : offsets[b+1]] (truncated to seq_len);

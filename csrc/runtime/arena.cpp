@@ -384,4 +384,32 @@ void parallel_copy(uint8_t* dst, const uint8_t* src, uint64_t bytes, int n_threa
   });
 }
 
+void pack_columns(uint8_t* dst, const std::vector<const uint8_t*>& srcs, const std::vector<uint64_t>& widths,
+                  uint64_t elem_bytes, uint64_t n, int n_threads) {
+  // Window fill of the reference harness (tests/run_ddl.py:156-159): k
+  // row-major [n, w_g] column groups -> one interleaved [n, sum w] window.
+  // Row-blocked so every task writes a contiguous ~1 MiB span of dst and
+  // streams each group's matching rows (k sequential read streams).
+  if (srcs.size() != widths.size()) throw std::invalid_argument("pack_columns: srcs/widths length mismatch");
+  uint64_t row = 0;
+  for (uint64_t w : widths) row += w;
+  const uint64_t row_bytes = row * elem_bytes;
+  if (n == 0 || row_bytes == 0) return;
+  const uint64_t rows_per_task = std::max<uint64_t>(64, (1ull << 20) / row_bytes);
+  const int tasks = static_cast<int>((n + rows_per_task - 1) / rows_per_task);
+  std::lock_guard<std::mutex> lk(g_pool_call_mu);
+  Pool::get().run(tasks, n_threads, [&](int t) {
+    const uint64_t b = static_cast<uint64_t>(t) * rows_per_task;
+    const uint64_t e = std::min(n, b + rows_per_task);
+    uint64_t col = 0;
+    for (size_t g = 0; g < srcs.size(); ++g) {
+      const uint64_t gb = widths[g] * elem_bytes;
+      const uint8_t* s = srcs[g] + b * gb;
+      uint8_t* d = dst + b * row_bytes + col;
+      for (uint64_t i = b; i < e; ++i, s += gb, d += row_bytes) std::memcpy(d, s, gb);
+      col += gb;
+    }
+  });
+}
+
 }  // namespace ddl

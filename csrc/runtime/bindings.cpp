@@ -195,4 +195,16 @@ PYBIND11_MODULE(_ddl_runtime, m) {
                            bytes, n_threads);
       },
       py::arg("dst"), py::arg("src"), py::arg("bytes"), py::arg("n_threads") = 4);
+  m.def(
+      "pack_columns",
+      [](uintptr_t dst, std::vector<uintptr_t> srcs, std::vector<uint64_t> widths, uint64_t elem_bytes, uint64_t n,
+         int n_threads) {
+        std::vector<const uint8_t*> ptrs;
+        ptrs.reserve(srcs.size());
+        for (uintptr_t a : srcs) ptrs.push_back(reinterpret_cast<const uint8_t*>(a));
+        py::gil_scoped_release nogil;
+        ddl::pack_columns(reinterpret_cast<uint8_t*>(dst), ptrs, widths, elem_bytes, n, n_threads);
+      },
+      py::arg("dst"), py::arg("srcs"), py::arg("widths"), py::arg("elem_bytes"), py::arg("n"),
+      py::arg("n_threads") = 4, "k [n, w_g] column groups -> interleaved [n, sum w] (host window fill)");
 }

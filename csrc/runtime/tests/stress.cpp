@@ -63,6 +63,17 @@ int main(int argc, char** argv) {
       gather_rows(dst.data(), src.data(), 300, idx.data(), idx.size(), 64, 3);
       for (size_t i = 0; i < idx.size(); ++i)
         if (std::memcmp(&dst[i * 300], &src[idx[i] * 300], 300) != 0) errors++;
+      // pack 3 column groups (widths 3,5,1 floats as bytes x4) of 700 rows, row-blocked over the pool
+      const uint64_t pn = 700;
+      std::vector<uint8_t> ga(pn * 12), gb(pn * 20), gc(pn * 4), packed(pn * 36);
+      for (uint64_t i = 0; i < ga.size(); ++i) ga[i] = static_cast<uint8_t>(i + it);
+      for (uint64_t i = 0; i < gb.size(); ++i) gb[i] = static_cast<uint8_t>(i * 3 + it);
+      for (uint64_t i = 0; i < gc.size(); ++i) gc[i] = static_cast<uint8_t>(i * 5 + it);
+      pack_columns(packed.data(), {ga.data(), gb.data(), gc.data()}, {3, 5, 1}, 4, pn, 3);
+      for (uint64_t r = 0; r < pn; ++r)
+        if (std::memcmp(&packed[r * 36], &ga[r * 12], 12) || std::memcmp(&packed[r * 36 + 12], &gb[r * 20], 20) ||
+            std::memcmp(&packed[r * 36 + 32], &gc[r * 4], 4))
+          errors++;
       ++it;
     }
   });

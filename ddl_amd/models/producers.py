@@ -21,6 +21,7 @@ from typing import Any
 import numpy as np
 import torch
 
+from .. import ops
 from ..datapusher import DataProducerOnInitReturn
 from ..datasetwrapper import ProducerFunctionSkeleton
 from ..ops import _dtypes
@@ -55,7 +56,9 @@ class PointwiseProducer(ProducerFunctionSkeleton):
 
     def post_init(self, *args, **kwargs):
         super().post_init(*args, **kwargs)
-        self.my_ary[...] = np.concatenate([g.astype(np.float32) for g in self._groups], axis=1)
+        # K2 window fill on the native host pool (tests/run_ddl.py:156-159 does np.concatenate)
+        ops.pack_columns([torch.from_numpy(np.ascontiguousarray(g, dtype=np.float32)) for g in self._groups],
+                         out=torch.from_numpy(self.my_ary))
         self._groups = None
 
     def execute_function(self, *args, **kwargs):

@@ -315,6 +315,63 @@ def split_columns(src, splits: Sequence[int], index: torch.Tensor | None = None,
     return outs
 
 
+def ref_pack_columns(groups, index=None, perm=None, base=0, n_rows=None, out_dtype=None):
+    g0 = groups[0]
+    n_rows = _check_rows(g0, index, perm, base, n_rows)
+    rows = _ref_rows(g0.shape[0], n_rows, index, perm, base).to(g0.device)
+    out_dtype = out_dtype or g0.dtype
+    cat = torch.cat([g.index_select(0, rows) for g in groups], dim=1)
+    return cat if out_dtype == g0.dtype else cat.float().to(out_dtype)
+
+
+def pack_columns(groups: Sequence[torch.Tensor], index: torch.Tensor | None = None, *,
+                 perm: FeistelPermutation | None = None, base: int = 0, n_rows: int | None = None, out_dtype=None,
+                 out: torch.Tensor | None = None, host_threads: int = 4, stream=None) -> torch.Tensor:
+    """k [N, w_g] column groups -> one [B, sum w_g] row block.
+
+    The reference fills each producer window by concatenating the harness's
+    column groups on the host (tests/run_ddl.py:156-159). On the host this runs
+    on the native thread pool (row-blocked memcpy, GIL released); on the GPU it
+    is one gfx950 kernel fused with the row gather (index / Feistel perm) and
+    the dtype cast -- the inverse of ``split_columns``.
+    """
+    groups = list(groups)
+    if not 1 <= len(groups) <= 8:
+        raise ValueError("pack_columns takes 1..8 groups")
+    g0 = groups[0]
+    for g in groups:
+        if g.dim() != 2 or g.shape[0] != g0.shape[0] or g.dtype != g0.dtype or g.device != g0.device:
+            raise ValueError("groups must be 2-D with equal row counts, dtype and device")
+    widths = [int(g.shape[1]) for g in groups]
+    n_values = sum(widths)
+    out_dtype = _dtypes.to_torch_dtype(out_dtype) if out_dtype is not None else (
+        out.dtype if out is not None else g0.dtype)
+    n_rows = _check_rows(g0, index, perm, base, n_rows)
+    if out is None:
+        out = torch.empty((n_rows, n_values), dtype=out_dtype, device=g0.device)
+    if tuple(out.shape) != (n_rows, n_values) or out.dtype != out_dtype or not out.is_contiguous():
+        raise ValueError(f"out must be a contiguous {(n_rows, n_values)} {out_dtype} tensor")
+    groups = [g.contiguous() for g in groups]
+    if not g0.is_cuda:
+        if index is None and perm is None and out_dtype == g0.dtype:
+            esz = g0.element_size()
+            _native.runtime().pack_columns(out.data_ptr(), [g.data_ptr() + base * w * esz
+                                                            for g, w in zip(groups, widths)],
+                                           widths, esz, n_rows, host_threads)
+            return out
+        out.copy_(ref_pack_columns(groups, index, perm, base, n_rows, out_dtype))
+        return out
+    if out_dtype != g0.dtype and out_dtype not in (torch.bfloat16, torch.float32):
+        raise TypeError("pack_columns casts to bf16 or f32 only (same-dtype packs are raw copies)")
+    if out.device != g0.device:
+        raise ValueError("out must be on the groups' device")
+    _native.hip().pack_columns(
+        srcs=[g.data_ptr() for g in groups], widths=widths, in_dt=_dtypes.code(g0.dtype), dst=out.data_ptr(),
+        out_dt=_dtypes.code(out_dtype), n_rows=n_rows, n_values=n_values, stream=_stream_handle(stream),
+        **_index_kw(index, perm, base))
+    return out
+
+
 # --------------------------------------------------------------------- tokens
 def ref_pad_tokens(tokens: torch.Tensor, offsets: torch.Tensor, seq_len: int, pad_id: int = 0,
                    position_dtype=torch.int64):

@@ -132,6 +132,22 @@ def test_split_columns(src_dtype, out_dtype):
         assert torch.equal(a.cpu(), b)
 
 
+@pytest.mark.parametrize("src_dtype,out_dtype", [(torch.float32, torch.float32), (torch.float32, torch.bfloat16),
+                                                 (torch.uint8, torch.bfloat16), (torch.int64, torch.int64),
+                                                 (torch.bfloat16, torch.float32)])
+def test_pack_columns(src_dtype, out_dtype):
+    n = 4096 * 3
+    groups = [(torch.randn(n, w) * 100).to(src_dtype) for w in (3, 5, 1)]
+    p = FeistelPermutation(n, 0, 5)
+    ref = ops.ref_pack_columns(groups, perm=p, base=4096, n_rows=4096, out_dtype=out_dtype)
+    out = ops.pack_columns([g.to(_dev()) for g in groups], perm=p, base=4096, n_rows=4096, out_dtype=out_dtype)
+    assert torch.equal(out.cpu(), ref)
+    # round trip: split(pack(x)) == x (identity rows)
+    packed = ops.pack_columns([g.to(_dev()) for g in groups])
+    for a, b in zip(ops.split_columns(packed, (3, 5, 1)), groups):
+        assert torch.equal(a.cpu(), b)
+
+
 @pytest.mark.parametrize("seq_len", [4096, 130])
 def test_pad_tokens(seq_len):
     rng = np.random.default_rng(0)

@@ -214,3 +214,22 @@ def test_parallel_copy():
     dst = np.zeros_like(src)
     rt.parallel_copy(dst.ctypes.data, src.ctypes.data, src.nbytes, 4)
     assert np.array_equal(src, dst)
+
+
+@pytest.mark.parametrize("dtype,widths", [(np.float32, (3, 5, 1)), (np.uint8, (1, 7)), (np.int64, (4,))])
+@pytest.mark.parametrize("threads", [1, 4])
+def test_host_pack_columns(dtype, widths, threads):
+    import torch
+
+    from ddl_amd import ops
+
+    n = 70_001
+    rng = np.random.default_rng(3)
+    groups = [torch.from_numpy((rng.random((n, w)) * 100).astype(dtype)) for w in widths]
+    out = ops.pack_columns(groups, host_threads=threads)
+    assert torch.equal(out, torch.cat(groups, dim=1))
+    # identity slice with an offset + a permuted (reference-path) pack
+    part = ops.pack_columns(groups, base=123, n_rows=1000)
+    assert torch.equal(part, torch.cat(groups, dim=1)[123:1123])
+    idx = torch.from_numpy(rng.permutation(n)[:500].astype(np.int64))
+    assert torch.equal(ops.pack_columns(groups, idx), torch.cat(groups, dim=1)[idx])
