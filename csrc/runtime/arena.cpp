@@ -94,6 +94,14 @@ Arena* Arena::create(const std::string& name, const std::vector<uint64_t>& capac
     errno = e;
     throw sys_error("ftruncate(" + std::to_string(total) + ")");
   }
+  // Reserve the tmpfs pages now: an over-committed /dev/shm would otherwise
+  // surface as SIGBUS on the first producer write instead of an error here.
+  if (int rc = posix_fallocate(fd, 0, static_cast<off_t>(total)); rc != 0 && rc != EOPNOTSUPP && rc != EINVAL) {
+    close(fd);
+    shm_unlink(name.c_str());
+    errno = rc;
+    throw sys_error("posix_fallocate(" + std::to_string(total) + " bytes; /dev/shm too small?)");
+  }
   void* p = mmap(nullptr, total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
   if (p == MAP_FAILED) {
     int e = errno;
