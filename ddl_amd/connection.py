@@ -72,7 +72,8 @@ class _Pipe:
                 try:
                     tag, payload = self.conn.recv()
                 except (EOFError, OSError) as e:
-                    raise PeerDeathError(f"{self.name}: connection lost while waiting for {expect!r} ({e!r})") from None
+                    raise PeerDeathError(
+                        f"{self.name}: connection lost while waiting for {expect!r} ({e!r})") from None
                 if tag == "error":
                     raise PeerDeathError(f"{self.name} failed:\n{payload}")
                 if tag != expect:

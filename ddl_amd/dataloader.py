@@ -190,8 +190,9 @@ class DistributedDataLoader:
                 ex = md[0].extra
                 for key in ("global_batch", "n_samples", "order_seed"):
                     if chk.get(key) is not None and ex.get(key) is not None and chk[key] != ex[key]:
-                        raise ShapeMismatchError((key, chk[key], ex[key]),
-                                                 f"checkpoint {key}={chk[key]} does not match the producers' {ex[key]}")
+                        raise ShapeMismatchError(
+                            (key, chk[key], ex[key]),
+                            f"checkpoint {key}={chk[key]} does not match the producers' {ex[key]}")
                 if int(chk["batches_per_epoch"]) != self.windows_per_epoch:
                     raise ShapeMismatchError(chk, "checkpoint batches_per_epoch does not match")
         elif self.mode == "split_along_epoch":

@@ -77,8 +77,10 @@ class SharedTokenSource:
 
     @classmethod
     def create(cls, name: str, tokens: np.ndarray, offsets: np.ndarray) -> "SharedTokenSource":
-        t = SharedArraySource.create(name + "_tok", torch.from_numpy(np.ascontiguousarray(tokens, np.int32)).view(-1, 1))
-        o = SharedArraySource.create(name + "_off", torch.from_numpy(np.ascontiguousarray(offsets, np.int64)).view(-1, 1))
+        tok = torch.from_numpy(np.ascontiguousarray(tokens, np.int32)).view(-1, 1)
+        off = torch.from_numpy(np.ascontiguousarray(offsets, np.int64)).view(-1, 1)
+        t = SharedArraySource.create(name + "_tok", tok)
+        o = SharedArraySource.create(name + "_off", off)
         return cls(t, o, int(np.diff(offsets).max()) if len(offsets) > 1 else 0)
 
     @classmethod

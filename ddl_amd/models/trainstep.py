@@ -20,7 +20,8 @@ class PatchMLP(nn.Module):
         self.patch = patch
         self.embed = nn.Linear(in_ch * patch * patch, dim)
         self.blocks = nn.ModuleList(
-            nn.Sequential(nn.LayerNorm(dim), nn.Linear(dim, dim * mlp_ratio), nn.GELU(), nn.Linear(dim * mlp_ratio, dim))
+            nn.Sequential(nn.LayerNorm(dim), nn.Linear(dim, dim * mlp_ratio), nn.GELU(),
+                          nn.Linear(dim * mlp_ratio, dim))
             for _ in range(depth))
         self.norm = nn.LayerNorm(dim)
         self.head = nn.Linear(dim, n_classes)

@@ -180,7 +180,8 @@ def make_exchange(env: DDLEnv, method: str, fraction: float, n_rows: int, sample
     try:
         cls = _METHODS[method]
     except KeyError:
-        raise NotImplementedError(f"exchange method {method!r} is not implemented; one of {sorted(_METHODS)}") from None
+        raise NotImplementedError(
+            f"exchange method {method!r} is not implemented; one of {sorted(_METHODS)}") from None
     dtype = _dtypes.to_torch_dtype(dtype)
     sh = cls(env, fraction, n_rows, tuple(sample_shape), dtype, seed, device)
     logger.debug("global shuffle: %s, %d rows/window", cls.__name__, sh.n_exchange)
