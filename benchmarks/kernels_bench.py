@@ -70,6 +70,11 @@ def main():
     pp = FeistelPermutation(100_520, 5, 5)
     t = bench(lambda: ops.split_columns(pw, (3, 5, 1), perm=pp, base=0, n_rows=4096))
     report("split_columns 4096x(3,5,1) f32", t, 2 * 4096 * 36)
+    grp = [pw[:, :3].contiguous(), pw[:, 3:8].contiguous(), pw[:, 8:].contiguous()]
+    t = bench(lambda: ops.pack_columns(grp))
+    report("pack_columns window 100520x(3,5,1) f32", t, 2 * 100_520 * 36)
+    t = bench(lambda: ops.pack_columns(grp, perm=pp, base=0, n_rows=4096, out_dtype=torch.bfloat16))
+    report("pack_columns 4096 gather+bf16", t, 4096 * 36 + 4096 * 18)
     # tokens: 64 sequences, mean 2k, seq_len 4096 pack + pad
     rng = np.random.default_rng(0)
     lens = rng.integers(256, 4097, size=64)
