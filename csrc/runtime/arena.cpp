@@ -381,6 +381,11 @@ void gather_rows(uint8_t* dst, const uint8_t* src, uint64_t row_bytes, const int
   });
 }
 
+void pool_run(int n, int n_threads, const std::function<void(int)>& fn) {
+  std::lock_guard<std::mutex> lk(g_pool_call_mu);
+  Pool::get().run(n, n_threads, fn);
+}
+
 void parallel_copy(uint8_t* dst, const uint8_t* src, uint64_t bytes, int n_threads) {
   const uint64_t chunk = 8ull << 20;
   const int tasks = static_cast<int>((bytes + chunk - 1) / chunk);

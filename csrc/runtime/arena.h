@@ -22,6 +22,7 @@
 #include <atomic>
 #include <cstddef>
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -153,6 +154,9 @@ void gather_rows(uint8_t* dst, const uint8_t* src, uint64_t row_bytes, const int
                  uint64_t n, uint64_t src_rows, int n_threads);
 // Parallel memcpy (large contiguous copies: window replication).
 void parallel_copy(uint8_t* dst, const uint8_t* src, uint64_t bytes, int n_threads);
+// Run fn(i), i in [0, n), on the shared host worker pool (caller included).
+// fn must not throw: record errors and report them after the call.
+void pool_run(int n, int n_threads, const std::function<void(int)>& fn);
 // k row-major [n, widths[g]] groups -> interleaved [n, sum(widths)] (elements of elem_bytes).
 void pack_columns(uint8_t* dst, const std::vector<const uint8_t*>& srcs, const std::vector<uint64_t>& widths,
                   uint64_t elem_bytes, uint64_t n, int n_threads);

@@ -10,6 +10,7 @@
 
 #include "arena.h"
 #include "feistel.h"
+#include "fileio.h"
 
 namespace py = pybind11;
 using ddl::Arena;
@@ -207,4 +208,25 @@ PYBIND11_MODULE(_ddl_runtime, m) {
       },
       py::arg("dst"), py::arg("srcs"), py::arg("widths"), py::arg("elem_bytes"), py::arg("n"),
       py::arg("n_threads") = 4, "k [n, w_g] column groups -> interleaved [n, sum w] (host window fill)");
+  py::class_<ddl::FileHandle>(m, "RowsFile")
+      .def(py::init([](const std::string& path, bool direct) {
+             return std::make_unique<ddl::FileHandle>(ddl::open_rows_file(path, direct));
+           }),
+           py::arg("path"), py::arg("direct") = false)
+      .def_property_readonly("size", [](const ddl::FileHandle& h) { return h.size; })
+      .def_property_readonly("has_direct", [](const ddl::FileHandle& h) { return h.direct_fd >= 0; })
+      .def_property_readonly("closed", [](const ddl::FileHandle& h) { return h.fd < 0; })
+      .def("close", [](ddl::FileHandle& h) { ddl::close_rows_file(h); })
+      .def(
+          "read_rows",
+          [](const ddl::FileHandle& h, uint64_t base_offset, uint64_t row_bytes,
+             py::array_t<int64_t, py::array::c_style | py::array::forcecast> idx, uintptr_t dst, bool direct,
+             int n_threads) {
+            const int64_t* ip = idx.data();
+            const uint64_t n = static_cast<uint64_t>(idx.size());
+            py::gil_scoped_release nogil;
+            ddl::read_rows(h, base_offset, row_bytes, ip, n, reinterpret_cast<uint8_t*>(dst), direct, n_threads);
+          },
+          py::arg("base_offset"), py::arg("row_bytes"), py::arg("idx"), py::arg("dst"), py::arg("direct") = false,
+          py::arg("n_threads") = 4, "dst[i] = row idx[i] of the file (coalesced pread, optional O_DIRECT)");
 }

@@ -2,6 +2,7 @@
 
 from .datasets import (
     DummyDataset,
+    FileRowsSource,
     NpyMemmapSource,
     PointWiseData,
     SharedArraySource,
@@ -12,6 +13,7 @@ from .producers import ImageWindowProducer, IndexedProducer, PointwiseProducer
 
 __all__ = [
     "DummyDataset",
+    "FileRowsSource",
     "NpyMemmapSource",
     "PointWiseData",
     "SharedArraySource",

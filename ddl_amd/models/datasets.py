@@ -211,6 +211,74 @@ class NpyMemmapSource:
                                       np.ascontiguousarray(indices, np.int64), self.n, n_threads)
 
 
+class FileRowsSource:
+    """File-backed dataset [N, *sample_shape] read with native coalesced ``pread``.
+
+    For datasets larger than host RAM, or when 8 ranks x P producers should not
+    thrash a node's page cache: producers pull exactly the rows of their next
+    batch from disk into the pinned slot (``gather``), with ``direct=True``
+    bypassing the page cache (O_DIRECT; falls back to buffered reads on
+    filesystems that refuse it, e.g. tmpfs). The reference keeps each
+    producer's whole shard in memory (tests/run_ddl.py:80-104).
+
+    ``from_npy`` parses an ``.npy`` header (no pickles: object dtypes are
+    refused) and reads the C-order payload in place.
+    """
+
+    def __init__(self, path: str, sample_shape, dtype, n: int | None = None, offset: int = 0, direct: bool = False):
+        self.path = os.path.abspath(path)
+        self.sample_shape = tuple(int(d) for d in sample_shape)
+        self.dtype = _dtypes.to_torch_dtype(dtype)
+        self.offset = int(offset)
+        self.direct = bool(direct)
+        self.row_bytes = int(math.prod(self.sample_shape)) * _dtypes.itemsize(self.dtype)
+        size = os.path.getsize(self.path)
+        avail = (size - self.offset) // self.row_bytes if self.row_bytes else 0
+        self.n = int(avail if n is None else n)
+        if self.n > avail:
+            raise ValueError(f"{path}: {self.n} rows of {self.row_bytes} B do not fit in {size - self.offset} B")
+        self._f = None
+
+    @classmethod
+    def from_npy(cls, path: str, direct: bool = False) -> FileRowsSource:
+        from numpy.lib import format as npf
+
+        with open(path, "rb") as fh:
+            version = npf.read_magic(fh)
+            read_header = npf.read_array_header_1_0 if version == (1, 0) else npf.read_array_header_2_0
+            shape, fortran, dtype = read_header(fh)  # parses the header literal only; never unpickles
+            offset = fh.tell()
+        if fortran or dtype.hasobject or len(shape) < 1:
+            raise ValueError(f"{path}: need a C-order, non-object array with a leading sample axis")
+        return cls(path, shape[1:], dtype, n=shape[0], offset=offset, direct=direct)
+
+    def __getstate__(self):
+        st = dict(self.__dict__)
+        st["_f"] = None  # reopened lazily in the producer
+        return st
+
+    def _file(self):
+        if self._f is None or self._f.closed:
+            from .. import _native
+
+            self._f = _native.runtime().RowsFile(self.path, self.direct)
+        return self._f
+
+    def gather(self, indices: np.ndarray, dst_address: int, n_threads: int = 4) -> None:
+        idx = np.ascontiguousarray(indices, np.int64)
+        if idx.size and (idx.min() < 0 or idx.max() >= self.n):
+            raise IndexError(f"row index out of range [0, {self.n})")
+        self._file().read_rows(self.offset, self.row_bytes, idx, dst_address, self.direct, n_threads)
+
+    def read_range(self, row0: int, n_rows: int, dst_address: int, n_threads: int = 4) -> None:
+        self.gather(np.arange(row0, row0 + n_rows, dtype=np.int64), dst_address, n_threads)
+
+    def close(self) -> None:
+        if self._f is not None:
+            self._f.close()
+            self._f = None
+
+
 class SyntheticTokens:
     """Deterministic ragged token sequences: sequence i has length in [min_len, max_len]."""
 

@@ -66,6 +66,27 @@ def _source_address(source) -> tuple[int, int]:
     raise TypeError(f"unsupported source {type(source).__name__}")
 
 
+def _host_reader(source):
+    """``read(row0, n_rows, dst_address, n_threads)`` copying rows [row0, row0+n) of a source
+    into host memory: a parallel memcpy for in-memory sources, coalesced native
+    ``pread`` for file-backed ones (``FileRowsSource``)."""
+    if hasattr(source, "read_range"):
+        return source.read_range
+    addr, _ = _source_address(source)
+    geom, dt = _source_geometry(source)
+    row_bytes = (int(math.prod(geom)) if geom else 1) * _dtypes.itemsize(dt)
+    rt = _native.runtime()
+
+    def read(row0: int, n_rows: int, dst: int, n_threads: int) -> None:
+        rt.parallel_copy(dst, addr + row0 * row_bytes, n_rows * row_bytes, n_threads)
+
+    return read
+
+
+def _source_rows(source) -> int:
+    return int(source.n) if hasattr(source, "read_range") else _source_address(source)[1]
+
+
 def _source_geometry(source) -> tuple[tuple[int, ...], torch.dtype]:
     if isinstance(source, torch.Tensor):
         return tuple(source.shape[1:]), source.dtype
@@ -191,14 +212,14 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
             geom = [None]
             if self.rank == scatter_from:
                 shp, dt = _source_geometry(source)
-                geom = [(shp, str(dt).replace("torch.", ""), _source_address(source)[1])]
+                geom = [(shp, str(dt).replace("torch.", ""), _source_rows(source))]
             dist.broadcast_object_list(geom, src=scatter_from, group=self.env.control_group)
             shp, dt, n = geom[0]
             self.sample_shape, self.src_dtype = tuple(shp), _dtypes.to_torch_dtype(dt)
-            src_addr = _source_address(source)[0] if self.rank == scatter_from else 0
+            reader = _host_reader(source) if self.rank == scatter_from else None
         else:
             self.sample_shape, self.src_dtype = _source_geometry(source)
-            src_addr, n = _source_address(source)
+            reader, n = _host_reader(source), _source_rows(source)
         self.row_elems = int(math.prod(self.sample_shape)) if self.sample_shape else 1
         self.row_bytes = self.row_elems * _dtypes.itemsize(self.src_dtype)
         self.N = n
@@ -223,49 +244,47 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
         self.bytes_exchanged = 0
         t0 = time.perf_counter()
         if scatter_from is not None and self.W > 1:
-            self.shard = self._scatter_shards(src_addr, chunk_bytes, host_threads, scatter_from)
+            self.shard = self._scatter_shards(reader, chunk_bytes, host_threads, scatter_from)
         else:
-            self.shard = self._load_shard(src_addr, chunk_bytes, host_threads)
+            self.shard = self._load_shard(reader, chunk_bytes, host_threads)
         self.load_s = time.perf_counter() - t0
         self.prep_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
 
     # ----------------------------------------------------------------- load
-    def _load_shard(self, src_addr: int, chunk_bytes: int, host_threads: int) -> torch.Tensor:
+    def _load_shard(self, reader, chunk_bytes: int, host_threads: int) -> torch.Tensor:
         rows = self.hi - self.lo
         shard = torch.empty((rows,) + self.sample_shape, dtype=self.src_dtype, device=self.device)
         if rows == 0:
             return shard
-        base = src_addr + self.lo * self.row_bytes
-        total = rows * self.row_bytes
-        rt = _native.runtime()
         dst_bytes = shard.view(-1).view(torch.uint8)
         if self.device.type != "cuda":
-            rt.parallel_copy(dst_bytes.data_ptr(), base, total, host_threads)
+            reader(self.lo, rows, dst_bytes.data_ptr(), host_threads)
             return shard
-        # double-buffered pinned bounce buffers: host parallel memcpy || SDMA H2D
+        # double-buffered pinned bounce buffers: host read (memcpy / pread) || SDMA H2D
         hip = _native.hip()
-        chunk = max(self.row_bytes, min(chunk_bytes, total))
-        bufs = [torch.empty(chunk, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+        chunk_rows = max(1, min(chunk_bytes // max(self.row_bytes, 1), rows))
+        bufs = [torch.empty(chunk_rows * self.row_bytes, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
         evs = [torch.cuda.Event(), torch.cuda.Event()]
         used = [False, False]
         s = torch.cuda.Stream(self.device)
-        off, i = 0, 0
+        r, i = 0, 0
         with trace_range("ddl.resident.load"):
-            while off < total:
-                n = min(chunk, total - off)
+            while r < rows:
+                n = min(chunk_rows, rows - r)
                 b = i % 2
                 if used[b]:
                     evs[b].synchronize()
-                rt.parallel_copy(bufs[b].data_ptr(), base + off, n, host_threads)
-                hip.memcpy_h2d(dst_bytes.data_ptr() + off, bufs[b].data_ptr(), n, s.cuda_stream)
+                reader(self.lo + r, n, bufs[b].data_ptr(), host_threads)
+                hip.memcpy_h2d(dst_bytes.data_ptr() + r * self.row_bytes, bufs[b].data_ptr(), n * self.row_bytes,
+                               s.cuda_stream)
                 evs[b].record(s)
                 used[b] = True
-                off += n
+                r += n
                 i += 1
             s.synchronize()
         return shard
 
-    def _scatter_shards(self, src_addr: int, chunk_bytes: int, host_threads: int, src_rank: int) -> torch.Tensor:
+    def _scatter_shards(self, reader, chunk_bytes: int, host_threads: int, src_rank: int) -> torch.Tensor:
         """Rank ``src_rank`` streams the dataset H2D chunk by chunk and sends every
         peer the rows of its shard with grouped point-to-point ops (all peers at
         once: on an xGMI-connected node every link carries one peer's slice);
@@ -279,7 +298,6 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
         dist.all_reduce(probe, group=self.group)
         rows_per_chunk = max(1, chunk_bytes // self.row_bytes)
         bounds = [(q * self.S, min(self.N, (q + 1) * self.S)) for q in range(self.W)]
-        rt = _native.runtime()
         staging = None
         if self.rank == src_rank:
             staging = torch.empty((rows_per_chunk,) + self.sample_shape, dtype=self.src_dtype, device=self.device)
@@ -291,7 +309,7 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
                 ops_ = []
                 if self.rank == src_rank:
                     nbytes = (c1 - c0) * self.row_bytes
-                    rt.parallel_copy(bounce.data_ptr(), src_addr + c0 * self.row_bytes, nbytes, host_threads)
+                    reader(c0, c1 - c0, bounce.data_ptr(), host_threads)
                     stage = staging[: c1 - c0]
                     stage.view(-1).view(torch.uint8)[:nbytes].copy_(bounce[:nbytes], non_blocking=True)
                     for q, (lo, hi) in enumerate(bounds):
