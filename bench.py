@@ -143,7 +143,9 @@ def main(argv=None) -> int:
         if idle_steps:
             from ddl_amd.models.trainstep import TrainStep
 
-            step = TrainStep(dev, dim=args.model_dim, depth=args.model_depth)
+            # DP training step: DDP gradient all-reduce over RCCL when N > 1
+            step = TrainStep(dev, dim=args.model_dim, depth=args.model_depth,
+                             process_group=env.process_group if env.world_size > 1 else None)
             for _ in range(args.warmup // 2):
                 (x,) = next(it)
                 step(x)
@@ -193,9 +195,10 @@ def main(argv=None) -> int:
                     "exchange_fraction": args.exchange,
                     "source_dtype": args.source_dtype,
                 },
-                "gpu_idle_pct": None if not idle else round(idle["gpu_idle_pct"], 3),
+                "gpu_idle_pct": None if not idle or math.isnan(idle["gpu_idle_pct"]) else round(idle["gpu_idle_pct"], 3),
                 "train_step": None if not idle else {
-                    "model": f"PatchMLP dim={args.model_dim} depth={args.model_depth} fwd+bwd+SGD bf16",
+                    "model": f"PatchMLP dim={args.model_dim} depth={args.model_depth} fwd+bwd+SGD bf16"
+                             + (" (DDP all-reduce)" if env.world_size > 1 else ""),
                     "samples_per_s": round(idle["train_samples_per_s"], 1),
                     "busy_ms": round(idle["busy_ms"], 3), "wall_ms": round(idle["wall_ms"], 3)},
                 "loader": {"consumer_wait_s": round(stats["consumer_wait_s"], 4),

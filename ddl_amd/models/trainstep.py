@@ -37,10 +37,29 @@ class PatchMLP(nn.Module):
 
 
 class TrainStep:
-    """forward + backward + SGD on one [B, 3, H, W] batch (labels synthetic)."""
+    """forward + backward + SGD on one [B, 3, H, W] batch (labels synthetic).
 
-    def __init__(self, device, dim: int = 384, depth: int = 4, lr: float = 1e-3, dtype=torch.bfloat16):
+    With a ``process_group`` of more than one rank the model is wrapped in
+    ``DistributedDataParallel``: the gradient all-reduce (RCCL over xGMI on
+    GPUs) runs in buckets overlapped with backward, as in real DP training.
+    One bucket per ~the whole model (``bucket_cap_mb``) keeps it to a few large
+    collectives, which is what a per-link-bound xGMI ring wants.
+    """
+
+    def __init__(self, device, dim: int = 384, depth: int = 4, lr: float = 1e-3, dtype=torch.bfloat16,
+                 process_group=None, bucket_cap_mb: float = 16.0):
+        torch.manual_seed(0)  # identical init on every rank (DDP also broadcasts rank 0's weights)
         self.model = PatchMLP(dim=dim, depth=depth).to(device=device, dtype=dtype)
+        self.ddp = False
+        if process_group is not None:
+            import torch.distributed as dist
+
+            if dist.get_world_size(process_group) > 1:
+                dev = torch.device(device)
+                self.model = nn.parallel.DistributedDataParallel(
+                    self.model, device_ids=[dev.index] if dev.type == "cuda" else None,
+                    process_group=process_group, bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True)
+                self.ddp = True
         self.opt = torch.optim.SGD(self.model.parameters(), lr=lr)
         self.device = device
         self.dtype = dtype

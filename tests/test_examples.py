@@ -34,3 +34,27 @@ def test_example_two_ranks_torchrun():
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=dict(_env(), DDL_DEVICE="cpu"))
     assert r.returncode == 0, r.stderr[-3000:]
     assert "epoch 2/2: 4 batches" in r.stdout  # 4*10052/2 rows per window // 4096
+
+
+@pytest.mark.timeout(300)
+def test_bench_contract_two_ranks_torchrun():
+    """bench.py's driver contract at N=2 (the driver's launch line), rehearsed on CPU/gloo:
+    exchange 0.5 over the DP group, DDP train step, one strict-JSON line from rank 0."""
+    import json
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--steps", "6", "--warmup", "2", "--window", "64", "--batch", "16", "--idle-steps", "3",
+           "--model-dim", "64", "--model-depth", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=dict(_env(), DDL_DEVICE="cpu"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    out = json.loads(lines[0], parse_constant=lambda c: pytest.fail(f"non-JSON constant {c}"))
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in out, k
+    assert out["n_gpus"] == 2 and out["steps"] == 6 and out["warmup"] == 2 and out["value"] > 0
+    assert out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 32
+    assert out["config"]["exchange_fraction"] == 0.5
+    assert "DDP" in out["train_step"]["model"]
