@@ -85,6 +85,30 @@ def test_gpu_indexed_mode_world_size_invariant_order():
         src.close()
 
 
+def test_gpu_file_source_indexed_and_resident(tmp_path):
+    from ddl_amd.models import FileRowsSource, IndexedProducer
+    from ddl_amd.permutation import EpochOrder
+    from ddl_amd.resident import ResidentGlobalLoader
+
+    n, gb = 3000, 128
+    arr = np.random.default_rng(0).integers(0, 255, size=(n, 3, 8, 8), dtype=np.uint8)
+    path = tmp_path / "imgs.npy"
+    np.save(path, arr)
+    src = FileRowsSource.from_npy(str(path), direct=True)
+    order = EpochOrder(n, gb, 5)
+    ref = arr[order.perm(0).full()[: order.batches_per_epoch * gb]]
+    with ddl_amd.start(n_producers=2) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(IndexedProducer(src, gb), gb, conn, 1, mode="indexed", env=env,
+                                           auto_mark=True, seed=5)
+        got = torch.cat([b[0].cpu() for b in dl]).numpy()
+    assert np.array_equal(got.reshape(ref.shape), ref)
+    res = ResidentGlobalLoader(src, gb, seed=5, n_epochs=1, chunk_bytes=64 << 10)
+    assert res.shard.is_cuda
+    got = torch.cat([b.cpu() for b in res]).numpy()
+    assert np.array_equal(got, ref)
+    res.close()
+
+
 def test_gpu_uint8_normalised_and_hwc_collate():
     from ddl_amd.models.producers import ImageWindowProducer
 
