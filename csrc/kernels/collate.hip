@@ -66,8 +66,8 @@ __global__ void __launch_bounds__(kThreads) hwc_to_chw_kernel(void* __restrict__
                                                               RowIndex ri, Affine aff) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
   Tin* tile = reinterpret_cast<Tin*>(lds_raw);
-  const int64_t img = blockIdx.x / tiles;
-  const int64_t t = blockIdx.x % tiles;
+  const int64_t img = blockIdx.x / static_cast<uint32_t>(tiles);  // 32-bit: grid < 2^32 blocks
+  const int64_t t = blockIdx.x - static_cast<uint32_t>(img) * static_cast<uint32_t>(tiles);
   const int64_t p0 = t * kPix;
   const int npx = static_cast<int>(pixels - p0 < kPix ? pixels - p0 : kPix);
   const int64_t srow = source_row(ri, img);
@@ -101,59 +101,76 @@ __global__ void __launch_bounds__(kThreads) hwc_to_chw_kernel(void* __restrict__
   }
 }
 
-// Specialisation for the common case (uint8 RGB): each lane pulls its 8 pixels
-// (24 B) out of LDS with three conflict-free ds_read_b64 (lane stride 24 B ->
-// dword stride 6: the 32 lanes of a half-wave cover all 64 banks once) instead
-// of 24 single-byte reads, then de-interleaves in registers.
+// Specialisation for the common case (uint8 RGB). Each workgroup stages a
+// 4096-pixel (12 KB) tile: the kernel is bound by bytes in flight per CU
+// (HBM latency x bandwidth is ~50 KB per CU), and 8 resident workgroups x 12 KB
+// of loads cover it where 6 KB tiles did not (measured 77% -> see
+// docs/PERFORMANCE.md). Each lane owns two 8-pixel groups; for each it pulls
+// its 24 B out of LDS with three conflict-free ds_read_b64 (lane stride 24 B ->
+// dword stride 6: the 32 lanes of a half-wave cover all 64 banks once) and
+// de-interleaves in registers.
+constexpr int kPix3 = 4096;
+
 template <int OUT_BF16>
 __global__ void __launch_bounds__(kThreads) hwc3_u8_to_chw_kernel(void* __restrict__ dst, const uint8_t* __restrict__ src,
                                                                   int64_t pixels, int64_t tiles, RowIndex ri,
                                                                   Affine aff) {
-  __shared__ __attribute__((aligned(16))) uint8_t tile[kPix * 3];
-  const int64_t img = blockIdx.x / tiles;
-  const int64_t t = blockIdx.x % tiles;
-  const int64_t p0 = t * kPix;
-  const int npx = static_cast<int>(pixels - p0 < kPix ? pixels - p0 : kPix);
+  __shared__ __attribute__((aligned(16))) uint8_t tile[kPix3 * 3];
+  const int64_t img = blockIdx.x / static_cast<uint32_t>(tiles);  // 32-bit: grid < 2^32 blocks
+  const int64_t t = blockIdx.x - static_cast<uint32_t>(img) * static_cast<uint32_t>(tiles);
+  const int64_t p0 = t * kPix3;
+  const int npx = static_cast<int>(pixels - p0 < kPix3 ? pixels - p0 : kPix3);
   const uint8_t* s = src + (source_row(ri, img) * pixels + p0) * 3;
   const int bytes = npx * 3;
   if ((reinterpret_cast<uintptr_t>(s) & 15u) == 0 && (bytes & 15) == 0) {
+    static_assert(kPix3 * 3 / 16 == 3 * kThreads, "three 16 B loads per lane");
     const uint4* s4 = reinterpret_cast<const uint4*>(s);
     uint4* l4 = reinterpret_cast<uint4*>(tile);
-    for (int i = threadIdx.x; i < bytes / 16; i += kThreads) l4[i] = s4[i];
+    const int n16 = bytes / 16;
+    const int i0 = threadIdx.x, i1 = i0 + kThreads, i2 = i1 + kThreads;
+    uint4 v0{}, v1{}, v2{};  // all loads issued before the first LDS write
+    if (i0 < n16) v0 = s4[i0];
+    if (i1 < n16) v1 = s4[i1];
+    if (i2 < n16) v2 = s4[i2];
+    if (i0 < n16) l4[i0] = v0;
+    if (i1 < n16) l4[i1] = v1;
+    if (i2 < n16) l4[i2] = v2;
   } else {
     for (int i = threadIdx.x; i < bytes; i += kThreads) tile[i] = s[i];
   }
   __syncthreads();
-  const int px = threadIdx.x * 8;
-  if (px >= npx) return;
   const int64_t out_img = img * 3 * pixels;
-  if (px + 8 <= npx) {
-    const uint64_t* l8 = reinterpret_cast<const uint64_t*>(tile + px * 3);
-    const uint64_t w[3] = {l8[0], l8[1], l8[2]};
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const float sc = aff.enabled ? aff.scale[c] : 1.f;
-      const float bi = aff.enabled ? aff.bias[c] : 0.f;
-      float f[8];
+  for (int g = 0; g < kPix3 / (kThreads * 8); ++g) {
+    const int px = (g * kThreads + static_cast<int>(threadIdx.x)) * 8;
+    if (px + 8 <= npx) {
+      const uint64_t* l8 = reinterpret_cast<const uint64_t*>(tile + px * 3);
+      const uint64_t w[3] = {l8[0], l8[1], l8[2]};
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int b = 3 * k + c;  // byte index inside the lane's 24 bytes
-        f[k] = fmaf(static_cast<float>((w[b >> 3] >> (8 * (b & 7))) & 0xffu), sc, bi);
+      for (int c = 0; c < 3; ++c) {
+        const float sc = aff.enabled ? aff.scale[c] : 1.f;
+        const float bi = aff.enabled ? aff.bias[c] : 0.f;
+        float f[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int b = 3 * k + c;  // byte index inside the lane's 24 bytes
+          f[k] = fmaf(static_cast<float>((w[b >> 3] >> (8 * (b & 7))) & 0xffu), sc, bi);
+        }
+        const int64_t o = out_img + c * pixels + p0 + px;
+        if ((o & 7) == 0) {
+          Out8<OUT_BF16>::store(dst, o, f);
+        } else {
+          for (int k = 0; k < 8; ++k) Out8<OUT_BF16>::store1(dst, o + k, f[k]);
+        }
       }
-      const int64_t o = out_img + c * pixels + p0 + px;
-      if ((o & 7) == 0) {
-        Out8<OUT_BF16>::store(dst, o, f);
-      } else {
-        for (int k = 0; k < 8; ++k) Out8<OUT_BF16>::store1(dst, o + k, f[k]);
+    } else if (px < npx) {
+      for (int c = 0; c < 3; ++c) {
+        const float sc = aff.enabled ? aff.scale[c] : 1.f;
+        const float bi = aff.enabled ? aff.bias[c] : 0.f;
+        for (int k = 0; k < 8 && px + k < npx; ++k)
+          Out8<OUT_BF16>::store1(dst, out_img + c * pixels + p0 + px + k,
+                                 fmaf(static_cast<float>(tile[(px + k) * 3 + c]), sc, bi));
       }
-    }
-  } else {
-    for (int c = 0; c < 3; ++c) {
-      const float sc = aff.enabled ? aff.scale[c] : 1.f;
-      const float bi = aff.enabled ? aff.bias[c] : 0.f;
-      for (int k = 0; k < 8 && px + k < npx; ++k)
-        Out8<OUT_BF16>::store1(dst, out_img + c * pixels + p0 + px + k,
-                               fmaf(static_cast<float>(tile[(px + k) * 3 + c]), sc, bi));
     }
   }
 }
@@ -166,12 +183,14 @@ int launch_hwc(void* dst, int32_t out_dt, const void* src, int64_t batch, int64_
   const dim3 grid(static_cast<uint32_t>(batch * tiles));
   if constexpr (sizeof(Tin) == 1) {
     if (channels == 3 && (out_dt == kBF16 || out_dt == kF32)) {
+      const int64_t tiles3 = (pixels + kPix3 - 1) / kPix3;
+      const dim3 grid3(static_cast<uint32_t>(batch * tiles3));
       if (out_dt == kBF16)
-        hipLaunchKernelGGL(hwc3_u8_to_chw_kernel<1>, grid, dim3(kThreads), 0, st, dst,
-                           static_cast<const uint8_t*>(src), pixels, tiles, ri, aff);
+        hipLaunchKernelGGL(hwc3_u8_to_chw_kernel<1>, grid3, dim3(kThreads), 0, st, dst,
+                           static_cast<const uint8_t*>(src), pixels, tiles3, ri, aff);
       else
-        hipLaunchKernelGGL(hwc3_u8_to_chw_kernel<0>, grid, dim3(kThreads), 0, st, dst,
-                           static_cast<const uint8_t*>(src), pixels, tiles, ri, aff);
+        hipLaunchKernelGGL(hwc3_u8_to_chw_kernel<0>, grid3, dim3(kThreads), 0, st, dst,
+                           static_cast<const uint8_t*>(src), pixels, tiles3, ri, aff);
       return static_cast<int>(hipGetLastError());
     }
   }
@@ -196,7 +215,7 @@ __global__ void __launch_bounds__(kThreads) split_columns_kernel(SplitSpec spec,
   const int64_t total = n_rows * n_values;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
   for (int64_t e = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; e < total; e += stride) {
-    const int64_t row = e / n_values;
+    const int64_t row = div_small(e, n_values, total);
     int col = static_cast<int>(e - row * n_values);
     const float v = Px<Tin>::get(src + source_row(ri, row) * n_values, col);
     int g = 0;
@@ -219,7 +238,7 @@ __global__ void __launch_bounds__(kThreads) split_columns_raw_kernel(SplitSpec s
   const int64_t total = n_rows * n_values;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
   for (int64_t e = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; e < total; e += stride) {
-    const int64_t row = e / n_values;
+    const int64_t row = div_small(e, n_values, total);
     int col = static_cast<int>(e - row * n_values);
     const T v = src[source_row(ri, row) * n_values + col];
     int g = 0;
@@ -242,7 +261,7 @@ __global__ void __launch_bounds__(kThreads) pack_columns_kernel(SplitSpec spec, 
   const int64_t total = n_rows * n_values;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
   for (int64_t e = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; e < total; e += stride) {
-    const int64_t row = e / n_values;
+    const int64_t row = div_small(e, n_values, total);
     int col = static_cast<int>(e - row * n_values);
     int g = 0;
     while (g < spec.n_groups - 1 && col >= spec.width[g]) {

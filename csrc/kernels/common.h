@@ -75,6 +75,14 @@ struct Affine {
   int32_t enabled;
 };
 
+// a / b for non-negative a < bound: 32-bit unsigned division when the bound fits (a short
+// v_rcp_iflag sequence), the 64-bit expansion otherwise. `bound` is a kernel argument, so the
+// branch is wave-uniform.
+__device__ __forceinline__ int64_t div_small(int64_t a, int64_t b, int64_t bound) {
+  if (bound <= static_cast<int64_t>(UINT32_MAX)) return static_cast<uint32_t>(a) / static_cast<uint32_t>(b);
+  return a / b;
+}
+
 // bf16 helpers: the plain cast lowers to v_cvt_pk_bf16_f32 (RNE, NaN-safe) at
 // -O3 on gfx950 (MI355X_MICROARCH "Correctness boundaries").
 __device__ __forceinline__ uint16_t f32_to_bf16_bits(float f) {

@@ -33,8 +33,9 @@ __global__ void __launch_bounds__(kThreads) move_rows_chunked(uint8_t* __restric
   // Grid-stride over (row, chunk) tiles: normally one tile per workgroup; a capped
   // grid (zero-copy host gathers) keeps the PCIe-latency-bound kernel on few CUs.
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-  const int64_t row = tile / chunks_per_row;
-  const int64_t chunk = tile % chunks_per_row;
+  // tiles < 2^31 (host-checked): 32-bit division, not the 64-bit expansion
+  const int64_t row = static_cast<uint32_t>(tile) / static_cast<uint32_t>(chunks_per_row);
+  const int64_t chunk = static_cast<uint32_t>(tile) - static_cast<uint32_t>(row) * static_cast<uint32_t>(chunks_per_row);
   const int64_t mapped = source_row(ri, row);
   const int64_t srow = scatter ? row : mapped;
   const int64_t drow = scatter ? mapped : row;
@@ -61,7 +62,7 @@ __global__ void __launch_bounds__(kThreads) move_rows_flat(uint8_t* __restrict__
                                                            int scatter) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
   for (int64_t u = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; u < total_units; u += stride) {
-    const int64_t row = u / units_per_row;
+    const int64_t row = div_small(u, units_per_row, total_units);
     const int64_t col = u - row * units_per_row;
     const int64_t mapped = source_row(ri, row);
     const int64_t srow = scatter ? row : mapped;
@@ -163,11 +164,29 @@ struct Elem<F16Tag> {
   }
 };
 
+// Channel of in-row element `elem`. Rows hold < 2^31 elements (checked on the host), so this is
+// 32-bit unsigned division (a short v_rcp_iflag sequence) instead of the long 64-bit expansion.
+__device__ __forceinline__ int affine_channel(const Affine& a, int64_t elem) {
+  return static_cast<int>((static_cast<uint32_t>(elem) / static_cast<uint32_t>(a.plane)) %
+                          static_cast<uint32_t>(a.channels));
+}
+
 __device__ __forceinline__ void apply_affine(const Affine& a, int64_t elem, float (&f)[8]) {
   if (!a.enabled) return;
   // 8 consecutive elements share a channel when plane % 8 == 0 (checked on host).
-  const int ch = static_cast<int>((elem / a.plane) % a.channels);
-  const float s = a.scale[ch], b = a.bias[ch];
+  const int ch = affine_channel(a, elem);
+  // <= 4 channels (RGB / RGBA): select among values loaded with constant indices
+  // (scalar kernel-argument loads) instead of a per-lane dynamic load.
+  float s, b;
+  if (a.channels <= 4) {
+    const float s0 = a.scale[0], s1 = a.scale[1], s2 = a.scale[2], s3 = a.scale[3];
+    const float b0 = a.bias[0], b1 = a.bias[1], b2 = a.bias[2], b3 = a.bias[3];
+    s = ch == 0 ? s0 : (ch == 1 ? s1 : (ch == 2 ? s2 : s3));
+    b = ch == 0 ? b0 : (ch == 1 ? b1 : (ch == 2 ? b2 : b3));
+  } else {
+    s = a.scale[ch];
+    b = a.bias[ch];
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) f[i] = fmaf(f[i], s, b);
 }
@@ -177,8 +196,9 @@ __global__ void __launch_bounds__(kThreads) convert_rows_chunked(Tout* __restric
                                                                  int64_t row_elems, int64_t chunks_per_row,
                                                                  int64_t n_tiles, RowIndex ri, Affine aff) {
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-  const int64_t row = tile / chunks_per_row;
-  const int64_t chunk = tile % chunks_per_row;
+  // tiles < 2^31 (host-checked): 32-bit division, not the 64-bit expansion
+  const int64_t row = static_cast<uint32_t>(tile) / static_cast<uint32_t>(chunks_per_row);
+  const int64_t chunk = static_cast<uint32_t>(tile) - static_cast<uint32_t>(row) * static_cast<uint32_t>(chunks_per_row);
   const int64_t srow = source_row(ri, row);
   const Tin* s = src + srow * row_elems;
   Tout* d = dst + row * row_elems;
@@ -200,34 +220,44 @@ __global__ void __launch_bounds__(kThreads) convert_rows_chunked(Tout* __restric
   }
 }
 
-// uint8 sources: 16 elements per lane per access (16 B loads, 2 x 16 B bf16 stores).
+// uint8 sources: 8 elements (8 B) per lane per load, 8 outputs (16 B of bf16) per
+// lane per store, so every load AND every store instruction of a wave covers one
+// contiguous span (512 B in, 1 KB out). (16 B u8 loads -> 2 x 16 B stores left
+// each store instruction with 16 B holes between lanes: 85-87% of HBM.) The
+// kU raw loads are all issued before any conversion: the kernel is bound by
+// bytes in flight per CU (16 KB of loads per workgroup).
+constexpr int kU8Loads = 8;
+
 template <typename Tout>
 __global__ void __launch_bounds__(kThreads) convert_u8_rows_chunked(Tout* __restrict__ dst,
                                                                     const uint8_t* __restrict__ src, int64_t row_elems,
                                                                     int64_t chunks_per_row, int64_t n_tiles, RowIndex ri,
                                                                     Affine aff) {
-  constexpr int kU = 2;
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-  const int64_t row = tile / chunks_per_row;
-  const int64_t chunk = tile % chunks_per_row;
+  // tiles < 2^31 (host-checked): 32-bit division, not the 64-bit expansion
+  const int64_t row = static_cast<uint32_t>(tile) / static_cast<uint32_t>(chunks_per_row);
+  const int64_t chunk = static_cast<uint32_t>(tile) - static_cast<uint32_t>(row) * static_cast<uint32_t>(chunks_per_row);
   const int64_t srow = source_row(ri, row);
   const uint8_t* s = src + srow * row_elems;
   Tout* d = dst + row * row_elems;
-  const int64_t e0 = (chunk * (kThreads * kU) + threadIdx.x) * 16;
-  float lo[kU][8], hi[kU][8];
+  const int64_t e0 = (chunk * (kThreads * kU8Loads) + threadIdx.x) * 8;
+  uint2 raw[kU8Loads];
 #pragma unroll
-  for (int k = 0; k < kU; ++k) {
-    const int64_t e = e0 + static_cast<int64_t>(k) * kThreads * 16;
-    if (e < row_elems) Elem<uint8_t>::load16(s + e, lo[k], hi[k]);
+  for (int k = 0; k < kU8Loads; ++k) {
+    const int64_t e = e0 + static_cast<int64_t>(k) * kThreads * 8;
+    raw[k] = e < row_elems ? *reinterpret_cast<const uint2*>(s + e) : uint2{};
   }
 #pragma unroll
-  for (int k = 0; k < kU; ++k) {
-    const int64_t e = e0 + static_cast<int64_t>(k) * kThreads * 16;
+  for (int k = 0; k < kU8Loads; ++k) {
+    const int64_t e = e0 + static_cast<int64_t>(k) * kThreads * 8;
     if (e < row_elems) {
-      apply_affine(aff, e, lo[k]);
-      apply_affine(aff, e + 8, hi[k]);
-      Elem<Tout>::store8(d + e, lo[k]);
-      Elem<Tout>::store8(d + e + 8, hi[k]);
+      float f[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) f[i] = static_cast<float>((raw[k].x >> (8 * i)) & 0xffu);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) f[4 + i] = static_cast<float>((raw[k].y >> (8 * i)) & 0xffu);
+      apply_affine(aff, e, f);
+      Elem<Tout>::store8(d + e, f);
     }
   }
   }
@@ -238,11 +268,11 @@ __global__ void __launch_bounds__(kThreads) convert_rows_flat(Tout* __restrict__
                                                               int64_t row_elems, int64_t total, RowIndex ri, Affine aff) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
   for (int64_t e = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; e < total; e += stride) {
-    const int64_t row = e / row_elems;
+    const int64_t row = div_small(e, row_elems, total);
     const int64_t col = e - row * row_elems;
     float v = Elem<Tin>::load1(src + source_row(ri, row) * row_elems + col);
     if (aff.enabled) {
-      const int ch = static_cast<int>((col / aff.plane) % aff.channels);
+      const int ch = affine_channel(aff, col);
       v = fmaf(v, aff.scale[ch], aff.bias[ch]);
     }
     Elem<Tout>::store1(dst + e, v);
@@ -284,8 +314,8 @@ template <typename Tin, typename Tout>
 void launch_convert(void* dst, const void* src, int64_t n_rows, int64_t row_elems, const RowIndex& ri, const Affine& aff,
                     bool vec_ok, int64_t max_blocks, hipStream_t st) {
   if constexpr (sizeof(Tin) == 1) {
-    if (vec_ok && row_elems % 16 == 0 && row_elems >= kThreads * 16) {
-      const int64_t chunks = (row_elems + kThreads * 2 * 16 - 1) / (kThreads * 2 * 16);
+    if (vec_ok && row_elems >= kThreads * 8) {  // vec_ok: row_elems % 8 == 0, 16 B aligned
+      const int64_t chunks = (row_elems + kThreads * kU8Loads * 8 - 1) / (kThreads * kU8Loads * 8);
       hipLaunchKernelGGL((convert_u8_rows_chunked<Tout>), tile_grid(n_rows * chunks, max_blocks), dim3(kThreads), 0,
                          st, static_cast<Tout*>(dst), static_cast<const uint8_t*>(src), row_elems, chunks,
                          n_rows * chunks, ri, aff);
@@ -327,6 +357,8 @@ __global__ void __launch_bounds__(kThreads) feistel_fill(int64_t* __restrict__ o
 int gather_rows(void* dst, int32_t out_dt, const void* src, int32_t in_dt, int64_t n_rows, int64_t row_elems,
                 const RowIndex& ri, const Affine& aff, int scatter, int64_t max_blocks, hipStream_t st) {
   if (n_rows <= 0 || row_elems <= 0) return 0;
+  // the chunked kernels index tiles and in-row elements with 32-bit arithmetic
+  if (n_rows >= (int64_t{1} << 31) || n_rows * row_elems >= (int64_t{1} << 40)) return -4;
   const bool same = (out_dt == in_dt) && !aff.enabled;
   if (same) {
     const int64_t row_bytes = row_elems * dtype_size(in_dt);
@@ -340,6 +372,7 @@ int gather_rows(void* dst, int32_t out_dt, const void* src, int32_t in_dt, int64
     return static_cast<int>(hipGetLastError());
   }
   if (scatter) return -2;  // converting scatters are not needed by the loader
+  if (row_elems >= (int64_t{1} << 31) || (aff.enabled && aff.plane >= (int64_t{1} << 31))) return -4;
   const uintptr_t align = reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src);
   bool vec_ok = (row_elems % 8 == 0) && (align % 16 == 0);
   if (aff.enabled && (aff.plane % 8 != 0)) vec_ok = false;

@@ -104,7 +104,7 @@ def test_feistel_device_matches_host(n):
 
 
 @pytest.mark.parametrize("in_dtype", [torch.uint8, torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("hw", [(224, 224), (17, 13), (32, 32)])
+@pytest.mark.parametrize("hw", [(224, 224), (17, 13), (32, 32), (45, 45), (2, 8)])
 def test_collate_hwc_to_chw(in_dtype, hw):
     n, c = 24, 3
     src = (torch.rand((n, *hw, c)) * 255).to(in_dtype)
