@@ -10,11 +10,6 @@
 
 namespace ddl {
 
-// device.hip ----------------------------------------------------------------
-// Workgroups of `kernel` resident on the current device at once (CUs x per-CU
-// occupancy for this block size / LDS); cached; 0 if the query fails.
-int resident_blocks(const void* kernel, int threads, size_t lds);
-
 // permute.hip ---------------------------------------------------------------
 // dst[r, :] = cast(src[source_row(ri, r), :]) (scatter=0)
 // dst[source_row(ri, r), :] = src[r, :]       (scatter=1, same dtype only)
