@@ -195,7 +195,8 @@ def main(argv=None) -> int:
                     "exchange_fraction": args.exchange,
                     "source_dtype": args.source_dtype,
                 },
-                "gpu_idle_pct": None if not idle or math.isnan(idle["gpu_idle_pct"]) else round(idle["gpu_idle_pct"], 3),
+                "gpu_idle_pct": (None if not idle or math.isnan(idle["gpu_idle_pct"])
+                                 else round(idle["gpu_idle_pct"], 3)),
                 "train_step": None if not idle else {
                     "model": f"PatchMLP dim={args.model_dim} depth={args.model_depth} fwd+bwd+SGD bf16"
                              + (" (DDP all-reduce)" if env.world_size > 1 else ""),
