@@ -97,7 +97,7 @@ def main(argv=None) -> int:
             producer, args.batch, conn, n_epochs, args.exchange, args.exchange_method, env.rank, env.world_size,
             env=env, device=dev, out_dtype=torch.bfloat16, shuffle=args.shuffle, seed=args.seed,
             n_slots=args.slots, prefetch_depth=args.depth, normalize=norm)
-        acc = torch.zeros(1, dtype=torch.int64, device=dev)
+        acc = ops.ChecksumAccumulator(dev)  # one streaming launch per batch
 
         def batches():
             while True:
@@ -120,12 +120,12 @@ def main(argv=None) -> int:
         # ---------------- phase 1: feed rate
         for _ in range(args.warmup):
             (x,) = next(it)
-            ops.checksum(x, out=acc)
+            acc.add(x)
         barrier()
         t0 = time.perf_counter()
         for _ in range(args.steps):
             (x,) = next(it)
-            ops.checksum(x, out=acc)
+            acc.add(x)
         sync()
         t1 = time.perf_counter()
         barrier()

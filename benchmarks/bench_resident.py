@@ -54,7 +54,7 @@ def main(argv=None):
             for depth in [int(x) for x in a.depths.split(",")]:
                 dl = ResidentGlobalLoader(src, a.batch * env.world_size, env, seed=1, depth=depth,
                                           out_dtype=torch.bfloat16, normalize=norm)
-                acc = torch.zeros(1, dtype=torch.int64, device=dev)
+                acc = ops.ChecksumAccumulator(dev)  # one streaming launch per batch
 
                 def gen():
                     while True:
@@ -62,13 +62,13 @@ def main(argv=None):
 
                 it = gen()
                 for _ in range(a.warmup):
-                    ops.checksum(next(it), out=acc)
+                    acc.add(next(it))
                 torch.cuda.synchronize()
                 if env.world_size > 1:
                     dist.barrier(group=env.control_group)
                 t0 = time.perf_counter()
                 for _ in range(a.steps):
-                    ops.checksum(next(it), out=acc)
+                    acc.add(next(it))
                 torch.cuda.synchronize()
                 el = time.perf_counter() - t0
                 if env.world_size > 1:

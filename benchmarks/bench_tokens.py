@@ -61,7 +61,7 @@ def main(argv=None):
             dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(source, gb, a.seq_len, a.mode), a.batch, conn,
                                                n_epochs, mode="indexed", env=env, collate="tokens", auto_mark=True)
             dev = torch.device(env.device)
-            acc = torch.zeros(1, dtype=torch.int64, device=dev)
+            acc = ops.ChecksumAccumulator(dev)  # one streaming launch per batch
 
             def gen():
                 while True:
@@ -71,7 +71,7 @@ def main(argv=None):
             real = 0
             for _ in range(a.warmup):
                 b = next(it)
-                ops.checksum(b["input_ids"], out=acc)
+                acc.add(b["input_ids"])
             torch.cuda.synchronize()
             if env.world_size > 1:
                 dist.barrier(group=env.control_group)
@@ -79,7 +79,7 @@ def main(argv=None):
             rows = 0
             for _ in range(a.steps):
                 b = next(it)
-                ops.checksum(b["input_ids"], out=acc)
+                acc.add(b["input_ids"])
                 rows += b["input_ids"].shape[0]
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0

@@ -59,7 +59,7 @@ def main(argv=None):
             for mb in [int(x) for x in a.blocks.split(",")]:
                 dl = ZeroCopyLoader(src, a.batch * env.world_size, env, seed=1, out_dtype=torch.bfloat16,
                                     normalize=norm, max_blocks=mb, depth=2)
-                acc = torch.zeros(1, dtype=torch.int64, device=dev)
+                acc = ops.ChecksumAccumulator(dev)  # one streaming launch per batch
 
                 def gen():
                     while True:
@@ -67,11 +67,11 @@ def main(argv=None):
 
                 it = gen()
                 for _ in range(a.warmup):
-                    ops.checksum(next(it), out=acc)
+                    acc.add(next(it))
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 for _ in range(a.steps):
-                    ops.checksum(next(it), out=acc)
+                    acc.add(next(it))
                 torch.cuda.synchronize()
                 el = time.perf_counter() - t0
                 rate = a.batch * a.steps * env.world_size / el

@@ -63,6 +63,9 @@ def main():
     report("scatter_rows bf16", t, 2 * B * img * 2)
     t = bench(lambda: ops.checksum(out_bf16))
     report("checksum (reduce)", t, B * img * 2)
+    cacc = ops.ChecksumAccumulator(dev)
+    t = bench(lambda: cacc.add(out_bf16))
+    report("checksum accumulate (streaming consumer)", t, B * img * 2)
     t = bench(lambda: ops.feistel_indices(FeistelPermutation(1 << 24, 3, 3), 0, 1 << 24, device=dev), reps=10)
     report("feistel_indices 16M", t, (1 << 24) * 8)
     # pointwise (reference CI shape): 100,520 x 9 f32 window, 4096-row batch split (3,5,1)

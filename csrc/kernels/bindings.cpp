@@ -296,6 +296,22 @@ PYBIND11_MODULE(_ddl_hip, m) {
       py::arg("stream"));
   m.attr("CHECKSUM_MAX_BLOCKS") = ddl::kChecksumMaxBlocks;
   m.def(
+      "checksum_accumulate",
+      [](uintptr_t ptr, int64_t bytes, uintptr_t partials, int64_t n_partials, uintptr_t stream) {
+        check_rc(ddl::checksum_accumulate(as_ptr<const void>(ptr), bytes, as_ptr<uint64_t>(partials), n_partials,
+                                          as_stream(stream)),
+                 "checksum_accumulate");
+      },
+      py::arg("ptr"), py::arg("bytes"), py::arg("partials"), py::arg("n_partials"), py::arg("stream"));
+  m.def(
+      "checksum_finalize",
+      [](uintptr_t partials, int64_t n_partials, uintptr_t out, uintptr_t stream) {
+        check_rc(ddl::checksum_finalize(as_ptr<const uint64_t>(partials), n_partials, as_ptr<uint64_t>(out),
+                                        as_stream(stream)),
+                 "checksum_finalize");
+      },
+      py::arg("partials"), py::arg("n_partials"), py::arg("out"), py::arg("stream"));
+  m.def(
       "column_stats",
       [](uintptr_t src, int64_t n, int64_t cols, uintptr_t sum, uintptr_t sumsq, uintptr_t mn, uintptr_t mx,
          uintptr_t stream) {

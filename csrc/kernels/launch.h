@@ -75,6 +75,10 @@ int pad_pack_tokens(const TokenSpec& spec, hipStream_t st);
 constexpr int64_t kChecksumMaxBlocks = 1024;
 int checksum_words(const void* ptr, int64_t bytes, uint64_t* out, uint64_t* scratch, int64_t scratch_len,
                    hipStream_t st);
+// Streaming form: partials[b] += block b's share (grid = n_partials, fixed for the
+// life of the accumulator); checksum_finalize adds sum(partials) into *out.
+int checksum_accumulate(const void* ptr, int64_t bytes, uint64_t* partials, int64_t n_partials, hipStream_t st);
+int checksum_finalize(const uint64_t* partials, int64_t n_partials, uint64_t* out, hipStream_t st);
 // Per-column sum / sum of squares / min / max of an [n, cols] f32 matrix
 // (reference harness normalisation stats, tests/run_ddl.py:45-77).
 int column_stats(const float* src, int64_t n, int64_t cols, float* out_sum, float* out_sumsq, float* out_min,

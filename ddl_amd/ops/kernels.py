@@ -522,6 +522,46 @@ def checksum(x: torch.Tensor, out: torch.Tensor | None = None, stream=None) -> t
     return out
 
 
+class ChecksumAccumulator:
+    """Running checksum of many tensors: one streaming launch per ``add``.
+
+    Each of ``n_partials`` workgroups adds its share of every tensor into its own
+    64-bit slot (single writer, stream-ordered, no atomics); ``value()`` reduces
+    the slots. Same sum as ``checksum`` (u64 wrap-around of the 32-bit words).
+    Launches on one accumulator must be ordered on one stream.
+    """
+
+    def __init__(self, device, n_partials: int = 1024):
+        self.device = torch.device(device)
+        self.n = int(n_partials)
+        self.partials = torch.zeros(self.n, dtype=torch.int64, device=self.device) if self.device.type == "cuda" \
+            else None
+        self._cpu = 0
+
+    def add(self, x: torch.Tensor, stream=None) -> None:
+        if not x.is_contiguous():
+            raise ValueError("checksum needs a contiguous tensor")
+        nbytes = x.numel() * x.element_size()
+        if self.partials is None or not x.is_cuda:
+            self._cpu = (self._cpu + ref_checksum(x)) & ((1 << 64) - 1)
+            return
+        if x.device != self.device:
+            raise ValueError(f"tensor on {x.device}, accumulator on {self.device}")
+        _native.hip().checksum_accumulate(ptr=x.data_ptr(), bytes=nbytes - nbytes % 4,
+                                          partials=self.partials.data_ptr(), n_partials=self.n,
+                                          stream=_stream_handle(stream))
+
+    def value(self, stream=None) -> int:
+        """Sum so far as an unsigned 64-bit int (synchronises with the accumulating stream)."""
+        tot = self._cpu
+        if self.partials is not None:
+            out = torch.zeros(1, dtype=torch.int64, device=self.device)
+            _native.hip().checksum_finalize(partials=self.partials.data_ptr(), n_partials=self.n,
+                                            out=out.data_ptr(), stream=_stream_handle(stream))
+            tot += int(out.item())
+        return tot & ((1 << 64) - 1)
+
+
 def column_affine(stats: dict, mode: str = "standard", area_weighted: bool = False) -> tuple[list, list]:
     """(scale, bias) per column so that x*scale + bias normalises like the reference harness.
 

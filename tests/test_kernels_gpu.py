@@ -254,3 +254,20 @@ def test_normalize_columns_matches_reference_harness(mode):
         # the harness scales targets by max|x| instead of the half range: compare the parameter/x columns
         out, ref = out[:, :3], ref[:, :3]
     np.testing.assert_allclose(out, ref, rtol=2e-4, atol=2e-4)
+
+
+def test_checksum_accumulator_matches_reference():
+    xs = [torch.randint(0, 256, (n,), dtype=torch.uint8) for n in (4096 * 999 + 8, 1 << 22, 64, 12345 * 4)]
+    acc = ops.ChecksumAccumulator(_dev())
+    for _ in range(3):
+        for x in xs:
+            acc.add(x.to(_dev()))
+    expect = 3 * sum(ops.ref_checksum(x) for x in xs) & ((1 << 64) - 1)
+    assert acc.value() == expect
+    acc.add(xs[0].to(_dev()))  # keeps accumulating after a read
+    assert acc.value() == (expect + ops.ref_checksum(xs[0])) & ((1 << 64) - 1)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        out = ops.checksum(xs[1].to(_dev()))
+    s.synchronize()
+    assert out.item() & ((1 << 64) - 1) == ops.ref_checksum(xs[1])
