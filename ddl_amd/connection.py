@@ -202,6 +202,16 @@ class Connection:
         for p in self.pipes:
             p.send("barrier")
 
+    def lock_windows(self) -> None:
+        """Reference ``Lock_all`` passive-target epoch (ddl/connection.py:39-43).
+
+        Nothing to do here: slot ownership is the arena's per-slot state word
+        (acquire/release atomics + futex), so there is no RMA epoch to open.
+        """
+
+    def unlock_windows(self) -> None:
+        """Reference ``Unlock_all`` (ddl/connection.py:45-49); see ``lock_windows``."""
+
     # ------------------------------------------------------------ hand-off
     def acquire(self, p: int, s: int, timeout_s: float | None = None) -> dict:
         """Wait until producer ``p`` publishes slot ``s``; take it (READY -> HELD).
