@@ -374,7 +374,8 @@ class DistributedDataLoader:
                 x = ops.collate_hwc_to_chw(win, perm=perm, base=local * B, n_rows=B, out_dtype=out_dtype,
                                            mean=norm.get("mean"), std=norm.get("std"))
                 return (x,)
-            if (self.contiguous or self.copy_batches) and len(splits) > 1 and len(self.sample_shape) == 1:
+            if (self.contiguous or self.copy_batches) and len(splits) > 1 and len(self.sample_shape) == 1 \
+                    and norm is None:
                 return ops.split_columns(win, splits, perm=perm, base=local * B, n_rows=B, out_dtype=out_dtype)
             if perm is None and out_dtype == wdt and norm is None and not self.copy_batches:
                 x = win[local * B:(local + 1) * B]  # zero-copy view (reference semantics)
@@ -383,13 +384,16 @@ class DistributedDataLoader:
                 if norm is not None:
                     plane = int(math.prod(self.sample_shape[1:])) if len(self.sample_shape) > 1 else 1
                     c = self.sample_shape[0] if len(self.sample_shape) > 1 else len(norm.get("mean", [0]))
-                    sc, bi = ops.norm_affine(c, norm.get("mean"), norm.get("std"), norm.get("scale"), norm.get("bias"))
+                    sc, bi = ops.norm_affine(c, norm.get("mean"), norm.get("std"), norm.get("scale"),
+                                             norm.get("bias"), ops.pixel_max(wdt))
                     kw = dict(scale=sc, bias=bi, plane=plane)
                 x = ops.gather_rows(win, perm=perm, base=local * B, n_rows=B, out_dtype=out_dtype, **kw)
         if len(splits) == 1:
             return (x,)
-        flat = x.reshape(B, -1)
-        return tuple(torch.split(flat, splits, dim=1))
+        parts = torch.split(x.reshape(B, -1), splits, dim=1)
+        if self.contiguous or self.copy_batches:  # normalised tabular rows: own each column group
+            return tuple(t.contiguous() for t in parts)
+        return parts
 
     def __iter__(self) -> Iterator:
         n = self._len

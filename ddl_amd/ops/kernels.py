@@ -232,7 +232,7 @@ def ref_collate_hwc_to_chw(src, index=None, perm=None, base=0, n_rows=None, out_
     n_rows = _check_rows(x, index, perm, base, n_rows)
     rows = x.index_select(0, _ref_rows(x.shape[0], n_rows, index, perm, base).to(x.device))
     c = rows.shape[-1]
-    sc, bi = norm_affine(c, mean, std, scale, bias)
+    sc, bi = norm_affine(c, mean, std, scale, bias, pixel_max(x.dtype))
     y = rows.double().movedim(-1, 1)  # [B, C, H, W]
     if sc:
         s = torch.tensor(sc, dtype=torch.float64, device=y.device).view(1, c, *([1] * (y.dim() - 2)))
@@ -241,14 +241,23 @@ def ref_collate_hwc_to_chw(src, index=None, perm=None, base=0, n_rows=None, out_
     return y.float().to(out_dtype).contiguous()
 
 
-def norm_affine(c, mean=None, std=None, scale=None, bias=None):
-    """(x/255 - mean)/std  ==  x*scale + bias  with scale=1/(255*std), bias=-mean/std."""
+def pixel_max(dtype) -> float:
+    """Value range the mean/std convention refers to: uint8 pixels are read as x/255
+    (torchvision convention on [0, 1] images); every other dtype as raw values."""
+    return 255.0 if _dtypes.to_torch_dtype(dtype) == torch.uint8 else 1.0
+
+
+def norm_affine(c, mean=None, std=None, scale=None, bias=None, in_max: float = 255.0):
+    """(x/in_max - mean)/std  ==  x*scale + bias  with scale=1/(in_max*std), bias=-mean/std.
+
+    ``in_max`` is ``pixel_max(source dtype)``: 255 for uint8 sources, 1 otherwise.
+    """
     if mean is not None or std is not None:
         mean = list(mean) if mean is not None else [0.0] * c
         std = list(std) if std is not None else [1.0] * c
         if len(mean) != c or len(std) != c:
             raise ValueError("mean/std must have one entry per channel")
-        return [1.0 / (255.0 * s) for s in std], [-m / s for m, s in zip(mean, std)]
+        return [1.0 / (in_max * s) for s in std], [-m / s for m, s in zip(mean, std)]
     return _affine_lists(scale, bias)
 
 
@@ -257,8 +266,9 @@ def collate_hwc_to_chw(src, index: torch.Tensor | None = None, *, perm: FeistelP
                        scale=None, bias=None, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
     """[N, H, W, C] (u8/f32/bf16, HWC) rows -> [B, C, H, W] normalised bf16/f32 (LDS-staged de-interleave).
 
-    ``mean``/``std`` follow the torchvision convention on [0, 1] pixels
-    (``(x/255 - mean)/std``); alternatively pass a raw ``scale``/``bias``.
+    ``mean``/``std`` follow the torchvision convention on [0, 1] pixels for uint8
+    sources (``(x/255 - mean)/std``) and apply to raw values for float sources;
+    alternatively pass a raw ``scale``/``bias``.
     """
     out_dtype = _dtypes.to_torch_dtype(out_dtype)
     if src.dim() < 3:
@@ -273,7 +283,7 @@ def collate_hwc_to_chw(src, index: torch.Tensor | None = None, *, perm: FeistelP
     n_rows = _check_rows(src, index, perm, base, n_rows)
     spatial = tuple(src.shape[1:-1])
     pixels = int(math.prod(spatial))
-    sc, bi = norm_affine(c, mean, std, scale, bias)
+    sc, bi = norm_affine(c, mean, std, scale, bias, pixel_max(src.dtype))
     if out is None:
         out = torch.empty((n_rows, c) + spatial, dtype=out_dtype, device=src.device)
     _native.hip().collate_hwc_to_chw(

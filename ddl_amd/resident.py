@@ -129,7 +129,8 @@ class PrefetchedIndexedLoader:
             return {}
         c = self.sample_shape[0] if len(self.sample_shape) > 1 else len(norm.get("mean", [0]))
         plane = int(math.prod(self.sample_shape[1:])) if len(self.sample_shape) > 1 else 1
-        sc, bi = ops.norm_affine(c, norm.get("mean"), norm.get("std"), norm.get("scale"), norm.get("bias"))
+        sc, bi = ops.norm_affine(c, norm.get("mean"), norm.get("std"), norm.get("scale"), norm.get("bias"),
+                                 ops.pixel_max(self.src_dtype))
         return dict(scale=sc, bias=bi, plane=plane)
 
     def _total_steps(self) -> int | None:

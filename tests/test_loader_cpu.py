@@ -103,6 +103,28 @@ def test_auto_mark_dataloader_dropin_with_slots():
         assert rows[:, 1].unique().tolist() == [e % 2]
 
 
+@pytest.mark.parametrize("auto_mark", [False, True])
+def test_column_normalisation_applies_with_owned_batches(auto_mark):
+    # per-column affine on tabular windows; owned (contiguous) batches must not skip it
+    mean, std = [1.0, 2.0, 3.0, 4.0], [2.0, 4.0, 0.5, 1.0]
+    with ddl_amd.start(n_producers=1) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(IdProducer(20, 4, dtype="float32"), 5, conn, 1, env=env,
+                                           auto_mark=auto_mark, normalize={"mean": mean, "std": std})
+        got = []
+        for b in dl:
+            assert all(t.is_contiguous() for t in b) or not auto_mark
+            got.append(torch.cat(b, 1).clone())
+            if not auto_mark:
+                dl.mark(Marker.END_OF_BATCH)
+        if not auto_mark:
+            dl.mark(Marker.END_OF_EPOCH)
+    rows = torch.cat(got)
+    i = torch.arange(20, dtype=torch.float32)
+    raw = torch.stack([torch.zeros(20), torch.zeros(20), i, torch.zeros(20)], 1)
+    ref = (raw - torch.tensor(mean)) / torch.tensor(std)
+    torch.testing.assert_close(rows, ref)
+
+
 def test_host_device_shuffle_uses_feistel_order():
     from ddl_amd.permutation import FeistelPermutation
 
