@@ -46,6 +46,7 @@ from .ops import _dtypes
 from .permutation import FeistelPermutation
 from .types import DDLEnv, Marker, MetaData_Consumer_To_Producer, MetaData_Producer_To_Consumer
 from .utils.logging import for_all_methods, logger, with_logging
+from .utils import streams
 from .utils.tracing import LoaderMetrics, trace_range
 
 STATE_VERSION = 1
@@ -313,7 +314,7 @@ class DistributedDataLoader:
         """Build batch ``local`` of window ``sw`` on the batch stream; returns (outputs, ready event)."""
         bs = self._batch_stream
         bs.wait_event(self._stager.ready_events[sw.buffer])
-        with torch.cuda.stream(bs):
+        with streams.on_stream(bs):
             out = self._batch_from_window(sw, p, s, local)
             ev = torch.cuda.Event()
             ev.record(bs)
@@ -325,7 +326,7 @@ class DistributedDataLoader:
         stream only waits on an event (no host sync)."""
         hit = self._lookahead.pop((self.window, local), None)
         out, ev = hit if hit is not None else self._enqueue_batch(sw, p, s, local)
-        cur = torch.cuda.current_stream(self.device)
+        cur = streams.current(self.device.index)
         cur.wait_event(ev)
         for t in (out.values() if isinstance(out, dict) else out):
             if isinstance(t, torch.Tensor) and t.is_cuda:

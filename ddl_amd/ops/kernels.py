@@ -53,7 +53,8 @@ class HostRows:
 
 def _stream_handle(stream) -> int:
     if stream is None:
-        return torch.cuda.current_stream().cuda_stream
+        # == torch.cuda.current_stream().cuda_stream, without building a Stream object (per-launch host cost)
+        return torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice())
     if isinstance(stream, int):
         return stream
     return stream.cuda_stream
@@ -317,7 +318,13 @@ def split_columns(src, splits: Sequence[int], index: torch.Tensor | None = None,
     if out_dtype != src.dtype and out_dtype not in (torch.bfloat16, torch.float32):
         raise TypeError("split_columns casts to bf16 or f32 only (same-dtype splits are raw copies)")
     n_rows = _check_rows(src, index, perm, base, n_rows)
-    outs = tuple(torch.empty((n_rows, w), dtype=out_dtype, device=src.device) for w in splits)
+    # one allocation, k contiguous [n_rows, w] views (a caching-allocator call costs ~2.5 us of host time)
+    buf = torch.empty(n_rows * sum(splits), dtype=out_dtype, device=src.device)
+    outs, off = [], 0
+    for w in splits:
+        outs.append(buf[off:off + n_rows * w].view(n_rows, w))
+        off += n_rows * w
+    outs = tuple(outs)
     _native.hip().split_columns(
         dsts=[o.data_ptr() for o in outs], widths=[int(w) for w in splits], out_dt=_dtypes.code(out_dtype),
         src=_src_addr(src), in_dt=_dtypes.code(src.dtype), n_rows=n_rows, n_values=src.shape[1],

@@ -14,34 +14,52 @@
 
 from __future__ import annotations
 
-import contextlib
 import dataclasses
 import os
 import time
-from typing import Any, Iterator
+from typing import Any
 
 _ROCTX_ENABLED = os.environ.get("DDL_ROCTX", "1") != "0"
 
 
-@contextlib.contextmanager
-def trace_range(name: str) -> Iterator[None]:
-    pushed = False
-    if _ROCTX_ENABLED:
-        try:
-            import torch
+_ROCTX = None  # (push, pop) once resolved; () when markers are off or there is no GPU
 
-            if torch.cuda.is_available():
-                torch.cuda.nvtx.range_push(name)
-                pushed = True
-        except Exception:
-            pushed = False
-    try:
-        yield
-    finally:
-        if pushed:
-            import torch
 
-            torch.cuda.nvtx.range_pop()
+def _roctx():
+    global _ROCTX
+    if _ROCTX is None:
+        _ROCTX = ()
+        if _ROCTX_ENABLED:
+            try:
+                import torch
+
+                if torch.cuda.is_available():
+                    _ROCTX = (torch.cuda.nvtx.range_push, torch.cuda.nvtx.range_pop)
+            except Exception:
+                _ROCTX = ()
+    return _ROCTX
+
+
+class trace_range:  # noqa: N801  (used like a function: ``with trace_range("name"):``)
+    """roctx range around a block (a plain class: this sits on the per-batch host path)."""
+
+    __slots__ = ("name", "pushed")
+
+    def __init__(self, name: str):
+        self.name = name
+        self.pushed = False
+
+    def __enter__(self):
+        r = _ROCTX if _ROCTX is not None else _roctx()
+        if r:
+            r[0](self.name)
+            self.pushed = True
+        return self
+
+    def __exit__(self, *exc):
+        if self.pushed:
+            _ROCTX[1]()
+        return False
 
 
 @dataclasses.dataclass
