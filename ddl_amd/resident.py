@@ -47,6 +47,7 @@ from .ops import _dtypes
 from .permutation import EpochOrder
 from .types import DDLEnv
 from .utils.logging import logger
+from .utils import streams
 from .utils.tracing import trace_range
 
 STATE_VERSION = 1
@@ -155,7 +156,7 @@ class PrefetchedIndexedLoader:
             tq, batch, ev = self._queue.popleft()
             assert tq == t, (tq, t)
             if ev is not None:
-                cur = torch.cuda.current_stream(self.device)
+                cur = streams.current(self.device.index)
                 cur.wait_event(ev)
                 batch.record_stream(cur)
             self.cursor = t - self.epoch * bpe
@@ -350,7 +351,7 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
         e, g = divmod(t, self.order.batches_per_epoch)
         perm = self.order.perm(e)
         kw = self._norm_kw()
-        ctx = torch.cuda.stream(self.prep_stream) if self.prep_stream is not None else contextlib.nullcontext()
+        ctx = streams.on_stream(self.prep_stream) if self.prep_stream is not None else contextlib.nullcontext()
         with ctx, trace_range("ddl.resident.assemble"):
             if self.W == 1:
                 batch = ops.gather_rows(self.shard, perm=perm, base=g * self.GB, n_rows=self.LB,

@@ -40,6 +40,7 @@ import torch
 from . import _native
 from .exceptions import DDLTimeoutError, ShutdownError
 from .utils.logging import logger
+from .utils import streams
 from .utils.tracing import trace_range
 
 
@@ -148,7 +149,7 @@ class WindowStager:
             if self.depth >= 2 and w + 1 < self.first + self.total:
                 self._post(w + 1)  # one window ahead, in lockstep on every rank
         sw = self._wait_staged(w)
-        torch.cuda.current_stream(self.device).wait_event(self.ready_events[sw.buffer])
+        streams.current(self.device.index).wait_event(self.ready_events[sw.buffer])
         return sw
 
     def peek(self, w: int) -> StagedWindow | None:
@@ -193,7 +194,7 @@ class WindowStager:
                 return
             self._posted.discard(w)
             ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(self.device))
+            ev.record(streams.current(self.device.index))
             self.free_events[sw.buffer] = ev
             self._released_upto = max(self._released_upto, w + 1)
             self._cv.notify_all()

@@ -34,6 +34,7 @@ from .ops import _dtypes
 from .permutation import EpochOrder
 from .resident import PrefetchedIndexedLoader, _source_address, _source_geometry
 from .types import DDLEnv
+from .utils import streams
 
 _PAGE = 4096
 
@@ -103,7 +104,7 @@ class ZeroCopyLoader(PrefetchedIndexedLoader):
         if self.prep_stream is None:
             return ops.gather_rows(self.rows, perm=self.order.perm(e), base=base, n_rows=self.LB,
                                    out_dtype=self.out_dtype, **kw), None
-        with torch.cuda.stream(self.prep_stream):
+        with streams.on_stream(self.prep_stream):
             batch = ops.gather_rows(self.rows, perm=self.order.perm(e), base=base, n_rows=self.LB,
                                     out_dtype=self.out_dtype, max_blocks=self.max_blocks, **kw)
             ev = torch.cuda.Event()
