@@ -109,14 +109,4 @@ inline int dtype_size(int32_t d) {
   return 0;
 }
 
-// XCD-aware block remap (guide §5.5 T1): consecutive logical tiles land on the
-// same XCD (blocks b and b+8 share an XCD under round-robin dispatch), so the
-// L2 of one XCD sees one contiguous span of every row instead of 1/8 of all.
-// Performance only -- any placement is correct.
-__device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nblocks) {
-  const uint32_t per = nblocks / 8u;
-  if (per == 0u || b >= per * 8u) return b;
-  return (b % 8u) * per + (b / 8u);
-}
-
 }  // namespace ddl
