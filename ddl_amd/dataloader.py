@@ -398,7 +398,7 @@ class DistributedDataLoader:
 
     def __iter__(self) -> Iterator:
         n = self._len
-        start = self.epoch_batch if self.auto_mark else 0  # resumed mid-epoch: continue at the cursor
+        start = self.epoch_batch  # 0 at an epoch start; the resumed cursor after load_state_dict
         for i in range(start, n):
             item = self[i]
             self._pending = self.auto_mark  # yielded, not yet marked: counts as consumed in state_dict
@@ -548,12 +548,11 @@ class DistributedDataLoader:
             self.batch = 0
             self._resume_check = sd
             return
-        if sd.get("batch", 0):
-            logger.warning("resuming mid-window: the partially consumed window is skipped")
-        skip = 1 if sd.get("batch", 0) else 0
-        self.window = int(sd["window"]) + skip
-        self.window_in_epoch = int(sd["window_in_epoch"]) + skip
-        self.batch = 0
+        # exact resume, also mid-window: the producers restart at this window's round
+        # (deterministic content per round) and the cursor skips its consumed batches
+        self.window = int(sd["window"])
+        self.window_in_epoch = int(sd["window_in_epoch"])
+        self.batch = int(sd.get("batch", 0))
         self.epoch_batch = int(sd.get("epoch_batch", 0))
 
     def load_state_dict(self, sd: dict) -> None:

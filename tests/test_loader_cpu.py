@@ -180,6 +180,43 @@ def test_resume_from_state_dict():
         assert torch.equal(a, b)  # the resumed run continues bit-identically
 
 
+@pytest.mark.parametrize("auto_mark", [False, True])
+def test_resume_mid_window_is_exact(auto_mark):
+    """Checkpoint after 6 of 12 batches (windows of 4 batches: mid-window of epoch 1), resume in a fresh job."""
+    kw = dict(env=None, copy_batches=True, shuffle="device", seed=7, auto_mark=auto_mark)
+
+    def run(n_batches, resume=None):
+        rows, sd = [], None
+        with ddl_amd.start(n_producers=3) as (env, conn):
+            dl = ddl_amd.DistributedDataLoader(IdProducer(16, 4), 4, conn, 3, **dict(kw, env=env),
+                                               resume_state=resume)
+            done = 0
+            while dl.epoch < 3 and done < n_batches:
+                for b in dl:
+                    rows.append(torch.cat(b, 1).clone())
+                    done += 1
+                    if not auto_mark:
+                        dl.mark(Marker.END_OF_BATCH)
+                    if done == n_batches:
+                        sd = dl.state_dict()
+                        break
+                else:
+                    if not auto_mark:
+                        dl.mark(Marker.END_OF_EPOCH)
+                    continue
+                break
+            dl.close()
+        return rows, sd
+
+    head, sd = run(6)
+    assert sd["epoch"] == 1 and sd["batch"] == 2 and sd["epoch_batch"] == 2  # mid-window
+    tail, _ = run(10 ** 9, resume=sd)
+    full, _ = run(10 ** 9)
+    assert len(head) + len(tail) == len(full) == 12
+    for a, b in zip(head + tail, full):
+        assert torch.equal(a, b)
+
+
 def test_producer_on_init_failure_is_reported():
     with pytest.raises(PeerDeathError, match="boom in on_init"):
         with ddl_amd.start(n_producers=2) as (env, conn):

@@ -138,3 +138,30 @@ def test_gpu_uint8_normalised_and_hwc_collate():
         for i in range(len(dl)):
             dl.mark(Marker.END_OF_BATCH)
         dl.mark(Marker.END_OF_EPOCH)
+
+
+def test_gpu_resume_mid_window_is_exact():
+    def run(n_batches, resume=None):
+        rows, sd = [], None
+        with ddl_amd.start(n_producers=3) as (env, conn):
+            dl = ddl_amd.DistributedDataLoader(IdProducer(64, 8), 16, conn, 3, env=env, copy_batches=True,
+                                               shuffle="device", seed=5, auto_mark=True, resume_state=resume)
+            assert dl.device.type == "cuda"
+            done = 0
+            while dl.epoch < 3 and done < n_batches:
+                for b in dl:
+                    rows.append(torch.cat(b, 1).cpu())
+                    done += 1
+                    if done == n_batches:
+                        sd = dl.state_dict()
+                        break
+            dl.close()
+        return rows, sd
+
+    head, sd = run(7)
+    assert sd["epoch"] == 1 and sd["batch"] == 3
+    tail, _ = run(10 ** 9, resume=sd)
+    full, _ = run(10 ** 9)
+    assert len(head) + len(tail) == len(full) == 12
+    for a, b in zip(head + tail, full):
+        assert torch.equal(a, b)
