@@ -21,6 +21,7 @@
 
 #include "common.h"
 #include "launch.h"
+#include "stager.h"
 
 namespace py = pybind11;
 
@@ -28,6 +29,19 @@ namespace {
 
 void check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+py::dict staged_dict(const ddl::StagedInfo& i) {
+  py::dict d;
+  d["window"] = i.window;
+  d["buffer"] = i.buffer;
+  d["producer"] = i.producer;
+  d["slot"] = i.slot;
+  d["seq"] = i.seq;
+  d["used_bytes"] = i.used_bytes;
+  d["tag"] = py::make_tuple(i.tag[0], i.tag[1], i.tag[2], i.tag[3]);
+  d["t_ready_host"] = i.t_ready_host;
+  return d;
 }
 
 void check_rc(int rc, const char* what) {
@@ -168,6 +182,64 @@ PYBIND11_MODULE(_ddl_hip, m) {
       },
       py::arg("state_word"), py::arg("value"), py::arg("stream"),
       "Store `value` into the shm slot state word (+ futex wake) once the stream reaches this point.");
+
+  // ---------------------------------------------------------- native stager
+  m.attr("ARENA_ABI") = ddl::arena_abi();
+  py::class_<ddl::NativeStager>(m, "NativeStager")
+      .def(py::init([](uintptr_t arena, int32_t n_producers, int32_t n_slots, int64_t first, int64_t total,
+                       std::vector<uintptr_t> buffers, uint64_t buffer_bytes, uintptr_t copy_stream, int device,
+                       std::vector<int32_t> peer_pids, int64_t timeout_ms, std::vector<uintptr_t> ready,
+                       std::vector<uintptr_t> copy_done, bool post_copy) {
+             std::vector<void*> bufs;
+             for (auto b : buffers) bufs.push_back(as_ptr<void>(b));
+             std::vector<hipEvent_t> rd, cd;
+             for (auto e : ready) rd.push_back(reinterpret_cast<hipEvent_t>(e));
+             for (auto e : copy_done) cd.push_back(reinterpret_cast<hipEvent_t>(e));
+             return std::make_unique<ddl::NativeStager>(
+                 reinterpret_cast<const ddl::Arena*>(arena), n_producers, n_slots, first, total, std::move(bufs),
+                 buffer_bytes, as_stream(copy_stream), device, std::move(peer_pids), timeout_ms, std::move(rd),
+                 std::move(cd), post_copy);
+           }),
+           py::arg("arena"), py::arg("n_producers"), py::arg("n_slots"), py::arg("first"), py::arg("total"),
+           py::arg("buffers"), py::arg("buffer_bytes"), py::arg("copy_stream"), py::arg("device"),
+           py::arg("peer_pids"), py::arg("timeout_ms"), py::arg("ready"), py::arg("copy_done"),
+           py::arg("post_copy"))
+      .def(
+          "wait",
+          [](ddl::NativeStager& st, int64_t w, int64_t timeout_ms) {
+            ddl::StagedInfo info;
+            int32_t fp = -1;
+            int rc;
+            {
+              py::gil_scoped_release nogil;
+              rc = st.wait(w, timeout_ms, &info, &fp);
+            }
+            return py::make_tuple(rc, fp, rc == 0 ? staged_dict(info) : py::dict());
+          },
+          py::arg("window"), py::arg("timeout_ms"),
+          "(0, -1, info) once window w is staged, else (code, producer, {}): 1 shutdown, 2 timeout, 3 peer dead, "
+          "4 peer failed, -1 internal error (see error())")
+      .def(
+          "peek",
+          [](ddl::NativeStager& st, int64_t w) -> py::object {
+            ddl::StagedInfo info;
+            if (!st.peek(w, &info)) return py::none();
+            return staged_dict(info);
+          },
+          py::arg("window"))
+      .def(
+          "release", [](ddl::NativeStager& st, int64_t w, uintptr_t ev) { st.release(w, reinterpret_cast<hipEvent_t>(ev)); },
+          py::arg("window"), py::arg("free_event"))
+      .def(
+          "close",
+          [](ddl::NativeStager& st) {
+            py::gil_scoped_release nogil;
+            st.close();
+          })
+      .def("error", &ddl::NativeStager::error)
+      .def_property_readonly("bytes_h2d", &ddl::NativeStager::bytes_h2d)
+      .def_property_readonly("windows_staged", &ddl::NativeStager::windows_staged)
+      .def_property_readonly("wait_producer_s", &ddl::NativeStager::wait_producer_s);
 
   // --------------------------------------------------------------- kernels
   m.def(

@@ -1,0 +1,206 @@
+// See stager.h.
+#include "stager.h"
+
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <climits>
+
+namespace ddl {
+namespace {
+
+double mono_s() {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return static_cast<double>(ts.tv_sec) + 1e-9 * static_cast<double>(ts.tv_nsec);
+}
+
+struct SlotRelease {
+  std::atomic<uint32_t>* word;
+};
+
+// Host callback on the copy stream: the DMA out of the slot retired, hand the
+// slot back to its producer (state store + futex wake of the producer).
+void release_slot_cb(void* p) {
+  auto* r = static_cast<SlotRelease*>(p);
+  r->word->store(kEmpty, std::memory_order_release);
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(r->word), FUTEX_WAKE, INT32_MAX, nullptr, nullptr, 0);
+  delete r;
+}
+
+}  // namespace
+
+NativeStager::NativeStager(const Arena* arena, int32_t n_producers, int32_t n_slots, int64_t first, int64_t total,
+                           std::vector<void*> buffers, uint64_t buffer_bytes, hipStream_t copy_stream, int device,
+                           std::vector<int32_t> peer_pids, int64_t timeout_ms, std::vector<hipEvent_t> ready,
+                           std::vector<hipEvent_t> copy_done, bool post_copy)
+    : arena_(arena),
+      P_(n_producers),
+      n_slots_(n_slots),
+      first_(first),
+      total_(total),
+      buffers_(std::move(buffers)),
+      buffer_bytes_(buffer_bytes),
+      copy_stream_(copy_stream),
+      device_(device),
+      peer_pids_(std::move(peer_pids)),
+      timeout_ms_(timeout_ms),
+      ready_(std::move(ready)),
+      copy_done_(std::move(copy_done)),
+      post_copy_(post_copy),
+      depth_(static_cast<int>(buffers_.size())),
+      free_events_(buffers_.size(), nullptr),
+      released_upto_(first) {
+  if (P_ < 1 || n_slots_ < 1 || depth_ < 1 || ready_.size() != buffers_.size() ||
+      (post_copy_ && copy_done_.size() != buffers_.size()) || static_cast<int32_t>(peer_pids_.size()) != P_)
+    throw std::invalid_argument("NativeStager: inconsistent arguments");
+  thread_ = std::thread([this] { run(); });
+}
+
+NativeStager::~NativeStager() { close(); }
+
+void NativeStager::fail(int code, int32_t producer, const std::string& msg) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (error_code_ == 0) {
+    error_code_ = code;
+    error_producer_ = producer;
+    error_msg_ = msg;
+  }
+  cv_.notify_all();
+}
+
+void NativeStager::run() {
+  if (hipSetDevice(device_) != hipSuccess) return fail(-1, -1, "hipSetDevice failed in the stager thread");
+  for (int64_t w = first_; w < first_ + total_; ++w) {
+    const int b = static_cast<int>((w - first_) % depth_);
+    hipEvent_t free_ev = nullptr;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return stop_ || w - depth_ < released_upto_; });
+      if (stop_) return;
+      free_ev = free_events_[b];
+    }
+    // the consumer's kernels reading this ring buffer (window w - depth) finish first
+    if (free_ev != nullptr && hipStreamWaitEvent(copy_stream_, free_ev, 0) != hipSuccess)
+      return fail(-1, -1, "hipStreamWaitEvent(free) failed");
+    const uint32_t p = static_cast<uint32_t>(w % P_);
+    const uint32_t s = static_cast<uint32_t>((w / P_) % n_slots_);
+    // futex wait in short slices so close() never waits behind a long timeout
+    const auto t0 = std::chrono::steady_clock::now();
+    const uint64_t deadline_ns = timeout_ms_ < 0 ? UINT64_MAX : now_ns() + static_cast<uint64_t>(timeout_ms_) * 1000000ull;
+    WaitResult rc;
+    for (;;) {
+      rc = arena_->wait_state(p, s, kReady, 100, peer_pids_[p], static_cast<int32_t>(p));
+      if (rc != kTimeout) break;
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (stop_) return;
+      }
+      if (now_ns() >= deadline_ns) break;
+    }
+    wait_producer_ns_ += static_cast<uint64_t>(
+        std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
+    if (rc == kShutdown) {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (!stop_ && error_code_ == 0) {
+        error_code_ = kShutdown;
+        error_producer_ = static_cast<int32_t>(p);
+        error_msg_ = "arena shutdown while waiting for producer " + std::to_string(p);
+      }
+      cv_.notify_all();
+      return;
+    }
+    if (rc != kOk)
+      return fail(rc, static_cast<int32_t>(p),
+                  "waiting for producer " + std::to_string(p) + " slot " + std::to_string(s));
+    arena_->set_state(p, s, kHeld);
+    const SlotHeader* sh = arena_->slot(p, s);
+    StagedInfo info;
+    info.window = w;
+    info.buffer = b;
+    info.producer = static_cast<int32_t>(p);
+    info.slot = static_cast<int32_t>(s);
+    info.seq = sh->seq.load(std::memory_order_acquire);
+    info.used_bytes = sh->used_bytes.load(std::memory_order_acquire);
+    for (int k = 0; k < 4; ++k) info.tag[k] = sh->tag[k].load(std::memory_order_acquire);
+    if (info.used_bytes > buffer_bytes_)
+      return fail(-1, static_cast<int32_t>(p),
+                  "window of " + std::to_string(info.used_bytes) + " B exceeds the staging buffer");
+    if (info.used_bytes > 0 &&
+        hipMemcpyAsync(buffers_[b], arena_->slot_data(p, s), info.used_bytes, hipMemcpyHostToDevice, copy_stream_) !=
+            hipSuccess)
+      return fail(-1, static_cast<int32_t>(p), "hipMemcpyAsync H2D failed");
+    auto* req = new SlotRelease{&arena_->slot(p, s)->state};
+    if (hipLaunchHostFunc(copy_stream_, release_slot_cb, req) != hipSuccess) {
+      delete req;
+      return fail(-1, static_cast<int32_t>(p), "hipLaunchHostFunc(release) failed");
+    }
+    if (hipEventRecord(post_copy_ ? copy_done_[b] : ready_[b], copy_stream_) != hipSuccess)
+      return fail(-1, static_cast<int32_t>(p), "hipEventRecord failed");
+    info.t_ready_host = mono_s();
+    bytes_h2d_ += info.used_bytes;
+    windows_staged_ += 1;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      staged_[w] = info;
+    }
+    cv_.notify_all();
+  }
+}
+
+int NativeStager::wait(int64_t w, int64_t timeout_ms, StagedInfo* out, int32_t* failed_producer) {
+  std::unique_lock<std::mutex> lk(mu_);
+  auto ready = [&] { return staged_.count(w) != 0 || error_code_ != 0 || stop_; };
+  if (timeout_ms < 0) {
+    cv_.wait(lk, ready);
+  } else if (!cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), ready)) {
+    *failed_producer = static_cast<int32_t>(w % P_);
+    return kTimeout;
+  }
+  auto it = staged_.find(w);
+  if (it != staged_.end()) {
+    *out = it->second;
+    return 0;
+  }
+  *failed_producer = error_producer_;
+  if (error_code_ != 0) return error_code_;
+  return kShutdown;  // closed
+}
+
+bool NativeStager::peek(int64_t w, StagedInfo* out) {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = staged_.find(w);
+  if (it == staged_.end()) return false;
+  *out = it->second;
+  return true;
+}
+
+void NativeStager::release(int64_t w, hipEvent_t free_event) {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = staged_.find(w);
+  if (it == staged_.end()) return;
+  free_events_[it->second.buffer] = free_event;
+  staged_.erase(it);
+  released_upto_ = std::max(released_upto_, w + 1);
+  cv_.notify_all();
+}
+
+void NativeStager::close() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  if (thread_.joinable()) thread_.join();
+}
+
+std::string NativeStager::error() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return error_msg_;
+}
+
+}  // namespace ddl

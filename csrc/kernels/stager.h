@@ -1,0 +1,110 @@
+// Native H2D window stager: producer shm slots -> HBM ring on a prefetch stream.
+//
+// Replaces the reference's missing device path (tests/run_ddl.py:233-235 keeps
+// batches on the host; ddl/connection.py:89-92 leaves pinned memory / H2D as a
+// TODO). One std::thread per consumer walks the window schedule ahead of the
+// training loop WITHOUT the Python GIL:
+//
+//   wait until the ring buffer for window w is free (consumer released w-depth;
+//   its free event -> hipStreamWaitEvent on the copy stream)
+//   futex-wait for producer p = w % P to publish slot s = (w / P) % n_slots
+//   READY -> HELD; hipMemcpyAsync H2D (SDMA) from the pinned arena
+//   hipLaunchHostFunc: slot -> EMPTY + futex wake once the DMA retires
+//   hipEventRecord(ready or copy_done) ; publish "window w staged"
+//
+// The consumer thread only waits on a condition variable (GIL released) and
+// makes its compute stream wait on the ready event on the device. A Python
+// staging thread needed the GIL for every window and could be held off for a
+// full interpreter switch interval (5 ms) by a Python-heavy training loop.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <map>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "arena.h"
+
+namespace ddl {
+
+struct StagedInfo {
+  int64_t window = 0;
+  int32_t buffer = 0;
+  int32_t producer = 0;
+  int32_t slot = 0;
+  uint64_t seq = 0;
+  uint64_t used_bytes = 0;
+  int64_t tag[4] = {0, 0, 0, 0};
+  double t_ready_host = 0.0;  // CLOCK_MONOTONIC seconds when the copy was enqueued
+};
+
+class NativeStager {
+ public:
+  // arena: the consumer's Arena (its mapping is the hipHostRegister'ed one).
+  // buffers: `depth` device buffers of buffer_bytes each. ready/copy_done:
+  // `depth` hipEvents each (owned by the caller). With post_copy the stager
+  // records copy_done[b] and the consumer runs the post-copy work + records
+  // ready[b]; without, the stager records ready[b] itself.
+  NativeStager(const Arena* arena, int32_t n_producers, int32_t n_slots, int64_t first, int64_t total,
+               std::vector<void*> buffers, uint64_t buffer_bytes, hipStream_t copy_stream, int device,
+               std::vector<int32_t> peer_pids, int64_t timeout_ms, std::vector<hipEvent_t> ready,
+               std::vector<hipEvent_t> copy_done, bool post_copy);
+  ~NativeStager();
+
+  NativeStager(const NativeStager&) = delete;
+  NativeStager& operator=(const NativeStager&) = delete;
+
+  // Block until window w is staged (or the stager failed / timed out / was
+  // closed). Returns 0 and fills `out`, else a WaitResult-style code (1
+  // shutdown, 2 timeout, 3 peer dead, 4 peer failed) or -1 (HIP / internal
+  // error, see error()); `failed_producer` names the producer concerned.
+  int wait(int64_t w, int64_t timeout_ms, StagedInfo* out, int32_t* failed_producer);
+  // Non-blocking: true + info if window w is staged.
+  bool peek(int64_t w, StagedInfo* out);
+  // The consumer is done with window w; `free_event` (recorded on its compute
+  // stream) must complete before the ring buffer is overwritten.
+  void release(int64_t w, hipEvent_t free_event);
+  void close();
+
+  std::string error() const;
+  uint64_t bytes_h2d() const { return bytes_h2d_.load(); }
+  uint64_t windows_staged() const { return windows_staged_.load(); }
+  double wait_producer_s() const { return wait_producer_ns_.load() * 1e-9; }
+
+ private:
+  void run();
+  void fail(int code, int32_t producer, const std::string& msg);
+
+  const Arena* arena_;
+  const int32_t P_, n_slots_;
+  const int64_t first_, total_;
+  const std::vector<void*> buffers_;
+  const uint64_t buffer_bytes_;
+  hipStream_t copy_stream_;
+  const int device_;
+  const std::vector<int32_t> peer_pids_;
+  const int64_t timeout_ms_;
+  const std::vector<hipEvent_t> ready_, copy_done_;
+  const bool post_copy_;
+  const int depth_;
+
+  mutable std::mutex mu_;
+  std::condition_variable cv_;
+  std::map<int64_t, StagedInfo> staged_;
+  std::vector<hipEvent_t> free_events_;  // per ring buffer, null until first release
+  int64_t released_upto_;
+  bool stop_ = false;
+  int error_code_ = 0;
+  int32_t error_producer_ = -1;
+  std::string error_msg_;
+  std::atomic<uint64_t> bytes_h2d_{0}, windows_staged_{0}, wait_producer_ns_{0};
+  std::thread thread_;
+};
+
+}  // namespace ddl

@@ -91,6 +91,12 @@ struct alignas(128) SlotHeader {
 
 uint64_t now_ns();
 
+class Arena;
+// Layout fingerprint of Arena: the HIP extension compiles arena.cpp too and
+// drives the consumer's Arena object (by address) from its native stager; both
+// modules must agree on the class layout.
+constexpr uint64_t arena_abi();
+
 class Arena {
  public:
   // Create a new named segment (shm_open O_EXCL). capacities[p] = bytes per
@@ -160,5 +166,7 @@ void pool_run(int n, int n_threads, const std::function<void(int)>& fn);
 // k row-major [n, widths[g]] groups -> interleaved [n, sum(widths)] (elements of elem_bytes).
 void pack_columns(uint8_t* dst, const std::vector<const uint8_t*>& srcs, const std::vector<uint64_t>& widths,
                   uint64_t elem_bytes, uint64_t n, int n_threads);
+
+constexpr uint64_t arena_abi() { return (static_cast<uint64_t>(sizeof(Arena)) << 32) | (sizeof(SlotHeader) << 16) | kArenaVersion; }
 
 }  // namespace ddl

@@ -53,6 +53,7 @@ PYBIND11_MODULE(_ddl_runtime, m) {
   m.attr("STATUS_DONE") = static_cast<uint32_t>(ddl::kStatusDone);
   m.attr("STATUS_FAILED") = static_cast<uint32_t>(ddl::kStatusFailed);
   m.attr("DATA_ALIGN") = ddl::kDataAlign;
+  m.attr("ARENA_ABI") = ddl::arena_abi();
 
   m.def("now_ns", &ddl::now_ns);
   m.def("pid_alive", &ddl::pid_alive, py::arg("pid"));
@@ -69,6 +70,8 @@ PYBIND11_MODULE(_ddl_runtime, m) {
           py::arg("name"))
       .def("unlink", &Arena::unlink)
       .def_property_readonly("name", &Arena::name)
+      .def_property_readonly("address", [](const Arena& a) { return reinterpret_cast<uintptr_t>(&a); },
+                             "address of this C++ Arena object (for the HIP extension's native stager)")
       .def_property_readonly("base_address",
                              [](const Arena& a) { return reinterpret_cast<uintptr_t>(a.base()); })
       .def_property_readonly("total_bytes", &Arena::total_bytes)

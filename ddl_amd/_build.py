@@ -105,6 +105,10 @@ def build_hip(force: bool = False, jobs: int = 8) -> str:
     out = hip_target()
     kernel_srcs = _kernel_sources()
     binding = os.path.join(CSRC, "kernels", "bindings.cpp")
+    # host-only C++ compiled into the HIP module: the native stager and its own copy
+    # of the arena implementation (it drives the consumer's Arena object by address)
+    host_srcs = [os.path.join(CSRC, "kernels", "stager.cpp"), os.path.join(CSRC, "runtime", "arena.cpp")]
+    headers = headers + [os.path.join(CSRC, "runtime", "arena.h")]
 
     jobs_list: list[tuple[list[str], str]] = []
     objs: list[str] = []
@@ -115,6 +119,11 @@ def build_hip(force: bool = False, jobs: int = 8) -> str:
         if force or _newer(obj, [src] + headers):
             cmd = [hipcc, f"--offload-arch={ARCH}", "-c", src, "-o", obj, "-munsafe-fp-atomics"] + common
             jobs_list.append((cmd, obj))
+    for src in host_srcs:
+        obj = os.path.join(BUILD, "hip_" + os.path.basename(src) + ".o")
+        objs.append(obj)
+        if force or _newer(obj, [src] + headers):
+            jobs_list.append(([hipcc, "-c", src, "-o", obj, "-fvisibility=hidden"] + common, obj))
     bobj = os.path.join(BUILD, "bindings.cpp.o")
     objs.append(bobj)
     if force or _newer(bobj, [binding] + headers):

@@ -213,7 +213,7 @@ class DistributedDataLoader:
             from .staging import WindowStager
 
             max_bytes = max(math.prod(s) * _dtypes.itemsize(d) for s, d in zip(self.shapes, self.dtypes))
-            self._stager = WindowStager(connection, self._schedule, self.total_windows, self.prefetch_depth,
+            self._stager = WindowStager(connection, self.n_slots, self.total_windows, self.prefetch_depth,
                                         self.device, max_bytes, post_copy=self._exchange_fn,
                                         timeout_s=self.timeout_s, first_window=self.window)
             if self._produces_copy():

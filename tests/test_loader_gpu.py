@@ -165,3 +165,20 @@ def test_gpu_resume_mid_window_is_exact():
     assert len(head) + len(tail) == len(full) == 12
     for a, b in zip(head + tail, full):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("fault,exc", [("1:1:exit", "PeerDeathError"), ("0:1:raise", "PeerDeathError"),
+                                       ("0:1:hang", "DDLTimeoutError")])
+def test_gpu_native_stager_surfaces_producer_faults(monkeypatch, fault, exc):
+    """The native stager thread reports a dead / failing / hung producer to the consumer as a typed error."""
+    from ddl_amd import exceptions
+
+    monkeypatch.setenv("DDL_FAULT_PRODUCER", fault)
+    with pytest.raises(getattr(exceptions, exc)):
+        with ddl_amd.start(n_producers=2, timeout_s=4) as (env, conn):
+            dl = ddl_amd.DistributedDataLoader(IdProducer(8, 4), 4, conn, 10, env=env, shuffle="device")
+            assert dl._stager is not None
+            for _ in range(10):
+                for _b in dl:
+                    dl.mark(Marker.END_OF_BATCH)
+                dl.mark(Marker.END_OF_EPOCH)
