@@ -19,8 +19,8 @@ import numpy as np
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--batch", type=int, default=64, help="sequences per rank per step")
     ap.add_argument("--seq-len", type=int, default=4096)
     ap.add_argument("--min-len", type=int, default=256)

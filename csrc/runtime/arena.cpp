@@ -381,6 +381,88 @@ void gather_rows(uint8_t* dst, const uint8_t* src, uint64_t row_bytes, const int
   });
 }
 
+uint64_t gather_ragged(uint8_t* dst, int64_t* dst_offsets, const uint8_t* src, const int64_t* src_offsets,
+                       uint64_t n_src, const int64_t* idx, uint64_t n, uint64_t elem_bytes, uint64_t dst_capacity,
+                       int n_threads) {
+  // Token windows of the north-star LM config: one producer round = one local
+  // batch of ragged sequences. Offsets first (serial prefix sum, n is a batch),
+  // then the copies on the pool, ~1 MiB per task.
+  dst_offsets[0] = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (idx[i] < 0 || static_cast<uint64_t>(idx[i]) >= n_src)
+      throw std::out_of_range("gather_ragged: sequence " + std::to_string(idx[i]) + " out of range");
+    const int64_t len = src_offsets[idx[i] + 1] - src_offsets[idx[i]];
+    if (len < 0) throw std::invalid_argument("gather_ragged: decreasing source offsets");
+    dst_offsets[i + 1] = dst_offsets[i] + len;
+  }
+  const uint64_t total = n ? static_cast<uint64_t>(dst_offsets[n]) : 0;
+  if (total > dst_capacity)
+    throw std::length_error("gather_ragged: " + std::to_string(total) + " elements exceed the window capacity " +
+                            std::to_string(dst_capacity));
+  if (total == 0) return 0;
+  // tasks = contiguous runs of sequences holding ~1 MiB each
+  std::vector<uint64_t> cuts{0};
+  const uint64_t target = std::max<uint64_t>(1, (1ull << 20) / std::max<uint64_t>(elem_bytes, 1));
+  uint64_t acc = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    acc += static_cast<uint64_t>(dst_offsets[i + 1] - dst_offsets[i]);
+    if (acc >= target && i + 1 < n) {
+      cuts.push_back(i + 1);
+      acc = 0;
+    }
+  }
+  cuts.push_back(n);
+  std::lock_guard<std::mutex> lk(g_pool_call_mu);
+  Pool::get().run(static_cast<int>(cuts.size() - 1), n_threads, [&](int t) {
+    for (uint64_t i = cuts[t]; i < cuts[t + 1]; ++i) {
+      const uint64_t len = static_cast<uint64_t>(dst_offsets[i + 1] - dst_offsets[i]);
+      std::memcpy(dst + static_cast<uint64_t>(dst_offsets[i]) * elem_bytes,
+                  src + static_cast<uint64_t>(src_offsets[idx[i]]) * elem_bytes, len * elem_bytes);
+    }
+  });
+  return total;
+}
+
+std::pair<int64_t, int64_t> pack_plan(const int64_t* offs, int64_t n_seq, int64_t seq_len, int64_t* row_start,
+                                      int64_t* row_end, int64_t max_rows, int64_t* seg_offsets, int64_t max_segs) {
+  if (seq_len <= 0) throw std::invalid_argument("pack_plan: seq_len must be > 0");
+  int64_t n_seg = 0, n_rows = 0;
+  int64_t cur_s = -1, cur_e = -1, last_seg_end = 0;
+  auto emit_row = [&]() {
+    if (n_rows >= max_rows) throw std::length_error("pack_plan: more rows than the window holds");
+    row_start[n_rows] = cur_s;
+    row_end[n_rows] = cur_e;
+    ++n_rows;
+  };
+  auto add_segment = [&](int64_t s, int64_t e) {
+    if (n_seg >= max_segs) throw std::length_error("pack_plan: more segments than the window holds");
+    seg_offsets[n_seg++] = s;
+    last_seg_end = e;
+    if (cur_s < 0) {
+      cur_s = s;
+      cur_e = e;
+    } else if (e - cur_s <= seq_len && s == cur_e) {
+      cur_e = e;  // contiguous and still fits: extend the row
+    } else {
+      emit_row();
+      cur_s = s;
+      cur_e = e;
+    }
+  };
+  for (int64_t i = 0; i < n_seq; ++i) {
+    int64_t s = offs[i];
+    const int64_t e = offs[i + 1];
+    while (e - s > seq_len) {  // over-long sequence: seq_len chunks
+      add_segment(s, s + seq_len);
+      s += seq_len;
+    }
+    if (e > s) add_segment(s, e);
+  }
+  if (cur_s >= 0) emit_row();
+  seg_offsets[n_seg] = last_seg_end;
+  return {n_rows, n_seg};
+}
+
 void pool_run(int n, int n_threads, const std::function<void(int)>& fn) {
   std::lock_guard<std::mutex> lk(g_pool_call_mu);
   Pool::get().run(n, n_threads, fn);

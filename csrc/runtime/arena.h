@@ -24,6 +24,7 @@
 #include <cstdint>
 #include <functional>
 #include <string>
+#include <utility>
 #include <vector>
 
 namespace ddl {
@@ -160,6 +161,20 @@ void gather_rows(uint8_t* dst, const uint8_t* src, uint64_t row_bytes, const int
                  uint64_t n, uint64_t src_rows, int n_threads);
 // Parallel memcpy (large contiguous copies: window replication).
 void parallel_copy(uint8_t* dst, const uint8_t* src, uint64_t bytes, int n_threads);
+// Ragged (variable-length) gather: sequence idx[i] = src[src_offsets[idx[i]] :
+// src_offsets[idx[i]+1]) (elements of elem_bytes) is appended to dst;
+// dst_offsets[0..n] receives the running offsets. Throws if the result exceeds
+// dst_capacity elements or an index is out of [0, n_src). Returns the total.
+uint64_t gather_ragged(uint8_t* dst, int64_t* dst_offsets, const uint8_t* src, const int64_t* src_offsets,
+                       uint64_t n_src, const int64_t* idx, uint64_t n, uint64_t elem_bytes, uint64_t dst_capacity,
+                       int n_threads);
+// Greedy in-order packing of the sequences [offs[i], offs[i+1]) into rows of
+// seq_len tokens; sequences longer than seq_len are split into seq_len
+// chunks. Writes row_start/row_end (<= max_rows) and seg_offsets (segment
+// starts + end, <= max_segs + 1); returns {n_rows, n_segs}. Throws when the
+// output arrays are too small.
+std::pair<int64_t, int64_t> pack_plan(const int64_t* offs, int64_t n_seq, int64_t seq_len, int64_t* row_start,
+                                      int64_t* row_end, int64_t max_rows, int64_t* seg_offsets, int64_t max_segs);
 // Run fn(i), i in [0, n), on the shared host worker pool (caller included).
 // fn must not throw: record errors and report them after the call.
 void pool_run(int n, int n_threads, const std::function<void(int)>& fn);

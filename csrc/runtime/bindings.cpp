@@ -232,4 +232,29 @@ PYBIND11_MODULE(_ddl_runtime, m) {
           },
           py::arg("base_offset"), py::arg("row_bytes"), py::arg("idx"), py::arg("dst"), py::arg("direct") = false,
           py::arg("n_threads") = 4, "dst[i] = row idx[i] of the file (coalesced pread, optional O_DIRECT)");
+  m.def(
+      "gather_ragged",
+      [](uintptr_t dst, uintptr_t dst_offsets, uintptr_t src, uintptr_t src_offsets, uint64_t n_src,
+         py::array_t<int64_t, py::array::c_style | py::array::forcecast> idx, uint64_t elem_bytes, uint64_t capacity,
+         int n_threads) {
+        const int64_t* ip = idx.data();
+        const uint64_t n = static_cast<uint64_t>(idx.size());
+        py::gil_scoped_release nogil;
+        return ddl::gather_ragged(reinterpret_cast<uint8_t*>(dst), reinterpret_cast<int64_t*>(dst_offsets),
+                                  reinterpret_cast<const uint8_t*>(src), reinterpret_cast<const int64_t*>(src_offsets),
+                                  n_src, ip, n, elem_bytes, capacity, n_threads);
+      },
+      py::arg("dst"), py::arg("dst_offsets"), py::arg("src"), py::arg("src_offsets"), py::arg("n_src"), py::arg("idx"),
+      py::arg("elem_bytes"), py::arg("capacity"), py::arg("n_threads") = 4,
+      "append sequences idx[i] of a ragged source to dst; dst_offsets[0..n] = running offsets; returns the total");
+  m.def(
+      "pack_plan",
+      [](uintptr_t offs, int64_t n_seq, int64_t seq_len, uintptr_t row_start, uintptr_t row_end, int64_t max_rows,
+         uintptr_t seg_offsets, int64_t max_segs) {
+        return ddl::pack_plan(reinterpret_cast<const int64_t*>(offs), n_seq, seq_len,
+                              reinterpret_cast<int64_t*>(row_start), reinterpret_cast<int64_t*>(row_end), max_rows,
+                              reinterpret_cast<int64_t*>(seg_offsets), max_segs);
+      },
+      py::arg("offsets"), py::arg("n_seq"), py::arg("seq_len"), py::arg("row_start"), py::arg("row_end"),
+      py::arg("max_rows"), py::arg("seg_offsets"), py::arg("max_segs"), "greedy in-order packing plan -> (n_rows, n_segs)");
 }

@@ -20,7 +20,7 @@ import torch
 
 from ..datapusher import DataProducerOnInitReturn
 from ..datasetwrapper import ProducerFunctionSkeleton
-from ..ops.kernels import pack_plan
+from .. import _native
 from ..permutation import EpochOrder
 from .datasets import SharedArraySource
 
@@ -101,11 +101,12 @@ class TokenBatchProducer(ProducerFunctionSkeleton):
     """One window = this rank's slice of a global batch of sequences, shipped ragged."""
 
     def __init__(self, source: SharedTokenSource, global_batch: int, seq_len: int = 4096, mode: str = "pad",
-                 seed: int | None = None):
+                 seed: int | None = None, host_threads: int = 2):
         super().__init__()
         if mode not in ("pad", "pack"):
             raise ValueError("mode must be 'pad' or 'pack'")
         self.source, self.global_batch, self.seq_len, self.mode, self.seed = source, global_batch, seq_len, mode, seed
+        self.host_threads = host_threads
         self.order = None
         self.layout = None
 
@@ -132,22 +133,17 @@ class TokenBatchProducer(ProducerFunctionSkeleton):
         v = self.layout.views(buf)
         toks = self.source.tokens.tensor().view(-1)
         offs = self.source.offsets.tensor().view(-1)
-        starts, ends = offs[idx], offs[idx + 1]
-        lens = ends - starts
-        o = v["offsets"]
-        o[0] = 0
-        torch.cumsum(lens, 0, out=o[1:])
-        dst = v["tokens"]
-        for i in range(len(idx)):  # one contiguous memcpy per sequence
-            dst[int(o[i]):int(o[i + 1])].copy_(toks[int(starts[i]):int(ends[i])])
-        n_tokens = int(o[-1])
+        rt = _native.runtime()
+        o, dst = v["offsets"], v["tokens"]
+        # native ragged gather (thread pool, GIL released): sequences -> window, offsets alongside
+        n_tokens = int(rt.gather_ragged(dst.data_ptr(), o.data_ptr(), toks.data_ptr(), offs.data_ptr(),
+                                        self.source.n, np.ascontiguousarray(idx, np.int64), 4, dst.numel(),
+                                        self.host_threads))
         n_rows = n_seg = 0
-        if self.mode == "pack":
-            rs, re_, so = pack_plan(o.numpy(), self.seq_len)
-            n_rows, n_seg = len(rs), len(so) - 1
-            v["row_start"][:n_rows] = torch.from_numpy(rs)
-            v["row_end"][:n_rows] = torch.from_numpy(re_)
-            v["seg_offsets"][: n_seg + 1] = torch.from_numpy(so)
+        if self.mode == "pack":  # packing plan written straight into the window (native)
+            cap = self.layout.max_segments
+            n_rows, n_seg = rt.pack_plan(o.data_ptr(), len(idx), self.seq_len, v["row_start"].data_ptr(),
+                                         v["row_end"].data_ptr(), cap, v["seg_offsets"].data_ptr(), cap)
         tok_off = self.layout.regions()["tokens"][0]
         return {"tags": [n_tokens, n_rows, n_seg], "used_bytes": tok_off + 4 * n_tokens}
 

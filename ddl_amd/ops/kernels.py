@@ -428,7 +428,30 @@ def pad_tokens(tokens: torch.Tensor, offsets: torch.Tensor, seq_len: int, pad_id
 
 
 def pack_plan(seq_offsets: np.ndarray, seq_len: int, max_rows: int | None = None):
-    """Greedy in-order packing of sequences into rows of ``seq_len`` tokens.
+    """Greedy in-order packing of sequences into rows of ``seq_len`` tokens (native C++).
+
+    Sequences longer than ``seq_len`` are split into ``seq_len`` chunks (each
+    chunk restarts its position ids). Returns (row_start, row_end, seg_offsets)
+    int64 arrays: row r holds flat tokens [row_start[r], row_end[r]);
+    seg_offsets are the (split) sequence starts plus the end. ``max_rows``
+    truncates the plan (reference implementation).
+    """
+    offs = np.ascontiguousarray(seq_offsets, dtype=np.int64)
+    if max_rows is not None:
+        return ref_pack_plan(offs, seq_len, max_rows)
+    n = len(offs) - 1
+    lens = np.diff(offs)
+    max_segs = int(np.sum(-(-lens // seq_len))) if n > 0 else 0
+    rs = np.empty(max(max_segs, 1), np.int64)
+    re_ = np.empty(max(max_segs, 1), np.int64)
+    so = np.empty(max_segs + 1, np.int64)
+    n_rows, n_seg = _native.runtime().pack_plan(offs.ctypes.data, n, int(seq_len), rs.ctypes.data, re_.ctypes.data,
+                                               max(max_segs, 1), so.ctypes.data, max_segs)
+    return rs[:n_rows].copy(), re_[:n_rows].copy(), so[: n_seg + 1].copy()
+
+
+def ref_pack_plan(seq_offsets: np.ndarray, seq_len: int, max_rows: int | None = None):
+    """Pure-Python reference of ``pack_plan``.
 
     Sequences longer than ``seq_len`` are split into ``seq_len`` chunks (each
     chunk restarts its position ids). Returns (row_start, row_end, seg_offsets)

@@ -66,3 +66,39 @@ def test_token_batches_gpu(corpus, mode):
                 m = batch["attention_mask"].bool().cpu()
                 flat = batch["input_ids"].cpu()[m]
                 assert np.array_equal(flat.numpy(), np.concatenate(expected_tokens(corpus, idx)))
+
+
+@pytest.mark.parametrize("seq_len", [4096, 100, 7])
+def test_native_pack_plan_matches_reference(seq_len):
+    from ddl_amd import ops
+
+    rng = np.random.default_rng(seq_len)
+    for n in (0, 1, 5, 64):
+        lens = rng.integers(0, 3 * seq_len, size=n)
+        offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        got = ops.pack_plan(offs, seq_len)
+        ref = ops.ref_pack_plan(offs, seq_len)
+        for a, b in zip(got, ref):
+            assert np.array_equal(a, b), (n, a, b)
+
+
+def test_native_gather_ragged():
+    from ddl_amd import _native
+
+    rng = np.random.default_rng(0)
+    lens = rng.integers(0, 5000, size=300)
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    toks = rng.integers(0, 1 << 30, size=int(offs[-1]), dtype=np.int32)
+    idx = rng.permutation(300)[:77]
+    cap = int(lens[idx].sum())
+    dst = np.zeros(cap, np.int32)
+    dofs = np.zeros(78, np.int64)
+    rt = _native.runtime()
+    n = rt.gather_ragged(dst.ctypes.data, dofs.ctypes.data, toks.ctypes.data, offs.ctypes.data, 300, idx, 4, cap, 3)
+    assert n == cap
+    ref = np.concatenate([toks[offs[i]:offs[i + 1]] for i in idx])
+    assert np.array_equal(dst, ref) and np.array_equal(dofs[1:], np.cumsum(lens[idx]))
+    with pytest.raises(ValueError):  # std::length_error -> capacity
+        rt.gather_ragged(dst.ctypes.data, dofs.ctypes.data, toks.ctypes.data, offs.ctypes.data, 300, idx, 4, cap - 1, 3)
+    with pytest.raises(IndexError):
+        rt.gather_ragged(dst.ctypes.data, dofs.ctypes.data, toks.ctypes.data, offs.ctypes.data, 300, [300], 4, cap, 1)
