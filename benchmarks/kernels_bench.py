@@ -68,6 +68,14 @@ def main():
     report("checksum accumulate (streaming consumer)", t, B * img * 2)
     t = bench(lambda: ops.feistel_indices(FeistelPermutation(1 << 24, 3, 3), 0, 1 << 24, device=dev), reps=10)
     report("feistel_indices 16M", t, (1 << 24) * 8)
+    # augmentation: RandomResizedCrop 256x320 u8 -> 224x224 bf16 (+ flip + normalise), CHW and HWC sources
+    for layout in ("chw", "hwc"):
+        shp = (1024, 3, 256, 320) if layout == "chw" else (1024, 256, 320, 3)
+        raw = torch.randint(0, 255, shp, dtype=torch.uint8, device=dev)
+        p1k = FeistelPermutation(1024, 1, 3)
+        t = bench(lambda: ops.random_resized_crop(raw, perm=p1k, base=0, n_rows=B, size=(224, 224), seed=1,
+                                                  layout=layout, mean=[0.5] * 3, std=[0.25] * 3))
+        report(f"random_resized_crop {layout} u8 256x320 -> bf16 224x224", t, B * img * 2)
     # pointwise (reference CI shape): 100,520 x 9 f32 window, 4096-row batch split (3,5,1)
     pw = torch.randn(100_520, 9, device=dev)
     pp = FeistelPermutation(100_520, 5, 5)

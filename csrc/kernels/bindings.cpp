@@ -307,6 +307,37 @@ PYBIND11_MODULE(_ddl_hip, m) {
       py::arg("n_values"), py::arg("mode"), py::arg("idx"), py::arg("base"), py::arg("keys"), py::arg("n_domain"),
       py::arg("half_bits"), py::arg("stream"));
   m.def(
+      "random_resized_crop",
+      [](uintptr_t dst, int out_dt, uintptr_t src, int in_dt, int64_t batch, bool hwc, int in_h, int in_w, int channels,
+         int out_h, int out_w, uint64_t seed, int64_t sample_base, float scale_min, float scale_max, float ratio_min,
+         float ratio_max, float flip_p, int mode, uintptr_t idx, int64_t base, std::vector<uint64_t> keys,
+         uint64_t n_domain, uint32_t half_bits, std::vector<float> scale, std::vector<float> bias, uintptr_t boxes_out,
+         uintptr_t stream) {
+        ddl::AugmentSpec a{};
+        a.seed = seed;
+        a.sample_base = sample_base;
+        a.in_h = in_h;
+        a.in_w = in_w;
+        a.out_h = out_h;
+        a.out_w = out_w;
+        a.channels = channels;
+        a.scale_min = scale_min;
+        a.scale_max = scale_max;
+        a.ratio_min = ratio_min;
+        a.ratio_max = ratio_max;
+        a.flip_p = flip_p;
+        const ddl::RowIndex ri = make_index(mode, idx, base, keys, n_domain, half_bits);
+        const ddl::Affine aff = make_affine(scale, bias, 1);
+        check_rc(ddl::random_resized_crop(as_ptr<void>(dst), out_dt, as_ptr<const void>(src), in_dt, batch, a,
+                                          hwc ? 1 : 0, ri, aff, as_ptr<int32_t>(boxes_out), as_stream(stream)),
+                 "random_resized_crop");
+      },
+      py::arg("dst"), py::arg("out_dt"), py::arg("src"), py::arg("in_dt"), py::arg("batch"), py::arg("hwc"),
+      py::arg("in_h"), py::arg("in_w"), py::arg("channels"), py::arg("out_h"), py::arg("out_w"), py::arg("seed"),
+      py::arg("sample_base"), py::arg("scale_min"), py::arg("scale_max"), py::arg("ratio_min"), py::arg("ratio_max"),
+      py::arg("flip_p"), py::arg("mode"), py::arg("idx"), py::arg("base"), py::arg("keys"), py::arg("n_domain"),
+      py::arg("half_bits"), py::arg("scale"), py::arg("bias"), py::arg("boxes_out"), py::arg("stream"));
+  m.def(
       "pack_columns",
       [](std::vector<uintptr_t> srcs, std::vector<int> widths, int in_dt, uintptr_t dst, int out_dt, int64_t n_rows,
          int64_t n_values, int mode, uintptr_t idx, int64_t base, std::vector<uint64_t> keys, uint64_t n_domain,

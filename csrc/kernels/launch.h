@@ -41,6 +41,25 @@ int split_columns(const SplitSpec& spec, const void* src, int32_t in_dt, int64_t
 int pack_columns(const SplitSpec& spec, void* dst, int32_t in_dt, int64_t n_rows, int64_t n_values,
                  const RowIndex& ri, hipStream_t st);
 
+// augment.hip ---------------------------------------------------------------
+// RandomResizedCrop (+ flip, + per-channel affine, + cast) of gathered images:
+// src rows [in_h, in_w, C] (hwc=1) or [C, in_h, in_w]; out [B, C, out_h, out_w].
+// Crop parameters are drawn on the device from hash(seed, sample_base + source
+// row) by a per-image pre-pass into boxes_out (required, [B, 5] int32 device
+// buffer: y, x, h, w, flip), which the resampling kernel then reads.
+struct AugmentSpec {
+  uint64_t seed;
+  int64_t sample_base;
+  int32_t in_h, in_w, out_h, out_w, channels;
+  float scale_min, scale_max, ratio_min, ratio_max, flip_p;
+};
+struct CropBox {
+  int32_t y, x, h, w, flip;
+};
+int random_resized_crop(void* dst, int32_t out_dt, const void* src, int32_t in_dt, int64_t batch,
+                        const AugmentSpec& a, int hwc, const RowIndex& ri, const Affine& aff, int32_t* boxes_out,
+                        hipStream_t st);
+
 // tokens.hip ----------------------------------------------------------------
 // Pad: row b takes tokens[offsets[b] : offsets[b+1]] (truncated to seq_len);
 // writes out_tokens [B, S] (pad_id fill), attn_mask [B, S] (u8 or null) and

@@ -53,6 +53,14 @@ STATE_VERSION = 1
 MODES = ("do_not_split_along_epoch", "split_along_epoch", "window", "indexed")
 
 
+def _mix(a: int, b: int) -> int:
+    """64-bit mix of two ints (splitmix64 finaliser over a*phi + b)."""
+    z = (int(a) * 0x9E3779B97F4A7C15 + int(b) + 0x632BE59BD9B4E019) & ((1 << 64) - 1)
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & ((1 << 64) - 1)
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & ((1 << 64) - 1)
+    return z ^ (z >> 31)
+
+
 @for_all_methods(with_logging, exclude=["__getitem__", "__len__", "__iter__", "mark", "_on_batch_end",
                                         "_window", "_batch_from_window", "_schedule"])
 class DistributedDataLoader:
@@ -75,6 +83,7 @@ class DistributedDataLoader:
         prefetch_depth: int = 2,
         mode: str = "window",
         normalize: dict | None = None,
+        augment: dict | None = None,
         contiguous: bool = False,
         env: DDLEnv | None = None,
         auto_mark: bool = False,
@@ -103,6 +112,12 @@ class DistributedDataLoader:
         self.prefetch_depth = int(prefetch_depth)
         self.mode = "do_not_split_along_epoch" if mode == "window" else mode
         self.normalize = normalize
+        # on-device RandomResizedCrop + flip (GPU only): {"size": (224, 224), "scale": (0.08, 1.0),
+        # "ratio": (3/4, 4/3), "flip_p": 0.5, "layout": "chw" | "hwc"}; normalize's mean/std apply after it
+        aug_keys = {"size", "scale", "ratio", "flip_p", "layout"}
+        if augment is not None and not set(augment) <= aug_keys:
+            raise ValueError(f"unknown augment keys {sorted(set(augment) - aug_keys)}")
+        self.augment = augment
         self.contiguous = contiguous
         self.env = env
         self.auto_mark = auto_mark
@@ -138,6 +153,8 @@ class DistributedDataLoader:
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
+        if self.augment is not None and self.device.type != "cuda":
+            raise ValueError("augment= runs on the GPU (device-side crop boxes); this loader is on the CPU")
         self.out_dtype = _dtypes.to_torch_dtype(out_dtype) if out_dtype is not None else None
 
         self._finalized = False
@@ -307,7 +324,7 @@ class DistributedDataLoader:
     # ---------------------------------------------------------- batch stream
     def _produces_copy(self) -> bool:
         """True when a batch is built by a kernel (not a zero-copy view of the window)."""
-        return (self.shuffle == "device" or self.out_dtype not in (None, self.window_dtype)
+        return (self.shuffle == "device" or self.out_dtype not in (None, self.window_dtype) or self.augment is not None
                 or self.normalize is not None or self.copy_batches or self.contiguous or self.collate is not None)
 
     def _enqueue_batch(self, sw, p: int, s: int, local: int):
@@ -368,6 +385,15 @@ class DistributedDataLoader:
                                             ex["token_mode"], tags, self.pad_id)
         perm = self._perm_for(p, seq)
         out_dtype = self.out_dtype or (torch.float32 if self.normalize is not None else wdt)
+        if self.augment is not None:
+            aug, norm = self.augment, self.normalize or {}
+            # crop randomness keyed by (seed, epoch) and the window row's identity (producer, round, row)
+            return (ops.random_resized_crop(
+                win, perm=perm, base=local * B, n_rows=B, size=aug.get("size", (224, 224)),
+                scale=aug.get("scale", (0.08, 1.0)), ratio=aug.get("ratio", (3.0 / 4.0, 4.0 / 3.0)),
+                flip_p=aug.get("flip_p", 0.5), seed=_mix(self.seed, self.epoch),
+                sample_base=_mix(p, seq) & ~0xFFFFFFFF & ((1 << 63) - 1), layout=aug.get("layout", "chw"),
+                out_dtype=self.out_dtype or torch.bfloat16, mean=norm.get("mean"), std=norm.get("std")),)
         splits = list(self.splits[p])
         norm = self.normalize
         with trace_range("ddl.consumer.batch"):

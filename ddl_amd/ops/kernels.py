@@ -50,6 +50,9 @@ class HostRows:
     def device(self):
         return torch.device("cuda", torch.cuda.current_device())
 
+    def dim(self) -> int:
+        return self.cpu.dim()
+
 
 def _stream_handle(stream) -> int:
     if stream is None:
@@ -292,6 +295,75 @@ def collate_hwc_to_chw(src, index: torch.Tensor | None = None, *, perm: FeistelP
         batch=n_rows, pixels=pixels, channels=c, scale=sc, bias=bi, stream=_stream_handle(stream),
         **_index_kw(index, perm, base))
     return out
+
+
+# ---------------------------------------------------------------- augment
+def ref_random_resized_crop(src, boxes, size, layout: str = "chw", index=None, perm=None, base=0, n_rows=None,
+                            out_dtype=torch.bfloat16, mean=None, std=None) -> torch.Tensor:
+    """Torch reference of ``random_resized_crop`` for given crop boxes [B, 5] (y, x, h, w, flip)."""
+    import torch.nn.functional as F
+
+    x = src.cpu if isinstance(src, HostRows) else src
+    n_rows = _check_rows(x, index, perm, base, n_rows)
+    rows = x.index_select(0, _ref_rows(x.shape[0], n_rows, index, perm, base).to(x.device)).cpu()
+    if layout == "hwc":
+        rows = rows.movedim(-1, 1)
+    imgs = rows.float()
+    c = imgs.shape[1]
+    sc, bi = norm_affine(c, mean, std, None, None, pixel_max(x.dtype))
+    oh, ow = size
+    out = torch.empty((n_rows, c, oh, ow), dtype=torch.float32)
+    for i, (y0, x0, h, w, flip) in enumerate(boxes.tolist()):
+        crop = imgs[i:i + 1, :, y0:y0 + h, x0:x0 + w]
+        r = F.interpolate(crop, size=(oh, ow), mode="bilinear", align_corners=False, antialias=False)[0]
+        if flip:
+            r = r.flip(-1)
+        if sc:
+            r = r * torch.tensor(sc).view(c, 1, 1) + torch.tensor(bi).view(c, 1, 1)
+        out[i] = r
+    return out.to(out_dtype)
+
+
+def random_resized_crop(src, index: torch.Tensor | None = None, *, perm: FeistelPermutation | None = None,
+                        base: int = 0, n_rows: int | None = None, size=(224, 224), scale=(0.08, 1.0),
+                        ratio=(3.0 / 4.0, 4.0 / 3.0), flip_p: float = 0.5, seed: int = 0, sample_base: int = 0,
+                        layout: str = "chw", out_dtype=torch.bfloat16, mean=None, std=None,
+                        return_boxes: bool = False, stream=None):
+    """Gathered images -> RandomResizedCrop + horizontal flip + normalise + cast, one gfx950 kernel.
+
+    ``src`` rows are [C, H, W] (``layout="chw"``) or [H, W, C] (``"hwc"``),
+    uint8 / bf16 / f32. Crop boxes follow torchvision's RandomResizedCrop
+    (``scale``, ``ratio``) and are drawn on the device from
+    hash(``seed``, ``sample_base`` + source row): the same sample gets the same
+    crop under the same seed whichever rank or batch it lands in.
+    Returns [B, C, size[0], size[1]] (and the [B, 5] int32 boxes y, x, h, w,
+    flip with ``return_boxes``).
+    """
+    out_dtype = _dtypes.to_torch_dtype(out_dtype)
+    if layout not in ("chw", "hwc") or src.dim() != 4:
+        raise ValueError("random_resized_crop expects [N, C, H, W] (chw) or [N, H, W, C] (hwc) rows")
+    if not _is_gpu(src):
+        raise RuntimeError("random_resized_crop runs on the GPU (crop boxes are drawn on the device)")
+    if out_dtype not in (torch.bfloat16, torch.float32):
+        raise TypeError("random_resized_crop writes bf16 or f32")
+    n_rows = _check_rows(src, index, perm, base, n_rows)
+    if layout == "hwc":
+        h, w, c = src.shape[1:]
+    else:
+        c, h, w = src.shape[1:]
+    oh, ow = (int(size), int(size)) if isinstance(size, int) else (int(size[0]), int(size[1]))
+    sc, bi = norm_affine(c, mean, std, None, None, pixel_max(src.dtype))
+    dev = src.device if isinstance(src, torch.Tensor) else torch.device("cuda", torch.cuda.current_device())
+    out = torch.empty((n_rows, c, oh, ow), dtype=out_dtype, device=dev)
+    boxes = torch.empty((n_rows, 5), dtype=torch.int32, device=dev)  # drawn by a per-image pre-pass
+    _native.hip().random_resized_crop(
+        dst=out.data_ptr(), out_dt=_dtypes.code(out_dtype), src=_src_addr(src), in_dt=_dtypes.code(src.dtype),
+        batch=n_rows, hwc=layout == "hwc", in_h=int(h), in_w=int(w), channels=int(c), out_h=oh, out_w=ow,
+        seed=int(seed) & ((1 << 64) - 1), sample_base=int(sample_base), scale_min=float(scale[0]),
+        scale_max=float(scale[1]), ratio_min=float(ratio[0]), ratio_max=float(ratio[1]), flip_p=float(flip_p),
+        scale=sc, bias=bi, boxes_out=boxes.data_ptr(), stream=_stream_handle(stream),
+        **_index_kw(index, perm, base))
+    return (out, boxes) if return_boxes else out
 
 
 def ref_split_columns(src, splits, index=None, perm=None, base=0, n_rows=None, out_dtype=None):

@@ -271,3 +271,46 @@ def test_checksum_accumulator_matches_reference():
         out = ops.checksum(xs[1].to(_dev()))
     s.synchronize()
     assert out.item() & ((1 << 64) - 1) == ops.ref_checksum(xs[1])
+
+
+@pytest.mark.parametrize("layout", ["chw", "hwc"])
+@pytest.mark.parametrize("in_dtype", [torch.uint8, torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("hw,size", [((256, 320), (224, 224)), ((32, 40), (64, 48))])
+def test_random_resized_crop_matches_torch(layout, in_dtype, hw, size):
+    n, c = 12, 3
+    shape = (n, c, *hw) if layout == "chw" else (n, *hw, c)
+    src = (torch.rand(shape) * 255).to(in_dtype)
+    p = FeistelPermutation(n, 9, 1)
+    mean, std = [0.485, 0.456, 0.406], [0.229, 0.224, 0.225]
+    out, boxes = ops.random_resized_crop(src.to(_dev()), perm=p, base=2, n_rows=8, size=size, seed=123,
+                                         layout=layout, mean=mean, std=std, out_dtype=torch.float32,
+                                         return_boxes=True)
+    ref = ops.ref_random_resized_crop(src, boxes.cpu(), size, layout, perm=p, base=2, n_rows=8,
+                                      out_dtype=torch.float32, mean=mean, std=std)
+    torch.testing.assert_close(out.cpu(), ref, rtol=1e-4, atol=1e-3)
+    out16 = ops.random_resized_crop(src.to(_dev()), perm=p, base=2, n_rows=8, size=size, seed=123, layout=layout,
+                                    mean=mean, std=std)
+    torch.testing.assert_close(out16.float().cpu(), ref, rtol=1e-2, atol=2e-2)
+
+
+def test_random_resized_crop_box_distribution_and_determinism():
+    n, H, W = 4000, 180, 240
+    src = torch.zeros((n, 3, H, W), dtype=torch.uint8, device=_dev())
+    _, b = ops.random_resized_crop(src, size=(8, 8), seed=5, return_boxes=True)
+    b = b.cpu().double()
+    y, x, h, w, flip = b.unbind(1)
+    assert bool(((y >= 0) & (x >= 0) & (y + h <= H) & (x + w <= W) & (h >= 1) & (w >= 1)).all())
+    area = h * w / (H * W)
+    # torchvision's get_params simulated in numpy for this 180x240 source: mean area 0.432, min 0.079
+    assert area.min() > 0.07 and area.max() <= 1.0 and 0.41 < area.mean() < 0.455
+    aspect = w / h
+    assert aspect.min() > 0.7 and aspect.max() < 1.45
+    assert 0.46 < flip.mean() < 0.54
+    # deterministic per (seed, sample): same seed -> same boxes; boxes follow the sample, not its batch slot
+    _, b2 = ops.random_resized_crop(src, size=(8, 8), seed=5, return_boxes=True)
+    assert torch.equal(b2.cpu().double(), b)
+    idx = torch.tensor([7, 3, 11], dtype=torch.int64, device=_dev())
+    _, b3 = ops.random_resized_crop(src, idx, size=(8, 8), seed=5, return_boxes=True)
+    assert torch.equal(b3.cpu().double(), b[[7, 3, 11]])
+    _, b4 = ops.random_resized_crop(src, size=(8, 8), seed=6, return_boxes=True)
+    assert not torch.equal(b4.cpu().double(), b)

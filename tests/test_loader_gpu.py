@@ -182,3 +182,32 @@ def test_gpu_native_stager_surfaces_producer_faults(monkeypatch, fault, exc):
                 for _b in dl:
                     dl.mark(Marker.END_OF_BATCH)
                 dl.mark(Marker.END_OF_EPOCH)
+
+
+def test_gpu_augment_random_resized_crop_in_loader():
+    from ddl_amd.models.producers import ImageWindowProducer
+
+    mean, std = [0.485, 0.456, 0.406], [0.229, 0.224, 0.225]
+
+    def run():
+        outs = []
+        with ddl_amd.start(n_producers=2) as (env, conn):
+            dl = ddl_amd.DistributedDataLoader(
+                ImageWindowProducer(32, (3, 64, 80), "uint8", refill="none"), 8, conn, 2, env=env,
+                shuffle="device", seed=3, normalize={"mean": mean, "std": std}, copy_batches=True,
+                augment={"size": (32, 32), "scale": (0.2, 1.0), "flip_p": 0.5})
+            for _ in range(2):
+                for (x,) in dl:
+                    assert x.shape == (8, 3, 32, 32) and x.dtype == torch.bfloat16 and x.is_cuda
+                    outs.append(x.float().cpu())
+                    dl.mark(Marker.END_OF_BATCH)
+                dl.mark(Marker.END_OF_EPOCH)
+        return outs
+
+    a, b = run(), run()
+    assert len(a) == 8
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)  # deterministic for a seed
+    lo, hi = (0 - max(mean)) / min(std), (1 - min(mean)) / min(std)
+    assert all(float(x.min()) >= lo - 0.05 and float(x.max()) <= hi + 0.05 for x in a)
+    assert not torch.equal(a[0], a[4])  # epoch 2 revisits window 0 with new crops

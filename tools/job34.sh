@@ -1,0 +1,3 @@
+source tools/gpu_job.sh
+run 600 gpu_rrc python -m pytest tests/test_kernels_gpu.py -q -x -k "random_resized"
+run 300 kernels python benchmarks/kernels_bench.py
