@@ -117,6 +117,7 @@ class Connection:
         self.pipes = [_Pipe(c, p, f"producer {i}") for i, (c, p) in enumerate(zip(pipes, procs))]
         self.processes = list(procs)
         self.arena = None
+        self._finalizers: list = []
         self.window_shapes: list[tuple[int, ...]] = []
         self.window_dtypes: list[torch.dtype] = []
         self.n_slots = 1
@@ -253,11 +254,23 @@ class Connection:
             except (BrokenPipeError, OSError):
                 pass
 
+    def add_finalizer(self, fn) -> None:
+        """Run ``fn()`` in ``finalize`` after the shutdown signal and before the arena is
+        unpinned: consumers with native threads on the arena (the stager) stop there,
+        even when the loader itself was never closed (an exception unwound the job)."""
+        self._finalizers.append(fn)
+
     def finalize(self, join_timeout_s: float = 10.0) -> None:
         if self._closed:
             return
         self._closed = True
         self.shutdown_operation()
+        for fn in self._finalizers:
+            try:
+                fn()
+            except Exception as e:  # pragma: no cover - best effort
+                logger.warning("finalizer %r failed: %s", fn, e)
+        self._finalizers.clear()
         for proc in self.processes:
             if proc is None:
                 continue

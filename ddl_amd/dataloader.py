@@ -233,6 +233,7 @@ class DistributedDataLoader:
             self._stager = WindowStager(connection, self.n_slots, self.total_windows, self.prefetch_depth,
                                         self.device, max_bytes, post_copy=self._exchange_fn,
                                         timeout_s=self.timeout_s, first_window=self.window)
+            connection.add_finalizer(self._stager.close)  # stop the native thread before the arena is unpinned
             if self._produces_copy():
                 self._batch_stream = torch.cuda.Stream(self.device)
         self._update_len()

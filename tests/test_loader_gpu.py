@@ -211,3 +211,19 @@ def test_gpu_augment_random_resized_crop_in_loader():
     lo, hi = (0 - max(mean)) / min(std), (1 - min(mean)) / min(std)
     assert all(float(x.min()) >= lo - 0.05 and float(x.max()) <= hi + 0.05 for x in a)
     assert not torch.equal(a[0], a[4])  # epoch 2 revisits window 0 with new crops
+
+
+def test_gpu_exception_unwinds_cleanly_with_native_stager():
+    """A user exception mid-epoch (loader never closed): leaving start() stops the native stager
+    before the arena is unpinned, and does not hang behind a slow producer."""
+    import time
+
+    t0 = time.monotonic()
+    with pytest.raises(KeyError):
+        with ddl_amd.start(n_producers=2) as (env, conn):
+            dl = ddl_amd.DistributedDataLoader(IdProducer(64, 8, delay_s=2.0), 16, conn, 5, env=env,
+                                               shuffle="device", n_slots=2, prefetch_depth=2)
+            next(iter(dl))
+            raise KeyError("user error")
+    assert time.monotonic() - t0 < 30
+    assert dl._stager._closed
