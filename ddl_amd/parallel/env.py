@@ -66,7 +66,9 @@ def read_env(n_producers: int | None = None) -> DDLEnv:
         local_world_size=local_world,
         node_rank=rank // max(local_world, 1),
         n_producers=n_producers,
-        hostname=socket.gethostname(),
+        # DDL_HOSTNAME overrides the node identity (containers with unreliable hostnames, and the
+        # multi-node rehearsal tests that run several "nodes" on one box)
+        hostname=os.environ.get("DDL_HOSTNAME") or socket.gethostname(),
     )
 
 

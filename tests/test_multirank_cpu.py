@@ -128,3 +128,50 @@ def test_npy_memmap_source_indexed(tmp_path):
         got = torch.cat([b[0].cpu() for b in dl]).numpy()
     ref = EpochOrder(500, 50, 2).perm(0).full()
     assert np.array_equal(got[:, 0], ref) and np.array_equal(got[:, 1], ref * 2)
+
+
+def _topology_rank(rank, world, method):
+    import ddl_amd
+
+    with ddl_amd.start(n_producers=1) as (env, conn):
+        info = (env.hostname, env.node_rank, env.local_rank, env.local_world_size)
+        from tests.helpers import IdProducer
+
+        dl = ddl_amd.DistributedDataLoader(IdProducer(40, 4), 8, conn, 2, 0.5, method, env.rank, env.world_size,
+                                           env=env, copy_batches=True)
+        rows = []
+        for _ in range(2):
+            for b in dl:
+                rows.append(torch.cat(b, 1).clone())
+                dl.mark(ddl_amd.Marker.END_OF_BATCH)
+            dl.mark(ddl_amd.Marker.END_OF_EPOCH)
+    return info, torch.cat(rows).numpy()
+
+
+@pytest.mark.parametrize("method", ["alltoall", "sendrecv_replace"])
+def test_two_node_rehearsal(method):
+    """2 "nodes" x 2 ranks (DDL_HOSTNAME per node): node ranks / local ranks come out right, the
+    node-locality check passes, and the global-shuffle exchange spans both nodes."""
+    res = run_ranks(_topology_rank, 4, method, nodes=2)
+    infos = [r[0] for r in res]
+    assert infos == [("rehearsal-node0", 0, 0, 2), ("rehearsal-node0", 0, 1, 2),
+                     ("rehearsal-node1", 1, 0, 2), ("rehearsal-node1", 1, 1, 2)]
+    rows = np.concatenate([r[1] for r in res])
+    keys = {tuple(x) for x in rows[:, :4].tolist()}  # (rank, producer, i, round): exchanged, never duplicated
+    assert len(keys) == len(rows) == 4 * 2 * 40
+    foreign = [int((r[1][:, 0] != k).sum()) for k, r in enumerate(res)]
+    assert all(f > 0 for f in foreign)  # every rank received rows from others (incl. the other node)
+
+
+def _bad_topology_rank(rank, world):
+    import ddl_amd
+
+    with ddl_amd.start(n_producers=0):
+        pass
+
+
+def test_node_locality_mismatch_is_rejected():
+    # 4 ranks laid out 2 per node (local ranks 0,1,0,1) but all claiming one host: the hostname
+    # all-gather sees local ranks [0, 0, 1, 1] there and rejects the layout
+    with pytest.raises(AssertionError, match="TopologyError"):
+        run_ranks(_bad_topology_rank, 4, env={"DDL_HOSTNAME": "same-host"}, nodes=2)
