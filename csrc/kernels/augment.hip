@@ -11,10 +11,19 @@
 // (scale, log-uniform ratio), then the centre-crop fallback); resampling is
 // bilinear with align_corners=False (torch.nn.functional.interpolate).
 //
-// Mapping: one thread per output pixel (all channels), 256 pixels per
-// workgroup, workgroups of one image contiguous; consecutive lanes write
-// consecutive output pixels of each channel plane (coalesced), and read
-// neighbouring source pixels (L1/L2 hits).
+// Mapping: one workgroup per (image, band of R output rows). The band's source
+// rows -- at most ceil((R-1) * in_h / out_h) + 3 rows of the crop, every
+// channel, only the crop's columns -- are first copied into LDS with aligned
+// 16 B loads (all of a lane's loads issued before its LDS writes), then every
+// bilinear tap is an LDS read. The earlier form read each tap straight from
+// global memory: 48 one-byte VMEM instructions per lane for 4 uint8 pixels,
+// which PMC showed to be memory-instruction-issue bound (SQ_WAIT_INST_ANY
+// ~2.6x the active cycles, profiles/r1_augment/). Consecutive lanes write
+// consecutive output pixels of each channel plane (8 B / 16 B stores,
+// coalesced). A geometry whose band does not fit the LDS budget runs the same
+// kernel with the taps read from global memory.
+#include <algorithm>
+
 #include "common.h"
 #include "launch.h"
 
@@ -22,6 +31,8 @@ namespace ddl {
 namespace {
 
 constexpr int kThreads = 256;
+constexpr int kBandMaxRows = 16;
+constexpr int64_t kBandLdsBudget = 32 * 1024;  // 4-5 workgroups (16-20 waves) per CU
 static_assert(sizeof(CropBox) == 5 * sizeof(int32_t), "CropBox must match the [B, 5] int32 boxes tensor");
 
 __device__ __forceinline__ float unit_uniform(uint64_t seed, uint64_t sample, uint32_t k) {
@@ -84,107 +95,210 @@ __global__ void __launch_bounds__(kThreads) rrc_boxes_kernel(AugmentSpec a, int6
   boxes[img] = draw_crop(a, static_cast<uint64_t>(a.sample_base + source_row(ri, img)));
 }
 
-// HWC=1: src rows are [H, W, C]; else [C, H, W]. out: [B, C, OH, OW].
-// Each thread produces kPx consecutive output pixels (all channels): 12 * kPx
-// independent tap loads in flight per lane (the kernel is latency-bound, one
-// pixel per thread left most of each wave's life waiting on memory), the box
-// and index math amortised, and one 8 B store per channel when the row allows.
+// Bilinear source coordinate of output index o, align_corners=False:
+// src = (dst + 0.5) * in/out - 0.5, clamped at 0. The band bounds and the taps
+// both come from this one function, so they agree bit for bit.
+__device__ __forceinline__ float src_coord(int o, float f) {
+  return fmaxf((static_cast<float>(o) + 0.5f) * f - 0.5f, 0.f);
+}
+
+// Each thread produces kPx consecutive output pixels of the band (all
+// channels): the box and index math are amortised, 4 * kPx independent taps
+// per channel are in flight, and one 8 B (bf16) / 16 B (f32) store per
+// channel when the output row allows. tap(c, y, x) reads crop-relative source
+// pixel (y, x) of channel c.
 constexpr int kPx = 4;
 
-template <typename Tin, int HWC, int OUT_BF16>
-__global__ void __launch_bounds__(kThreads) rrc_kernel(void* __restrict__ dst, const Tin* __restrict__ src,
-                                                      AugmentSpec a, int64_t tiles, RowIndex ri, Affine aff,
-                                                      const CropBox* __restrict__ boxes) {
-  const int64_t img = blockIdx.x / static_cast<uint32_t>(tiles);
-  const int64_t t = blockIdx.x - static_cast<uint32_t>(img) * static_cast<uint32_t>(tiles);
-  const int64_t srow = source_row(ri, img);
-  const CropBox b = boxes[img];  // wave-uniform (scalar) load
-  const int opix = a.out_h * a.out_w;
-  const int q0 = (static_cast<int>(t) * kThreads + static_cast<int>(threadIdx.x)) * kPx;
-  if (q0 >= opix) return;
-  const int C = a.channels;
-  const int64_t plane = static_cast<int64_t>(a.in_h) * a.in_w;
-  const Tin* s = src + srow * plane * C;
+template <int OUT_BF16, typename Tap>
+__device__ __forceinline__ void resample_band(void* __restrict__ dst, int64_t img, const AugmentSpec& a,
+                                              const CropBox& b, int oy0, int oy1, const Affine& aff, Tap tap) {
+  const int ow = a.out_w, C = a.channels;
+  const int64_t opix = static_cast<int64_t>(a.out_h) * ow;
+  const int n = (oy1 - oy0) * ow;
   const float fy = static_cast<float>(b.h) / a.out_h, fx = static_cast<float>(b.w) / a.out_w;
-  int64_t i00[kPx], i01[kPx], i10[kPx], i11[kPx];
-  float wy[kPx], wx[kPx];
-#pragma unroll
-  for (int k = 0; k < kPx; ++k) {
-    const int q = min(q0 + k, opix - 1);  // tail lanes recompute the last pixel (not stored)
-    const int oy = q / a.out_w;
-    int ox = q - oy * a.out_w;
-    if (b.flip) ox = a.out_w - 1 - ox;
-    // bilinear, align_corners=False: src = (dst + 0.5) * in/out - 0.5, clamped at 0
-    const float sy = fmaxf((static_cast<float>(oy) + 0.5f) * fy - 0.5f, 0.f);
-    const float sx = fmaxf((static_cast<float>(ox) + 0.5f) * fx - 0.5f, 0.f);
-    const int y0 = min(static_cast<int>(sy), b.h - 1), x0 = min(static_cast<int>(sx), b.w - 1);
-    const int y1 = y0 + (y0 < b.h - 1 ? 1 : 0), x1 = x0 + (x0 < b.w - 1 ? 1 : 0);
-    wy[k] = sy - static_cast<float>(y0);
-    wx[k] = sx - static_cast<float>(x0);
-    const int64_t r0 = static_cast<int64_t>(b.y + y0) * a.in_w, r1 = static_cast<int64_t>(b.y + y1) * a.in_w;
-    const int64_t c0 = b.x + x0, c1 = b.x + x1;
-    i00[k] = r0 + c0;
-    i01[k] = r0 + c1;
-    i10[k] = r1 + c0;
-    i11[k] = r1 + c1;
-  }
-  const bool vec = (opix % kPx == 0) && (q0 + kPx <= opix);  // 4 contiguous outputs per channel, 8 B aligned
-  const int64_t o = img * static_cast<int64_t>(C) * opix + q0;
-  for (int c = 0; c < C; ++c) {
-    float v[kPx];
+  const bool vec_ok = (ow % kPx) == 0;  // band rows start 4-aligned in the plane: aligned vector stores
+  for (int q0 = static_cast<int>(threadIdx.x) * kPx; q0 < n; q0 += kThreads * kPx) {
+    int ya[kPx], yb[kPx], xa[kPx], xb[kPx];
+    float wy[kPx], wx[kPx];
 #pragma unroll
     for (int k = 0; k < kPx; ++k) {
-      float v00, v01, v10, v11;
-      if constexpr (HWC) {
-        v00 = ld(s + i00[k] * C + c);
-        v01 = ld(s + i01[k] * C + c);
-        v10 = ld(s + i10[k] * C + c);
-        v11 = ld(s + i11[k] * C + c);
-      } else {
-        const Tin* sc = s + c * plane;
-        v00 = ld(sc + i00[k]);
-        v01 = ld(sc + i01[k]);
-        v10 = ld(sc + i10[k]);
-        v11 = ld(sc + i11[k]);
-      }
-      const float top = v00 + (v01 - v00) * wx[k];
-      const float bot = v10 + (v11 - v10) * wx[k];
-      v[k] = top + (bot - top) * wy[k];
-      if (aff.enabled) v[k] = fmaf(v[k], aff.scale[c], aff.bias[c]);
+      const int q = min(q0 + k, n - 1);  // tail lanes recompute the last pixel (not stored)
+      const int r = static_cast<int>(static_cast<uint32_t>(q) / static_cast<uint32_t>(ow));
+      int ox = q - r * ow;
+      if (b.flip) ox = ow - 1 - ox;
+      const float sy = src_coord(oy0 + r, fy), sx = src_coord(ox, fx);
+      const int y0 = min(static_cast<int>(sy), b.h - 1), x0 = min(static_cast<int>(sx), b.w - 1);
+      ya[k] = y0;
+      yb[k] = y0 + (y0 < b.h - 1 ? 1 : 0);
+      xa[k] = x0;
+      xb[k] = x0 + (x0 < b.w - 1 ? 1 : 0);
+      wy[k] = sy - static_cast<float>(y0);
+      wx[k] = sx - static_cast<float>(x0);
     }
-    const int64_t oc = o + static_cast<int64_t>(c) * opix;
-    if constexpr (OUT_BF16) {
-      uint16_t* d = static_cast<uint16_t*>(dst) + oc;
-      if (vec) {
-        *reinterpret_cast<uint2*>(d) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-      } else {
-        for (int k = 0; k < kPx && q0 + k < opix; ++k) d[k] = f32_to_bf16_bits(v[k]);
+    const bool vec = vec_ok && (q0 + kPx <= n);
+    const int64_t o = img * C * opix + static_cast<int64_t>(oy0) * ow + q0;
+    for (int c = 0; c < C; ++c) {
+      float v[kPx];
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) {
+        const float v00 = tap(c, ya[k], xa[k]), v01 = tap(c, ya[k], xb[k]);
+        const float v10 = tap(c, yb[k], xa[k]), v11 = tap(c, yb[k], xb[k]);
+        const float top = v00 + (v01 - v00) * wx[k];
+        const float bot = v10 + (v11 - v10) * wx[k];
+        v[k] = top + (bot - top) * wy[k];
+        if (aff.enabled) v[k] = fmaf(v[k], aff.scale[c], aff.bias[c]);
       }
-    } else {
-      float* d = static_cast<float*>(dst) + oc;
-      if (vec) {
-        *reinterpret_cast<float4*>(d) = make_float4(v[0], v[1], v[2], v[3]);
+      const int64_t oc = o + static_cast<int64_t>(c) * opix;
+      if constexpr (OUT_BF16) {
+        uint16_t* d = static_cast<uint16_t*>(dst) + oc;
+        if (vec) {
+          *reinterpret_cast<uint2*>(d) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+        } else {
+          for (int k = 0; k < kPx && q0 + k < n; ++k) d[k] = f32_to_bf16_bits(v[k]);
+        }
       } else {
-        for (int k = 0; k < kPx && q0 + k < opix; ++k) d[k] = v[k];
+        float* d = static_cast<float*>(dst) + oc;
+        if (vec) {
+          *reinterpret_cast<float4*>(d) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+          for (int k = 0; k < kPx && q0 + k < n; ++k) d[k] = v[k];
+        }
       }
     }
   }
 }
 
+// HWC=1: src rows are [H, W, C]; else [C, H, W]. out: [B, C, OH, OW].
+// LDS layout: (plane p, band row r) rows of `stride` bytes; row (p, r) holds
+// the 16 B-aligned global chunks covering the crop's span of that source row,
+// which therefore starts head(p, r) = (global address & 15) bytes into it.
+template <typename Tin, int HWC, int OUT_BF16>
+__global__ void __launch_bounds__(kThreads) rrc_band_kernel(void* __restrict__ dst, const Tin* __restrict__ src,
+                                                           AugmentSpec a, int32_t bands, int32_t band_rows,
+                                                           int32_t lds_cap, RowIndex ri, Affine aff,
+                                                           const CropBox* __restrict__ boxes) {
+  extern __shared__ uint4 lds4[];
+  const uint32_t img = blockIdx.x / static_cast<uint32_t>(bands);
+  const int band = static_cast<int>(blockIdx.x - img * static_cast<uint32_t>(bands));
+  const int64_t srow = source_row(ri, img);
+  const CropBox b = boxes[img];  // wave-uniform (scalar) load
+  const int oy0 = band * band_rows, oy1 = min(oy0 + band_rows, a.out_h);
+  const int C = a.channels;
+  constexpr int kSz = static_cast<int>(sizeof(Tin));
+  const int planes = HWC ? 1 : C, cin = HWC ? C : 1;
+  const int64_t plane_elems = static_cast<int64_t>(a.in_h) * a.in_w;
+  const int64_t row_pitch = static_cast<int64_t>(a.in_w) * cin;  // elements
+  const Tin* s = src + srow * plane_elems * C;
+
+  const float fy = static_cast<float>(b.h) / a.out_h;
+  const int ylo = min(static_cast<int>(src_coord(oy0, fy)), b.h - 1);
+  const int ylast = min(static_cast<int>(src_coord(oy1 - 1, fy)), b.h - 1);
+  const uint32_t nrows = static_cast<uint32_t>(ylast + (ylast < b.h - 1 ? 1 : 0) - ylo + 1);
+  // 16 B chunks per LDS row: the crop span (b.w pixels) starting anywhere in a chunk
+  const uint32_t cpr = (15u + static_cast<uint32_t>(b.w * cin * kSz) + 15u) >> 4;
+  const uint32_t stride = cpr << 4;
+
+  if (static_cast<int64_t>(planes) * nrows * stride > lds_cap) {  // taps from global memory
+    resample_band<OUT_BF16>(dst, img, a, b, oy0, oy1, aff, [&](int c, int y, int x) {
+      const int p = HWC ? 0 : c, ci = HWC ? c : 0;
+      return ld(s + p * plane_elems + (b.y + y) * row_pitch + static_cast<int64_t>(b.x + x) * cin + ci);
+    });
+    return;
+  }
+
+  // ---- stage the band: crop rows ylo .. ylo+nrows-1 of every plane, 16 B chunks
+  const uint8_t* sb = reinterpret_cast<const uint8_t*>(s);
+  const uintptr_t img_lo = reinterpret_cast<uintptr_t>(s);
+  const uintptr_t img_hi = img_lo + static_cast<uintptr_t>(plane_elems * C * kSz);
+  const uintptr_t band_base =
+      img_lo + static_cast<uintptr_t>(((b.y + ylo) * row_pitch + static_cast<int64_t>(b.x) * cin) * kSz);
+  const uintptr_t plane_b = static_cast<uintptr_t>(plane_elems * kSz), pitch_b = static_cast<uintptr_t>(row_pitch * kSz);
+  const uint32_t total = static_cast<uint32_t>(planes) * nrows * cpr;
+  constexpr int kIlp = 4;
+  for (uint32_t w0 = threadIdx.x; w0 < total; w0 += kIlp * kThreads) {
+    uint4 v[kIlp];
+#pragma unroll
+    for (int k = 0; k < kIlp; ++k) {
+      const uint32_t w = w0 + k * kThreads;
+      if (w < total) {
+        const uint32_t pr = w / cpr, ch = w - pr * cpr;
+        const uint32_t p = pr / nrows, r = pr - p * nrows;
+        const uintptr_t row = band_base + p * plane_b + r * pitch_b;
+        const uintptr_t g = (row & ~static_cast<uintptr_t>(15)) + 16u * ch;
+        // addressed off the kernel argument (not an integer round trip) so the
+        // compiler keeps the global address space: global_load_dwordx4, not flat
+        const uint8_t* gp = sb + static_cast<intptr_t>(g - img_lo);
+        if (g >= img_lo && g + 16 <= img_hi) {
+          v[k] = *reinterpret_cast<const uint4*>(gp);
+        } else {  // chunk straddles the image bounds: the bytes outside are never sampled
+          uint32_t wv[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+          for (int j = 0; j < 16; ++j)
+            if (g + j >= img_lo && g + j < img_hi) wv[j >> 2] |= static_cast<uint32_t>(gp[j]) << ((j & 3) * 8);
+          v[k] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kIlp; ++k)
+      if (w0 + k * kThreads < total) lds4[w0 + k * kThreads] = v[k];
+  }
+  __syncthreads();
+
+  const uint8_t* lds = reinterpret_cast<const uint8_t*>(lds4);
+  // low bits of the per-row global addresses (mod 2^32 is enough for & 15)
+  const uint32_t base_lo = static_cast<uint32_t>(band_base);
+  const uint32_t plane_lo = static_cast<uint32_t>(plane_b), pitch_lo = static_cast<uint32_t>(pitch_b);
+  resample_band<OUT_BF16>(dst, img, a, b, oy0, oy1, aff, [&](int c, int y, int x) {
+    const uint32_t p = HWC ? 0u : static_cast<uint32_t>(c);
+    const uint32_t ci = HWC ? static_cast<uint32_t>(c) : 0u;
+    const uint32_t r = static_cast<uint32_t>(y - ylo);
+    const uint32_t head = (base_lo + p * plane_lo + r * pitch_lo) & 15u;
+    const uint32_t off = (p * nrows + r) * stride + head + (static_cast<uint32_t>(x) * cin + ci) * kSz;
+    return ld(reinterpret_cast<const Tin*>(lds + off));
+  });
+}
+
+// Band height and LDS allocation for the worst case (crop = whole image):
+// rows <= ceil((R-1) * in_h / out_h) + 3, each row the 16 B chunks covering
+// in_w * cin elements that may start anywhere in a chunk.
+struct BandPlan {
+  int32_t rows;
+  int64_t lds;  // 0: taps from global memory
+};
+
+BandPlan plan_band(const AugmentSpec& a, int hwc, int elem, int path) {
+  const int planes = hwc ? 1 : a.channels, cin = hwc ? a.channels : 1;
+  const int64_t stride = (static_cast<int64_t>(a.in_w) * cin * elem + 15 + 15) / 16 * 16;
+  for (int R = kBandMaxRows; R >= 1 && path != 2; R /= 2) {
+    const int64_t rows =
+        std::min<int64_t>((static_cast<int64_t>(R - 1) * a.in_h + a.out_h - 1) / a.out_h + 3, a.in_h + 1);
+    const int64_t lds = planes * rows * stride;
+    if (lds <= kBandLdsBudget) return {R, lds};
+  }
+  return {kBandMaxRows, 0};
+}
+
 template <typename Tin, int HWC>
 int launch_rrc(void* dst, int32_t out_dt, const void* src, int64_t batch, const AugmentSpec& a, const RowIndex& ri,
-               const Affine& aff, int32_t* boxes_out, hipStream_t st) {
+               const Affine& aff, int32_t* boxes_out, int path, hipStream_t st) {
+  const BandPlan pl = plan_band(a, HWC, static_cast<int>(sizeof(Tin)), path);
+  if (path == 1 && pl.lds == 0) return -5;  // LDS path requested but the geometry does not fit the budget
+  const int64_t bands = (a.out_h + pl.rows - 1) / pl.rows;
+  if (batch * bands >= (int64_t{1} << 31)) return -4;
   auto* boxes = reinterpret_cast<CropBox*>(boxes_out);
   hipLaunchKernelGGL(rrc_boxes_kernel, dim3(static_cast<uint32_t>((batch + kThreads - 1) / kThreads)), dim3(kThreads),
                      0, st, a, batch, ri, boxes);
-  const int64_t tiles = (static_cast<int64_t>(a.out_h) * a.out_w + kThreads * kPx - 1) / (kThreads * kPx);
-  const dim3 grid(static_cast<uint32_t>(batch * tiles));
+  const dim3 grid(static_cast<uint32_t>(batch * bands));
+  const auto* s = static_cast<const Tin*>(src);
+  const size_t lds = static_cast<size_t>(pl.lds);
+  const int32_t nb = static_cast<int32_t>(bands), cap = static_cast<int32_t>(pl.lds);
   if (out_dt == kBF16)
-    hipLaunchKernelGGL((rrc_kernel<Tin, HWC, 1>), grid, dim3(kThreads), 0, st, dst, static_cast<const Tin*>(src), a,
-                       tiles, ri, aff, boxes);
+    hipLaunchKernelGGL((rrc_band_kernel<Tin, HWC, 1>), grid, dim3(kThreads), lds, st, dst, s, a, nb, pl.rows, cap, ri,
+                       aff, boxes);
   else if (out_dt == kF32)
-    hipLaunchKernelGGL((rrc_kernel<Tin, HWC, 0>), grid, dim3(kThreads), 0, st, dst, static_cast<const Tin*>(src), a,
-                       tiles, ri, aff, boxes);
+    hipLaunchKernelGGL((rrc_band_kernel<Tin, HWC, 0>), grid, dim3(kThreads), lds, st, dst, s, a, nb, pl.rows, cap, ri,
+                       aff, boxes);
   else
     return -1;
   return static_cast<int>(hipGetLastError());
@@ -194,22 +308,22 @@ int launch_rrc(void* dst, int32_t out_dt, const void* src, int64_t batch, const 
 
 int random_resized_crop(void* dst, int32_t out_dt, const void* src, int32_t in_dt, int64_t batch,
                         const AugmentSpec& a, int hwc, const RowIndex& ri, const Affine& aff, int32_t* boxes_out,
-                        hipStream_t st) {
+                        int path, hipStream_t st) {
   if (batch <= 0) return 0;
   if (boxes_out == nullptr) return -3;  // [batch, 5] int32 device buffer: boxes are drawn there first
   if (a.channels < 1 || a.channels > kMaxAffineChannels || a.in_h < 1 || a.in_w < 1 || a.out_h < 1 || a.out_w < 1)
     return -2;
-  if (batch * ((static_cast<int64_t>(a.out_h) * a.out_w + kThreads - 1) / kThreads) >= (int64_t{1} << 31)) return -4;
+  if (path < 0 || path > 2) return -2;
   switch (in_dt) {
     case kU8:
-      return hwc ? launch_rrc<uint8_t, 1>(dst, out_dt, src, batch, a, ri, aff, boxes_out, st)
-                 : launch_rrc<uint8_t, 0>(dst, out_dt, src, batch, a, ri, aff, boxes_out, st);
+      return hwc ? launch_rrc<uint8_t, 1>(dst, out_dt, src, batch, a, ri, aff, boxes_out, path, st)
+                 : launch_rrc<uint8_t, 0>(dst, out_dt, src, batch, a, ri, aff, boxes_out, path, st);
     case kF32:
-      return hwc ? launch_rrc<float, 1>(dst, out_dt, src, batch, a, ri, aff, boxes_out, st)
-                 : launch_rrc<float, 0>(dst, out_dt, src, batch, a, ri, aff, boxes_out, st);
+      return hwc ? launch_rrc<float, 1>(dst, out_dt, src, batch, a, ri, aff, boxes_out, path, st)
+                 : launch_rrc<float, 0>(dst, out_dt, src, batch, a, ri, aff, boxes_out, path, st);
     case kBF16:
-      return hwc ? launch_rrc<uint16_t, 1>(dst, out_dt, src, batch, a, ri, aff, boxes_out, st)
-                 : launch_rrc<uint16_t, 0>(dst, out_dt, src, batch, a, ri, aff, boxes_out, st);
+      return hwc ? launch_rrc<uint16_t, 1>(dst, out_dt, src, batch, a, ri, aff, boxes_out, path, st)
+                 : launch_rrc<uint16_t, 0>(dst, out_dt, src, batch, a, ri, aff, boxes_out, path, st);
   }
   return -1;
 }

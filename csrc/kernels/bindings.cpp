@@ -312,7 +312,7 @@ PYBIND11_MODULE(_ddl_hip, m) {
          int out_h, int out_w, uint64_t seed, int64_t sample_base, float scale_min, float scale_max, float ratio_min,
          float ratio_max, float flip_p, int mode, uintptr_t idx, int64_t base, std::vector<uint64_t> keys,
          uint64_t n_domain, uint32_t half_bits, std::vector<float> scale, std::vector<float> bias, uintptr_t boxes_out,
-         uintptr_t stream) {
+         int path, uintptr_t stream) {
         ddl::AugmentSpec a{};
         a.seed = seed;
         a.sample_base = sample_base;
@@ -329,14 +329,15 @@ PYBIND11_MODULE(_ddl_hip, m) {
         const ddl::RowIndex ri = make_index(mode, idx, base, keys, n_domain, half_bits);
         const ddl::Affine aff = make_affine(scale, bias, 1);
         check_rc(ddl::random_resized_crop(as_ptr<void>(dst), out_dt, as_ptr<const void>(src), in_dt, batch, a,
-                                          hwc ? 1 : 0, ri, aff, as_ptr<int32_t>(boxes_out), as_stream(stream)),
+                                          hwc ? 1 : 0, ri, aff, as_ptr<int32_t>(boxes_out), path, as_stream(stream)),
                  "random_resized_crop");
       },
       py::arg("dst"), py::arg("out_dt"), py::arg("src"), py::arg("in_dt"), py::arg("batch"), py::arg("hwc"),
       py::arg("in_h"), py::arg("in_w"), py::arg("channels"), py::arg("out_h"), py::arg("out_w"), py::arg("seed"),
       py::arg("sample_base"), py::arg("scale_min"), py::arg("scale_max"), py::arg("ratio_min"), py::arg("ratio_max"),
       py::arg("flip_p"), py::arg("mode"), py::arg("idx"), py::arg("base"), py::arg("keys"), py::arg("n_domain"),
-      py::arg("half_bits"), py::arg("scale"), py::arg("bias"), py::arg("boxes_out"), py::arg("stream"));
+      py::arg("half_bits"), py::arg("scale"), py::arg("bias"), py::arg("boxes_out"), py::arg("path"),
+      py::arg("stream"));
   m.def(
       "pack_columns",
       [](std::vector<uintptr_t> srcs, std::vector<int> widths, int in_dt, uintptr_t dst, int out_dt, int64_t n_rows,
@@ -365,7 +366,8 @@ PYBIND11_MODULE(_ddl_hip, m) {
       "pad_pack_tokens",
       [](uintptr_t tokens, uintptr_t offsets, uintptr_t row_start, uintptr_t row_end, uintptr_t seg_offsets,
          int64_t n_seg, uintptr_t out_tokens, uintptr_t attn_mask, uintptr_t position_ids, bool pos_is_i64,
-         uintptr_t segment_ids, int64_t rows, int64_t seq_len, int pad_id, int mode, uintptr_t stream) {
+         uintptr_t segment_ids, uintptr_t cu_seqlens_out, int64_t rows, int64_t seq_len, int pad_id, int mode,
+         uintptr_t stream) {
         ddl::TokenSpec sp{};
         sp.tokens = as_ptr<const int32_t>(tokens);
         sp.offsets = as_ptr<const int64_t>(offsets);
@@ -378,6 +380,7 @@ PYBIND11_MODULE(_ddl_hip, m) {
         sp.position_ids = as_ptr<void>(position_ids);
         sp.pos_is_i64 = pos_is_i64 ? 1 : 0;
         sp.segment_ids = as_ptr<int32_t>(segment_ids);
+        sp.cu_seqlens_out = as_ptr<int64_t>(cu_seqlens_out);
         sp.rows = rows;
         sp.seq_len = seq_len;
         sp.pad_id = pad_id;
@@ -386,8 +389,8 @@ PYBIND11_MODULE(_ddl_hip, m) {
       },
       py::arg("tokens"), py::arg("offsets"), py::arg("row_start"), py::arg("row_end"), py::arg("seg_offsets"),
       py::arg("n_seg"), py::arg("out_tokens"), py::arg("attn_mask"), py::arg("position_ids"), py::arg("pos_is_i64"),
-      py::arg("segment_ids"), py::arg("rows"), py::arg("seq_len"), py::arg("pad_id"), py::arg("mode"),
-      py::arg("stream"));
+      py::arg("segment_ids"), py::arg("cu_seqlens_out"), py::arg("rows"), py::arg("seq_len"), py::arg("pad_id"),
+      py::arg("mode"), py::arg("stream"));
   m.def(
       "checksum_words",
       [](uintptr_t ptr, int64_t bytes, uintptr_t out, uintptr_t scratch, int64_t scratch_len, uintptr_t stream) {

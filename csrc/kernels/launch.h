@@ -58,7 +58,7 @@ struct CropBox {
 };
 int random_resized_crop(void* dst, int32_t out_dt, const void* src, int32_t in_dt, int64_t batch,
                         const AugmentSpec& a, int hwc, const RowIndex& ri, const Affine& aff, int32_t* boxes_out,
-                        hipStream_t st);
+                        int path, hipStream_t st);
 
 // tokens.hip ----------------------------------------------------------------
 // Pad: row b takes tokens[offsets[b] : offsets[b+1]] (truncated to seq_len);
@@ -78,6 +78,7 @@ struct TokenSpec {
   uint8_t* attn_mask;
   void* position_ids;
   int32_t* segment_ids;        // pack mode only (or null)
+  int64_t* cu_seqlens_out;     // pack mode: copy of seg_offsets[0..n_seg] (or null)
   int64_t rows;
   int64_t seq_len;
   int32_t pad_id;

@@ -8,31 +8,104 @@
 // position id restarts at every sequence boundary and a segment id marks
 // which sequence a token belongs to (what varlen attention consumes).
 //
-// One workgroup per output row; each lane writes 4 consecutive positions so
-// the three outputs are stored as 16 B (tokens, i32 ids) / 4 B (mask) vectors.
+// Grid: one workgroup per (row, chunk of kSpan positions), so a 64 x 4096
+// batch is 512 workgroups (the first form ran one workgroup per row: 64 of the
+// 256 CUs busy). Each lane writes 4 consecutive positions as 16 B (tokens,
+// i32 ids) / 4 B (mask) vectors. Pack mode copies the sequence starts into
+// LDS once per workgroup (one coalesced read) and binary-searches there; the
+// first form binary-searched global memory for every token, a chain of
+// ~log2(n_seg) dependent loads per position.
 #include "common.h"
 #include "launch.h"
 
 namespace ddl {
 namespace {
 
-constexpr int kThreads = 256;
+constexpr int kThreads = 128;
+constexpr int kSpan = kThreads * 4;  // positions per workgroup
+constexpr int kSegCap = 1024;        // sequence starts staged in LDS (8 KB)
 
-__device__ __forceinline__ int64_t upper_bound_i64(const int64_t* a, int64_t n, int64_t v) {
+// index of the last entry <= v of the sorted a[0..n) (a[0] <= v)
+template <typename At>
+__device__ __forceinline__ int64_t last_le(At at, int64_t n, int64_t v) {
   int64_t lo = 0, hi = n;
   while (lo < hi) {
     const int64_t mid = (lo + hi) >> 1;
-    if (a[mid] <= v)
+    if (at(mid) <= v)
       lo = mid + 1;
     else
       hi = mid;
   }
-  return lo;
+  return lo - 1;
 }
 
-__global__ void __launch_bounds__(kThreads) pad_pack_kernel(TokenSpec sp) {
-  const int64_t row = blockIdx.x;
+template <typename At>
+__device__ __forceinline__ void emit4(const TokenSpec& sp, int64_t row, int64_t p0, int64_t start, int64_t len,
+                                      At seg_at) {
   const int64_t S = sp.seq_len;
+  const int32_t* src = sp.tokens + start;
+  int32_t tok[4], pos[4], seg[4];
+  uint8_t msk[4];
+  int64_t s = -1;  // current sequence (pack mode): searched once, then advanced
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t p = p0 + k;
+    const bool valid = p < len;
+    tok[k] = valid ? src[p] : sp.pad_id;
+    msk[k] = valid ? 1 : 0;
+    if (sp.mode == 0) {
+      pos[k] = valid ? static_cast<int32_t>(p) : 0;
+      seg[k] = 0;
+    } else if (valid) {
+      const int64_t g = start + p;  // flat token index
+      if (s < 0)
+        s = last_le(seg_at, sp.n_seg + 1, g);
+      else
+        while (s + 1 <= sp.n_seg && seg_at(s + 1) <= g) ++s;
+      pos[k] = static_cast<int32_t>(g - seg_at(s));
+      seg[k] = static_cast<int32_t>(s);
+    } else {
+      pos[k] = 0;
+      seg[k] = -1;
+    }
+  }
+  const int64_t o = row * S + p0;
+  if (p0 + 4 <= S && (S % 4 == 0)) {
+    *reinterpret_cast<int4*>(sp.out_tokens + o) = make_int4(tok[0], tok[1], tok[2], tok[3]);
+    if (sp.attn_mask) {
+      const uint32_t m = msk[0] | (msk[1] << 8) | (msk[2] << 16) | (static_cast<uint32_t>(msk[3]) << 24);
+      *reinterpret_cast<uint32_t*>(sp.attn_mask + o) = m;
+    }
+    if (sp.position_ids) {
+      if (sp.pos_is_i64) {
+        int64_t* pp = static_cast<int64_t*>(sp.position_ids) + o;
+        *reinterpret_cast<longlong2*>(pp) = make_longlong2(pos[0], pos[1]);
+        *reinterpret_cast<longlong2*>(pp + 2) = make_longlong2(pos[2], pos[3]);
+      } else {
+        *reinterpret_cast<int4*>(static_cast<int32_t*>(sp.position_ids) + o) = make_int4(pos[0], pos[1], pos[2], pos[3]);
+      }
+    }
+    if (sp.segment_ids) *reinterpret_cast<int4*>(sp.segment_ids + o) = make_int4(seg[0], seg[1], seg[2], seg[3]);
+  } else {
+    for (int k = 0; k < 4 && p0 + k < S; ++k) {
+      sp.out_tokens[o + k] = tok[k];
+      if (sp.attn_mask) sp.attn_mask[o + k] = msk[k];
+      if (sp.position_ids) {
+        if (sp.pos_is_i64)
+          static_cast<int64_t*>(sp.position_ids)[o + k] = pos[k];
+        else
+          static_cast<int32_t*>(sp.position_ids)[o + k] = pos[k];
+      }
+      if (sp.segment_ids) sp.segment_ids[o + k] = seg[k];
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) pad_pack_kernel(TokenSpec sp, int32_t chunks) {
+  __shared__ int64_t seg_lds[kSegCap];
+  const uint32_t row = blockIdx.x / static_cast<uint32_t>(chunks);
+  const int64_t p0 = static_cast<int64_t>(blockIdx.x - row * static_cast<uint32_t>(chunks)) * kSpan +
+                     static_cast<int64_t>(threadIdx.x) * 4;
   int64_t start, len;
   if (sp.mode == 0) {
     start = sp.offsets[row];
@@ -41,68 +114,19 @@ __global__ void __launch_bounds__(kThreads) pad_pack_kernel(TokenSpec sp) {
     start = sp.row_start[row];
     len = sp.row_end[row] - start;
   }
-  if (len > S) len = S;
+  if (len > sp.seq_len) len = sp.seq_len;
   if (len < 0) len = 0;
-  int32_t* out_tok = sp.out_tokens + row * S;
-  const int32_t* src = sp.tokens + start;
-  for (int64_t p0 = static_cast<int64_t>(threadIdx.x) * 4; p0 < S; p0 += kThreads * 4) {
-    int32_t tok[4];
-    int32_t pos[4];
-    int32_t seg[4];
-    uint8_t msk[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int64_t p = p0 + k;
-      const bool valid = p < len;
-      tok[k] = valid ? src[p] : sp.pad_id;
-      msk[k] = valid ? 1 : 0;
-      if (sp.mode == 0) {
-        pos[k] = valid ? static_cast<int32_t>(p) : 0;
-        seg[k] = 0;
-      } else if (valid) {
-        const int64_t g = start + p;  // flat token index
-        const int64_t s = upper_bound_i64(sp.seg_offsets, sp.n_seg + 1, g) - 1;
-        pos[k] = static_cast<int32_t>(g - sp.seg_offsets[s]);
-        seg[k] = static_cast<int32_t>(s);
-      } else {
-        pos[k] = 0;
-        seg[k] = -1;
-      }
-    }
-    const bool full = (p0 + 4 <= S);
-    if (full && (S % 4 == 0)) {
-      *reinterpret_cast<int4*>(out_tok + p0) = make_int4(tok[0], tok[1], tok[2], tok[3]);
-      if (sp.attn_mask) {
-        const uint32_t m = msk[0] | (msk[1] << 8) | (msk[2] << 16) | (static_cast<uint32_t>(msk[3]) << 24);
-        *reinterpret_cast<uint32_t*>(sp.attn_mask + row * S + p0) = m;
-      }
-      if (sp.position_ids) {
-        if (sp.pos_is_i64) {
-          int64_t* pp = static_cast<int64_t*>(sp.position_ids) + row * S + p0;
-          *reinterpret_cast<longlong2*>(pp) = make_longlong2(pos[0], pos[1]);
-          *reinterpret_cast<longlong2*>(pp + 2) = make_longlong2(pos[2], pos[3]);
-        } else {
-          *reinterpret_cast<int4*>(static_cast<int32_t*>(sp.position_ids) + row * S + p0) =
-              make_int4(pos[0], pos[1], pos[2], pos[3]);
-        }
-      }
-      if (sp.segment_ids)
-        *reinterpret_cast<int4*>(sp.segment_ids + row * S + p0) = make_int4(seg[0], seg[1], seg[2], seg[3]);
-    } else {
-      for (int k = 0; k < 4 && p0 + k < S; ++k) {
-        const int64_t o = row * S + p0 + k;
-        out_tok[p0 + k] = tok[k];
-        if (sp.attn_mask) sp.attn_mask[o] = msk[k];
-        if (sp.position_ids) {
-          if (sp.pos_is_i64)
-            static_cast<int64_t*>(sp.position_ids)[o] = pos[k];
-          else
-            static_cast<int32_t*>(sp.position_ids)[o] = pos[k];
-        }
-        if (sp.segment_ids) sp.segment_ids[o] = seg[k];
-      }
-    }
-  }
+  const bool staged = sp.mode == 1 && sp.n_seg + 1 <= kSegCap;  // kernel-uniform
+  if (staged)
+    for (int64_t i = threadIdx.x; i <= sp.n_seg; i += kThreads) seg_lds[i] = sp.seg_offsets[i];
+  if (sp.cu_seqlens_out != nullptr && blockIdx.x == 0)  // owned copy of the sequence starts (cu_seqlens)
+    for (int64_t i = threadIdx.x; i <= sp.n_seg; i += kThreads) sp.cu_seqlens_out[i] = sp.seg_offsets[i];
+  __syncthreads();
+  if (p0 >= sp.seq_len) return;
+  if (staged)
+    emit4(sp, row, p0, start, len, [&](int64_t i) { return seg_lds[i]; });
+  else
+    emit4(sp, row, p0, start, len, [&](int64_t i) { return sp.seg_offsets[i]; });
 }
 
 }  // namespace
@@ -111,7 +135,10 @@ int pad_pack_tokens(const TokenSpec& spec, hipStream_t st) {
   if (spec.rows <= 0 || spec.seq_len <= 0) return 0;
   if (spec.mode == 0 && !spec.offsets) return -2;
   if (spec.mode == 1 && (!spec.row_start || !spec.row_end || !spec.seg_offsets)) return -2;
-  hipLaunchKernelGGL(pad_pack_kernel, dim3(static_cast<uint32_t>(spec.rows)), dim3(kThreads), 0, st, spec);
+  const int64_t chunks = (spec.seq_len + kSpan - 1) / kSpan;
+  if (spec.rows * chunks >= (int64_t{1} << 31)) return -4;
+  hipLaunchKernelGGL(pad_pack_kernel, dim3(static_cast<uint32_t>(spec.rows * chunks)), dim3(kThreads), 0, st, spec,
+                     static_cast<int32_t>(chunks));
   return static_cast<int>(hipGetLastError());
 }
 

@@ -213,6 +213,16 @@ class Connection:
     def unlock_windows(self) -> None:
         """Reference ``Unlock_all`` (ddl/connection.py:45-49); see ``lock_windows``."""
 
+    def sync(self, target: int = 0) -> None:
+        """Reference ``Win.Sync`` memory barrier (ddl/connection.py:61-63, 144-151).
+
+        Nothing to do: every hand-off stores the slot state word with release and
+        loads it with acquire semantics (csrc/runtime/arena.cpp), which orders the
+        window bytes; device reads are ordered by the H2D copy's stream events.
+        """
+
+    _sync = sync
+
     # ------------------------------------------------------------ hand-off
     def acquire(self, p: int, s: int, timeout_s: float | None = None) -> dict:
         """Wait until producer ``p`` publishes slot ``s``; take it (READY -> HELD).
@@ -325,6 +335,12 @@ class ProducerConnection:
     def Barrier(self) -> None:  # noqa: N802
         self.pipe.send("barrier")
         self.pipe.recv("barrier", self.timeout_s)
+
+    def sync(self, target: int = 0) -> None:
+        """Reference ``Win.Sync`` (ddl/connection.py:61-63): ordering comes from the
+        release/acquire slot state word, see ``Connection.sync``."""
+
+    _sync = sync
 
     def Istart_access_epoch(self, slot: int) -> WorkerInfo:  # noqa: N802
         """Wait until the consumer hands ``slot`` back (EMPTY), or shutdown."""

@@ -34,6 +34,7 @@ from __future__ import annotations
 
 import math
 import time
+from abc import ABC, abstractmethod
 from typing import Any, Iterator
 
 import torch
@@ -61,9 +62,42 @@ def _mix(a: int, b: int) -> int:
     return z ^ (z >> 31)
 
 
+class DistributedDataloaderABC(ABC):
+    """The reference's abstract consumer interface (ddl/mpi_dataloader.py:31-103).
+
+    ``_start_access_epoch`` / ``_end_access_epoch`` take / hand back the
+    current producer window, ``_advance_to_next_producer`` moves the cursor to
+    the next window of the round-robin, ``mark`` drives the state machine.
+    """
+
+    @abstractmethod
+    def __len__(self) -> int: ...
+
+    @abstractmethod
+    def __getitem__(self, index: int): ...
+
+    @abstractmethod
+    def _advance_to_next_producer(self) -> None: ...
+
+    @abstractmethod
+    def _finalize(self) -> None: ...
+
+    @abstractmethod
+    def _start_access_epoch(self, target_rank: int = 0) -> None: ...
+
+    @abstractmethod
+    def _end_access_epoch(self, target_rank: int = 0) -> None: ...
+
+    @abstractmethod
+    def _can_continue(self) -> bool: ...
+
+    @abstractmethod
+    def mark(self, mark: Marker) -> None: ...
+
+
 @for_all_methods(with_logging, exclude=["__getitem__", "__len__", "__iter__", "mark", "_on_batch_end",
                                         "_window", "_batch_from_window", "_schedule"])
-class DistributedDataLoader:
+class DistributedDataLoader(DistributedDataloaderABC):
     def __init__(
         self,
         producer_function: ProducerFunctionSkeleton,
@@ -459,13 +493,29 @@ class DistributedDataLoader:
             self.connection.release(p, s)
             self._host_window = None
 
-    def _advance_window(self) -> None:
-        self._release_window()
+    # reference protocol names (ddl/mpi_dataloader.py:200-218): the same state machine
+    def _start_access_epoch(self, target_rank: int = 0) -> None:
+        """Take the current window (staged in HBM, or the shm slot on the host path)."""
+        if self.connection is not None and self.connection.n_producers and not self._finalized:
+            self._window()
+
+    def _end_access_epoch(self, target_rank: int = 0) -> None:
+        """Hand the current window back to its producer."""
+        if self.connection is not None and self.connection.n_producers:
+            self._release_window()
+
+    def _advance_to_next_producer(self) -> None:
+        """Move the cursor to the next window of the producer round-robin."""
         self.window += 1
         self.window_in_epoch += 1
         self.batch = 0
-        P = self.connection.n_producers
-        self.target_rank = self.window % P + 1
+        self.target_rank = self.window % self.connection.n_producers + 1
+        if self.mode == "do_not_split_along_epoch":
+            self._update_len()
+
+    def _advance_window(self) -> None:
+        self._end_access_epoch()
+        self._advance_to_next_producer()
 
     def _on_batch_end(self) -> None:
         if self._finalized:

@@ -24,6 +24,7 @@ import dataclasses
 import math
 import os
 import time
+from abc import ABC, abstractmethod
 from typing import Any
 
 import numpy as np
@@ -65,8 +66,27 @@ class DataProducerOnInitReturn:
             raise ShapeMismatchError(self.splits, f"splits must sum to nValues={self.nValues}")
 
 
-@for_all_methods(with_logging, exclude=["_fill_round"])
-class DataPusher:
+class DataPusherABC(ABC):
+    """The reference's abstract producer engine (ddl/datapusher.py:22-41)."""
+
+    @abstractmethod
+    def push_data(self) -> None: ...
+
+    @abstractmethod
+    def _start_access_epoch(self, target_rank: int = -1) -> None: ...
+
+    @abstractmethod
+    def _end_access_epoch(self, target_rank: int = -1) -> None: ...
+
+    @abstractmethod
+    def sync(self) -> None: ...
+
+    @abstractmethod
+    def _finalize(self) -> None: ...
+
+
+@for_all_methods(with_logging, exclude=["_fill_round", "_istart_access_epoch", "_iend_access_epoch", "sync"])
+class DataPusher(DataPusherABC):
     def __init__(self, connection: ProducerConnection, rank_global: int = 0, world_size: int = 1):
         self.connection = connection
         self.rank_global = rank_global
@@ -139,6 +159,29 @@ class DataPusher:
             return [int(x) for x in ret], self.window_bytes
         return [], self.window_bytes
 
+    # ------------------------------------------------- reference protocol names
+    def sync(self) -> None:
+        """The reference's ``Win.Sync`` barrier (ddl/datapusher.py:126-127). Here the
+        slot state word is stored with release / loaded with acquire semantics
+        around every hand-off, which orders the window bytes: nothing to do."""
+
+    def _start_access_epoch(self, target_rank: int = -1) -> None:
+        """No-op, as in the reference (ddl/datapusher.py:129-130)."""
+
+    def _end_access_epoch(self, target_rank: int = -1) -> None:
+        """No-op, as in the reference (ddl/datapusher.py:132-133)."""
+
+    def _istart_access_epoch(self, slot: int) -> WorkerInfo:
+        """Wait until the consumer hands ``slot`` back, or shutdown (ddl/datapusher.py:135-136)."""
+        return self.connection.Istart_access_epoch(slot)
+
+    def _iend_access_epoch(self, slot: int, rnd: int, used: int, tags: list) -> WorkerInfo:
+        """Publish ``slot`` to the consumer (ddl/datapusher.py:138-139)."""
+        return self.connection.Iend_access_epoch(slot, seq=rnd, used_bytes=used, epoch=rnd, tags=tags)
+
+    def _finalize(self) -> None:
+        self.connection.finalize()
+
     def push_data(self) -> None:
         """Hot loop (reference ddl/datapusher.py:147-170)."""
         conn = self.connection
@@ -148,20 +191,21 @@ class DataPusher:
         slot = rnd % n_slots
         while True:
             t0 = time.perf_counter_ns()
-            if conn.Istart_access_epoch(slot) is WorkerInfo.STOP:
+            if self._istart_access_epoch(slot) is WorkerInfo.STOP:
                 break
             t1 = time.perf_counter_ns()
             faults.maybe_fail_producer(self.index, rnd)
+            self.sync()
             tags, used = self._fill_round(slot, rnd)
             t2 = time.perf_counter_ns()
-            if conn.Iend_access_epoch(slot, seq=rnd, used_bytes=used, epoch=rnd, tags=tags) is WorkerInfo.STOP:
+            if self._iend_access_epoch(slot, rnd, used, tags) is WorkerInfo.STOP:
                 break
             conn.arena.heartbeat(self.index, t2 - t1, t1 - t0)
             execute_callbacks("on_shuffle_end", self.callbacks, round=rnd, slot=slot)
             rnd += 1
             slot = (slot + 1) % n_slots
         execute_callbacks("on_push_end", self.callbacks)
-        conn.finalize()
+        self._finalize()
 
 
 def producer_main(pipe, producer_index: int, consumer_pid: int, rank: int, world_size: int,

@@ -14,6 +14,7 @@ token batches share the indexed-mode checkpoint format.
 from __future__ import annotations
 
 import dataclasses
+import functools
 
 import numpy as np
 import torch
@@ -23,6 +24,18 @@ from ..datasetwrapper import ProducerFunctionSkeleton
 from .. import _native
 from ..permutation import EpochOrder
 from .datasets import SharedArraySource
+
+
+@functools.lru_cache(maxsize=64)
+def _regions(batch: int, max_segments: int, max_len: int) -> dict[str, tuple[int, int]]:
+    out, off = {}, 0
+    for name, count, size in (("offsets", batch + 1, 8), ("row_start", max_segments, 8),
+                              ("row_end", max_segments, 8), ("seg_offsets", max_segments + 1, 8),
+                              ("tokens", batch * max_len, 4)):
+        out[name] = (off, count)
+        off += -(-count * size // 8) * 8
+    out["_total"] = (off, 0)
+    return out
 
 
 @dataclasses.dataclass(frozen=True)
@@ -38,15 +51,8 @@ class TokenWindowLayout:
         return self.batch * max(1, -(-self.max_len // self.seq_len))
 
     def regions(self) -> dict[str, tuple[int, int]]:
-        """name -> (byte offset, element count)."""
-        out, off = {}, 0
-        for name, count, size in (("offsets", self.batch + 1, 8), ("row_start", self.max_segments, 8),
-                                  ("row_end", self.max_segments, 8), ("seg_offsets", self.max_segments + 1, 8),
-                                  ("tokens", self.batch * self.max_len, 4)):
-            out[name] = (off, count)
-            off += -(-count * size // 8) * 8
-        out["_total"] = (off, 0)
-        return out
+        """name -> (byte offset, element count). Computed once per layout (per-batch host path)."""
+        return _regions(self.batch, self.max_segments, self.max_len)
 
     @property
     def nbytes(self) -> int:
@@ -170,16 +176,21 @@ def collate_token_window(buf: torch.Tensor, layout: TokenWindowLayout, mode: str
     mask = torch.empty((n_rows, s), dtype=torch.uint8, device=dev)
     pos = torch.empty((n_rows, s), dtype=torch.int64, device=dev)
     seg = torch.empty((n_rows, s), dtype=torch.int32, device=dev)
-    from .. import _native
     from ..ops.kernels import _stream_handle
 
-    _native.hip().pad_pack_tokens(
-        tokens=tokens.data_ptr(), offsets=0, row_start=v["row_start"].data_ptr(), row_end=v["row_end"].data_ptr(),
-        seg_offsets=v["seg_offsets"].data_ptr(), n_seg=n_seg, out_tokens=ids.data_ptr(), attn_mask=mask.data_ptr(),
-        position_ids=pos.data_ptr(), pos_is_i64=True, segment_ids=seg.data_ptr(), rows=n_rows, seq_len=s,
-        pad_id=pad_id, mode=1, stream=_stream_handle(None))
-    return {"input_ids": ids, "attention_mask": mask, "position_ids": pos, "segment_ids": seg,
-            "cu_seqlens": v["seg_offsets"][: n_seg + 1]}
+    # cu_seqlens is written by the kernel into a tensor of its own: a view of the
+    # staging buffer would be overwritten when the buffer is re-staged
+    if n_rows == 0:
+        cu = v["seg_offsets"][: n_seg + 1].clone()
+    else:
+        cu = torch.empty(n_seg + 1, dtype=torch.int64, device=dev)
+        _native.hip().pad_pack_tokens(
+            tokens=tokens.data_ptr(), offsets=0, row_start=v["row_start"].data_ptr(),
+            row_end=v["row_end"].data_ptr(), seg_offsets=v["seg_offsets"].data_ptr(), n_seg=n_seg,
+            out_tokens=ids.data_ptr(), attn_mask=mask.data_ptr(), position_ids=pos.data_ptr(), pos_is_i64=True,
+            segment_ids=seg.data_ptr(), cu_seqlens_out=cu.data_ptr(), rows=n_rows, seq_len=s, pad_id=pad_id, mode=1,
+            stream=_stream_handle(None))
+    return {"input_ids": ids, "attention_mask": mask, "position_ids": pos, "segment_ids": seg, "cu_seqlens": cu}
 
 
 def expected_tokens(source: SharedTokenSource, idx) -> list[np.ndarray]:

@@ -328,7 +328,7 @@ def random_resized_crop(src, index: torch.Tensor | None = None, *, perm: Feistel
                         base: int = 0, n_rows: int | None = None, size=(224, 224), scale=(0.08, 1.0),
                         ratio=(3.0 / 4.0, 4.0 / 3.0), flip_p: float = 0.5, seed: int = 0, sample_base: int = 0,
                         layout: str = "chw", out_dtype=torch.bfloat16, mean=None, std=None,
-                        return_boxes: bool = False, stream=None):
+                        return_boxes: bool = False, impl: str = "auto", stream=None):
     """Gathered images -> RandomResizedCrop + horizontal flip + normalise + cast, one gfx950 kernel.
 
     ``src`` rows are [C, H, W] (``layout="chw"``) or [H, W, C] (``"hwc"``),
@@ -337,8 +337,14 @@ def random_resized_crop(src, index: torch.Tensor | None = None, *, perm: Feistel
     hash(``seed``, ``sample_base`` + source row): the same sample gets the same
     crop under the same seed whichever rank or batch it lands in.
     Returns [B, C, size[0], size[1]] (and the [B, 5] int32 boxes y, x, h, w,
-    flip with ``return_boxes``).
+    flip with ``return_boxes``). ``impl``: ``"auto"`` stages each band of
+    output rows' source pixels in LDS when the band fits the kernel's LDS
+    budget, ``"lds"`` requires that (ValueError otherwise), ``"direct"`` reads
+    every tap from global memory; all three give identical results.
     """
+    paths = {"auto": 0, "lds": 1, "direct": 2}
+    if impl not in paths:
+        raise ValueError(f"impl must be one of {sorted(paths)}")
     out_dtype = _dtypes.to_torch_dtype(out_dtype)
     if layout not in ("chw", "hwc") or src.dim() != 4:
         raise ValueError("random_resized_crop expects [N, C, H, W] (chw) or [N, H, W, C] (hwc) rows")
@@ -361,7 +367,7 @@ def random_resized_crop(src, index: torch.Tensor | None = None, *, perm: Feistel
         batch=n_rows, hwc=layout == "hwc", in_h=int(h), in_w=int(w), channels=int(c), out_h=oh, out_w=ow,
         seed=int(seed) & ((1 << 64) - 1), sample_base=int(sample_base), scale_min=float(scale[0]),
         scale_max=float(scale[1]), ratio_min=float(ratio[0]), ratio_max=float(ratio[1]), flip_p=float(flip_p),
-        scale=sc, bias=bi, boxes_out=boxes.data_ptr(), stream=_stream_handle(stream),
+        scale=sc, bias=bi, boxes_out=boxes.data_ptr(), path=paths[impl], stream=_stream_handle(stream),
         **_index_kw(index, perm, base))
     return (out, boxes) if return_boxes else out
 
@@ -494,8 +500,8 @@ def pad_tokens(tokens: torch.Tensor, offsets: torch.Tensor, seq_len: int, pad_id
     _native.hip().pad_pack_tokens(
         tokens=tokens.data_ptr(), offsets=offsets.data_ptr(), row_start=0, row_end=0, seg_offsets=0, n_seg=0,
         out_tokens=out.data_ptr(), attn_mask=mask.data_ptr(), position_ids=pos.data_ptr(),
-        pos_is_i64=position_dtype == torch.int64, segment_ids=0, rows=b, seq_len=seq_len, pad_id=pad_id, mode=0,
-        stream=_stream_handle(stream))
+        pos_is_i64=position_dtype == torch.int64, segment_ids=0, cu_seqlens_out=0, rows=b, seq_len=seq_len,
+        pad_id=pad_id, mode=0, stream=_stream_handle(stream))
     return out, mask, pos
 
 
@@ -600,9 +606,9 @@ def pack_tokens(tokens: torch.Tensor, seq_offsets, seq_len: int, pad_id: int = 0
     _native.hip().pad_pack_tokens(
         tokens=tokens.data_ptr(), offsets=0, row_start=rs_d.data_ptr(), row_end=re_d.data_ptr(),
         seg_offsets=so_d.data_ptr(), n_seg=len(so) - 1, out_tokens=out.data_ptr(), attn_mask=mask.data_ptr(),
-        position_ids=pos.data_ptr(), pos_is_i64=position_dtype == torch.int64, segment_ids=seg.data_ptr(), rows=r,
-        seq_len=seq_len, pad_id=pad_id, mode=1, stream=_stream_handle(stream))
-    return out, mask, pos, seg, cu.to(dev)
+        position_ids=pos.data_ptr(), pos_is_i64=position_dtype == torch.int64, segment_ids=seg.data_ptr(),
+        cu_seqlens_out=0, rows=r, seq_len=seq_len, pad_id=pad_id, mode=1, stream=_stream_handle(stream))
+    return out, mask, pos, seg, so_d
 
 
 # ----------------------------------------------------------------- reductions

@@ -1,6 +1,6 @@
 """Parallelism: rank topology, launcher, cross-GPU global shuffle (RCCL/xGMI)."""
 
-from .env import init_distributed, read_env
+from .env import init_distributed, init_mpi, read_env
 from .launcher import distributed_dataloader, spawn_producers, start
 from .shuffle import (
     AllToAllGlobalShuffler,
@@ -12,6 +12,7 @@ from .shuffle import (
 
 __all__ = [
     "init_distributed",
+    "init_mpi",
     "read_env",
     "distributed_dataloader",
     "spawn_producers",

@@ -110,6 +110,24 @@ def init_distributed(env: DDLEnv, backend: str | None = None, timeout_s: float =
     return env
 
 
+def init_mpi(n_instances: int | None = None, n_producers: int | None = None, backend: str | None = None) -> DDLEnv:
+    """Reference entry point ``init_mpi(n_instances)`` (ddl/ddl_env.py:33-97).
+
+    The reference splits ``mpirun``'s ranks into per-GPU groups of one consumer
+    and P producers. Here the ranks ARE the GPUs (one process each; producers
+    are child processes spawned by ``start`` / ``distributed_dataloader``), so
+    ``n_instances`` must equal the world size, and the reference's ``Abort(1)``
+    on a rank count that does not divide (ddl/ddl_env.py:25-30) becomes a
+    ``TopologyError``. Returns the environment with the DP groups created.
+    """
+    env = read_env(n_producers)
+    if n_instances is not None and n_instances != env.world_size:
+        raise TopologyError((n_instances, env.world_size),
+                            f"n_instances={n_instances} GPUs but the job has {env.world_size} ranks "
+                            "(one rank per GPU)")
+    return init_distributed(env, backend)
+
+
 def check_node_locality(env: DDLEnv) -> None:
     """Hostname all-gather: ranks sharing a host must be exactly its local ranks.
 

@@ -90,3 +90,24 @@ class DDLEnv:
     @property
     def color_nth_pusher(self) -> int:
         return 0
+
+    @property
+    def comm_global(self) -> Any:
+        """The reference's WORLD communicator: the DP process group (None for a single rank)."""
+        return self.process_group
+
+    @property
+    def comm_nth_pusher(self) -> Any:
+        """The reference's k-th-pusher communicator, over which its GPUs exchange rows
+        (ddl/ddl_env.py:74-81). Here the consumers exchange on the DP group."""
+        return self.process_group
+
+    @property
+    def comm_per_gpu(self) -> None:
+        """No per-GPU communicator: a rank's producers are its child processes."""
+        return None
+
+    comm_per_gpu_shm = comm_per_gpu
+
+
+MPI_Env = DDLEnv  # reference name (ddl/types.py:24-32)

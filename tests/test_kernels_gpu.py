@@ -176,6 +176,21 @@ def test_pack_tokens(seq_len):
     assert torch.equal(ref[0][mask], toks)
 
 
+def test_pack_tokens_many_short_sequences():
+    """More sequence starts than the kernel stages in LDS (1024): positions from the global-memory search."""
+    rng = np.random.default_rng(5)
+    lens = rng.integers(0, 5, size=3000)
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    toks = torch.from_numpy(rng.integers(0, 50000, size=int(offs[-1])).astype(np.int32))
+    rs, re_, so = ops.pack_plan(offs, 4096)
+    assert len(so) > 1025
+    ref = ops.ref_pack_tokens(toks, rs, re_, so, 4096, pad_id=3)
+    out = ops.pack_tokens(toks.to(_dev()), offs, 4096, pad_id=3)
+    for a, b in zip(out[:4], ref):
+        assert torch.equal(a.cpu(), b)
+    assert torch.equal(out[4].cpu(), torch.from_numpy(so))
+
+
 @pytest.mark.parametrize("nbytes", [4, 1000, 4096 * 77 + 12, 256 * 3 * 224 * 224 * 2])
 def test_checksum(nbytes):
     x = torch.randint(0, 256, (nbytes,), dtype=torch.uint8)
@@ -291,6 +306,35 @@ def test_random_resized_crop_matches_torch(layout, in_dtype, hw, size):
     out16 = ops.random_resized_crop(src.to(_dev()), perm=p, base=2, n_rows=8, size=size, seed=123, layout=layout,
                                     mean=mean, std=std)
     torch.testing.assert_close(out16.float().cpu(), ref, rtol=1e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("layout", ["chw", "hwc"])
+@pytest.mark.parametrize("in_dtype", [torch.uint8, torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("hw,size", [((256, 320), (224, 224)), ((33, 41), (64, 48)), ((97, 130), (31, 29))])
+def test_random_resized_crop_lds_and_direct_paths_agree(layout, in_dtype, hw, size):
+    """The LDS-staged bands and the global-tap path compute the same bits (odd widths: unaligned rows)."""
+    n, c = 10, 3
+    shape = (n, c, *hw) if layout == "chw" else (n, *hw, c)
+    src = (torch.rand(shape) * 255).to(in_dtype).to(_dev())
+    p = FeistelPermutation(n, 4, 2)
+    kw = dict(perm=p, base=1, n_rows=9, size=size, seed=77, layout=layout, mean=[0.4] * 3, std=[0.2] * 3,
+              scale=(0.05, 1.0))
+    for out_dtype in (torch.float32, torch.bfloat16):
+        a = ops.random_resized_crop(src, impl="lds", out_dtype=out_dtype, **kw)
+        b = ops.random_resized_crop(src, impl="direct", out_dtype=out_dtype, **kw)
+        c_ = ops.random_resized_crop(src, out_dtype=out_dtype, **kw)
+        assert torch.equal(a, b) and torch.equal(a, c_)
+
+
+def test_random_resized_crop_wide_rows_use_global_taps():
+    """f32 HWC rows of 1200 px: even a 1-row band exceeds the LDS budget -> global taps, still exact."""
+    src = torch.rand((4, 40, 1200, 3)) * 255
+    out, boxes = ops.random_resized_crop(src.to(_dev()), size=(24, 48), seed=3, layout="hwc",
+                                         out_dtype=torch.float32, return_boxes=True)
+    ref = ops.ref_random_resized_crop(src, boxes.cpu(), (24, 48), "hwc", out_dtype=torch.float32)
+    torch.testing.assert_close(out.cpu(), ref, rtol=1e-4, atol=1e-3)
+    with pytest.raises(ValueError):
+        ops.random_resized_crop(src.to(_dev()), size=(24, 48), seed=3, layout="hwc", impl="lds")
 
 
 def test_random_resized_crop_box_distribution_and_determinism():

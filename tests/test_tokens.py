@@ -5,6 +5,7 @@ import pytest
 import torch
 
 import ddl_amd
+from ddl_amd import ops
 from ddl_amd.models.tokens import SharedTokenSource, TokenBatchProducer, expected_tokens
 from ddl_amd.permutation import EpochOrder
 
@@ -57,6 +58,7 @@ def test_token_batches_gpu(corpus, mode):
     with ddl_amd.start(n_producers=2) as (env, conn):
         dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(corpus, gb, seq_len, mode), gb, conn, 1,
                                            mode="indexed", env=env, auto_mark=True, collate="tokens", seed=4)
+        held = None
         for g, batch in enumerate(dl):
             assert batch["input_ids"].is_cuda
             idx = order.indices(0, g)
@@ -66,6 +68,11 @@ def test_token_batches_gpu(corpus, mode):
                 m = batch["attention_mask"].bool().cpu()
                 flat = batch["input_ids"].cpu()[m]
                 assert np.array_equal(flat.numpy(), np.concatenate(expected_tokens(corpus, idx)))
+                if held is None:
+                    lens = [len(x) for x in expected_tokens(corpus, idx)]
+                    held = (batch["cu_seqlens"], ops.pack_plan(np.concatenate([[0], np.cumsum(lens)]), seq_len)[2])
+        if held is not None:  # cu_seqlens is owned: still intact after the staging buffers were reused
+            assert np.array_equal(held[0].cpu().numpy(), held[1])
 
 
 @pytest.mark.parametrize("seq_len", [4096, 100, 7])
