@@ -72,7 +72,7 @@ def main(argv=None) -> int:
     import ddl_amd
     from ddl_amd import Marker, ops
     from ddl_amd.models.producers import ImageWindowProducer
-    from ddl_amd.utils.tracing import ComputeIdleMeter
+    from ddl_amd.utils.tracing import ComputeIdleMeter, trace_range
 
     n_world = int(os.environ.get("WORLD_SIZE", "1"))
     if n_world != args.gpus:
@@ -123,10 +123,11 @@ def main(argv=None) -> int:
             acc.add(x)
         barrier()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
-            (x,) = next(it)
-            acc.add(x)
-        sync()
+        with trace_range("bench.phase1"):  # roctx: lets tools/trace_idle.py find the timed region
+            for _ in range(args.steps):
+                (x,) = next(it)
+                acc.add(x)
+            sync()
         t1 = time.perf_counter()
         barrier()
         elapsed = t1 - t0
@@ -152,14 +153,15 @@ def main(argv=None) -> int:
             meter = ComputeIdleMeter() if dev.type == "cuda" else None
             barrier()
             t2 = time.perf_counter()
-            for _ in range(idle_steps):
-                (x,) = next(it)
-                if meter:
-                    meter.step_begin()
-                step(x)
-                if meter:
-                    meter.step_end()
-            sync()
+            with trace_range("bench.phase2"):
+                for _ in range(idle_steps):
+                    (x,) = next(it)
+                    if meter:
+                        meter.step_begin()
+                    step(x)
+                    if meter:
+                        meter.step_end()
+                sync()
             t3 = time.perf_counter()
             idle = meter.result() if meter else {"gpu_idle_pct": float("nan"), "busy_ms": 0.0, "wall_ms": 0.0}
             idle["train_samples_per_s"] = args.batch * idle_steps * env.world_size / (t3 - t2)

@@ -205,3 +205,38 @@ def test_metrics_writer(tmp_path):
     last = json.loads(lines[-1])
     assert last["batches"] == 8 and last["samples"] == 32 and "consumer_wait_s" in last
     assert rec["producer_rounds"] and len(rec["producer_rounds"]) == 2
+
+
+def _trace_idle():
+    import importlib.util
+    import os
+
+    path = os.path.join(os.path.dirname(__file__), "..", "tools", "trace_idle.py")
+    spec = importlib.util.spec_from_file_location("trace_idle", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_trace_idle_union_and_gaps():
+    ti = _trace_idle()
+    busy, gaps = ti.union_ns([(10, 20), (15, 30), (50, 60), (95, 200)], 0, 100)
+    assert busy == 20 + 10 + 5
+    assert gaps == [(0, 10), (30, 50), (60, 95)]
+
+
+def test_trace_idle_analyse_regions():
+    ti = _trace_idle()
+
+    def k(a, b, name):
+        return {"Kernel_Name": name, "Start_Timestamp": str(a), "End_Timestamp": str(b)}
+
+    kernels = [k(100, 400, "move_rows_chunked<...>"), k(300, 600, "Cijk_gemm"), k(700, 1000, "checksum_acc")]
+    copies = [{"Start_Timestamp": "0", "End_Timestamp": "500"}]
+    markers = [{"Function": "bench.phase2", "Start_Timestamp": "0", "End_Timestamp": "1000"},
+               {"Function": "ddl.consumer.batch", "Start_Timestamp": "5", "End_Timestamp": "6"}]
+    r = ti.analyse(kernels, copies, markers)["bench.phase2"]
+    assert r["device_idle_pct"] == 20.0  # busy 100..600 and 700..1000 of 0..1000
+    assert r["loader_kernel_pct"] == 60.0
+    assert r["copy_busy_pct"] == 50.0
+    assert r["kernel_dispatches"] == 3
