@@ -348,6 +348,8 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
         """Enqueue the assembly of global step t = epoch*bpe + g; returns (batch, ready event)."""
         import torch.distributed as dist
 
+        if self.shard is None:
+            raise RuntimeError("ResidentGlobalLoader is closed (its HBM shard was released)")
         e, g = divmod(t, self.order.batches_per_epoch)
         perm = self.order.perm(e)
         kw = self._norm_kw()
@@ -387,8 +389,12 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
                 "shard_bytes": (self.hi - self.lo) * self.row_bytes, "load_s": self.load_s}
 
     def close(self) -> None:
+        """Drain the prep stream and release the HBM shard (a 150-190 GB shard must be
+        gone before the next loader allocates its own, even while a generator still
+        references this object)."""
         if self.prep_stream is not None:
             self.prep_stream.synchronize()
         self._queue.clear()
         logger.debug("resident loader closed: %s", self.stats())
+        self.shard = None
 

@@ -98,3 +98,26 @@ def test_resident_scatter_from_one_rank(src, world):
     merged = np.concatenate([r[1].reshape(bpe, gb // world) for r in res], axis=1)
     assert np.array_equal(merged, ref)
     assert res[0][4] > 0
+
+
+def _close_rank(rank, world, name, n, gb):
+    import ddl_amd
+    from ddl_amd.models import SharedArraySource
+    from ddl_amd.resident import ResidentGlobalLoader
+
+    src = SharedArraySource(name, n, (3,), "int64")
+    with ddl_amd.start(n_producers=0) as (env, _):
+        dl = ResidentGlobalLoader(src, gb, env, seed=11, depth=2)
+        it = iter(dl)
+        next(it)
+        dl.close()  # releases the shard even though `it` still references the loader
+        assert dl.shard is None and dl.stats()["shard_rows"] == dl.hi - dl.lo
+        try:
+            next(it)
+        except RuntimeError as e:
+            return "closed" in str(e)
+        return False
+
+
+def test_resident_close_releases_shard(src):
+    assert run_ranks(_close_rank, 1, src.name, src.n, 48) == [True]
