@@ -1,6 +1,6 @@
 """Parallelism: rank topology, launcher, cross-GPU global shuffle (RCCL/xGMI)."""
 
-from .env import init_distributed, init_mpi, read_env
+from .env import init_distributed, init_mpi, init_mpi_error_handling, read_env
 from .launcher import distributed_dataloader, spawn_producers, start
 from .shuffle import (
     AllToAllGlobalShuffler,
@@ -13,6 +13,7 @@ from .shuffle import (
 __all__ = [
     "init_distributed",
     "init_mpi",
+    "init_mpi_error_handling",
     "read_env",
     "distributed_dataloader",
     "spawn_producers",

@@ -76,6 +76,8 @@ def init_distributed(env: DDLEnv, backend: str | None = None, timeout_s: float =
                      device: str | None = None) -> DDLEnv:
     """Create the DP (RCCL or gloo) group and a gloo control group; set the device.
 
+    ``backend`` defaults to ``$DDL_BACKEND``, else RCCL ("nccl") on a GPU and gloo on
+    the CPU; at world size 1 no group is built unless a backend is named.
     ``device="cpu"`` (or ``$DDL_DEVICE=cpu``) keeps the rank off the GPU even
     when one is visible (CPU rehearsals of multi-rank runs). Touches the GPU
     otherwise: call it only after producer workers have been spawned.
@@ -92,9 +94,12 @@ def init_distributed(env: DDLEnv, backend: str | None = None, timeout_s: float =
         env.device = f"cuda:{dev_index}"
     else:
         env.device = "cpu"
-    if env.world_size == 1:
-        env.backend = None
+    backend = backend or os.environ.get("DDL_BACKEND") or None
+    if env.world_size == 1 and backend is None:
+        env.backend = None  # no process group: nothing to exchange with
         return env
+    # an explicit backend at world size 1 builds a 1-rank group, so the collective path (the
+    # global-shuffle exchange over RCCL) can be exercised and timed on a single GPU
     backend = backend or ("nccl" if use_gpu else "gloo")
     env.backend = backend
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -108,6 +113,21 @@ def init_distributed(env: DDLEnv, backend: str | None = None, timeout_s: float =
     env.control_group = dist.new_group(backend="gloo") if backend != "gloo" else dist.group.WORLD
     check_node_locality(env)
     return env
+
+
+def init_mpi_error_handling(env: DDLEnv, n_instances: int) -> None:
+    """Reference ``init_mpi_error_handling(comm_global, n_instances)`` (ddl/ddl_env.py:12-30).
+
+    The reference warns on a single rank and ``Abort(1)``s the whole MPI job when
+    the rank count is not a multiple of ``n_instances``. Here a rank is a GPU, so
+    the check is ``world_size % n_instances``, and it raises ``TopologyError``
+    (the launcher tears the job down) instead of aborting.
+    """
+    if env.world_size < 2 and env.rank == 0:
+        logger.warning("Using only a single rank!")
+    if n_instances < 1 or env.world_size % n_instances != 0:
+        raise TopologyError((env.world_size, n_instances),
+                            f"number of ranks ({env.world_size}) must be a multiple of {n_instances}")
 
 
 def init_mpi(n_instances: int | None = None, n_producers: int | None = None, backend: str | None = None) -> DDLEnv:

@@ -140,6 +140,12 @@ class SendRecvReplaceGlobalShuffler(GlobalShuffler):
         rng = np.random.default_rng([self.seed & 0xFFFFFFFF, window])
         return derangement_partners(self.world, self.rank, rng)
 
+    def _calculate_comm_partner(self, window: int = 0) -> tuple[int, int]:
+        """Reference name (ddl/shuffle.py:32-79). The reference draws one pattern per
+        producer from a seed shared by the k-th producers; here it is drawn per
+        window from (seed, window), identical on every rank, nothing communicated."""
+        return self.partners(window)
+
     def global_shuffle(self, win_bytes: torch.Tensor, window: int) -> None:
         import torch.distributed as dist
 

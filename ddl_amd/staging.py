@@ -8,7 +8,7 @@ ddl/connection.py:89-92). This is the MI355X-native replacement of that gap
 * a native C++ stager thread (``csrc/kernels/stager.cpp``, no GIL) walks the
   consumer's window schedule ahead of the training loop: it futex-waits for
   producer ``p`` to publish slot ``s``, enqueues ``hipMemcpyAsync`` H2D from
-  the pinned arena into HBM buffer ``w % depth`` on the **prefetch stream**,
+  the pinned arena into HBM ring buffer ``w % n_buffers`` on the **prefetch stream**,
   then enqueues (``hipLaunchHostFunc``) the hand-back of the slot to its
   producer, so the producer refills it the moment the DMA retires -- the
   consumer thread is never involved;
@@ -25,7 +25,8 @@ ddl/connection.py:89-92). This is the MI355X-native replacement of that gap
   read it (permute/cast/collate) finish first.
 
 HBM is plentiful on MI355X (288 GB): windows are staged whole, ``depth``
-windows deep (default 2 = double buffering against the training step).
+windows deep (default 2 = double buffering against the training step), plus
+one ring buffer for the exchange lookahead when the exchange is on.
 """
 
 from __future__ import annotations
@@ -83,12 +84,17 @@ class WindowStager:
         # w+1's DMA instead of idling the copy engine.
         self.copy_stream = torch.cuda.Stream(device=self.device)
         self.stream = torch.cuda.Stream(device=self.device) if post_copy is not None else self.copy_stream
-        self.buffers = [torch.empty(max_window_bytes, dtype=torch.uint8, device=self.device) for _ in range(depth)]
-        self.ready_events = [torch.cuda.Event() for _ in range(depth)]
-        self._copy_done = [torch.cuda.Event() for _ in range(depth)]
+        # The consumer posts window w+1's exchange when it starts window w, which needs w+1 staged:
+        # that lookahead holds one ring buffer, so give it its own. With `depth` buffers the copy of
+        # w+2 would wait for the consumer to finish w and the DMA engine would idle for the
+        # consumer's share of every window.
+        n_buf = depth + 1 if post_copy is not None and depth >= 2 else depth
+        self.buffers = [torch.empty(max_window_bytes, dtype=torch.uint8, device=self.device) for _ in range(n_buf)]
+        self.ready_events = [torch.cuda.Event() for _ in range(n_buf)]
+        self._copy_done = [torch.cuda.Event() for _ in range(n_buf)]
         for ev in self.ready_events + self._copy_done:  # materialise the hipEvents (lazy in torch)
             ev.record(self.copy_stream)
-        self._free_refs: list[list] = [[] for _ in range(depth)]  # keep free events alive for the stager
+        self._free_refs: list[list] = [[] for _ in range(n_buf)]  # keep free events alive for the stager
         self._staged: dict[int, StagedWindow] = {}
         self._posted: set[int] = set()
         self._closed = False

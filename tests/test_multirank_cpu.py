@@ -175,3 +175,24 @@ def test_node_locality_mismatch_is_rejected():
     # all-gather sees local ranks [0, 0, 1, 1] there and rejects the layout
     with pytest.raises(AssertionError, match="TopologyError"):
         run_ranks(_bad_topology_rank, 4, env={"DDL_HOSTNAME": "same-host"}, nodes=2)
+
+
+def test_explicit_backend_builds_a_one_rank_group():
+    """DDL_BACKEND at world size 1 builds a 1-rank group, so the exchange path runs (and can be
+    timed) on a single device; without it a lone rank has no group and no exchange."""
+    res, = run_ranks(_exchange_rank, 1, "alltoall", 0.5, env={"DDL_BACKEND": "gloo"})
+    eps, n_ex = res
+    assert n_ex == 20
+    for rows in eps:  # world 1: every exchanged row comes back to its own window
+        assert len({tuple(x) for x in rows[:, :3].tolist()}) == len(rows) == 40
+
+
+def test_init_mpi_error_handling_rejects_non_multiple():
+    from ddl_amd.exceptions import TopologyError
+    from ddl_amd.parallel import init_mpi_error_handling
+    from ddl_amd.types import DDLEnv
+
+    init_mpi_error_handling(DDLEnv(rank=0, world_size=8), 4)
+    init_mpi_error_handling(DDLEnv(rank=0, world_size=1), 1)  # single rank: warning only
+    with pytest.raises(TopologyError):
+        init_mpi_error_handling(DDLEnv(rank=0, world_size=6), 4)
