@@ -154,11 +154,28 @@ class TokenBatchProducer(ProducerFunctionSkeleton):
         return {"tags": [n_tokens, n_rows, n_seg], "used_bytes": tok_off + 4 * n_tokens}
 
 
+_VIEW_CACHE: dict = {}
+
+
+def _cached_views(buf: torch.Tensor, layout: TokenWindowLayout) -> dict[str, torch.Tensor]:
+    """``layout.views(buf)`` memoised per (buffer address, size, layout): the consumer collates out of
+    the same few staging buffers every step, and building five views costs ~9 us per batch. A cached
+    view keeps its (window-sized) buffer alive, so no other allocation can take that address while
+    the entry exists; the cache is bounded."""
+    key = (buf.data_ptr(), buf.numel(), buf.device, layout)
+    v = _VIEW_CACHE.get(key)
+    if v is None:
+        if len(_VIEW_CACHE) >= 32:
+            _VIEW_CACHE.clear()
+        v = _VIEW_CACHE[key] = layout.views(buf)
+    return v
+
+
 def collate_token_window(buf: torch.Tensor, layout: TokenWindowLayout, mode: str, tags, pad_id: int = 0):
     """Expand one (device or host) token window into model inputs."""
     from .. import ops
 
-    v = layout.views(buf.view(-1))
+    v = _cached_views(buf.view(-1), layout)
     n_tokens, n_rows, n_seg = (int(x) for x in tags[:3])
     tokens = v["tokens"][:n_tokens]
     if mode == "pad":
@@ -172,18 +189,27 @@ def collate_token_window(buf: torch.Tensor, layout: TokenWindowLayout, mode: str
                 "cu_seqlens": v["seg_offsets"][: n_seg + 1].clone()}
     dev = tokens.device
     s = layout.seq_len
-    ids = torch.empty((n_rows, s), dtype=torch.int32, device=dev)
-    mask = torch.empty((n_rows, s), dtype=torch.uint8, device=dev)
-    pos = torch.empty((n_rows, s), dtype=torch.int64, device=dev)
-    seg = torch.empty((n_rows, s), dtype=torch.int32, device=dev)
+    # one allocation for all five outputs (8-byte-aligned regions: position_ids i64, cu_seqlens i64,
+    # input_ids i32, segment_ids i32, attention_mask u8). cu_seqlens is written by the kernel into
+    # memory of its own: a view of the staging buffer would be overwritten when it is re-staged
+    n = n_rows * s
+    cu_n = -(-(n_seg + 1) // 2) * 2  # i64 count rounded so the i32 regions stay 16-byte aligned
+    whole = torch.empty(8 * n + 8 * cu_n + 4 * n + 4 * n + n, dtype=torch.uint8, device=dev)
+    o = 0
+    pos = whole[o:o + 8 * n].view(torch.int64).view(n_rows, s)
+    o += 8 * n
+    cu = whole[o:o + 8 * (n_seg + 1)].view(torch.int64)
+    o += 8 * cu_n
+    ids = whole[o:o + 4 * n].view(torch.int32).view(n_rows, s)
+    o += 4 * n
+    seg = whole[o:o + 4 * n].view(torch.int32).view(n_rows, s)
+    o += 4 * n
+    mask = whole[o:o + n].view(n_rows, s)
     from ..ops.kernels import _stream_handle
 
-    # cu_seqlens is written by the kernel into a tensor of its own: a view of the
-    # staging buffer would be overwritten when the buffer is re-staged
     if n_rows == 0:
-        cu = v["seg_offsets"][: n_seg + 1].clone()
+        cu.copy_(v["seg_offsets"][: n_seg + 1])
     else:
-        cu = torch.empty(n_seg + 1, dtype=torch.int64, device=dev)
         _native.hip().pad_pack_tokens(
             tokens=tokens.data_ptr(), offsets=0, row_start=v["row_start"].data_ptr(),
             row_end=v["row_end"].data_ptr(), seg_offsets=v["seg_offsets"].data_ptr(), n_seg=n_seg,

@@ -32,6 +32,19 @@ acc = ops.ChecksumAccumulator(dev)
 out = {}
 out["Event()"] = t(lambda: torch.cuda.Event())
 out["ev.record(bs)"] = t(lambda: ev.record(bs))
+out["Event().record(bs) (new hipEvent each call)"] = t(lambda: torch.cuda.Event().record(bs))
+# re-recording the SAME event with nothing enqueued in between is a fast path (~1.4 us); a ring of
+# pre-created events costs as much as a fresh one (~6 us): the price is the marker, not the creation
+ring = [torch.cuda.Event() for _ in range(8)]
+_k = [0]
+
+
+def ring_record():
+    _k[0] = (_k[0] + 1) % 8
+    ring[_k[0]].record(bs)
+
+
+out["ring of 8 events .record(bs)"] = t(ring_record)
 out["cur.wait_event"] = t(lambda: cur.wait_event(ev))
 out["bs.wait_event"] = t(lambda: bs.wait_event(ev))
 
