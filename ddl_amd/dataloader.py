@@ -481,12 +481,15 @@ class DistributedDataLoader(DistributedDataloaderABC):
 
     def _release_window(self) -> None:
         if self._stager is not None:
+            stream = None
             if self._batch_stream is not None:
-                # batch kernels read the window too: the free event must follow them
+                # only the batch kernels read the window (the consumer gets copies made on the batch
+                # stream), so the free event goes on the batch stream, behind them: no cross-stream
+                # wait, and the compute stream never waits on a lookahead gather
                 for key in [k for k in self._lookahead if k[0] <= self.window]:
                     del self._lookahead[key]
-                torch.cuda.current_stream(self.device).wait_stream(self._batch_stream)
-            self._stager.release(self.window)
+                stream = self._batch_stream
+            self._stager.release(self.window, stream)
             self._cur = None
         elif self._host_window == self.window:
             p, s = self._schedule(self.window)
