@@ -168,6 +168,76 @@ __device__ __forceinline__ void resample_band(void* __restrict__ dst, int64_t im
   }
 }
 
+// Fast form of resample_band over an LDS band whose rows all start at the same
+// offset `head` within their 16 B chunk (row pitch and plane size multiples of
+// 16 B: every standard image geometry) and whose output rows are a multiple of
+// kPx wide. A thread's kPx pixels then share one output row, so the vertical
+// coordinate and both source-row offsets are computed once instead of per
+// pixel, the horizontal offsets once per pixel instead of per tap and channel,
+// and every tap is one add + one LDS read (PMC of the generic form: ~1960 VALU
+// instructions per wave, issue-stalled 44% of its cycles, profiles/r1_augment_v2/).
+// Same float math in the same order as resample_band: bit-identical output.
+template <int OUT_BF16, typename Tin, int HWC>
+__device__ __forceinline__ void resample_band_rows(void* __restrict__ dst, int64_t img, const AugmentSpec& a,
+                                                   const CropBox& b, int oy0, int oy1, const Affine& aff,
+                                                   const uint8_t* __restrict__ lds, uint32_t head, uint32_t stride,
+                                                   uint32_t nrows, int ylo) {
+  constexpr uint32_t kSz = static_cast<uint32_t>(sizeof(Tin));
+  const int ow = a.out_w, C = a.channels;
+  const uint32_t cin = HWC ? static_cast<uint32_t>(C) : 1u;
+  const uint32_t cstep = HWC ? kSz : nrows * stride;  // LDS bytes from one channel to the next
+  const int64_t opix = static_cast<int64_t>(a.out_h) * ow;
+  const int n = (oy1 - oy0) * ow;
+  const float fy = static_cast<float>(b.h) / a.out_h, fx = static_cast<float>(b.w) / a.out_w;
+  for (int q0 = static_cast<int>(threadIdx.x) * kPx; q0 < n; q0 += kThreads * kPx) {
+    const int r = static_cast<int>(static_cast<uint32_t>(q0) / static_cast<uint32_t>(ow));
+    const int ox0 = q0 - r * ow;
+    const float sy = src_coord(oy0 + r, fy);
+    const int y0 = min(static_cast<int>(sy), b.h - 1);
+    const int y1 = y0 + (y0 < b.h - 1 ? 1 : 0);
+    const float wy = sy - static_cast<float>(y0);
+    const uint32_t ra = static_cast<uint32_t>(y0 - ylo) * stride + head;
+    const uint32_t rb = static_cast<uint32_t>(y1 - ylo) * stride + head;
+    uint32_t xa[kPx], xb[kPx];
+    float wx[kPx];
+#pragma unroll
+    for (int k = 0; k < kPx; ++k) {
+      int ox = ox0 + k;
+      if (b.flip) ox = ow - 1 - ox;
+      const float sx = src_coord(ox, fx);
+      const int x0 = min(static_cast<int>(sx), b.w - 1);
+      const int x1 = x0 + (x0 < b.w - 1 ? 1 : 0);
+      wx[k] = sx - static_cast<float>(x0);
+      xa[k] = static_cast<uint32_t>(x0) * cin * kSz;
+      xb[k] = static_cast<uint32_t>(x1) * cin * kSz;
+    }
+    const int64_t o = img * C * opix + static_cast<int64_t>(oy0) * ow + q0;
+    for (int c = 0; c < C; ++c) {
+      const uint8_t* la = lds + static_cast<uint32_t>(c) * cstep + ra;
+      const uint8_t* lb = lds + static_cast<uint32_t>(c) * cstep + rb;
+      float v[kPx];
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) {
+        const float v00 = ld(reinterpret_cast<const Tin*>(la + xa[k]));
+        const float v01 = ld(reinterpret_cast<const Tin*>(la + xb[k]));
+        const float v10 = ld(reinterpret_cast<const Tin*>(lb + xa[k]));
+        const float v11 = ld(reinterpret_cast<const Tin*>(lb + xb[k]));
+        const float top = v00 + (v01 - v00) * wx[k];
+        const float bot = v10 + (v11 - v10) * wx[k];
+        v[k] = top + (bot - top) * wy;
+        if (aff.enabled) v[k] = fmaf(v[k], aff.scale[c], aff.bias[c]);
+      }
+      const int64_t oc = o + static_cast<int64_t>(c) * opix;
+      if constexpr (OUT_BF16) {
+        *reinterpret_cast<uint2*>(static_cast<uint16_t*>(dst) + oc) =
+            make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+      } else {
+        *reinterpret_cast<float4*>(static_cast<float*>(dst) + oc) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+  }
+}
+
 // HWC=1: src rows are [H, W, C]; else [C, H, W]. out: [B, C, OH, OW].
 // LDS layout: (plane p, band row r) rows of `stride` bytes; row (p, r) holds
 // the 16 B-aligned global chunks covering the crop's span of that source row,
@@ -249,6 +319,11 @@ __global__ void __launch_bounds__(kThreads) rrc_band_kernel(void* __restrict__ d
   // low bits of the per-row global addresses (mod 2^32 is enough for & 15)
   const uint32_t base_lo = static_cast<uint32_t>(band_base);
   const uint32_t plane_lo = static_cast<uint32_t>(plane_b), pitch_lo = static_cast<uint32_t>(pitch_b);
+  if ((pitch_lo & 15u) == 0 && (planes == 1 || (plane_lo & 15u) == 0) && (a.out_w % kPx) == 0) {
+    // every LDS row starts `base_lo & 15` bytes into its first chunk (kernel-uniform branch)
+    resample_band_rows<OUT_BF16, Tin, HWC>(dst, img, a, b, oy0, oy1, aff, lds, base_lo & 15u, stride, nrows, ylo);
+    return;
+  }
   resample_band<OUT_BF16>(dst, img, a, b, oy0, oy1, aff, [&](int c, int y, int x) {
     const uint32_t p = HWC ? 0u : static_cast<uint32_t>(c);
     const uint32_t ci = HWC ? static_cast<uint32_t>(c) : 0u;
