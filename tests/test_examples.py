@@ -58,3 +58,24 @@ def test_bench_contract_two_ranks_torchrun():
     assert out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 32
     assert out["config"]["exchange_fraction"] == 0.5
     assert "DDP" in out["train_step"]["model"]
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("method", ["alltoall", "sendrecv_replace"])
+def test_bench_eight_ranks_torchrun(method):
+    """The driver's N=8 launch rehearsed on CPU/gloo: 8 ranks x 3 producers, a window exchange every
+    4 batches in both exchange methods, then 8-rank DDP. Checks that every rank issues the loader's
+    collectives and the DDP all-reduces in an order that completes (no cross-rank deadlock)."""
+    import json
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(REPO, "bench.py"),
+           "--gpus", "8", "--steps", "12", "--warmup", "2", "--window", "64", "--batch", "16", "--idle-steps", "3",
+           "--model-dim", "64", "--model-depth", "1", "--exchange-method", method]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=dict(_env(), DDL_DEVICE="cpu"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 8 and out["config"]["parallelism"] == "dp8" and out["config"]["global_batch"] == 128
+    assert out["config"]["exchange_fraction"] == 0.5 and out["value"] > 0
