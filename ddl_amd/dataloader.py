@@ -489,6 +489,11 @@ class DistributedDataLoader(DistributedDataloaderABC):
                 for key in [k for k in self._lookahead if k[0] <= self.window]:
                     del self._lookahead[key]
                 stream = self._batch_stream
+                sw = self._cur
+                if sw is not None and sw.index == self.window:
+                    # a window no batch was built from (skipped at a partial epoch end) can still have
+                    # its exchange running on the post-copy stream: the free event must follow it too
+                    stream.wait_event(self._stager.ready_events[sw.buffer])
             self._stager.release(self.window, stream)
             self._cur = None
         elif self._host_window == self.window:

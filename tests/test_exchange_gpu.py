@@ -66,3 +66,31 @@ def test_loader_with_exchange_enabled_on_gpu(rccl_env, monkeypatch):
         assert dl._exchange_fn.calls == 4
     finally:
         conn.finalize()
+
+
+def test_partial_epochs_with_exchange_keep_windows_intact(rccl_env):
+    """Partial epochs skip windows: a skipped window is staged and exchanged but no batch reads it.
+    Its buffer's free event must still follow that exchange, or the next copy into the buffer
+    races the scatter; every delivered row must carry its own window's round."""
+    import ddl_amd
+    from ddl_amd import Marker
+    from ddl_amd.parallel import launcher
+    from tests.helpers import IdProducer
+
+    P = 2
+    conn = launcher.spawn_producers(ddl_amd.parallel.read_env(P), mode="thread")
+    try:
+        dl = ddl_amd.DistributedDataLoader(IdProducer(256, 8), 16, conn, 12, 0.5, "alltoall", env=rccl_env,
+                                           shuffle="device", copy_batches=True, seed=5, mode="split_along_epoch")
+        for e in range(12):
+            w = dl.window
+            for i, (a, b) in enumerate(dl):
+                rows = torch.cat([a, b], 1).cpu()
+                assert (rows[:, 1] == w % P).all() and (rows[:, 3] == w // P).all(), (e, i)
+                dl.mark(Marker.END_OF_BATCH)
+                if i == 2:
+                    break  # partial epoch: the rest of this window and the epoch's next window are skipped
+            dl.mark(Marker.END_OF_EPOCH)
+        assert dl._exchange_fn.calls >= 12
+    finally:
+        conn.finalize()
