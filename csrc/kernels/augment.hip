@@ -95,6 +95,17 @@ __global__ void __launch_bounds__(kThreads) rrc_boxes_kernel(AugmentSpec a, int6
   boxes[img] = draw_crop(a, static_cast<uint64_t>(a.sample_base + source_row(ri, img)));
 }
 
+// Division by a runtime divisor d that is uniform across the workgroup, for
+// dividends with w * d < 2^32 (LDS chunk and pixel indices here): with
+// m = ceil(2^32 / d), floor(w / d) = umulhi(w, m) exactly in that range (the
+// rounding error of m is below 1 / d). Two VALU instructions instead of the
+// ~15 of a generic 32-bit udiv; m is computed once per workgroup.
+struct FastDiv {
+  uint32_t d, m;
+  __device__ __forceinline__ explicit FastDiv(uint32_t d_) : d(d_), m(d_ > 1 ? static_cast<uint32_t>(((1ull << 32) + d_ - 1) / d_) : 0u) {}
+  __device__ __forceinline__ uint32_t div(uint32_t w) const { return d > 1 ? __umulhi(w, m) : w; }
+};
+
 // Bilinear source coordinate of output index o, align_corners=False:
 // src = (dst + 0.5) * in/out - 0.5, clamped at 0. The band bounds and the taps
 // both come from this one function, so they agree bit for bit.
@@ -117,13 +128,14 @@ __device__ __forceinline__ void resample_band(void* __restrict__ dst, int64_t im
   const int n = (oy1 - oy0) * ow;
   const float fy = static_cast<float>(b.h) / a.out_h, fx = static_cast<float>(b.w) / a.out_w;
   const bool vec_ok = (ow % kPx) == 0;  // band rows start 4-aligned in the plane: aligned vector stores
+  const FastDiv div_ow(static_cast<uint32_t>(ow));  // q < 16 * ow, out_w <= 8192 (host check)
   for (int q0 = static_cast<int>(threadIdx.x) * kPx; q0 < n; q0 += kThreads * kPx) {
     int ya[kPx], yb[kPx], xa[kPx], xb[kPx];
     float wy[kPx], wx[kPx];
 #pragma unroll
     for (int k = 0; k < kPx; ++k) {
       const int q = min(q0 + k, n - 1);  // tail lanes recompute the last pixel (not stored)
-      const int r = static_cast<int>(static_cast<uint32_t>(q) / static_cast<uint32_t>(ow));
+      const int r = static_cast<int>(div_ow.div(static_cast<uint32_t>(q)));
       int ox = q - r * ow;
       if (b.flip) ox = ow - 1 - ox;
       const float sy = src_coord(oy0 + r, fy), sx = src_coord(ox, fx);
@@ -177,20 +189,22 @@ __device__ __forceinline__ void resample_band(void* __restrict__ dst, int64_t im
 // and every tap is one add + one LDS read (PMC of the generic form: ~1960 VALU
 // instructions per wave, issue-stalled 44% of its cycles, profiles/r1_augment_v2/).
 // Same float math in the same order as resample_band: bit-identical output.
-template <int OUT_BF16, typename Tin, int HWC>
+template <int OUT_BF16, typename Tin, int HWC, int NC>
 __device__ __forceinline__ void resample_band_rows(void* __restrict__ dst, int64_t img, const AugmentSpec& a,
                                                    const CropBox& b, int oy0, int oy1, const Affine& aff,
                                                    const uint8_t* __restrict__ lds, uint32_t head, uint32_t stride,
                                                    uint32_t nrows, int ylo) {
   constexpr uint32_t kSz = static_cast<uint32_t>(sizeof(Tin));
-  const int ow = a.out_w, C = a.channels;
+  const int ow = a.out_w;
+  const int C = NC > 0 ? NC : a.channels;  // NC: channel count known at compile time (3), 0: runtime
   const uint32_t cin = HWC ? static_cast<uint32_t>(C) : 1u;
   const uint32_t cstep = HWC ? kSz : nrows * stride;  // LDS bytes from one channel to the next
   const int64_t opix = static_cast<int64_t>(a.out_h) * ow;
   const int n = (oy1 - oy0) * ow;
   const float fy = static_cast<float>(b.h) / a.out_h, fx = static_cast<float>(b.w) / a.out_w;
+  const FastDiv div_ow(static_cast<uint32_t>(ow));
   for (int q0 = static_cast<int>(threadIdx.x) * kPx; q0 < n; q0 += kThreads * kPx) {
-    const int r = static_cast<int>(static_cast<uint32_t>(q0) / static_cast<uint32_t>(ow));
+    const int r = static_cast<int>(div_ow.div(static_cast<uint32_t>(q0)));
     const int ox0 = q0 - r * ow;
     const float sy = src_coord(oy0 + r, fy);
     const int y0 = min(static_cast<int>(sy), b.h - 1);
@@ -212,20 +226,29 @@ __device__ __forceinline__ void resample_band_rows(void* __restrict__ dst, int64
       xb[k] = static_cast<uint32_t>(x1) * cin * kSz;
     }
     const int64_t o = img * C * opix + static_cast<int64_t>(oy0) * ow + q0;
-    for (int c = 0; c < C; ++c) {
-      const uint8_t* la = lds + static_cast<uint32_t>(c) * cstep + ra;
-      const uint8_t* lb = lds + static_cast<uint32_t>(c) * cstep + rb;
+    for (int c = 0; c < C; ++c) {  // fully unrolled by the compiler when NC > 0
+      const uint32_t cb = static_cast<uint32_t>(c) * cstep;
+      const uint8_t* la = lds + (cb + ra);
+      const uint8_t* lb = lds + (cb + rb);
+      float v00[kPx], v01[kPx], v10[kPx], v11[kPx];
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) {  // all 4 * kPx taps issued before any use
+        v00[k] = ld(reinterpret_cast<const Tin*>(la + xa[k]));
+        v01[k] = ld(reinterpret_cast<const Tin*>(la + xb[k]));
+        v10[k] = ld(reinterpret_cast<const Tin*>(lb + xa[k]));
+        v11[k] = ld(reinterpret_cast<const Tin*>(lb + xb[k]));
+      }
       float v[kPx];
 #pragma unroll
       for (int k = 0; k < kPx; ++k) {
-        const float v00 = ld(reinterpret_cast<const Tin*>(la + xa[k]));
-        const float v01 = ld(reinterpret_cast<const Tin*>(la + xb[k]));
-        const float v10 = ld(reinterpret_cast<const Tin*>(lb + xa[k]));
-        const float v11 = ld(reinterpret_cast<const Tin*>(lb + xb[k]));
-        const float top = v00 + (v01 - v00) * wx[k];
-        const float bot = v10 + (v11 - v10) * wx[k];
+        const float top = v00[k] + (v01[k] - v00[k]) * wx[k];
+        const float bot = v10[k] + (v11[k] - v10[k]) * wx[k];
         v[k] = top + (bot - top) * wy;
-        if (aff.enabled) v[k] = fmaf(v[k], aff.scale[c], aff.bias[c]);
+      }
+      if (aff.enabled) {  // kernel-uniform
+        const float sc = aff.scale[c], bi = aff.bias[c];
+#pragma unroll
+        for (int k = 0; k < kPx; ++k) v[k] = fmaf(v[k], sc, bi);
       }
       const int64_t oc = o + static_cast<int64_t>(c) * opix;
       if constexpr (OUT_BF16) {
@@ -285,14 +308,15 @@ __global__ void __launch_bounds__(kThreads) rrc_band_kernel(void* __restrict__ d
   const uintptr_t plane_b = static_cast<uintptr_t>(plane_elems * kSz), pitch_b = static_cast<uintptr_t>(row_pitch * kSz);
   const uint32_t total = static_cast<uint32_t>(planes) * nrows * cpr;
   constexpr int kIlp = 4;
+  const FastDiv div_cpr(cpr), div_rows(nrows);  // total <= lds_cap / 16 = 2048 chunks
   for (uint32_t w0 = threadIdx.x; w0 < total; w0 += kIlp * kThreads) {
     uint4 v[kIlp];
 #pragma unroll
     for (int k = 0; k < kIlp; ++k) {
       const uint32_t w = w0 + k * kThreads;
       if (w < total) {
-        const uint32_t pr = w / cpr, ch = w - pr * cpr;
-        const uint32_t p = pr / nrows, r = pr - p * nrows;
+        const uint32_t pr = div_cpr.div(w), ch = w - pr * cpr;
+        const uint32_t p = div_rows.div(pr), r = pr - p * nrows;
         const uintptr_t row = band_base + p * plane_b + r * pitch_b;
         const uintptr_t g = (row & ~static_cast<uintptr_t>(15)) + 16u * ch;
         // addressed off the kernel argument (not an integer round trip) so the
@@ -321,7 +345,10 @@ __global__ void __launch_bounds__(kThreads) rrc_band_kernel(void* __restrict__ d
   const uint32_t plane_lo = static_cast<uint32_t>(plane_b), pitch_lo = static_cast<uint32_t>(pitch_b);
   if ((pitch_lo & 15u) == 0 && (planes == 1 || (plane_lo & 15u) == 0) && (a.out_w % kPx) == 0) {
     // every LDS row starts `base_lo & 15` bytes into its first chunk (kernel-uniform branch)
-    resample_band_rows<OUT_BF16, Tin, HWC>(dst, img, a, b, oy0, oy1, aff, lds, base_lo & 15u, stride, nrows, ylo);
+    if (a.channels == 3)
+      resample_band_rows<OUT_BF16, Tin, HWC, 3>(dst, img, a, b, oy0, oy1, aff, lds, base_lo & 15u, stride, nrows, ylo);
+    else
+      resample_band_rows<OUT_BF16, Tin, HWC, 0>(dst, img, a, b, oy0, oy1, aff, lds, base_lo & 15u, stride, nrows, ylo);
     return;
   }
   resample_band<OUT_BF16>(dst, img, a, b, oy0, oy1, aff, [&](int c, int y, int x) {
@@ -386,7 +413,8 @@ int random_resized_crop(void* dst, int32_t out_dt, const void* src, int32_t in_d
                         int path, hipStream_t st) {
   if (batch <= 0) return 0;
   if (boxes_out == nullptr) return -3;  // [batch, 5] int32 device buffer: boxes are drawn there first
-  if (a.channels < 1 || a.channels > kMaxAffineChannels || a.in_h < 1 || a.in_w < 1 || a.out_h < 1 || a.out_w < 1)
+  if (a.channels < 1 || a.channels > kMaxAffineChannels || a.in_h < 1 || a.in_w < 1 || a.out_h < 1 || a.out_w < 1 ||
+      a.out_w > 8192)  // FastDiv range: (band pixel index) * out_w < 2^32
     return -2;
   if (path < 0 || path > 2) return -2;
   switch (in_dt) {
