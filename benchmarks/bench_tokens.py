@@ -27,6 +27,10 @@ def main(argv=None):
     ap.add_argument("--n-seqs", type=int, default=8192)
     ap.add_argument("--producers", type=int, default=4)
     ap.add_argument("--mode", default="pack", choices=["pad", "pack"])
+    ap.add_argument("--idle-steps", type=int, default=200,
+                    help="phase 2: steps of a fixed-cost token train step, for GPU idle %% (0 disables)")
+    ap.add_argument("--model-dim", type=int, default=256)
+    ap.add_argument("--model-depth", type=int, default=2)
     a = ap.parse_args(argv)
 
     import torch
@@ -57,7 +61,7 @@ def main(argv=None):
                 source = SharedTokenSource(t, o, int(np.diff(offs).max()))
             else:
                 source = src
-            n_epochs = (a.warmup + a.steps) // (a.n_seqs // gb) + 2
+            n_epochs = (a.warmup + a.steps + a.idle_steps + a.warmup // 2) // (a.n_seqs // gb) + 2
             dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(source, gb, a.seq_len, a.mode), a.batch, conn,
                                                n_epochs, mode="indexed", env=env, collate="tokens", auto_mark=True)
             dev = torch.device(env.device)
@@ -88,6 +92,31 @@ def main(argv=None):
                 t = torch.tensor([dt], dtype=torch.float64)
                 dist.all_reduce(t, op=dist.ReduceOp.MAX, group=env.control_group)
                 dt = float(t.item())
+            idle = None
+            if a.idle_steps and dev.type == "cuda":
+                # phase 2: GPU idle % behind a fixed-cost bf16 token train step (BASELINE config 4)
+                from ddl_amd.models.trainstep import TokenTrainStep
+                from ddl_amd.utils.tracing import ComputeIdleMeter
+
+                step = TokenTrainStep(dev, seq_len=a.seq_len, dim=a.model_dim, depth=a.model_depth)
+                for _ in range(max(1, a.warmup // 2)):
+                    step(next(it))
+                meter = ComputeIdleMeter()
+                torch.cuda.synchronize()
+                t2 = time.perf_counter()
+                for _ in range(a.idle_steps):
+                    b = next(it)
+                    meter.step_begin()
+                    step(b)
+                    meter.step_end()
+                torch.cuda.synchronize()
+                t3 = time.perf_counter()
+                idle = meter.result()
+                idle["train_sequences_per_s"] = a.idle_steps * a.batch * env.world_size / (t3 - t2)
+                if env.world_size > 1:
+                    t = torch.tensor([idle["gpu_idle_pct"]], dtype=torch.float64)
+                    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=env.control_group)
+                    idle["gpu_idle_pct"] = float(t.item())
             toks = source.offsets.tensor().view(-1).numpy()
             mean_len = float(np.diff(toks).mean())
             real_tokens = a.steps * a.batch * mean_len * env.world_size
@@ -100,7 +129,13 @@ def main(argv=None):
                     "packed_rows_per_step": round(rows / a.steps, 2), "n_gpus": env.world_size,
                     "steps": a.steps, "ms_per_step": round(1000 * dt / a.steps, 3), "batch_seqs": a.batch,
                     "producers": a.producers, "mean_len": round(mean_len, 1),
-                    "consumer_wait_s": round(st["consumer_wait_s"], 3)}), flush=True)
+                    "consumer_wait_s": round(st["consumer_wait_s"], 3),
+                    "gpu_idle_pct": None if idle is None else round(idle["gpu_idle_pct"], 3),
+                    "train_step": None if idle is None else {
+                        "model": f"TokenMLP dim={a.model_dim} depth={a.model_depth} fwd+bwd+SGD bf16",
+                        "sequences_per_s": round(idle["train_sequences_per_s"], 1),
+                        "busy_ms": round(idle["busy_ms"], 3), "wall_ms": round(idle["wall_ms"], 3)}}),
+                    flush=True)
     finally:
         if src is not None:
             src.close()

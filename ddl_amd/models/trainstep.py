@@ -72,3 +72,50 @@ class TrainStep:
         loss.backward()
         self.opt.step()
         return loss.detach()
+
+
+class TokenMLP(nn.Module):
+    """Token-model stand-in for config 4: token + position embeddings, pre-norm MLP blocks over every
+    position (masked padding), a small per-token head. GEMM cost scales with rows x seq_len x dim."""
+
+    def __init__(self, vocab: int = 50257, seq_len: int = 4096, dim: int = 256, depth: int = 2, mlp_ratio: int = 4,
+                 n_out: int = 256):
+        super().__init__()
+        self.tok = nn.Embedding(vocab, dim)
+        self.pos = nn.Embedding(seq_len, dim)
+        self.blocks = nn.ModuleList(
+            nn.Sequential(nn.LayerNorm(dim), nn.Linear(dim, dim * mlp_ratio), nn.GELU(),
+                          nn.Linear(dim * mlp_ratio, dim))
+            for _ in range(depth))
+        self.norm = nn.LayerNorm(dim)
+        self.head = nn.Linear(dim, n_out)
+
+    def forward(self, ids: torch.Tensor, pos: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+        x = self.tok(ids.long()) + self.pos(pos.long())
+        x = x * mask.unsqueeze(-1).to(x.dtype)
+        for blk in self.blocks:
+            x = x + blk(x)
+        return self.head(self.norm(x))
+
+
+class TokenTrainStep:
+    """forward + backward + SGD on one collated token batch (``input_ids``, ``position_ids``,
+    ``attention_mask``); the target is the next token id folded into ``n_out`` classes, padding ignored."""
+
+    def __init__(self, device, seq_len: int = 4096, dim: int = 256, depth: int = 2, n_out: int = 256,
+                 lr: float = 1e-3, dtype=torch.bfloat16, vocab: int = 50257):
+        torch.manual_seed(0)
+        self.model = TokenMLP(vocab, seq_len, dim, depth, n_out=n_out).to(device=device, dtype=dtype)
+        self.opt = torch.optim.SGD(self.model.parameters(), lr=lr)
+        self.n_out = n_out
+
+    def __call__(self, batch: dict) -> torch.Tensor:
+        ids, pos, mask = batch["input_ids"], batch["position_ids"], batch["attention_mask"]
+        logits = self.model(ids, pos, mask)
+        target = torch.roll(ids, -1, dims=1).long() % self.n_out
+        target = target.masked_fill(mask == 0, -100)
+        loss = F.cross_entropy(logits.float().flatten(0, 1), target.flatten(), ignore_index=-100)
+        self.opt.zero_grad(set_to_none=True)
+        loss.backward()
+        self.opt.step()
+        return loss.detach()
