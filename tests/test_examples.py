@@ -79,3 +79,17 @@ def test_bench_eight_ranks_torchrun(method):
     out = json.loads(lines[0])
     assert out["n_gpus"] == 8 and out["config"]["parallelism"] == "dp8" and out["config"]["global_batch"] == 128
     assert out["config"]["exchange_fraction"] == 0.5 and out["value"] > 0
+
+
+@pytest.mark.timeout(200)
+def test_bench_plumbing_config1_two_ranks():
+    """BASELINE config 1 (1k x 3x32x32, world 2, CPU): exactly-once delivery every epoch, one JSON line."""
+    import json
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(REPO, "benchmarks", "bench_plumbing.py"), "--epochs", "3"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=180, env=dict(_env(), DDL_DEVICE="cpu"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert out["world_size"] == 2 and out["exactly_once_every_epoch"] is True and out["samples_per_s"] > 0
