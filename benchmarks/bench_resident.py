@@ -23,6 +23,8 @@ def main(argv=None):
     ap.add_argument("--n-samples", type=int, default=16384, help="global dataset size")
     ap.add_argument("--dtype", default="bfloat16", choices=["bfloat16", "uint8"])
     ap.add_argument("--depths", default="1,2,4")
+    ap.add_argument("--augment", action="store_true",
+                    help="RandomResizedCrop(224) + flip + normalise on the device instead of the plain gather")
     a = ap.parse_args(argv)
 
     import torch
@@ -58,7 +60,8 @@ def main(argv=None):
             dev = torch.device(env.device)
             for depth in [int(x) for x in a.depths.split(",")]:
                 dl = ResidentGlobalLoader(src, a.batch * env.world_size, env, seed=1, depth=depth,
-                                          out_dtype=torch.bfloat16, normalize=norm)
+                                          out_dtype=torch.bfloat16, normalize=norm,
+                                          augment={"size": (224, 224)} if a.augment else None)
                 acc = ops.ChecksumAccumulator(dev)  # one streaming launch per batch
 
                 def gen():
@@ -90,6 +93,7 @@ def main(argv=None):
                 torch.cuda.empty_cache()  # hand the freed shard back before the next depth allocates its own
             if env.rank == 0:
                 print(json.dumps({"metric": "samples/s fed to GPU, HBM-resident exact global shuffle",
+                                  "augment": "RandomResizedCrop(224)+flip+normalise" if a.augment else None,
                                   "n_gpus": env.world_size, "batch_per_gpu": a.batch, "dtype_src": a.dtype,
                                   "dtype_out": "bf16", "n_samples": a.n_samples, "sweep": results}), flush=True)
     finally:

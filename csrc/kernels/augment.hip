@@ -92,7 +92,8 @@ __global__ void __launch_bounds__(kThreads) rrc_boxes_kernel(AugmentSpec a, int6
                                                             CropBox* __restrict__ boxes) {
   const int64_t img = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
   if (img >= batch) return;
-  boxes[img] = draw_crop(a, static_cast<uint64_t>(a.sample_base + source_row(ri, img)));
+  const int64_t key = a.sample_ids != nullptr ? a.sample_ids[img] : source_row(ri, img);
+  boxes[img] = draw_crop(a, static_cast<uint64_t>(a.sample_base + key));
 }
 
 // Division by a runtime divisor d that is uniform across the workgroup, for

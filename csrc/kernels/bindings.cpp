@@ -312,10 +312,11 @@ PYBIND11_MODULE(_ddl_hip, m) {
          int out_h, int out_w, uint64_t seed, int64_t sample_base, float scale_min, float scale_max, float ratio_min,
          float ratio_max, float flip_p, int mode, uintptr_t idx, int64_t base, std::vector<uint64_t> keys,
          uint64_t n_domain, uint32_t half_bits, std::vector<float> scale, std::vector<float> bias, uintptr_t boxes_out,
-         int path, uintptr_t stream) {
+         int path, uintptr_t stream, uintptr_t sample_ids) {
         ddl::AugmentSpec a{};
         a.seed = seed;
         a.sample_base = sample_base;
+        a.sample_ids = as_ptr<const int64_t>(sample_ids);
         a.in_h = in_h;
         a.in_w = in_w;
         a.out_h = out_h;
@@ -337,7 +338,7 @@ PYBIND11_MODULE(_ddl_hip, m) {
       py::arg("sample_base"), py::arg("scale_min"), py::arg("scale_max"), py::arg("ratio_min"), py::arg("ratio_max"),
       py::arg("flip_p"), py::arg("mode"), py::arg("idx"), py::arg("base"), py::arg("keys"), py::arg("n_domain"),
       py::arg("half_bits"), py::arg("scale"), py::arg("bias"), py::arg("boxes_out"), py::arg("path"),
-      py::arg("stream"));
+      py::arg("stream"), py::arg("sample_ids") = 0);
   m.def(
       "pack_columns",
       [](std::vector<uintptr_t> srcs, std::vector<int> widths, int in_dt, uintptr_t dst, int out_dt, int64_t n_rows,

@@ -50,6 +50,9 @@ int pack_columns(const SplitSpec& spec, void* dst, int32_t in_dt, int64_t n_rows
 struct AugmentSpec {
   uint64_t seed;
   int64_t sample_base;
+  // optional [batch] crop keys (e.g. global sample ids of rows that were exchanged between ranks);
+  // null: the key is sample_base + the image's source row
+  const int64_t* sample_ids;
   int32_t in_h, in_w, out_h, out_w, channels;
   float scale_min, scale_max, ratio_min, ratio_max, flip_p;
 };

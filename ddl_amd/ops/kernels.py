@@ -328,7 +328,8 @@ def random_resized_crop(src, index: torch.Tensor | None = None, *, perm: Feistel
                         base: int = 0, n_rows: int | None = None, size=(224, 224), scale=(0.08, 1.0),
                         ratio=(3.0 / 4.0, 4.0 / 3.0), flip_p: float = 0.5, seed: int = 0, sample_base: int = 0,
                         layout: str = "chw", out_dtype=torch.bfloat16, mean=None, std=None,
-                        return_boxes: bool = False, impl: str = "auto", stream=None):
+                        return_boxes: bool = False, impl: str = "auto", stream=None,
+                        sample_ids: torch.Tensor | None = None):
     """Gathered images -> RandomResizedCrop + horizontal flip + normalise + cast, one gfx950 kernel.
 
     ``src`` rows are [C, H, W] (``layout="chw"``) or [H, W, C] (``"hwc"``),
@@ -341,6 +342,9 @@ def random_resized_crop(src, index: torch.Tensor | None = None, *, perm: Feistel
     output rows' source pixels in LDS when the band fits the kernel's LDS
     budget, ``"lds"`` requires that (ValueError otherwise), ``"direct"`` reads
     every tap from global memory; all three give identical results.
+    ``sample_ids`` (int64 [B] on the device) replaces the source row in the crop
+    key: rows gathered out of an exchange buffer keep the crop of their global
+    sample id.
     """
     paths = {"auto": 0, "lds": 1, "direct": 2}
     if impl not in paths:
@@ -362,13 +366,19 @@ def random_resized_crop(src, index: torch.Tensor | None = None, *, perm: Feistel
     dev = src.device if isinstance(src, torch.Tensor) else torch.device("cuda", torch.cuda.current_device())
     out = torch.empty((n_rows, c, oh, ow), dtype=out_dtype, device=dev)
     boxes = torch.empty((n_rows, 5), dtype=torch.int32, device=dev)  # drawn by a per-image pre-pass
+    ids_ptr = 0
+    if sample_ids is not None:
+        if sample_ids.dtype != torch.int64 or sample_ids.device != dev or sample_ids.numel() != n_rows \
+                or not sample_ids.is_contiguous():
+            raise ValueError("sample_ids must be a contiguous int64 [n_rows] tensor on the source's device")
+        ids_ptr = sample_ids.data_ptr()
     _native.hip().random_resized_crop(
         dst=out.data_ptr(), out_dt=_dtypes.code(out_dtype), src=_src_addr(src), in_dt=_dtypes.code(src.dtype),
         batch=n_rows, hwc=layout == "hwc", in_h=int(h), in_w=int(w), channels=int(c), out_h=oh, out_w=ow,
         seed=int(seed) & ((1 << 64) - 1), sample_base=int(sample_base), scale_min=float(scale[0]),
         scale_max=float(scale[1]), ratio_min=float(ratio[0]), ratio_max=float(ratio[1]), flip_p=float(flip_p),
         scale=sc, bias=bi, boxes_out=boxes.data_ptr(), path=paths[impl], stream=_stream_handle(stream),
-        **_index_kw(index, perm, base))
+        sample_ids=ids_ptr, **_index_kw(index, perm, base))
     return (out, boxes) if return_boxes else out
 
 

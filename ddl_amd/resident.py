@@ -26,6 +26,10 @@ shard usually fits on the GPU, so here:
      with the dtype cast and per-channel normalisation.
   With W = 1 step 4 alone runs, straight out of the resident shard, with the
   permutation evaluated inside the kernel.
+* ``augment=`` replaces step 4 with the on-device RandomResizedCrop + flip +
+  normalise kernel: an ImageNet-size uint8 dataset stays resident (193 GB at
+  3x224x224) and every epoch sees fresh crops. The crop of a sample is keyed
+  by (seed, epoch, global sample id), so it does not depend on W.
 
 Checkpoint: the same ``kind="indexed"`` record as the loader
 (seed, epoch, global_batch_cursor) -- resumable at any world size.
@@ -203,8 +207,13 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
                  drop_last: bool = True, out_dtype: Any = None, normalize: dict | None = None, depth: int = 2,
                  device: str | torch.device | None = None, n_epochs: int | None = None,
                  resume_state: dict | None = None, chunk_bytes: int = 256 << 20, host_threads: int = 8,
-                 scatter_from: int | None = None):
+                 scatter_from: int | None = None, augment: dict | None = None):
         import torch.distributed as dist
+
+        aug_keys = {"size", "scale", "ratio", "flip_p", "layout"}
+        if augment is not None and not set(augment) <= aug_keys:
+            raise ValueError(f"unknown augment keys {sorted(set(augment) - aug_keys)}")
+        self.augment = augment
 
         self.env = env or DDLEnv()
         self.W, self.rank = self.env.world_size, self.env.rank
@@ -238,6 +247,8 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
             self.device = torch.device("cuda", torch.cuda.current_device())
         self.out_dtype = _dtypes.to_torch_dtype(out_dtype) if out_dtype is not None else self.src_dtype
         self.normalize = normalize
+        if augment is not None and (self.device.type != "cuda" or len(self.sample_shape) != 3):
+            raise ValueError("augment= needs a GPU and [C, H, W] / [H, W, C] image samples")
         self._init_cursor(seed, depth, n_epochs, resume_state)
         self.group = None
         if self.W > 1:
@@ -356,8 +367,11 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
         ctx = streams.on_stream(self.prep_stream) if self.prep_stream is not None else contextlib.nullcontext()
         with ctx, trace_range("ddl.resident.assemble"):
             if self.W == 1:
-                batch = ops.gather_rows(self.shard, perm=perm, base=g * self.GB, n_rows=self.LB,
-                                        out_dtype=self.out_dtype, **kw)
+                if self.augment is not None:  # rows of the shard ARE global sample ids at W = 1
+                    batch = self._crop(self.shard, e, perm=perm, base=g * self.GB, n_rows=self.LB)
+                else:
+                    batch = ops.gather_rows(self.shard, perm=perm, base=g * self.GB, n_rows=self.LB,
+                                            out_dtype=self.out_dtype, **kw)
             else:
                 pos = np.arange(g * self.GB, (g + 1) * self.GB, dtype=np.int64)
                 idx_all = perm(pos)
@@ -377,12 +391,27 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
                 dist.all_to_all_single(recv.view(self.LB, -1), send.view(send.shape[0], -1), recv_counts,
                                        send_counts, group=self.group)
                 self.bytes_exchanged += (len(send_rows) - send_counts[self.rank]) * self.row_bytes
-                batch = ops.gather_rows(recv, index=self._to_dev(inv), out_dtype=self.out_dtype, **kw)
+                if self.augment is not None:  # crop keyed by the global sample id, not the recv row
+                    ids = self._to_dev(idx_all[self.rank * self.LB:(self.rank + 1) * self.LB])
+                    batch = self._crop(recv, e, index=self._to_dev(inv), sample_ids=ids)
+                else:
+                    batch = ops.gather_rows(recv, index=self._to_dev(inv), out_dtype=self.out_dtype, **kw)
             ev = None
             if self.prep_stream is not None:
                 ev = torch.cuda.Event()
                 ev.record(self.prep_stream)
         return batch, ev
+
+    def _crop(self, src: torch.Tensor, epoch: int, **kw) -> torch.Tensor:
+        from .dataloader import _mix
+
+        aug, norm = self.augment, self.normalize or {}
+        return ops.random_resized_crop(
+            src, size=aug.get("size", (224, 224)), scale=aug.get("scale", (0.08, 1.0)),
+            ratio=aug.get("ratio", (3.0 / 4.0, 4.0 / 3.0)), flip_p=aug.get("flip_p", 0.5),
+            seed=_mix(self.seed, epoch), layout=aug.get("layout", "chw"),
+            out_dtype=self.out_dtype if self.out_dtype in (torch.bfloat16, torch.float32) else torch.bfloat16,
+            mean=norm.get("mean"), std=norm.get("std"), **kw)
 
     def stats(self) -> dict:
         return {"batches": self.batches, "bytes_exchanged": self.bytes_exchanged, "shard_rows": self.hi - self.lo,

@@ -358,3 +358,18 @@ def test_random_resized_crop_box_distribution_and_determinism():
     assert torch.equal(b3.cpu().double(), b[[7, 3, 11]])
     _, b4 = ops.random_resized_crop(src, size=(8, 8), seed=6, return_boxes=True)
     assert not torch.equal(b4.cpu().double(), b)
+
+
+def test_random_resized_crop_sample_ids_key_the_crop():
+    """Rows gathered out of an exchange buffer, cropped with explicit sample ids, get the same crops
+    (and pixels) as the same samples read straight out of the dataset by index."""
+    n = 40
+    src = (torch.rand((n, 3, 37, 45)) * 255).to(torch.uint8).to(_dev())
+    ids = torch.tensor([7, 3, 31, 0, 19, 22, 5, 38], dtype=torch.int64, device=_dev())
+    kw = dict(size=(24, 24), seed=11, mean=[0.5] * 3, std=[0.25] * 3, out_dtype=torch.float32, return_boxes=True)
+    a, ba = ops.random_resized_crop(src, index=ids, **kw)
+    shuffled = src[ids.flip(0)].contiguous()  # rows in another order, e.g. as received from peers
+    b, bb = ops.random_resized_crop(shuffled, index=torch.arange(7, -1, -1, device=_dev()), sample_ids=ids, **kw)
+    assert torch.equal(ba, bb) and torch.equal(a, b)
+    with pytest.raises(ValueError):
+        ops.random_resized_crop(src, index=ids, sample_ids=ids[:4], **kw)

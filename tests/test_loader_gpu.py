@@ -227,3 +227,32 @@ def test_gpu_exception_unwinds_cleanly_with_native_stager():
             raise KeyError("user error")
     assert time.monotonic() - t0 < 30
     assert dl._stager._closed
+
+
+def test_gpu_resident_augment_matches_direct_crop():
+    """ResidentGlobalLoader(augment=...) crops every epoch's global order out of the HBM shard,
+    keyed by (seed, epoch, sample id): identical to cropping the dataset directly."""
+    from ddl_amd import ops
+    from ddl_amd.dataloader import _mix
+    from ddl_amd.models import SharedArraySource
+    from ddl_amd.resident import ResidentGlobalLoader
+
+    n, gb = 96, 16
+    data = (torch.rand((n, 3, 40, 52)) * 255).to(torch.uint8)
+    src = SharedArraySource.create(f"ddl_amd_resaug_{np.random.randint(1 << 30)}", data)
+    norm = {"mean": [0.485, 0.456, 0.406], "std": [0.229, 0.224, 0.225]}
+    try:
+        with ddl_amd.start(n_producers=0) as (env, _):
+            dl = ResidentGlobalLoader(src, gb, env, seed=4, n_epochs=2, out_dtype=torch.bfloat16, normalize=norm,
+                                      augment={"size": (32, 32), "flip_p": 0.5})
+            full = data.cuda()
+            for e in range(2):
+                perm = dl.order.perm(e)
+                for g, b in enumerate(dl):
+                    assert b.shape == (gb, 3, 32, 32) and b.dtype == torch.bfloat16
+                    ref = ops.random_resized_crop(full, perm=perm, base=g * gb, n_rows=gb, size=(32, 32),
+                                                  seed=_mix(4, e), **norm)
+                    assert torch.equal(b, ref), (e, g)
+            dl.close()
+    finally:
+        src.close()

@@ -121,3 +121,12 @@ def _close_rank(rank, world, name, n, gb):
 
 def test_resident_close_releases_shard(src):
     assert run_ranks(_close_rank, 1, src.name, src.n, 48) == [True]
+
+
+def test_resident_augment_needs_gpu_and_known_keys(src):
+    from ddl_amd.resident import ResidentGlobalLoader
+
+    with pytest.raises(ValueError):
+        ResidentGlobalLoader(src, 48, augment={"size": (4, 4)}, device="cpu")  # CPU, and rows are not images
+    with pytest.raises(ValueError):
+        ResidentGlobalLoader(src, 48, augment={"bogus": 1}, device="cpu")
