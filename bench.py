@@ -64,6 +64,41 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
+def phase2(args, env, dev, it, idle_steps: int, barrier, sync) -> dict:
+    """GPU idle % behind a fixed-cost bf16 train step (DDP gradient all-reduce over RCCL when N > 1)."""
+    import torch
+    import torch.distributed as dist
+
+    from ddl_amd.models.trainstep import TrainStep
+    from ddl_amd.utils.tracing import ComputeIdleMeter, trace_range
+
+    step = TrainStep(dev, dim=args.model_dim, depth=args.model_depth,
+                     process_group=env.process_group if env.world_size > 1 else None)
+    for _ in range(args.warmup // 2):
+        (x,) = next(it)
+        step(x)
+    meter = ComputeIdleMeter() if dev.type == "cuda" else None
+    barrier()
+    t2 = time.perf_counter()
+    with trace_range("bench.phase2"):
+        for _ in range(idle_steps):
+            (x,) = next(it)
+            if meter:
+                meter.step_begin()
+            step(x)
+            if meter:
+                meter.step_end()
+        sync()
+    t3 = time.perf_counter()
+    idle = meter.result() if meter else {"gpu_idle_pct": float("nan"), "busy_ms": 0.0, "wall_ms": 0.0}
+    idle["train_samples_per_s"] = args.batch * idle_steps * env.world_size / (t3 - t2)
+    if env.world_size > 1:
+        t = torch.tensor([idle["gpu_idle_pct"]], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=env.control_group)
+        idle["gpu_idle_pct"] = float(t.item())
+    return idle
+
+
 def main(argv=None) -> int:
     args = parse(argv)
     import torch
@@ -72,7 +107,7 @@ def main(argv=None) -> int:
     import ddl_amd
     from ddl_amd import Marker, ops
     from ddl_amd.models.producers import ImageWindowProducer
-    from ddl_amd.utils.tracing import ComputeIdleMeter, trace_range
+    from ddl_amd.utils.tracing import trace_range
 
     n_world = int(os.environ.get("WORLD_SIZE", "1"))
     if n_world != args.gpus:
@@ -141,35 +176,17 @@ def main(argv=None) -> int:
 
         # ---------------- phase 2: GPU idle % behind a fixed-cost train step
         idle = {}
-        if idle_steps:
-            from ddl_amd.models.trainstep import TrainStep
+        phase2_error = None
+        try:
+            if idle_steps:
+                idle = phase2(args, env, dev, it, idle_steps, barrier, sync)
+        except Exception as e:  # the feed rate (phase 1) is still reported; the error goes into the JSON line
+            import traceback
 
-            # DP training step: DDP gradient all-reduce over RCCL when N > 1
-            step = TrainStep(dev, dim=args.model_dim, depth=args.model_depth,
-                             process_group=env.process_group if env.world_size > 1 else None)
-            for _ in range(args.warmup // 2):
-                (x,) = next(it)
-                step(x)
-            meter = ComputeIdleMeter() if dev.type == "cuda" else None
-            barrier()
-            t2 = time.perf_counter()
-            with trace_range("bench.phase2"):
-                for _ in range(idle_steps):
-                    (x,) = next(it)
-                    if meter:
-                        meter.step_begin()
-                    step(x)
-                    if meter:
-                        meter.step_end()
-                sync()
-            t3 = time.perf_counter()
-            idle = meter.result() if meter else {"gpu_idle_pct": float("nan"), "busy_ms": 0.0, "wall_ms": 0.0}
-            idle["train_samples_per_s"] = args.batch * idle_steps * env.world_size / (t3 - t2)
-            if env.world_size > 1:
-                t = torch.tensor([idle["gpu_idle_pct"]], dtype=torch.float64)
-                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=env.control_group)
-                idle["gpu_idle_pct"] = float(t.item())
+            traceback.print_exc()
+            phase2_error, idle = repr(e)[:300], {}
         dl.close()
+
 
         if env.rank == 0:
             out = {
@@ -204,6 +221,7 @@ def main(argv=None) -> int:
                              + (" (DDP all-reduce)" if env.world_size > 1 else ""),
                     "samples_per_s": round(idle["train_samples_per_s"], 1),
                     "busy_ms": round(idle["busy_ms"], 3), "wall_ms": round(idle["wall_ms"], 3)},
+                "phase2_error": phase2_error,
                 "loader": {"consumer_wait_s": round(stats["consumer_wait_s"], 4),
                            "stager_wait_producer_s": round(stats.get("stager_wait_producer_s", 0.0), 4),
                            "windows_staged": stats.get("windows_staged")},
