@@ -93,3 +93,21 @@ def test_bench_plumbing_config1_two_ranks():
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     assert out["world_size"] == 2 and out["exactly_once_every_epoch"] is True and out["samples_per_s"] > 0
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("script,args", [("resident_images.py", ["--n-samples", "512", "--epochs", "2"]),
+                                         ("tokens_packed.py", ["--n-seqs", "256", "--epochs", "2"]),
+                                         ("tokens_packed.py", ["--n-seqs", "256", "--epochs", "1", "--mode", "pad"])])
+@pytest.mark.parametrize("ranks", [1, 2])
+def test_usage_examples(script, args, ranks):
+    """The usage examples run end to end on CPU, alone and as two torchrun ranks (gloo)."""
+    path = os.path.join(REPO, "examples", script)
+    if ranks == 1:
+        cmd = [sys.executable, path, *args]
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", str(free_port()), path, *args]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=dict(_env(), DDL_DEVICE="cpu"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "epoch 0:" in r.stdout
