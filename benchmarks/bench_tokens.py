@@ -27,6 +27,8 @@ def main(argv=None):
     ap.add_argument("--n-seqs", type=int, default=8192)
     ap.add_argument("--producers", type=int, default=4)
     ap.add_argument("--mode", default="pack", choices=["pad", "pack"])
+    ap.add_argument("--pack-order", default="ffd", choices=["in_order", "ffd"],
+                    help="pack mode: first-fit-decreasing rows (~95%% dense) or in-order (~75%%)")
     ap.add_argument("--idle-steps", type=int, default=200,
                     help="phase 2: steps of a fixed-cost token train step, for GPU idle %% (0 disables)")
     ap.add_argument("--model-dim", type=int, default=256)
@@ -62,7 +64,7 @@ def main(argv=None):
             else:
                 source = src
             n_epochs = (a.warmup + a.steps + a.idle_steps + a.warmup // 2) // (a.n_seqs // gb) + 2
-            dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(source, gb, a.seq_len, a.mode), a.batch, conn,
+            dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(source, gb, a.seq_len, a.mode, pack_order=a.pack_order), a.batch, conn,
                                                n_epochs, mode="indexed", env=env, collate="tokens", auto_mark=True)
             dev = torch.device(env.device)
             acc = ops.ChecksumAccumulator(dev)  # one streaming launch per batch
@@ -126,7 +128,9 @@ def main(argv=None):
                     "metric": "tokens/s fed to GPU (seq_len 4096, on-device pad/pack)", "mode": a.mode,
                     "value": round(real_tokens / dt, 1), "unit": "tokens/s (real, est. from mean length)",
                     "sequences_per_s": round(a.steps * a.batch * env.world_size / dt, 1),
-                    "packed_rows_per_step": round(rows / a.steps, 2), "n_gpus": env.world_size,
+                    "packed_rows_per_step": round(rows / a.steps, 2),
+                    "pack_order": a.pack_order if a.mode == "pack" else None,
+                    "row_density": round(a.batch * mean_len / (rows / a.steps) / a.seq_len, 3), "n_gpus": env.world_size,
                     "steps": a.steps, "ms_per_step": round(1000 * dt / a.steps, 3), "batch_seqs": a.batch,
                     "producers": a.producers, "mean_len": round(mean_len, 1),
                     "consumer_wait_s": round(st["consumer_wait_s"], 3),

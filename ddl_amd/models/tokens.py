@@ -103,14 +103,70 @@ class SharedTokenSource:
         self.offsets.close()
 
 
+def ffd_order(lengths: np.ndarray, seq_len: int) -> tuple[np.ndarray, int]:
+    """First-fit-decreasing bin packing of sequences into rows of ``seq_len`` tokens.
+
+    Returns the batch-local sequence order and the number of rows that in-order
+    packing (``pack_plan``) of that order produces. A sequence longer than ``seq_len``
+    takes ``L // seq_len`` full rows; its remainder ``L % seq_len`` is packed like a
+    short sequence, into a bin that holds no other remainder, and the whole sequence
+    is emitted at the head of that bin, so its tokens stay contiguous. Each other bin
+    lists its sequences longest first. In-order packing of the result therefore
+    breaks rows exactly at bin boundaries. A bin's first item is either a full chunk,
+    which fits nowhere, or the bin's longest sequence, which did not fit in any earlier
+    bin when it was placed (earlier bins only fill up).
+    """
+    lengths = np.asarray(lengths, dtype=np.int64)
+    S = int(seq_len)
+    rem_len = np.where(lengths > S, lengths % S, lengths)
+    full = np.where(lengths > S, lengths // S, 0)
+    items = np.nonzero(rem_len > 0)[0]
+    items = items[np.argsort(-rem_len[items], kind="stable")]
+    left = np.empty(len(items), dtype=np.int64)
+    has_long = np.zeros(len(items), dtype=bool)
+    bins: list[list[int]] = []
+    for i in items:
+        is_long = lengths[i] > S
+        ok = left[: len(bins)] >= rem_len[i]
+        if is_long:
+            ok &= ~has_long[: len(bins)]
+        fit = np.nonzero(ok)[0]
+        if len(fit):
+            b = int(fit[0])
+        else:
+            b = len(bins)
+            bins.append([])
+            left[b] = S
+            has_long[b] = False
+        bins[b].append(int(i))
+        left[b] -= rem_len[i]
+        has_long[b] |= is_long
+    order: list[int] = []
+    for members in bins:
+        head = [i for i in members if lengths[i] > S]  # at most one: its full chunks, then its remainder
+        order += head + [i for i in members if lengths[i] <= S]
+    exact = [int(i) for i in np.nonzero((lengths > S) & (rem_len == 0))[0]]  # only full chunks
+    order += exact
+    return np.asarray(order, dtype=np.int64), len(bins) + int(full.sum())
+
+
 class TokenBatchProducer(ProducerFunctionSkeleton):
-    """One window = this rank's slice of a global batch of sequences, shipped ragged."""
+    """One window = this rank's slice of a global batch of sequences, shipped ragged.
+
+    ``pack_order="ffd"`` (pack mode) reorders the batch's sequences by first-fit
+    decreasing before the ragged gather, so rows are packed bins: density rises
+    from ~75% (in-order packing of lengths uniform in [64, 4096]) to ~95%.
+    The batch holds the same sequences, and the cursor and checkpoint are unchanged.
+    """
 
     def __init__(self, source: SharedTokenSource, global_batch: int, seq_len: int = 4096, mode: str = "pad",
-                 seed: int | None = None, host_threads: int = 2):
+                 seed: int | None = None, host_threads: int = 2, pack_order: str = "in_order"):
         super().__init__()
         if mode not in ("pad", "pack"):
             raise ValueError("mode must be 'pad' or 'pack'")
+        if pack_order not in ("in_order", "ffd"):
+            raise ValueError("pack_order must be 'in_order' or 'ffd'")
+        self.pack_order = pack_order
         self.source, self.global_batch, self.seq_len, self.mode, self.seed = source, global_batch, seq_len, mode, seed
         self.host_threads = host_threads
         self.order = None
@@ -135,6 +191,10 @@ class TokenBatchProducer(ProducerFunctionSkeleton):
         g_total = rnd * (self.n_producers or 1) + (self.producer_index or 0)
         epoch, g = divmod(g_total, self.order.batches_per_epoch)
         idx = self.order.indices(epoch, g, self.rank_global or 0, self.world_size)
+        if self.mode == "pack" and self.pack_order == "ffd":
+            offs_all = self.source.offsets.tensor().view(-1).numpy()
+            idx = np.asarray(idx, dtype=np.int64)
+            idx = idx[ffd_order(offs_all[idx + 1] - offs_all[idx], self.seq_len)[0]]
         buf: torch.Tensor = kwargs["my_tensor"].view(-1)
         v = self.layout.views(buf)
         toks = self.source.tokens.tensor().view(-1)

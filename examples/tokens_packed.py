@@ -10,7 +10,8 @@ Producers gather each step's sequences in the world-size-invariant global order
 and ship them RAGGED, so only real tokens cross PCIe. The consumer expands a
 batch on the GPU with the pad/pack kernel:
 
-* ``pack``: sequences packed back to back into rows of ``seq_len`` (long ones split).
+* ``pack``: sequences packed into rows of ``seq_len`` by first-fit decreasing
+  (``pack_order="ffd"``, ~95% dense; long ones split).
   Returns ``input_ids``, ``attention_mask``, ``position_ids`` (restarting per
   sequence), ``segment_ids`` and ``cu_seqlens`` (for varlen attention).
 * ``pad``: one sequence per row, padded with ``pad_id``.
@@ -50,9 +51,9 @@ def main() -> None:
                 offs = SharedArraySource(name + "_off", a.n_seqs + 1, (1,), "int64")
                 n_tok = int(offs.tensor()[-1])
                 src = SharedTokenSource(SharedArraySource(name + "_tok", n_tok, (1,), "int32"), offs, a.seq_len)
-            dl = ddl_amd.DistributedDataLoader(
-                TokenBatchProducer(src, a.global_batch, a.seq_len, a.mode), a.global_batch // env.world_size, conn,
-                a.epochs, mode="indexed", env=env, collate="tokens", auto_mark=True)
+            producer = TokenBatchProducer(src, a.global_batch, a.seq_len, a.mode, pack_order="ffd")
+            dl = ddl_amd.DistributedDataLoader(producer, a.global_batch // env.world_size, conn, a.epochs,
+                                               mode="indexed", env=env, collate="tokens", auto_mark=True)
             for epoch in range(a.epochs):
                 real = rows = 0
                 for b in dl:

@@ -125,3 +125,44 @@ def test_token_train_step_on_collated_pack_batch():
     for _ in range(20):
         l1 = float(step(batch))
     assert np.isfinite(l0) and l1 < l0  # it learns: the step really runs fwd + bwd + update
+
+
+def test_ffd_order_rows_equal_bins_and_beat_in_order():
+    from ddl_amd.models.tokens import ffd_order
+
+    rng = np.random.default_rng(3)
+    tot_ffd = tot_in = 0
+    for _ in range(100):
+        S = int(rng.choice([7, 100, 4096]))
+        lens = rng.integers(1, 2 * S, size=int(rng.integers(1, 70)))
+        order, n_rows = ffd_order(lens, S)
+        assert sorted(order.tolist()) == list(range(len(lens)))
+        offs = np.concatenate([[0], np.cumsum(lens[order])])
+        assert len(ops.pack_plan(offs, S)[0]) == n_rows  # in-order packing of that order breaks at bin ends
+        tot_ffd += n_rows
+        tot_in += len(ops.pack_plan(np.concatenate([[0], np.cumsum(lens)]), S)[0])
+    assert tot_ffd < tot_in  # fewer rows overall (FFD can lose on a rare adversarial batch)
+
+
+def test_token_batches_ffd_pack_order(corpus, monkeypatch):
+    """pack_order="ffd": the same sequences per batch, in first-fit-decreasing order, packed into no more rows."""
+    from ddl_amd.models.tokens import ffd_order
+
+    monkeypatch.setenv("DDL_DEVICE", "cpu")
+    seq_len, gb = 256, 16
+    order = EpochOrder(corpus.n, gb, 4)
+    rows = {}
+    for po in ("in_order", "ffd"):
+        with ddl_amd.start(n_producers=2) as (env, conn):
+            dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(corpus, gb, seq_len, "pack", pack_order=po), gb,
+                                               conn, 1, mode="indexed", env=env, auto_mark=True, collate="tokens",
+                                               seed=4)
+            rows[po] = 0
+            for g, batch in enumerate(dl):
+                seqs = expected_tokens(corpus, order.indices(0, g))
+                if po == "ffd":
+                    seqs = [seqs[i] for i in ffd_order(np.array([len(x) for x in seqs]), seq_len)[0]]
+                flat = batch["input_ids"][batch["attention_mask"].bool()].numpy()
+                assert np.array_equal(flat, np.concatenate(seqs))  # every token once, in the packing order
+                rows[po] += batch["input_ids"].shape[0]
+    assert rows["ffd"] <= rows["in_order"]
