@@ -463,6 +463,49 @@ std::pair<int64_t, int64_t> pack_plan(const int64_t* offs, int64_t n_seq, int64_
   return {n_rows, n_seg};
 }
 
+int64_t ffd_order(const int64_t* len, int64_t n, int64_t seq_len, int64_t* order) {
+  if (seq_len <= 0) throw std::invalid_argument("ffd_order: seq_len must be > 0");
+  std::vector<int64_t> items, exact;  // items: sequences with a (remainder) part to bin
+  int64_t full_rows = 0;
+  auto part = [&](int64_t i) { return len[i] > seq_len ? len[i] % seq_len : len[i]; };
+  for (int64_t i = 0; i < n; ++i) {
+    if (len[i] < 0) throw std::invalid_argument("ffd_order: negative length");
+    if (len[i] > seq_len) full_rows += len[i] / seq_len;
+    if (part(i) > 0)
+      items.push_back(i);
+    else if (len[i] > 0)
+      exact.push_back(i);  // whole rows only
+    else
+      exact.push_back(i);  // empty sequence: contributes no tokens, kept in the order
+  }
+  std::stable_sort(items.begin(), items.end(), [&](int64_t a, int64_t b) { return part(a) > part(b); });
+  std::vector<int64_t> left;            // free tokens per bin
+  std::vector<int64_t> head;            // the long sequence whose remainder the bin holds, or -1
+  std::vector<std::vector<int64_t>> bins;
+  for (const int64_t i : items) {
+    const bool is_long = len[i] > seq_len;
+    size_t b = 0;
+    while (b < bins.size() && (left[b] < part(i) || (is_long && head[b] >= 0))) ++b;
+    if (b == bins.size()) {
+      bins.emplace_back();
+      left.push_back(seq_len);
+      head.push_back(-1);
+    }
+    left[b] -= part(i);
+    if (is_long)
+      head[b] = i;
+    else
+      bins[b].push_back(i);
+  }
+  int64_t k = 0;
+  for (size_t b = 0; b < bins.size(); ++b) {
+    if (head[b] >= 0) order[k++] = head[b];
+    for (const int64_t i : bins[b]) order[k++] = i;
+  }
+  for (const int64_t i : exact) order[k++] = i;
+  return static_cast<int64_t>(bins.size()) + full_rows;
+}
+
 void pool_run(int n, int n_threads, const std::function<void(int)>& fn) {
   std::lock_guard<std::mutex> lk(g_pool_call_mu);
   Pool::get().run(n, n_threads, fn);

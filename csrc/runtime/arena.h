@@ -175,6 +175,13 @@ uint64_t gather_ragged(uint8_t* dst, int64_t* dst_offsets, const uint8_t* src, c
 // output arrays are too small.
 std::pair<int64_t, int64_t> pack_plan(const int64_t* offs, int64_t n_seq, int64_t seq_len, int64_t* row_start,
                                       int64_t* row_end, int64_t max_rows, int64_t* seg_offsets, int64_t max_segs);
+// First-fit-decreasing order of n sequences (lengths len[i]) for rows of
+// seq_len tokens, such that pack_plan over that order breaks rows exactly at
+// bin ends: a sequence longer than seq_len takes len / seq_len full rows and
+// its remainder is binned (one remainder per bin, its sequence first in the
+// bin); each other bin lists its sequences longest first. Writes order[0..n)
+// and returns the row count pack_plan will produce.
+int64_t ffd_order(const int64_t* len, int64_t n, int64_t seq_len, int64_t* order);
 // Run fn(i), i in [0, n), on the shared host worker pool (caller included).
 // fn must not throw: record errors and report them after the call.
 void pool_run(int n, int n_threads, const std::function<void(int)>& fn);

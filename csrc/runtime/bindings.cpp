@@ -257,4 +257,14 @@ PYBIND11_MODULE(_ddl_runtime, m) {
       },
       py::arg("offsets"), py::arg("n_seq"), py::arg("seq_len"), py::arg("row_start"), py::arg("row_end"),
       py::arg("max_rows"), py::arg("seg_offsets"), py::arg("max_segs"), "greedy in-order packing plan -> (n_rows, n_segs)");
+  m.def(
+      "ffd_order",
+      [](py::array_t<int64_t, py::array::c_style | py::array::forcecast> lengths, int64_t seq_len) {
+        const int64_t n = static_cast<int64_t>(lengths.size());
+        py::array_t<int64_t> order(n);
+        const int64_t rows = ddl::ffd_order(lengths.data(), n, seq_len, order.mutable_data());
+        return py::make_tuple(order, rows);
+      },
+      py::arg("lengths"), py::arg("seq_len"),
+      "first-fit-decreasing sequence order whose in-order packing breaks rows at bin ends -> (order, n_rows)");
 }

@@ -104,6 +104,13 @@ class SharedTokenSource:
 
 
 def ffd_order(lengths: np.ndarray, seq_len: int) -> tuple[np.ndarray, int]:
+    """First-fit-decreasing order of one batch's sequences (native ``ffd_order`` in
+    ``csrc/runtime/arena.cpp``; ``ffd_order_py`` is its NumPy reference)."""
+    order, n_rows = _native.runtime().ffd_order(np.ascontiguousarray(lengths, dtype=np.int64), int(seq_len))
+    return order, int(n_rows)
+
+
+def ffd_order_py(lengths: np.ndarray, seq_len: int) -> tuple[np.ndarray, int]:
     """First-fit-decreasing bin packing of sequences into rows of ``seq_len`` tokens.
 
     Returns the batch-local sequence order and the number of rows that in-order
@@ -145,7 +152,7 @@ def ffd_order(lengths: np.ndarray, seq_len: int) -> tuple[np.ndarray, int]:
     for members in bins:
         head = [i for i in members if lengths[i] > S]  # at most one: its full chunks, then its remainder
         order += head + [i for i in members if lengths[i] <= S]
-    exact = [int(i) for i in np.nonzero((lengths > S) & (rem_len == 0))[0]]  # only full chunks
+    exact = [int(i) for i in np.nonzero(rem_len == 0)[0]]  # only full chunks, or empty
     order += exact
     return np.asarray(order, dtype=np.int64), len(bins) + int(full.sum())
 

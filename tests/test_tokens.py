@@ -144,6 +144,24 @@ def test_ffd_order_rows_equal_bins_and_beat_in_order():
     assert tot_ffd < tot_in  # fewer rows overall (FFD can lose on a rare adversarial batch)
 
 
+def test_ffd_order_native_matches_numpy_reference():
+    """The native C++ ffd_order (arena.cpp) equals its NumPy reference, empty and exact-multiple lengths included."""
+    from ddl_amd.models.tokens import ffd_order, ffd_order_py
+
+    rng = np.random.default_rng(11)
+    for _ in range(200):
+        S = int(rng.choice([1, 5, 64, 4096]))
+        lens = rng.integers(0, 3 * S + 1, size=int(rng.integers(0, 90)))
+        if len(lens) and rng.random() < 0.3:
+            lens[rng.integers(0, len(lens))] = 2 * S  # only full chunks
+        o_nat, r_nat = ffd_order(lens, S)
+        o_py, r_py = ffd_order_py(lens, S)
+        assert r_nat == r_py and o_nat.tolist() == o_py.tolist()
+        assert sorted(o_nat.tolist()) == list(range(len(lens)))
+    with pytest.raises(ValueError):
+        ffd_order(np.array([3]), 0)
+
+
 def test_token_batches_ffd_pack_order(corpus, monkeypatch):
     """pack_order="ffd": the same sequences per batch, in first-fit-decreasing order, packed into no more rows."""
     from ddl_amd.models.tokens import ffd_order
