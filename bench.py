@@ -2,8 +2,8 @@
 """Headline benchmark: samples/s fed to the GPU + GPU idle %, synthetic 3x224x224 bf16.
 
 Metric and config from BASELINE.json ("samples/sec fed to GPU + GPU idle%,
-synthetic 3x224x224 bf16 at 1/2/4/8 ranks"). One process per GPU (torchrun),
-each rank = one consumer with its own producer worker processes:
+synthetic 3x224x224 bf16 at 1/2/4/8 ranks"). One process per GPU, each rank =
+one consumer with its own producer worker processes:
 
   producers (host, pinned shm windows of synthetic bf16 images, refreshed every
   round) --hipMemcpyAsync on the prefetch stream--> HBM window ring
@@ -11,18 +11,30 @@ each rank = one consumer with its own producer worker processes:
   per-batch fused gfx950 Feistel-permutation gather --> bf16 [B,3,224,224]
   on the compute stream --> consumer step.
 
+Launch: under torchrun (RANK/WORLD_SIZE set) every process is one rank. Without
+a launcher, ``--gpus N`` > 1 makes this process spawn the N rank processes
+itself (before anything touches the GPU) and exit with their status; a
+WORLD_SIZE that disagrees with ``--gpus`` is an error, never a silent 1-rank run.
+
 With N > 1 every window also goes through the global-shuffle exchange: half of
 its rows are traded with all peers in one RCCL all-to-all over xGMI (BASELINE
-config 3), overlapped with the next window's DMA.
+config 3), on the DP group (one communicator and device order with the DDP
+all-reduce of phase 2, ``ddl_amd/parallel/order.py``).
 
 Phase 1 (the reported ``value``): the consumer step is a checksum kernel that
 reads every delivered byte, so the number is the loader's feed rate. Every
 sample crosses PCIe in every step (each window is re-copied H2D each visit;
 no caching). W warmup steps, then EXACTLY K timed steps bracketed by
-barrier + synchronize; max time over ranks; value = total samples/s of the job.
+barrier + synchronize; max time over ranks. ``value`` is the SMALLER of
+  * delivered: samples handed to the consumer in the timed region / time, and
+  * landed: samples whose H2D copy retired in the timed region / time
+    (counted by the stager's post-DMA host callback),
+so windows staged in HBM before t0 cannot inflate a short run; both are in
+the JSON line, with the H2D bytes and GB/s of the timed region.
 Phase 2 (``gpu_idle_pct``): a fixed-cost bf16 train step (PatchMLP fwd+bwd+SGD)
 consumes the batches; the compute stream's idle fraction is measured with HIP
-events (idle = 1 - busy/wall).
+events (idle = 1 - busy/wall). ``benchmarks/bench_idle_sweep.py`` sweeps a
+calibrated step across the feed rate.
 
 vs_baseline = value / (28,500 samples/s x N): BASELINE.md's reference
 ceiling for this shape (P=3 host producers, f32, no H2D) scaled linearly.
@@ -34,6 +46,8 @@ import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -46,7 +60,7 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
-    ap.add_argument("--window", type=int, default=1024, help="samples per producer window")
+    ap.add_argument("--window", type=int, default=256, help="samples per producer window")
     ap.add_argument("--producers", type=int, default=3)
     ap.add_argument("--slots", type=int, default=1, help="windows per producer")
     ap.add_argument("--depth", type=int, default=2, help="HBM prefetch depth (windows)")
@@ -62,6 +76,42 @@ def parse(argv=None):
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(n: int, argv: list[str]) -> int:
+    """Run this script as ``n`` rank processes on this node (torchrun-style env); return their status.
+
+    Called before anything touches the GPU. Rank 0's stdout is passed through (the JSON line);
+    if any rank fails the others are terminated and the failure's exit code is returned.
+    """
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        out = None if r == 0 else subprocess.DEVNULL
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env, stdout=out))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                print(f"bench: rank {procs.index(p)} exited with {code}; stopping the others", file=sys.stderr)
+                for q in pending:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
 
 
 def phase2(args, env, dev, it, idle_steps: int, barrier, sync) -> dict:
@@ -99,19 +149,36 @@ def phase2(args, env, dev, it, idle_steps: int, barrier, sync) -> dict:
     return idle
 
 
+def _landed(dl) -> tuple[int, int]:
+    st = getattr(dl, "_stager", None)
+    if st is None:  # CPU rehearsal: the host path has no H2D; every delivered window counts
+        return dl.window, 0
+    return st.windows_landed, st.bytes_landed
+
+
 def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else list(argv)
     args = parse(argv)
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            return self_launch(args.gpus, argv)
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}; refusing to run",
+              file=sys.stderr)
+        return 2
+
     import torch
     import torch.distributed as dist
 
     import ddl_amd
     from ddl_amd import Marker, ops
     from ddl_amd.models.producers import ImageWindowProducer
+    from ddl_amd.parallel.order import LEDGER, check_same_order
+    from ddl_amd.utils.numa import gpu_numa_node
     from ddl_amd.utils.tracing import trace_range
 
     n_world = int(os.environ.get("WORLD_SIZE", "1"))
-    if n_world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={n_world}", file=sys.stderr)
+    LEDGER.enable(n_world > 1)  # record every collective at issue; digests compared across ranks at the end
     idle_steps = args.steps if args.idle_steps < 0 else args.idle_steps
     if args.exchange is None:
         args.exchange = 0.5 if n_world > 1 else 0.0
@@ -121,6 +188,7 @@ def main(argv=None) -> int:
         raise SystemExit("--window must hold at least one --batch")
     n_epochs = math.ceil(total_steps / bpw) + 1
     shape = (3, 224, 224)
+    sample_bytes = math.prod(shape) * torch.empty((), dtype=getattr(torch, args.source_dtype)).element_size()
 
     with ddl_amd.start(n_producers=args.producers) as (env, conn):
         dev = torch.device(env.device)
@@ -157,6 +225,9 @@ def main(argv=None) -> int:
             (x,) = next(it)
             acc.add(x)
         barrier()
+        w_land0, b_land0 = _landed(dl)
+        w_cur0 = dl.window
+        bytes_enq0 = dl._stager.bytes_h2d if dl._stager is not None else 0
         t0 = time.perf_counter()
         with trace_range("bench.phase1"):  # roctx: lets tools/trace_idle.py find the timed region
             for _ in range(args.steps):
@@ -164,15 +235,37 @@ def main(argv=None) -> int:
                 acc.add(x)
             sync()
         t1 = time.perf_counter()
+        w_land1, b_land1 = _landed(dl)
+        bytes_enq1 = dl._stager.bytes_h2d if dl._stager is not None else 0
         barrier()
         elapsed = t1 - t0
-        if env.world_size > 1:
-            t = torch.tensor([elapsed], dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=env.control_group)
-            elapsed = float(t.item())
-        samples = args.batch * args.steps * env.world_size
-        value = samples / elapsed
+        landed_samples = (w_land1 - w_land0) * args.window
+        mine = {
+            "rank": env.rank,
+            "elapsed_s": elapsed,
+            "delivered_per_s": args.batch * args.steps / elapsed,
+            "landed_per_s": landed_samples / elapsed,
+            "h2d_bytes_timed": b_land1 - b_land0,
+            "h2d_gbps_timed": (b_land1 - b_land0) / elapsed / 1e9,
+            "h2d_enqueued_bytes_timed": bytes_enq1 - bytes_enq0,
+            "windows_prestaged_at_t0": max(0, w_land0 - w_cur0),
+            "numa_node": gpu_numa_node(env.local_rank) if dev.type == "cuda" else None,
+        }
         stats = dl.stats()
+        mine["stager_wait_producer_s"] = round(stats.get("stager_wait_producer_s", 0.0), 4)
+        mine["exchange_issue_wait_s"] = stats.get("exchange_issue_wait_s", 0.0)
+        mine["consumer_wait_s"] = round(stats["consumer_wait_s"], 4)
+        ex = getattr(dl, "_exchange_fn", None)
+        if ex is not None:
+            mine.update(ex.stats())
+        per_rank = [mine]
+        if env.world_size > 1:
+            per_rank = [None] * env.world_size
+            dist.all_gather_object(per_rank, mine, group=env.control_group)
+        elapsed = max(r["elapsed_s"] for r in per_rank)
+        delivered = args.batch * args.steps * env.world_size / elapsed
+        landed = sum(r["landed_per_s"] * r["elapsed_s"] for r in per_rank) / elapsed
+        value = min(delivered, landed) if landed > 0 else delivered
 
         # ---------------- phase 2: GPU idle % behind a fixed-cost train step
         idle = {}
@@ -186,9 +279,12 @@ def main(argv=None) -> int:
             traceback.print_exc()
             phase2_error, idle = repr(e)[:300], {}
         dl.close()
-
+        order = check_same_order(env.control_group) if env.world_size > 1 else None
 
         if env.rank == 0:
+            for r in per_rank:
+                for k in ("elapsed_s", "delivered_per_s", "landed_per_s", "h2d_gbps_timed"):
+                    r[k] = round(r[k], 4 if k != "delivered_per_s" and k != "landed_per_s" else 1)
             out = {
                 "metric": "samples/sec fed to GPU (synthetic 3x224x224 bf16)",
                 "value": round(value, 1),
@@ -212,8 +308,15 @@ def main(argv=None) -> int:
                     "prefetch_depth": args.depth,
                     "shuffle": args.shuffle,
                     "exchange_fraction": args.exchange,
+                    "exchange_method": args.exchange_method if args.exchange > 0 else None,
                     "source_dtype": args.source_dtype,
                 },
+                "delivered_samples_per_s": round(delivered, 1),
+                "landed_samples_per_s": round(landed, 1),
+                "h2d_bytes_timed": sum(r["h2d_bytes_timed"] for r in per_rank),
+                "h2d_gbps_timed": round(sum(r["h2d_bytes_timed"] for r in per_rank) / elapsed / 1e9, 3),
+                "sample_bytes": sample_bytes,
+                "windows_prestaged_at_t0": max(r["windows_prestaged_at_t0"] for r in per_rank),
                 "gpu_idle_pct": (None if not idle or math.isnan(idle["gpu_idle_pct"])
                                  else round(idle["gpu_idle_pct"], 3)),
                 "train_step": None if not idle else {
@@ -222,9 +325,8 @@ def main(argv=None) -> int:
                     "samples_per_s": round(idle["train_samples_per_s"], 1),
                     "busy_ms": round(idle["busy_ms"], 3), "wall_ms": round(idle["wall_ms"], 3)},
                 "phase2_error": phase2_error,
-                "loader": {"consumer_wait_s": round(stats["consumer_wait_s"], 4),
-                           "stager_wait_producer_s": round(stats.get("stager_wait_producer_s", 0.0), 4),
-                           "windows_staged": stats.get("windows_staged")},
+                "collective_order": order,
+                "per_rank": per_rank,
             }
             line = json.dumps(out)
             print(line, flush=True)

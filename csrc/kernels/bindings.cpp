@@ -239,6 +239,8 @@ PYBIND11_MODULE(_ddl_hip, m) {
       .def("error", &ddl::NativeStager::error)
       .def_property_readonly("bytes_h2d", &ddl::NativeStager::bytes_h2d)
       .def_property_readonly("windows_staged", &ddl::NativeStager::windows_staged)
+      .def_property_readonly("windows_landed", &ddl::NativeStager::windows_landed)
+      .def_property_readonly("bytes_landed", &ddl::NativeStager::bytes_landed)
       .def_property_readonly("wait_producer_s", &ddl::NativeStager::wait_producer_s);
 
   // --------------------------------------------------------------- kernels
@@ -381,7 +383,7 @@ PYBIND11_MODULE(_ddl_hip, m) {
         sp.position_ids = as_ptr<void>(position_ids);
         sp.pos_is_i64 = pos_is_i64 ? 1 : 0;
         sp.segment_ids = as_ptr<int32_t>(segment_ids);
-        sp.cu_seqlens_out = as_ptr<int64_t>(cu_seqlens_out);
+        sp.cu_seqlens_out = as_ptr<int32_t>(cu_seqlens_out);
         sp.rows = rows;
         sp.seq_len = seq_len;
         sp.pad_id = pad_id;

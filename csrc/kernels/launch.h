@@ -81,7 +81,7 @@ struct TokenSpec {
   uint8_t* attn_mask;
   void* position_ids;
   int32_t* segment_ids;        // pack mode only (or null)
-  int64_t* cu_seqlens_out;     // pack mode: copy of seg_offsets[0..n_seg] (or null)
+  int32_t* cu_seqlens_out;     // pack mode: int32 copy of seg_offsets[0..n_seg] (varlen-attention ABI; or null)
   int64_t rows;
   int64_t seq_len;
   int32_t pad_id;

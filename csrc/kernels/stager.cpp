@@ -21,12 +21,17 @@ double mono_s() {
 
 struct SlotRelease {
   std::atomic<uint32_t>* word;
+  std::atomic<uint64_t>* windows_landed;
+  std::atomic<uint64_t>* bytes_landed;
+  uint64_t bytes;
 };
 
 // Host callback on the copy stream: the DMA out of the slot retired, hand the
 // slot back to its producer (state store + futex wake of the producer).
 void release_slot_cb(void* p) {
   auto* r = static_cast<SlotRelease*>(p);
+  r->bytes_landed->fetch_add(r->bytes, std::memory_order_relaxed);
+  r->windows_landed->fetch_add(1, std::memory_order_release);
   r->word->store(kEmpty, std::memory_order_release);
   syscall(SYS_futex, reinterpret_cast<uint32_t*>(r->word), FUTEX_WAKE, INT32_MAX, nullptr, nullptr, 0);
   delete r;
@@ -134,7 +139,7 @@ void NativeStager::run() {
         hipMemcpyAsync(buffers_[b], arena_->slot_data(p, s), info.used_bytes, hipMemcpyHostToDevice, copy_stream_) !=
             hipSuccess)
       return fail(-1, static_cast<int32_t>(p), "hipMemcpyAsync H2D failed");
-    auto* req = new SlotRelease{&arena_->slot(p, s)->state};
+    auto* req = new SlotRelease{&arena_->slot(p, s)->state, &windows_landed_, &bytes_landed_, info.used_bytes};
     if (hipLaunchHostFunc(copy_stream_, release_slot_cb, req) != hipSuccess) {
       delete req;
       return fail(-1, static_cast<int32_t>(p), "hipLaunchHostFunc(release) failed");

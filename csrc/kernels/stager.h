@@ -75,6 +75,10 @@ class NativeStager {
   std::string error() const;
   uint64_t bytes_h2d() const { return bytes_h2d_.load(); }
   uint64_t windows_staged() const { return windows_staged_.load(); }
+  // Windows / bytes whose H2D copy has RETIRED (counted by the host callback that
+  // runs after the DMA): what has actually landed in HBM, as opposed to enqueued.
+  uint64_t windows_landed() const { return windows_landed_.load(); }
+  uint64_t bytes_landed() const { return bytes_landed_.load(); }
   double wait_producer_s() const { return wait_producer_ns_.load() * 1e-9; }
 
  private:
@@ -104,6 +108,7 @@ class NativeStager {
   int32_t error_producer_ = -1;
   std::string error_msg_;
   std::atomic<uint64_t> bytes_h2d_{0}, windows_staged_{0}, wait_producer_ns_{0};
+  std::atomic<uint64_t> windows_landed_{0}, bytes_landed_{0};
   std::thread thread_;
 };
 

@@ -120,7 +120,8 @@ __global__ void __launch_bounds__(kThreads) pad_pack_kernel(TokenSpec sp, int32_
   if (staged)
     for (int64_t i = threadIdx.x; i <= sp.n_seg; i += kThreads) seg_lds[i] = sp.seg_offsets[i];
   if (sp.cu_seqlens_out != nullptr && blockIdx.x == 0)  // owned copy of the sequence starts (cu_seqlens)
-    for (int64_t i = threadIdx.x; i <= sp.n_seg; i += kThreads) sp.cu_seqlens_out[i] = sp.seg_offsets[i];
+    for (int64_t i = threadIdx.x; i <= sp.n_seg; i += kThreads)
+      sp.cu_seqlens_out[i] = static_cast<int32_t>(sp.seg_offsets[i]);
   __syncthreads();
   if (p0 >= sp.seq_len) return;
   if (staged)

@@ -524,6 +524,20 @@ class DistributedDataLoader(DistributedDataloaderABC):
     def _advance_window(self) -> None:
         self._end_access_epoch()
         self._advance_to_next_producer()
+        self._begin_window()
+
+    def _begin_window(self) -> None:
+        """The cursor moved to a new window: issue its exchange collective now (consumer thread,
+        fixed point of the schedule, parallel/order.py) and start gathering its first batch."""
+        st = self._stager
+        if st is None or st.post_copy is None or self._finalized:
+            return
+        st.post(self.window)
+        if self._batch_stream is not None and (self.window, 0) not in self._lookahead:
+            sw = st.peek(self.window)
+            if sw is not None:
+                p, s = self._schedule(self.window)
+                self._lookahead[(self.window, 0)] = self._enqueue_batch(sw, p, s, 0)
 
     def _on_batch_end(self) -> None:
         if self._finalized:
@@ -563,6 +577,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
             self._finalize()
         else:
             self._update_len()
+            self._begin_window()
 
     def set_epoch(self, epoch: int) -> None:
         """torch-style hook; the order is driven by the internal cursor, so this only checks it."""

@@ -25,7 +25,12 @@ from ..ops import _dtypes
 
 
 class PointWiseData:
-    """Column groups [parameter | x | u | (sample weight)] (reference tests/run_ddl.py:20-77)."""
+    """Column groups [parameter | x | u | (sample weight)] (reference tests/run_ddl.py:20-77).
+
+    REFERENCE-PARITY FIXTURE: this class and ``DummyDataset`` deliberately reproduce
+    the reference harness's dataset (names, properties, normalisation and slice
+    arithmetic) so the CI workload (BASELINE config 1, ``examples/run_ddl.py``)
+    matches it sample for sample. It is test-fixture code, not loader logic."""
 
     def __init__(self, parameter_data, x_data, u_data, sample_weight=None):
         parts = [parameter_data, x_data, u_data] + ([sample_weight] if sample_weight is not None else [])

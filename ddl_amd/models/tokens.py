@@ -5,7 +5,15 @@ pack plan) -- so PCIe carries only real tokens (a padded [B, 4096] batch of
 sequences averaging 2k tokens would double the bytes); the consumer expands it
 on the GPU with the ``pad_pack_tokens`` gfx950 kernel into
 ``tokens [R, S]``, ``attention_mask [R, S]``, ``position_ids [R, S]`` (+
-``segment_ids`` / ``cu_seqlens`` in pack mode).
+``segment_ids`` / ``cu_seqlens`` / ``max_seqlen`` in pack mode).
+
+Pack-mode varlen metadata follows the varlen-attention ABI: ``cu_seqlens`` is
+int32 ``[n_seg + 1]`` and indexes the UNPADDED token stream
+``input_ids[attention_mask.bool()]`` (row-major; rows are packed in segment
+order and padded only at their ends), one entry per *segment*: a sequence
+longer than ``seq_len`` is split into ``seq_len`` chunks, each its own segment
+with its own position ids, and empty sequences have no segment.
+``max_seqlen`` is the longest segment (a Python int, from the producer).
 
 Sequence order is the world-size-invariant ``EpochOrder`` over sequences, so
 token batches share the indexed-mode checkpoint format.
@@ -110,6 +118,22 @@ def ffd_order(lengths: np.ndarray, seq_len: int) -> tuple[np.ndarray, int]:
     return order, int(n_rows)
 
 
+def in_order_rows(lengths: np.ndarray, seq_len: int) -> int:
+    """Rows that in-order packing (``pack_plan``) of sequences of these lengths produces:
+    over-long sequences become ``seq_len`` chunks, a row breaks where the next segment does not fit."""
+    S = int(seq_len)
+    rows, cur = 0, S  # cur = tokens in the open row (S: no open row)
+    for n in np.asarray(lengths, dtype=np.int64).tolist():
+        while n > 0:
+            seg = min(n, S)
+            if cur + seg > S:
+                rows += 1
+                cur = 0
+            cur += seg
+            n -= seg
+    return rows
+
+
 def ffd_order_py(lengths: np.ndarray, seq_len: int) -> tuple[np.ndarray, int]:
     """First-fit-decreasing bin packing of sequences into rows of ``seq_len`` tokens.
 
@@ -174,6 +198,9 @@ class TokenBatchProducer(ProducerFunctionSkeleton):
             raise ValueError("mode must be 'pad' or 'pack'")
         if pack_order not in ("in_order", "ffd"):
             raise ValueError("pack_order must be 'in_order' or 'ffd'")
+        if pack_order != "in_order" and mode != "pack":
+            raise ValueError(f"pack_order={pack_order!r} reorders rows of a PACKED batch; mode={mode!r} has "
+                             "one sequence per row")
         self.pack_order = pack_order
         self.source, self.global_batch, self.seq_len, self.mode, self.seed = source, global_batch, seq_len, mode, seed
         self.host_threads = host_threads
@@ -202,7 +229,10 @@ class TokenBatchProducer(ProducerFunctionSkeleton):
         if self.mode == "pack" and self.pack_order == "ffd":
             offs_all = self.source.offsets.tensor().view(-1).numpy()
             idx = np.asarray(idx, dtype=np.int64)
-            idx = idx[ffd_order(offs_all[idx + 1] - offs_all[idx], self.seq_len)[0]]
+            lens = offs_all[idx + 1] - offs_all[idx]
+            order, ffd_rows = ffd_order(lens, self.seq_len)
+            if ffd_rows < in_order_rows(lens, self.seq_len):  # FFD is a heuristic: keep it only if it wins
+                idx = idx[order]
         buf: torch.Tensor = kwargs["my_tensor"].view(-1)
         v = self.layout.views(buf)
         toks = self.source.tokens.tensor().view(-1)
@@ -213,13 +243,15 @@ class TokenBatchProducer(ProducerFunctionSkeleton):
         n_tokens = int(rt.gather_ragged(dst.data_ptr(), o.data_ptr(), toks.data_ptr(), offs.data_ptr(),
                                         self.source.n, np.ascontiguousarray(idx, np.int64), 4, dst.numel(),
                                         self.host_threads))
-        n_rows = n_seg = 0
+        n_rows = n_seg = max_seg = 0
         if self.mode == "pack":  # packing plan written straight into the window (native)
             cap = self.layout.max_segments
             n_rows, n_seg = rt.pack_plan(o.data_ptr(), len(idx), self.seq_len, v["row_start"].data_ptr(),
                                          v["row_end"].data_ptr(), cap, v["seg_offsets"].data_ptr(), cap)
+            if n_seg:
+                max_seg = int(np.diff(v["seg_offsets"][: n_seg + 1].numpy()).max())
         tok_off = self.layout.regions()["tokens"][0]
-        return {"tags": [n_tokens, n_rows, n_seg], "used_bytes": tok_off + 4 * n_tokens}
+        return {"tags": [n_tokens, n_rows, n_seg, max_seg], "used_bytes": tok_off + 4 * n_tokens}
 
 
 _VIEW_CACHE: dict = {}
@@ -245,6 +277,7 @@ def collate_token_window(buf: torch.Tensor, layout: TokenWindowLayout, mode: str
 
     v = _cached_views(buf.view(-1), layout)
     n_tokens, n_rows, n_seg = (int(x) for x in tags[:3])
+    max_seqlen = int(tags[3]) if len(tags) > 3 else 0
     tokens = v["tokens"][:n_tokens]
     if mode == "pad":
         ids, mask, pos = ops.pad_tokens(tokens, v["offsets"], layout.seq_len, pad_id)
@@ -254,20 +287,20 @@ def collate_token_window(buf: torch.Tensor, layout: TokenWindowLayout, mode: str
                                                   v["row_end"][:n_rows].numpy(), v["seg_offsets"][: n_seg + 1].numpy(),
                                                   layout.seq_len, pad_id)
         return {"input_ids": ids, "attention_mask": mask, "position_ids": pos, "segment_ids": seg,
-                "cu_seqlens": v["seg_offsets"][: n_seg + 1].clone()}
+                "cu_seqlens": v["seg_offsets"][: n_seg + 1].to(torch.int32), "max_seqlen": max_seqlen}
     dev = tokens.device
     s = layout.seq_len
-    # one allocation for all five outputs (8-byte-aligned regions: position_ids i64, cu_seqlens i64,
+    # one allocation for all five outputs (aligned regions: position_ids i64, cu_seqlens i32,
     # input_ids i32, segment_ids i32, attention_mask u8). cu_seqlens is written by the kernel into
     # memory of its own: a view of the staging buffer would be overwritten when it is re-staged
     n = n_rows * s
-    cu_n = -(-(n_seg + 1) // 2) * 2  # i64 count rounded so the i32 regions stay 16-byte aligned
-    whole = torch.empty(8 * n + 8 * cu_n + 4 * n + 4 * n + n, dtype=torch.uint8, device=dev)
+    cu_n = -(-(n_seg + 1) // 4) * 4  # i32 count rounded so the following regions stay 16-byte aligned
+    whole = torch.empty(8 * n + 4 * cu_n + 4 * n + 4 * n + n, dtype=torch.uint8, device=dev)
     o = 0
     pos = whole[o:o + 8 * n].view(torch.int64).view(n_rows, s)
     o += 8 * n
-    cu = whole[o:o + 8 * (n_seg + 1)].view(torch.int64)
-    o += 8 * cu_n
+    cu = whole[o:o + 4 * (n_seg + 1)].view(torch.int32)
+    o += 4 * cu_n
     ids = whole[o:o + 4 * n].view(torch.int32).view(n_rows, s)
     o += 4 * n
     seg = whole[o:o + 4 * n].view(torch.int32).view(n_rows, s)
@@ -275,6 +308,8 @@ def collate_token_window(buf: torch.Tensor, layout: TokenWindowLayout, mode: str
     mask = whole[o:o + n].view(n_rows, s)
     from ..ops.kernels import _stream_handle
 
+    if n_tokens > 0x7FFFFFFF:
+        raise ValueError(f"{n_tokens} tokens in one batch overflow int32 cu_seqlens")
     if n_rows == 0:
         cu.copy_(v["seg_offsets"][: n_seg + 1])
     else:
@@ -284,7 +319,8 @@ def collate_token_window(buf: torch.Tensor, layout: TokenWindowLayout, mode: str
             out_tokens=ids.data_ptr(), attn_mask=mask.data_ptr(), position_ids=pos.data_ptr(), pos_is_i64=True,
             segment_ids=seg.data_ptr(), cu_seqlens_out=cu.data_ptr(), rows=n_rows, seq_len=s, pad_id=pad_id, mode=1,
             stream=_stream_handle(None))
-    return {"input_ids": ids, "attention_mask": mask, "position_ids": pos, "segment_ids": seg, "cu_seqlens": cu}
+    return {"input_ids": ids, "attention_mask": mask, "position_ids": pos, "segment_ids": seg, "cu_seqlens": cu,
+            "max_seqlen": max_seqlen}
 
 
 def expected_tokens(source: SharedTokenSource, idx) -> list[np.ndarray]:

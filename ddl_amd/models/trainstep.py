@@ -60,6 +60,10 @@ class TrainStep:
                     self.model, device_ids=[dev.index] if dev.type == "cuda" else None,
                     process_group=process_group, bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True)
                 self.ddp = True
+                from ..parallel.order import LEDGER, ddp_ledger_hook
+
+                if LEDGER.enabled:  # record each bucket all-reduce at issue (collective-order check)
+                    self.model.register_comm_hook(None, ddp_ledger_hook(process_group))
         self.opt = torch.optim.SGD(self.model.parameters(), lr=lr)
         self.device = device
         self.dtype = dtype

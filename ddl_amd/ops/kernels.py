@@ -599,11 +599,11 @@ def pack_tokens(tokens: torch.Tensor, seq_offsets, seq_len: int, pad_id: int = 0
     """Pack a ragged token stream into rows of ``seq_len`` (varlen-attention layout).
 
     Returns (tokens [R,S] i32, mask [R,S] u8, position_ids [R,S], segment_ids [R,S] i32 (-1 = pad),
-    cu_seqlens [n_seg+1] i64).
+    cu_seqlens [n_seg+1] i32 over the unpadded stream ``tokens[mask.bool()]``).
     """
     rs, re_, so = pack_plan(np.asarray(seq_offsets.cpu() if torch.is_tensor(seq_offsets) else seq_offsets),
                             seq_len)
-    cu = torch.from_numpy(so)
+    cu = torch.from_numpy(so.astype(np.int32))
     if not tokens.is_cuda:
         return (*ref_pack_tokens(tokens, rs, re_, so, seq_len, pad_id, position_dtype), cu)
     dev = tokens.device
@@ -618,7 +618,7 @@ def pack_tokens(tokens: torch.Tensor, seq_offsets, seq_len: int, pad_id: int = 0
         seg_offsets=so_d.data_ptr(), n_seg=len(so) - 1, out_tokens=out.data_ptr(), attn_mask=mask.data_ptr(),
         position_ids=pos.data_ptr(), pos_is_i64=position_dtype == torch.int64, segment_ids=seg.data_ptr(),
         cu_seqlens_out=0, rows=r, seq_len=seq_len, pad_id=pad_id, mode=1, stream=_stream_handle(stream))
-    return out, mask, pos, seg, so_d
+    return out, mask, pos, seg, so_d.to(torch.int32)
 
 
 # ----------------------------------------------------------------- reductions

@@ -14,7 +14,9 @@ has been staged into HBM, on the prefetch stream, over RCCL/xGMI:
    identical formula on every rank, nothing communicated);
 2. the ``gather_rows`` HIP kernel packs them contiguously (Px evaluated
    inline, no index table);
-3. ``all_to_all_single`` on a dedicated loader process group (RCCL): an
+3. ``all_to_all_single`` on the DP process group (RCCL) -- the same group,
+   ncclComm and stream as the trainer's DDP all-reduce, so every collective of
+   the rank has one device-side order (``parallel/order.py``): an
    8-GPU MI355X node is fully connected by xGMI, and an all-to-all drives all 7
    links of every GPU at once, where the reference's 2-partner exchange
    drives 2 (SURVEY §5 "MI355X-native communication design");
@@ -37,6 +39,7 @@ from ..ops import _dtypes
 from ..permutation import FeistelPermutation
 from ..types import DDLEnv
 from ..utils.logging import logger
+from .order import LEDGER, loader_group
 
 _EXCHANGE_SALT = 0x5EED_C0DE
 
@@ -77,9 +80,9 @@ class GlobalShuffler:
         self.dtype = dtype
         self.seed = seed
         self.device = torch.device(device)
-        backend = "nccl" if self.device.type == "cuda" else "gloo"
-        # dedicated communicator: loader traffic never interleaves with the model's collectives
-        self.group = group if group is not None else dist.new_group(backend=backend)
+        # the DP group itself: one communicator (and one RCCL stream) for loader and trainer
+        # collectives, so their device order is the consumer thread's issue order (parallel/order.py)
+        self.group = group if group is not None else loader_group(env)
         if env.control_group is not None:
             # every rank must trade the same number of rows: agree on the smallest window
             t = torch.tensor([n_rows], dtype=torch.int64)
@@ -89,6 +92,9 @@ class GlobalShuffler:
         self.n_exchange = self._n_exchange()
         self.calls = 0
         self.bytes_sent = 0
+        self.host_s = 0.0
+        self._timing: list = []  # (start, end) device events of the exchanges, resolved by stats()
+        self._device_ms = 0.0
 
     def _n_exchange(self) -> int:
         return int(self.n_rows * self.fraction)
@@ -100,7 +106,35 @@ class GlobalShuffler:
         return win_bytes.view(self.dtype).view((-1,) + self.sample_shape)[: self.n_rows]
 
     def __call__(self, win_bytes: torch.Tensor, window: int, info: dict | None = None) -> None:
+        import time
+
+        if self.n_exchange == 0:
+            return
+        LEDGER.record("loader.exchange", window)
+        t0 = time.perf_counter()
+        ev = None
+        if self.device.type == "cuda":
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         self.global_shuffle(win_bytes, window)
+        if ev is not None:
+            ev[1].record()
+            self._timing.append(ev)
+            if len(self._timing) > 64:
+                self._resolve()
+        self.host_s += time.perf_counter() - t0
+
+    def _resolve(self) -> None:
+        for a, b in self._timing:
+            b.synchronize()
+            self._device_ms += a.elapsed_time(b)
+        self._timing.clear()
+
+    def stats(self) -> dict:
+        """Exchange counters: calls, bytes sent to peers, host issue time, device time (ms)."""
+        self._resolve()
+        return {"exchange_calls": self.calls, "rccl_bytes": self.bytes_sent,
+                "exchange_ms": round(self._device_ms, 3), "exchange_host_s": round(self.host_s, 4)}
 
     def global_shuffle(self, win_bytes: torch.Tensor, window: int) -> None:  # pragma: no cover - abstract
         raise NotImplementedError

@@ -48,6 +48,7 @@ import torch
 
 from . import _native, ops
 from .ops import _dtypes
+from .parallel.order import LEDGER, loader_group
 from .permutation import EpochOrder
 from .types import DDLEnv
 from .utils.logging import logger
@@ -252,8 +253,8 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
         self._init_cursor(seed, depth, n_epochs, resume_state)
         self.group = None
         if self.W > 1:
-            backend = "nccl" if self.device.type == "cuda" else "gloo"
-            self.group = dist.new_group(backend=backend)
+            # the DP group: one communicator / RCCL stream with the trainer's DDP (parallel/order.py)
+            self.group = loader_group(self.env)
         self.bytes_exchanged = 0
         t0 = time.perf_counter()
         if scatter_from is not None and self.W > 1:
@@ -388,6 +389,7 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
                 send = ops.gather_rows(self.shard, index=self._to_dev(send_rows)) if len(send_rows) else \
                     torch.empty((0,) + self.sample_shape, dtype=self.src_dtype, device=self.device)
                 recv = torch.empty((self.LB,) + self.sample_shape, dtype=self.src_dtype, device=self.device)
+                LEDGER.record("resident.all_to_all", t)
                 dist.all_to_all_single(recv.view(self.LB, -1), send.view(send.shape[0], -1), recv_counts,
                                        send_counts, group=self.group)
                 self.bytes_exchanged += (len(send_rows) - send_counts[self.rank]) * self.row_bytes

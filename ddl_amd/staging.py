@@ -26,12 +26,13 @@ ddl/connection.py:89-92). This is the MI355X-native replacement of that gap
 
 HBM is plentiful on MI355X (288 GB): windows are staged whole, ``depth``
 windows deep (default 2 = double buffering against the training step), plus
-one ring buffer for the exchange lookahead when the exchange is on.
+two ring buffers for the exchange lookahead when the exchange is on.
 """
 
 from __future__ import annotations
 
 import dataclasses
+import time
 from typing import Callable
 
 import torch
@@ -84,10 +85,10 @@ class WindowStager:
         # w+1's DMA instead of idling the copy engine.
         self.copy_stream = torch.cuda.Stream(device=self.device)
         self.stream = torch.cuda.Stream(device=self.device) if post_copy is not None else self.copy_stream
-        # The consumer posts window w+1's exchange when it starts window w, which needs w+1 staged:
-        # that lookahead holds one ring buffer, so give it its own. With `depth` buffers the copy of
-        # w+2 would wait for the consumer to finish w and the DMA engine would idle for the
-        # consumer's share of every window.
+        # The consumer posts window w+1's exchange when it hands window w back (the fixed,
+        # rank-identical issue point of the collective, parallel/order.py), and the first batch of
+        # w+1 is gathered right behind it: one ring buffer holds that posted window, so give it its
+        # own and keep `depth` windows of DMA in flight behind it.
         n_buf = depth + 1 if post_copy is not None and depth >= 2 else depth
         self.buffers = [torch.empty(max_window_bytes, dtype=torch.uint8, device=self.device) for _ in range(n_buf)]
         self.ready_events = [torch.cuda.Event() for _ in range(n_buf)]
@@ -98,6 +99,8 @@ class WindowStager:
         self._staged: dict[int, StagedWindow] = {}
         self._posted: set[int] = set()
         self._closed = False
+        self._n_released = 0
+        self.post_wait_s = 0.0  # host time blocked at a collective issue point waiting for its window
         self._native = hip.NativeStager(
             arena=connection.arena.address, n_producers=connection.n_producers, n_slots=n_slots,
             first=first_window, total=total_windows, buffers=[b.data_ptr() for b in self.buffers],
@@ -120,9 +123,7 @@ class WindowStager:
     def get(self, w: int) -> StagedWindow:
         """Window ``w`` staged in HBM; the current stream is made to wait for it (device-side)."""
         if self.post_copy is not None:
-            self._post(w)
-            if self.depth >= 2 and w + 1 < self.first + self.total:
-                self._post(w + 1)  # one window ahead, in lockstep on every rank
+            self._post(w)  # normally already posted by post() at the previous window's hand-back
         sw = self._wait_staged(w)
         streams.current(self.device.index).wait_event(self.ready_events[sw.buffer])
         return sw
@@ -138,10 +139,18 @@ class WindowStager:
         info = self._native.peek(w)
         return None if info is None else self._wrap(info)
 
+    def post(self, w: int) -> None:
+        """Issue window ``w``'s post-copy work (the exchange collective) now, from the consumer
+        thread; waits on the host until ``w`` is staged. A no-op without post-copy work."""
+        if self.post_copy is not None and w < self.first + self.total:
+            self._post(w)
+
     def _post(self, w: int) -> None:
         if w in self._posted:
             return
+        t0 = time.perf_counter()
         sw = self._wait_staged(w)
+        self.post_wait_s += time.perf_counter() - t0
         self.stream.wait_event(self._copy_done[sw.buffer])
         with streams.on_stream(self.stream), trace_range("ddl.stage.post_copy"):
             self.post_copy(sw.data, w, {"seq": sw.seq, "used_bytes": sw.nbytes, "tag": list(sw.tags)})
@@ -178,6 +187,7 @@ class WindowStager:
         if sw is None:
             return
         self._posted.discard(w)
+        self._n_released += 1
         ev = torch.cuda.Event()
         ev.record(stream if stream is not None else streams.current(self.device.index))
         refs = self._free_refs[sw.buffer]
@@ -199,8 +209,25 @@ class WindowStager:
 
     @property
     def windows_staged(self) -> int:
+        """Windows whose H2D copy has been enqueued."""
         return int(self._native.windows_staged)
+
+    @property
+    def windows_landed(self) -> int:
+        """Windows whose H2D copy has retired (the data is in HBM)."""
+        return int(self._native.windows_landed)
+
+    @property
+    def bytes_landed(self) -> int:
+        return int(self._native.bytes_landed)
+
+    @property
+    def windows_released(self) -> int:
+        """Windows the consumer has handed back (fully consumed)."""
+        return self._n_released
 
     def stats(self) -> dict:
         return {"bytes_h2d": self.bytes_h2d, "windows_staged": self.windows_staged,
-                "stager_wait_producer_s": float(self._native.wait_producer_s)}
+                "windows_landed": self.windows_landed, "bytes_landed": self.bytes_landed,
+                "stager_wait_producer_s": float(self._native.wait_producer_s),
+                "exchange_issue_wait_s": round(self.post_wait_s, 6)}

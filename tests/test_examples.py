@@ -61,24 +61,46 @@ def test_bench_contract_two_ranks_torchrun():
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("method", ["alltoall", "sendrecv_replace"])
-def test_bench_eight_ranks_torchrun(method):
-    """The driver's N=8 launch rehearsed on CPU/gloo: 8 ranks x 3 producers, a window exchange every
-    4 batches in both exchange methods, then 8-rank DDP. Checks that every rank issues the loader's
-    collectives and the DDP all-reduces in an order that completes (no cross-rank deadlock)."""
+@pytest.mark.parametrize("method,launch", [("alltoall", "torchrun"), ("sendrecv_replace", "self")])
+def test_bench_eight_ranks(method, launch):
+    """The driver's N=8 run rehearsed on CPU/gloo: 8 ranks x 3 producers, a window exchange every
+    4 batches in both exchange methods, then 8-rank DDP. Launched by torchrun (the driver's line) and
+    by ``python bench.py --gpus 8`` alone (bench.py spawns the ranks itself). Checks that every rank
+    issues the loader's exchanges and the DDP all-reduces in the same order (collective ledger
+    digests compared across ranks) and that the run completes (no cross-rank deadlock)."""
     import json
 
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
-           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(REPO, "bench.py"),
-           "--gpus", "8", "--steps", "12", "--warmup", "2", "--window", "64", "--batch", "16", "--idle-steps", "3",
-           "--model-dim", "64", "--model-depth", "1", "--exchange-method", method]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=dict(_env(), DDL_DEVICE="cpu"))
+    args = [os.path.join(REPO, "bench.py"), "--gpus", "8", "--steps", "12", "--warmup", "2", "--window", "64",
+            "--batch", "16", "--idle-steps", "3", "--model-dim", "64", "--model-depth", "1",
+            "--exchange-method", method]
+    if launch == "torchrun":
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+               "--master-addr", "127.0.0.1", "--master-port", str(free_port()), *args]
+        env = dict(_env(), DDL_DEVICE="cpu")
+    else:
+        cmd = [sys.executable, *args]
+        env = {k: v for k, v in _env().items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+        env["DDL_DEVICE"] = "cpu"
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1
     out = json.loads(lines[0])
     assert out["n_gpus"] == 8 and out["config"]["parallelism"] == "dp8" and out["config"]["global_batch"] == 128
     assert out["config"]["exchange_fraction"] == 0.5 and out["value"] > 0
+    order = out["collective_order"]
+    assert order["same_order"] is True
+    assert order["by_kind"]["loader.exchange"] >= 4 and order["by_kind"]["ddp.allreduce"] >= 4
+    assert len(out["per_rank"]) == 8 and all(r_["exchange_calls"] >= 3 for r_ in out["per_rank"])
+
+
+@pytest.mark.timeout(60)
+def test_bench_refuses_world_size_mismatch():
+    """--gpus N under a launcher with a different WORLD_SIZE exits non-zero instead of running 1 rank."""
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "8"], capture_output=True,
+                       text=True, timeout=50, env=dict(_env(), WORLD_SIZE="1", RANK="0", DDL_DEVICE="cpu"))
+    assert r.returncode == 2 and "refusing" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
 
 
 @pytest.mark.timeout(200)

@@ -188,7 +188,7 @@ def test_pack_tokens_many_short_sequences():
     out = ops.pack_tokens(toks.to(_dev()), offs, 4096, pad_id=3)
     for a, b in zip(out[:4], ref):
         assert torch.equal(a.cpu(), b)
-    assert torch.equal(out[4].cpu(), torch.from_numpy(so))
+    assert torch.equal(out[4].cpu(), torch.from_numpy(so.astype(np.int32)))
 
 
 @pytest.mark.parametrize("nbytes", [4, 1000, 4096 * 77 + 12, 256 * 3 * 224 * 224 * 2])

@@ -84,3 +84,11 @@ def test_lint(path: Path):
             if (node.arg == "weights_only" and bad is False) or (node.arg == "allow_pickle" and bad is True):
                 problems.append(f"{node.arg}={bad} at line {node.value.lineno}")
     assert not problems, f"{path.relative_to(ROOT)}: {problems}"
+
+
+def test_license_file():
+    """The package declares LGPL-2.1-or-later (pyproject, CITATION.cff) and ships the license text."""
+    text = (ROOT / "LICENSE").read_text()
+    assert text.lstrip().startswith("GNU LESSER GENERAL PUBLIC LICENSE") and "Version 2.1" in text[:200]
+    assert "LGPL-2.1" in (ROOT / "pyproject.toml").read_text()
+    assert "LGPL-2.1" in (ROOT / "CITATION.cff").read_text()

@@ -72,6 +72,7 @@ def test_token_batches_gpu(corpus, mode):
                     lens = [len(x) for x in expected_tokens(corpus, idx)]
                     held = (batch["cu_seqlens"], ops.pack_plan(np.concatenate([[0], np.cumsum(lens)]), seq_len)[2])
         if held is not None:  # cu_seqlens is owned: still intact after the staging buffers were reused
+            assert held[0].dtype == torch.int32
             assert np.array_equal(held[0].cpu().numpy(), held[1])
 
 
@@ -163,8 +164,9 @@ def test_ffd_order_native_matches_numpy_reference():
 
 
 def test_token_batches_ffd_pack_order(corpus, monkeypatch):
-    """pack_order="ffd": the same sequences per batch, in first-fit-decreasing order, packed into no more rows."""
-    from ddl_amd.models.tokens import ffd_order
+    """pack_order="ffd": the same sequences per batch, in first-fit-decreasing order when that packs into
+    fewer rows than the batch's own order (else the batch's order) -- so never more rows, batch by batch."""
+    from ddl_amd.models.tokens import ffd_order, in_order_rows
 
     monkeypatch.setenv("DDL_DEVICE", "cpu")
     seq_len, gb = 256, 16
@@ -178,9 +180,78 @@ def test_token_batches_ffd_pack_order(corpus, monkeypatch):
             rows[po] = 0
             for g, batch in enumerate(dl):
                 seqs = expected_tokens(corpus, order.indices(0, g))
+                lens = np.array([len(x) for x in seqs])
+                n_in = in_order_rows(lens, seq_len)
                 if po == "ffd":
-                    seqs = [seqs[i] for i in ffd_order(np.array([len(x) for x in seqs]), seq_len)[0]]
+                    o, n_ffd = ffd_order(lens, seq_len)
+                    if n_ffd < n_in:
+                        seqs = [seqs[i] for i in o]
                 flat = batch["input_ids"][batch["attention_mask"].bool()].numpy()
                 assert np.array_equal(flat, np.concatenate(seqs))  # every token once, in the packing order
+                assert batch["input_ids"].shape[0] <= n_in
                 rows[po] += batch["input_ids"].shape[0]
     assert rows["ffd"] <= rows["in_order"]
+
+
+def test_ffd_never_packs_into_more_rows():
+    """FFD is a heuristic: S=10, lengths [5,3,2,4,3,3] pack in order into 2 rows, FFD needs 3.
+    The producer keeps the batch's own order then."""
+    from ddl_amd.models.tokens import ffd_order, ffd_order_py, in_order_rows
+
+    lens = np.array([5, 3, 2, 4, 3, 3])
+    assert in_order_rows(lens, 10) == 2 == len(ops.pack_plan(np.concatenate([[0], np.cumsum(lens)]), 10)[0])
+    assert ffd_order(lens, 10)[1] == 3 == ffd_order_py(lens, 10)[1]
+    rng = np.random.default_rng(5)
+    for _ in range(200):  # in_order_rows equals the native planner's row count
+        S = int(rng.choice([1, 7, 100]))
+        ln = rng.integers(0, 3 * S + 1, size=int(rng.integers(0, 40)))
+        assert in_order_rows(ln, S) == len(ops.pack_plan(np.concatenate([[0], np.cumsum(ln)]), S)[0])
+
+
+def test_ffd_requires_pack_mode(corpus):
+    with pytest.raises(ValueError, match="pack_order"):
+        TokenBatchProducer(corpus, 16, 256, "pad", pack_order="ffd")
+
+
+def _attention(x, causal=True):
+    """softmax(x x^T / sqrt(d)) x for one sequence [L, d] (q = k = v = x), fp32."""
+    s = x @ x.T / x.shape[1] ** 0.5
+    if causal:
+        s = s.masked_fill(torch.triu(torch.ones_like(s, dtype=torch.bool), 1), float("-inf"))
+    return torch.softmax(s, dim=-1) @ x
+
+
+def _varlen_attention(x, cu):
+    """Reference varlen attention over a packed stream [T, d]: block-diagonal causal attention
+    between cu_seqlens boundaries (the flash-attn varlen semantics, in plain PyTorch)."""
+    T = x.shape[0]
+    seg = torch.bucketize(torch.arange(T), cu[1:].long(), right=True)
+    s = x @ x.T / x.shape[1] ** 0.5
+    allowed = (seg[:, None] == seg[None, :]) & ~torch.triu(torch.ones(T, T, dtype=torch.bool), 1)
+    return torch.softmax(s.masked_fill(~allowed, float("-inf")), dim=-1) @ x
+
+
+def test_cu_seqlens_drive_varlen_attention(corpus, monkeypatch):
+    """Pack mode: int32 cu_seqlens over input_ids[attention_mask.bool()] drive a varlen attention that
+    equals attention computed per segment (seq_len chunks of each sequence) -- over-long sequences
+    included (max_len 300 > seq_len 128); max_seqlen is the longest segment."""
+    monkeypatch.setenv("DDL_DEVICE", "cpu")
+    seq_len, gb = 128, 8
+    order = EpochOrder(corpus.n, gb, 4)
+    emb = torch.randn(50257, 16, generator=torch.Generator().manual_seed(0))
+    with ddl_amd.start(n_producers=1) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(corpus, gb, seq_len, "pack"), gb, conn, 1,
+                                           mode="indexed", env=env, auto_mark=True, collate="tokens", seed=4)
+        for g, batch in enumerate(dl):
+            if g == 3:
+                break
+            cu = batch["cu_seqlens"]
+            assert cu.dtype == torch.int32
+            stream = batch["input_ids"][batch["attention_mask"].bool()].long()
+            segs = [c for s in expected_tokens(corpus, order.indices(0, g))
+                    for c in (s[i:i + seq_len] for i in range(0, len(s), seq_len)) if len(c)]
+            assert cu.tolist() == np.concatenate([[0], np.cumsum([len(c) for c in segs])]).tolist()
+            assert batch["max_seqlen"] == max(len(c) for c in segs)
+            got = _varlen_attention(emb[stream], cu)
+            want = torch.cat([_attention(emb[torch.from_numpy(c.astype(np.int64))]) for c in segs])
+            torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-4)
