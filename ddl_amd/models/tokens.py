@@ -14,6 +14,7 @@ order and padded only at their ends), one entry per *segment*: a sequence
 longer than ``seq_len`` is split into ``seq_len`` chunks, each its own segment
 with its own position ids, and empty sequences have no segment.
 ``max_seqlen`` is the longest segment (a Python int, from the producer).
+Every batch also carries ``n_tokens``: the real tokens shipped for it.
 
 Sequence order is the world-size-invariant ``EpochOrder`` over sequences, so
 token batches share the indexed-mode checkpoint format.
@@ -281,13 +282,15 @@ def collate_token_window(buf: torch.Tensor, layout: TokenWindowLayout, mode: str
     tokens = v["tokens"][:n_tokens]
     if mode == "pad":
         ids, mask, pos = ops.pad_tokens(tokens, v["offsets"], layout.seq_len, pad_id)
-        return {"input_ids": ids, "attention_mask": mask, "position_ids": pos}
+        # n_tokens: tokens shipped (pad mode truncates sequences longer than seq_len: mask.sum() can be less)
+        return {"input_ids": ids, "attention_mask": mask, "position_ids": pos, "n_tokens": n_tokens}
     if not tokens.is_cuda:
         ids, mask, pos, seg = ops.ref_pack_tokens(tokens, v["row_start"][:n_rows].numpy(),
                                                   v["row_end"][:n_rows].numpy(), v["seg_offsets"][: n_seg + 1].numpy(),
                                                   layout.seq_len, pad_id)
         return {"input_ids": ids, "attention_mask": mask, "position_ids": pos, "segment_ids": seg,
-                "cu_seqlens": v["seg_offsets"][: n_seg + 1].to(torch.int32), "max_seqlen": max_seqlen}
+                "cu_seqlens": v["seg_offsets"][: n_seg + 1].to(torch.int32), "max_seqlen": max_seqlen,
+                "n_tokens": n_tokens}
     dev = tokens.device
     s = layout.seq_len
     # one allocation for all five outputs (aligned regions: position_ids i64, cu_seqlens i32,
@@ -320,7 +323,7 @@ def collate_token_window(buf: torch.Tensor, layout: TokenWindowLayout, mode: str
             segment_ids=seg.data_ptr(), cu_seqlens_out=cu.data_ptr(), rows=n_rows, seq_len=s, pad_id=pad_id, mode=1,
             stream=_stream_handle(None))
     return {"input_ids": ids, "attention_mask": mask, "position_ids": pos, "segment_ids": seg, "cu_seqlens": cu,
-            "max_seqlen": max_seqlen}
+            "max_seqlen": max_seqlen, "n_tokens": n_tokens}
 
 
 def expected_tokens(source: SharedTokenSource, idx) -> list[np.ndarray]:

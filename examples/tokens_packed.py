@@ -11,9 +11,10 @@ and ship them RAGGED, so only real tokens cross PCIe. The consumer expands a
 batch on the GPU with the pad/pack kernel:
 
 * ``pack``: sequences packed into rows of ``seq_len`` by first-fit decreasing
-  (``pack_order="ffd"``, ~95% dense; long ones split).
+  (``pack_order="ffd"``, ~93% dense measured; long ones split).
   Returns ``input_ids``, ``attention_mask``, ``position_ids`` (restarting per
-  sequence), ``segment_ids`` and ``cu_seqlens`` (for varlen attention).
+  sequence), ``segment_ids``, int32 ``cu_seqlens`` over ``input_ids[attention_mask.bool()]`` and
+  ``max_seqlen`` (the varlen-attention inputs; one entry per segment).
 * ``pad``: one sequence per row, padded with ``pad_id``.
 
 ``state_dict()`` is the indexed-kind cursor (seed, epoch, global batch), so a
@@ -60,7 +61,10 @@ def main() -> None:
                     real += int(b["attention_mask"].sum())
                     rows += b["input_ids"].shape[0]
                 if env.rank == 0:
-                    extra = f", {b['cu_seqlens'].numel() - 1} sequences in the last batch" if a.mode == "pack" else ""
+                    # cu_seqlens has one entry per SEGMENT: over-long sequences are split into seq_len chunks
+                    # and empty sequences have none, so this is not the sequence count
+                    extra = (f", {b['cu_seqlens'].numel() - 1} segments (max {b['max_seqlen']} tokens) in the "
+                             "last batch" if a.mode == "pack" else "")
                     print(f"epoch {epoch}: {rows} rows x {a.seq_len} on rank 0, {real} real tokens "
                           f"({100.0 * real / max(rows * a.seq_len, 1):.1f}% dense){extra}; keys {sorted(b)}",
                           flush=True)

@@ -47,7 +47,7 @@ def test_token_batches_cpu(corpus, mode, monkeypatch):
                     assert np.array_equal(flat.numpy(), ref)  # every token exactly once, in order
                     assert batch["input_ids"].shape[1] == seq_len
                     cu = batch["cu_seqlens"]
-                    assert int(cu[-1]) == len(ref)
+                    assert int(cu[-1]) == len(ref) == batch["n_tokens"] == int(batch["attention_mask"].sum())
 
 
 @pytest.mark.gpu
