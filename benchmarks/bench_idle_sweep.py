@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""GPU idle % under loader pressure: a calibrated step swept across the feed rate.
+
+``bench.py``'s phase 2 measures idle % behind a PatchMLP step that runs ~4x
+slower than the feed, which says nothing about overlap when the loader is the
+bottleneck. Here:
+
+1. phase 1 measures the loader's feed rate ``F`` (samples/s; the consumer only
+   checksums every delivered byte), as in ``bench.py``;
+2. for each ratio ``r`` a ``CalibratedStep`` (batch read + a bf16 GEMM chain
+   sized on this GPU) is built whose step capacity is ``C = r * F``, i.e. a
+   GPU step time of ``B / (r * F)``; the loop runs it on the loader's batches
+   and measures the compute stream's idle % with HIP events
+   (``ComputeIdleMeter``) and the achieved samples/s.
+
+If the loader overlaps perfectly, a step FASTER than the feed (``r > 1``) is
+starved exactly by the missing feed: ``idle = 1 - F / C_measured`` where
+``C_measured = B / (busy per step)``; a step slower than the feed (``r <= 1``)
+never waits: ``idle = 0``. So the prediction is ``max(0, 1 - F / C_measured)``
+and each point reports it next to the measurement. Every point is bracketed
+by a roctx range ``sweep.pNN`` so ``tools/trace_idle.py --names`` can
+cross-check it from a rocprofv3 kernel trace.
+
+Families: ``images`` (config 2: 3x224x224, bf16 source or ``--source-dtype
+uint8`` cast + normalised on the device) and ``tokens`` (config 4: seq_len
+4096, ragged H2D + on-device pack). One GPU; prints one JSON line per point
+and a summary line.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+RATIOS = (0.5, 0.75, 0.9, 1.0, 1.1, 1.25, 1.5, 2.0)
+
+
+def _parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--family", default="images", choices=["images", "tokens"])
+    ap.add_argument("--source-dtype", default="bfloat16", choices=["bfloat16", "uint8"])
+    ap.add_argument("--ratios", default=",".join(str(r) for r in RATIOS))
+    ap.add_argument("--feed-steps", type=int, default=300)
+    ap.add_argument("--steps", type=int, default=150, help="timed steps per sweep point")
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=None,
+                    help="images: 256 samples; tokens: 2048 sequences (a GPU step long enough to dominate the "
+                         "per-batch host cost)")
+    ap.add_argument("--window", type=int, default=256)
+    ap.add_argument("--producers", type=int, default=None)
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args(argv)
+
+
+def _image_loader(a, env, conn, n_steps):
+    import torch
+
+    import ddl_amd
+    from ddl_amd import Marker
+    from ddl_amd.models.producers import ImageWindowProducer
+
+    B = a.batch or 256
+    norm = None
+    if a.source_dtype == "uint8":
+        norm = {"mean": [0.485, 0.456, 0.406], "std": [0.229, 0.224, 0.225], "layout": "chw"}
+    n_epochs = math.ceil(n_steps / max(1, a.window // B)) + 2
+    dl = ddl_amd.DistributedDataLoader(
+        ImageWindowProducer(a.window, (3, 224, 224), a.source_dtype, refill="stamp"), B, conn, n_epochs,
+        env=env, device=torch.device(env.device), out_dtype=torch.bfloat16, shuffle="device", normalize=norm)
+
+    def gen():
+        while True:
+            for i in range(len(dl)):
+                yield dl[i]
+                dl.mark(Marker.END_OF_BATCH)
+            dl.mark(Marker.END_OF_EPOCH)
+
+    return dl, gen(), B, "samples"
+
+
+def _token_loader(a, env, conn, n_steps, src):
+    import ddl_amd
+    from ddl_amd.models.tokens import TokenBatchProducer
+
+    B = a.batch or 2048
+    n_epochs = n_steps // (src.n // B) + 2
+    dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(src, B, 4096, "pack", pack_order="ffd"), B, conn,
+                                       n_epochs, mode="indexed", env=env, collate="tokens", auto_mark=True)
+
+    def gen():
+        while True:
+            yield from dl
+
+    return dl, gen(), B, "sequences"
+
+
+def main(argv=None) -> int:
+    a = _parse(argv)
+    import torch
+
+    import ddl_amd
+    from ddl_amd import ops
+    from ddl_amd.models.trainstep import CalibratedStep
+    from ddl_amd.utils.tracing import ComputeIdleMeter, trace_range
+
+    ratios = [float(x) for x in a.ratios.split(",") if x]
+    n_steps = a.warmup + a.feed_steps + len(ratios) * (a.steps + a.warmup + 30)
+    src = None
+    if a.family == "tokens":
+        from ddl_amd.models.tokens import SharedTokenSource
+
+        src = SharedTokenSource.synthetic(f"ddl_amd_sweep_{os.getpid()}", 8192, 256, 4096, seed=1)
+    producers = a.producers or (3 if a.family == "images" else 4)
+    points = []
+    try:
+        with ddl_amd.start(n_producers=producers) as (env, conn):
+            if a.family == "images":
+                dl, it, B, unit = _image_loader(a, env, conn, n_steps)
+            else:
+                dl, it, B, unit = _token_loader(a, env, conn, n_steps, src)
+            dev = torch.device(env.device)
+            acc = ops.ChecksumAccumulator(dev)
+
+            def read(batch):
+                for t in (batch.values() if isinstance(batch, dict) else batch):
+                    if isinstance(t, torch.Tensor):
+                        acc.add(t)
+
+            # ---- phase 1: feed rate F
+            for _ in range(a.warmup):
+                read(next(it))
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            with trace_range("sweep.feed"):
+                for _ in range(a.feed_steps):
+                    read(next(it))
+                torch.cuda.synchronize()
+            feed = B * a.feed_steps / (time.perf_counter() - t0)
+            print(json.dumps({"family": a.family, "feed_per_s": round(feed, 1), "unit": unit}), flush=True)
+
+            # ---- sweep
+            for i, r in enumerate(ratios):
+                step = CalibratedStep(dev, step_ms=1000.0 * B / (r * feed))
+                step.calibrate(next(it))
+                for _ in range(a.warmup):
+                    step(next(it))
+                meter = ComputeIdleMeter()
+                torch.cuda.synchronize()
+                t2 = time.perf_counter()
+                with trace_range(f"sweep.p{i:02d}"):
+                    for _ in range(a.steps):
+                        batch = next(it)
+                        meter.step_begin()
+                        step(batch)
+                        meter.step_end()
+                    torch.cuda.synchronize()
+                t3 = time.perf_counter()
+                res = meter.result()
+                busy_per_step = res["busy_ms"] / max(1, res["steps"])
+                cap = 1000.0 * B / busy_per_step  # measured step capacity C
+                pred = 100.0 * max(0.0, 1.0 - feed / cap)
+                pt = {"point": f"sweep.p{i:02d}", "ratio_target": r, "step_ms_target": round(step.step_ms, 4),
+                      "gemm_reps": step.reps, "gemm_rows": step.a.shape[0], "busy_ms_per_step": round(busy_per_step, 4),
+                      "step_capacity_per_s": round(cap, 1), "ratio_measured": round(cap / feed, 3),
+                      "achieved_per_s": round(B * a.steps / (t3 - t2), 1),
+                      "gpu_idle_pct": round(res["gpu_idle_pct"], 3), "predicted_idle_pct": round(pred, 3),
+                      "error_pp": round(res["gpu_idle_pct"] - pred, 3)}
+                points.append(pt)
+                print(json.dumps(pt), flush=True)
+            stats = dl.stats()
+            dl.close()
+    finally:
+        if src is not None:
+            src.close()
+    summary = {"metric": f"GPU idle % vs step rate / feed rate ({a.family}, {a.source_dtype if a.family == 'images' else 'int32 tokens'})",
+               "feed_per_s": round(feed, 1), "unit": unit, "batch": B, "points": len(points),
+               "max_abs_error_pp": round(max(abs(p["error_pp"]) for p in points), 3) if points else None,
+               "consumer_wait_s": round(stats.get("consumer_wait_s", 0.0), 3)}
+    print(json.dumps(summary), flush=True)
+    if a.json_out:
+        with open(a.json_out, "w") as f:
+            for p in points:
+                f.write(json.dumps(p) + "\n")
+            f.write(json.dumps(summary) + "\n")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -395,6 +395,14 @@ PYBIND11_MODULE(_ddl_hip, m) {
       py::arg("segment_ids"), py::arg("cu_seqlens_out"), py::arg("rows"), py::arg("seq_len"), py::arg("pad_id"),
       py::arg("mode"), py::arg("stream"));
   m.def(
+      "stream_copy",
+      [](uintptr_t src, uintptr_t dst, int64_t bytes, int blocks, uintptr_t stream) {
+        check_rc(ddl::stream_copy(as_ptr<const void>(src), as_ptr<void>(dst), bytes, blocks,
+                                  reinterpret_cast<hipStream_t>(stream)),
+                 "stream_copy");
+      },
+      py::arg("src"), py::arg("dst"), py::arg("bytes"), py::arg("blocks"), py::arg("stream"));
+  m.def(
       "checksum_words",
       [](uintptr_t ptr, int64_t bytes, uintptr_t out, uintptr_t scratch, int64_t scratch_len, uintptr_t stream) {
         check_rc(ddl::checksum_words(as_ptr<const void>(ptr), bytes, as_ptr<uint64_t>(out), as_ptr<uint64_t>(scratch),

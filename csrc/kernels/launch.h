@@ -96,6 +96,8 @@ int pad_pack_tokens(const TokenSpec& spec, hipStream_t st);
 // stages through `scratch` (>= kChecksumMaxBlocks u64). Debug batch checksums
 // and the bench consumer step.
 constexpr int64_t kChecksumMaxBlocks = 1024;
+// Streaming 16 B copy (bandwidth roofline probe); bytes and both pointers 16 B aligned.
+int stream_copy(const void* src, void* dst, int64_t bytes, int blocks, hipStream_t st);
 int checksum_words(const void* ptr, int64_t bytes, uint64_t* out, uint64_t* scratch, int64_t scratch_len,
                    hipStream_t st);
 // Streaming form: partials[b] += block b's share (grid = n_partials, fixed for the

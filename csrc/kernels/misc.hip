@@ -198,6 +198,37 @@ __global__ void __launch_bounds__(kThreads) column_stats_wide_kernel(const float
 
 }  // namespace
 
+namespace {
+// Bandwidth roofline probe: a plain streaming copy, 16 B per lane, 4 independent loads in flight,
+// non-temporal stores, one grid-stride pass (benchmarks/kernels_bench.py reports every kernel
+// against the best of this and the runtime's D2D copy).
+constexpr int kCopyLoads = 4;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(kThreads) stream_copy_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                               int64_t n16) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  for (; i + (kCopyLoads - 1) * stride < n16; i += kCopyLoads * stride) {
+    u32x4 v[kCopyLoads];
+#pragma unroll
+    for (int k = 0; k < kCopyLoads; ++k) v[k] = __builtin_nontemporal_load(&src[i + k * stride]);
+#pragma unroll
+    for (int k = 0; k < kCopyLoads; ++k) __builtin_nontemporal_store(v[k], &dst[i + k * stride]);
+  }
+  for (; i < n16; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(&src[i]), &dst[i]);
+}
+}  // namespace
+
+int stream_copy(const void* src, void* dst, int64_t bytes, int blocks, hipStream_t st) {
+  if (bytes <= 0) return 0;
+  if (reinterpret_cast<uintptr_t>(src) % 16 != 0 || reinterpret_cast<uintptr_t>(dst) % 16 != 0 || bytes % 16 != 0)
+    return -2;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(stream_copy_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(kThreads), 0, st,
+                     static_cast<const u32x4*>(src), static_cast<u32x4*>(dst), bytes / 16);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int checksum_words(const void* ptr, int64_t bytes, uint64_t* out, uint64_t* scratch, int64_t scratch_len,
                    hipStream_t st) {
   if (bytes <= 0) return 0;

@@ -241,6 +241,34 @@ class Connection:
         """Hand slot ``s`` back to producer ``p`` now (reference ``end_access_epoch``)."""
         self.arena.set_state(p, s, _native.runtime().EMPTY)
 
+    def seek_producers(self, start_rounds: list[int]) -> None:
+        """Reposition every producer to continue at round ``start_rounds[p]`` (live resume).
+
+        The caller has stopped everything that reads the slots (stager thread joined, copies
+        retired). Protocol: ``seek`` to each producer; every slot set EMPTY, which wakes a
+        producer blocked on a slot (it may publish one stale round, then sees the message at
+        the top of its loop); wait for every ``seek_ack`` (each producer is now parked on its
+        pipe); discard whatever was published meanwhile (all slots EMPTY again); ``go`` with
+        the new round. Nothing runs concurrently with the final reset, so no stale window can
+        survive it.
+        """
+        if len(start_rounds) != self.n_producers:
+            raise ValueError("one start round per producer")
+        empty = _native.runtime().EMPTY
+        for p in self.pipes:
+            p.send("seek")
+        n_slots = self.arena.n_slots
+        for i in range(self.n_producers):
+            for s in range(n_slots):
+                self.arena.set_state(i, s, empty)
+        for p in self.pipes:
+            p.recv("seek_ack", self.timeout_s)
+        for i in range(self.n_producers):
+            for s in range(n_slots):
+                self.arena.set_state(i, s, empty)
+        for p, r in zip(self.pipes, start_rounds):
+            p.send("go", int(r))
+
     def release_on_stream(self, p: int, s: int, stream) -> None:
         """Hand the slot back when ``stream`` reaches this point (after its H2D copy)."""
         handle = stream if isinstance(stream, int) else stream.cuda_stream
@@ -269,6 +297,12 @@ class Connection:
         unpinned: consumers with native threads on the arena (the stager) stop there,
         even when the loader itself was never closed (an exception unwound the job)."""
         self._finalizers.append(fn)
+
+    def remove_finalizer(self, fn) -> None:
+        try:
+            self._finalizers.remove(fn)
+        except ValueError:
+            pass
 
     def finalize(self, join_timeout_s: float = 10.0) -> None:
         if self._closed:
@@ -303,7 +337,7 @@ class Connection:
         return [self.arena.producer_info(i) for i in range(self.n_producers)]
 
 
-@for_all_methods(with_logging, exclude=["Istart_access_epoch", "Iend_access_epoch"])
+@for_all_methods(with_logging, exclude=["Istart_access_epoch", "Iend_access_epoch", "poll_control"])
 class ProducerConnection:
     """Producer-side end: pipe to the consumer + the attached arena."""
 
@@ -341,6 +375,24 @@ class ProducerConnection:
         release/acquire slot state word, see ``Connection.sync``."""
 
     _sync = sync
+
+    def poll_control(self):
+        """Non-blocking: a pending control message from the consumer, ``(tag, payload)`` or None.
+
+        ``("seek", None)``: the consumer is repositioning the producers (live
+        ``load_state_dict`` / ``set_epoch``); answer with :meth:`pause_for_seek`.
+        """
+        if not self.pipe.conn.poll(0):
+            return None
+        try:
+            return self.pipe.conn.recv()
+        except (EOFError, OSError):
+            return None
+
+    def pause_for_seek(self) -> int:
+        """Acknowledge a seek and block until the consumer names the round to continue from."""
+        self.pipe.send("seek_ack")
+        return int(self.pipe.recv("go", self.timeout_s))
 
     def Istart_access_epoch(self, slot: int) -> WorkerInfo:  # noqa: N802
         """Wait until the consumer hands ``slot`` back (EMPTY), or shutdown."""

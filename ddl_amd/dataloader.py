@@ -62,6 +62,12 @@ def _mix(a: int, b: int) -> int:
     return z ^ (z >> 31)
 
 
+def window_perm_key(producer: int, round_: int) -> int:
+    """Key of the device permutation of one window visit (producer ``p``, round ``seq``): a 64-bit
+    mix of both, so every (producer, round) pair has its own order at any producer count."""
+    return _mix(producer, round_) & ((1 << 63) - 1)
+
+
 class DistributedDataloaderABC(ABC):
     """The reference's abstract consumer interface (ddl/mpi_dataloader.py:31-103).
 
@@ -205,6 +211,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
             return
 
         P = connection.n_producers
+        self._check_resume_layout(P)
         rounds0 = [self._first_round(p, P, self.window) for p in range(P)]
         base_meta = MetaData_Consumer_To_Producer(
             producer_function=producer_function,
@@ -237,16 +244,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
             if len(wpe) != 1 or 0 in wpe:
                 raise ShapeMismatchError(md, "indexed producers must announce one batches_per_epoch")
             self.windows_per_epoch = wpe.pop()
-            chk = getattr(self, "_resume_check", None)
-            if chk is not None:
-                ex = md[0].extra
-                for key in ("global_batch", "n_samples", "order_seed"):
-                    if chk.get(key) is not None and ex.get(key) is not None and chk[key] != ex[key]:
-                        raise ShapeMismatchError(
-                            (key, chk[key], ex[key]),
-                            f"checkpoint {key}={chk[key]} does not match the producers' {ex[key]}")
-                if int(chk["batches_per_epoch"]) != self.windows_per_epoch:
-                    raise ShapeMismatchError(chk, "checkpoint batches_per_epoch does not match")
+            self._check_indexed_resume()
         elif self.mode == "split_along_epoch":
             self.windows_per_epoch = P
         else:
@@ -269,7 +267,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
                                         timeout_s=self.timeout_s, first_window=self.window)
             connection.add_finalizer(self._stager.close)  # stop the native thread before the arena is unpinned
             if self._produces_copy():
-                self._batch_stream = torch.cuda.Stream(self.device)
+                self._batch_stream = streams.batch_stream(self.device)
         self._update_len()
 
     # --------------------------------------------------------------- schedule
@@ -398,8 +396,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
         if self.shuffle != "device":
             return None
         # key = (seed, producer, round): every window visit gets a fresh order.
-        return FeistelPermutation(self.metadata_from_producer[p].nData, self.seed,
-                                  (seq << 8) | (p & 0xFF))
+        return FeistelPermutation(self.metadata_from_producer[p].nData, self.seed, window_perm_key(p, seq))
 
     def _batch_from_window(self, sw, p: int, s: int, local: int):
         B = self.batch_size
@@ -580,9 +577,24 @@ class DistributedDataLoader(DistributedDataloaderABC):
             self._begin_window()
 
     def set_epoch(self, epoch: int) -> None:
-        """torch-style hook; the order is driven by the internal cursor, so this only checks it."""
-        if epoch != self.epoch:
-            logger.warning("set_epoch(%d) while the loader cursor is at epoch %d", epoch, self.epoch)
+        """torch-style ``sampler.set_epoch``: position the loader at the START of ``epoch``.
+
+        A no-op when the cursor is already there (the usual ``for e in range(n): dl.set_epoch(e)``
+        loop); otherwise a live seek (producers repositioned, staging restarted), so batches and
+        their order are exactly those of ``epoch`` in an uninterrupted run. Called mid-epoch for
+        the current epoch, it restarts that epoch.
+        """
+        epoch = int(epoch)
+        if epoch == self.epoch and self.epoch_batch == 0 and not self._pending:
+            return
+        if not 0 <= epoch < self.n_epochs:
+            raise ValueError(f"epoch {epoch} outside [0, {self.n_epochs})")
+        if self.connection is None or self.connection.n_producers == 0:
+            self.epoch = epoch
+            return
+        if self.mode == "indexed" or self.mode == "split_along_epoch" or self.mode == "do_not_split_along_epoch":
+            w = epoch * self.windows_per_epoch
+            self._seek(window=w, window_in_epoch=0, epoch=epoch, batch=0, epoch_batch=0)
 
     def _can_continue(self) -> bool:
         return self.epoch < self.n_epochs
@@ -650,14 +662,102 @@ class DistributedDataLoader(DistributedDataloaderABC):
             return
         # exact resume, also mid-window: the producers restart at this window's round
         # (deterministic content per round) and the cursor skips its consumed batches
+        self._resume_window_sd = sd
         self.window = int(sd["window"])
         self.window_in_epoch = int(sd["window_in_epoch"])
         self.batch = int(sd.get("batch", 0))
         self.epoch_batch = int(sd.get("epoch_batch", 0))
 
     def load_state_dict(self, sd: dict) -> None:
-        raise RuntimeError("pass the state as DistributedDataLoader(..., resume_state=sd): producers are started "
-                           "at construction and must begin at the checkpointed round")
+        """Restore a ``state_dict()`` on a LIVE loader (torch ``DataLoader``/``StatefulDataLoader`` style).
+
+        The staging ring is drained, the producers are repositioned to the checkpointed rounds
+        (``Connection.seek_producers``) and the cursor is rebuilt, so the next batch is exactly
+        the one an uninterrupted run would deliver after the checkpoint -- also mid-window, and
+        for ``kind="indexed"`` at a different world size (same global batch). Every rank of a
+        multi-rank job must call it at the same point (its exchange collectives restart from the
+        checkpointed window). Equivalent to constructing with ``resume_state=sd``.
+        """
+        if self._finalized:
+            raise RuntimeError("load_state_dict on a finished loader: construct a new one with resume_state=")
+        saved = (self.epoch, self.seed, self.window, self.window_in_epoch, self.batch, self.epoch_batch)
+        self._apply_state(sd)
+        try:
+            if self.connection is not None and self.connection.n_producers:
+                self._check_resume_layout(self.connection.n_producers)
+                if self.mode == "indexed":
+                    self._check_indexed_resume()
+        except Exception:
+            (self.epoch, self.seed, self.window, self.window_in_epoch, self.batch, self.epoch_batch) = saved
+            raise
+        if self.connection is None or self.connection.n_producers == 0:
+            return
+        self._seek(self.window, self.window_in_epoch, self.epoch, self.batch, self.epoch_batch)
+
+    def _check_resume_layout(self, n_producers: int) -> None:
+        """Window-kind checkpoints name producer rounds: the producer count must match (the slot
+        count may change -- content is a function of (producer, round), not of the slot)."""
+        sd = getattr(self, "_resume_window_sd", None)
+        if sd is None:
+            return
+        if int(sd.get("n_producers", n_producers)) != n_producers:
+            raise ShapeMismatchError((sd.get("n_producers"), n_producers),
+                                     f"window-kind checkpoint of {sd.get('n_producers')} producers cannot resume "
+                                     f"with {n_producers}: windows are (producer, round) pairs; use mode='indexed' "
+                                     "for a layout-independent order")
+        if sd.get("mode", self.mode) != self.mode:
+            raise ShapeMismatchError((sd.get("mode"), self.mode), "checkpoint window mode differs")
+
+    def _check_indexed_resume(self) -> None:
+        chk = getattr(self, "_resume_check", None)
+        if chk is None or not self.metadata_from_producer:
+            return
+        ex = self.metadata_from_producer[0].extra
+        for key in ("global_batch", "n_samples", "order_seed"):
+            if chk.get(key) is not None and ex.get(key) is not None and chk[key] != ex[key]:
+                raise ShapeMismatchError((key, chk[key], ex[key]),
+                                         f"checkpoint {key}={chk[key]} does not match the producers' {ex[key]}")
+        if int(chk["batches_per_epoch"]) != self.windows_per_epoch:
+            raise ShapeMismatchError(chk, "checkpoint batches_per_epoch does not match")
+
+    def _seek(self, window: int, window_in_epoch: int, epoch: int, batch: int, epoch_batch: int) -> None:
+        """Live reposition: drain staging, move the producers, rebuild the cursor and the stager."""
+        if epoch >= self.n_epochs:
+            raise ValueError(f"cannot seek to epoch {epoch} of a {self.n_epochs}-epoch loader")
+        P = self.connection.n_producers
+        with trace_range("ddl.consumer.seek"):
+            # 1. stop every reader of the slots / ring buffers
+            if self._batch_stream is not None:
+                self._lookahead.clear()
+                self._batch_stream.synchronize()
+            if self._stager is not None:
+                self._stager.close()  # joins the native thread; copies and their slot hand-backs retire
+            elif self._host_window is not None:
+                self._host_window = None  # seek_producers resets every slot, this one included
+            self._cur = None
+            self._pending = False
+            # 2. cursor
+            self.window, self.window_in_epoch, self.epoch = int(window), int(window_in_epoch), int(epoch)
+            self.batch, self.epoch_batch = int(batch), int(epoch_batch)
+            self.target_rank = self.window % P + 1
+            # 3. producers continue at the rounds of the new window schedule
+            self.connection.seek_producers([self._first_round(p, P, self.window) for p in range(P)])
+            # 4. a fresh staging ring starting at the new window
+            self.total_windows = self.n_epochs * self.windows_per_epoch - self.window
+            if self._stager is not None:
+                from .staging import WindowStager
+
+                old = self._stager
+                self.connection.remove_finalizer(old.close)
+                self._stager = WindowStager(self.connection, self.n_slots, self.total_windows, self.prefetch_depth,
+                                            self.device, old.max_window_bytes, post_copy=self._exchange_fn,
+                                            timeout_s=self.timeout_s, first_window=self.window)
+                self.connection.add_finalizer(self._stager.close)
+                self.metrics.bytes_h2d += old.bytes_h2d
+                del old
+            self._update_len()
+            if self.batch == 0:
+                self._begin_window()
 
     # --------------------------------------------------------------- teardown
     def _finalize(self) -> None:
@@ -670,7 +770,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
         if self.connection is not None:
             self.connection.shutdown_operation()
         if self._stager is not None:
-            self.metrics.bytes_h2d = self._stager.bytes_h2d
+            self.metrics.bytes_h2d += self._stager.bytes_h2d
             self._stager.close()
         if self.connection is not None:
             self.connection.finalize()

@@ -190,6 +190,13 @@ class DataPusher(DataPusherABC):
         rnd = self.meta.start_round
         slot = rnd % n_slots
         while True:
+            ctl = conn.poll_control()
+            if ctl is not None:
+                if ctl[0] != "seek":
+                    raise RuntimeError(f"producer {self.index}: unexpected control message {ctl[0]!r}")
+                rnd = conn.pause_for_seek()  # live load_state_dict / set_epoch on the consumer
+                slot = rnd % n_slots
+                continue
             t0 = time.perf_counter_ns()
             if self._istart_access_epoch(slot) is WorkerInfo.STOP:
                 break

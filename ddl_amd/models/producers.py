@@ -2,8 +2,9 @@
 
 * ``PointwiseProducer``  -- the reference harness's producer (reference
   tests/run_ddl.py:107-167): tabular shard, column groups (3, 5, 1), optional
-  host-side in-place row shuffle per round. Round-deterministic RNG (seeded by
-  (seed, rank, producer, round)) so a resumed run reproduces the windows.
+  host-side row shuffle per round: the pristine shard permuted by the RNG of
+  (seed, rank, producer, round), so a window is a function of its round and a
+  resumed run reproduces it (at any slot count).
 * ``ImageWindowProducer`` -- a window of synthetic 3x224x224 images (bf16 or
   uint8, CHW or HWC). ``execute_function`` stamps the round into every sample
   (a cheap refill that makes each window visit distinct) or regenerates it.
@@ -60,13 +61,21 @@ class PointwiseProducer(ProducerFunctionSkeleton):
         ops.pack_columns([torch.from_numpy(np.ascontiguousarray(g, dtype=np.float32)) for g in self._groups],
                          out=torch.from_numpy(self.my_ary))
         self._groups = None
+        self._base = self.my_ary.copy() if self.host_shuffle else None
 
     def execute_function(self, *args, **kwargs):
+        """Round r's window = the shard permuted by the RNG of (seed, rank, producer, r).
+
+        The reference shuffles the window in place, round after round (tests/run_ddl.py:163-167),
+        so its content depends on every earlier round and on which slot it lands in. Permuting a
+        pristine copy instead makes each window a function of its round only: a checkpoint
+        resumes it exactly, at any slot count.
+        """
         if not self.host_shuffle:
             return
         rng = np.random.default_rng([self.seed, self.rank_global or 0, self.producer_index or 0,
                                      int(kwargs.get("round", 0))])
-        rng.shuffle(self.my_ary)
+        np.take(self._base, rng.permutation(len(self._base)), axis=0, out=self.my_ary)
 
 
 class ImageWindowProducer(ProducerFunctionSkeleton):

@@ -123,3 +123,67 @@ class TokenTrainStep:
         loss.backward()
         self.opt.step()
         return loss.detach()
+
+
+class CalibratedStep:
+    """A consumer step of a chosen GPU duration: read the whole batch, then a chain of bf16 GEMMs.
+
+    Used to place the training step's rate at a chosen multiple of the loader's feed rate
+    (``benchmarks/bench_idle_sweep.py``), so GPU idle % is measured where the loader is the
+    bottleneck, not only behind a model far slower than the feed. The batch is read by the
+    streaming checksum kernel (every byte, one launch); the GEMM chain (``m x k @ k x k``,
+    hipBLASLt) is sized by timing it on this GPU: ``reps = round((step_ms - read_ms) / gemm_ms)``.
+    """
+
+    def __init__(self, device, step_ms: float, m: int | None = None, k: int = 4096, dtype=torch.bfloat16,
+                 min_reps: int = 8):
+        from .. import ops
+
+        self.device = torch.device(device)
+        self.step_ms = float(step_ms)
+        g = torch.Generator(device="cpu").manual_seed(0)
+        self.w = (torch.randn(k, k, generator=g) / k ** 0.5).to(self.device, dtype)
+        if m is None:  # rows of the GEMM: at least `min_reps` GEMMs per step, so the step time is finely tunable
+            probe = torch.empty(4096, k, dtype=dtype, device=self.device)
+            t4k = self._time(lambda: torch.mm(probe, self.w))
+            m = int(min(8192, max(256, 4096 * (self.step_ms / min_reps) / t4k)) // 256 * 256)
+            del probe
+        self.a = (torch.randn(m, k, generator=g) / k ** 0.5).to(self.device, dtype)
+        self.out = torch.empty(m, k, dtype=dtype, device=self.device)
+        self.acc = ops.ChecksumAccumulator(self.device)
+        self.gemm_ms = self._time(lambda: torch.mm(self.a, self.w, out=self.out))
+        self.reps = 0
+        self.read_ms = 0.0
+
+    def _time(self, fn, reps: int = 20) -> float:
+        fn()
+        torch.cuda.synchronize(self.device)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            fn()
+        e.record()
+        e.synchronize()
+        return s.elapsed_time(e) / reps
+
+    def calibrate(self, batch) -> "CalibratedStep":
+        """Time the batch read on a real batch and size the GEMM chain to fill the step."""
+        self.read_ms = self._time(lambda: self._read(batch))
+        self.reps = max(0, round((self.step_ms - self.read_ms) / self.gemm_ms))
+        return self
+
+    def _read(self, batch) -> None:
+        tensors = batch.values() if isinstance(batch, dict) else (batch if isinstance(batch, (tuple, list))
+                                                                  else (batch,))
+        for t in tensors:
+            if isinstance(t, torch.Tensor) and t.is_cuda:
+                self.acc.add(t)
+
+    @property
+    def planned_ms(self) -> float:
+        return self.read_ms + self.reps * self.gemm_ms
+
+    def __call__(self, batch) -> None:
+        self._read(batch)
+        for _ in range(self.reps):
+            torch.mm(self.a, self.w, out=self.out)

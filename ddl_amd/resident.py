@@ -119,6 +119,7 @@ class PrefetchedIndexedLoader:
         self._pending = False
         self._queue: collections.deque = collections.deque()
         self._next_t = None
+        self._generation = 0
         self.batches = 0
 
     def __len__(self) -> int:
@@ -151,12 +152,21 @@ class PrefetchedIndexedLoader:
     def __iter__(self) -> Iterator[torch.Tensor]:
         """One epoch of batches ([LB, *sample_shape] in ``out_dtype``)."""
         bpe = self.order.batches_per_epoch
+        if self._pending:  # the previous iterator was left after yielding: that batch counts as consumed
+            self._pending = False
+            self.cursor += 1
+            if self.cursor >= bpe:
+                self.epoch, self.cursor = self.epoch + 1, 0
+        self._generation += 1  # at most one live iterator: an older one stops at its next step
+        gen = self._generation
         if self.n_epochs is not None and self.epoch >= self.n_epochs:
             return
         t0 = self.epoch * bpe + self.cursor
         if self._next_t is None:
             self._next_t = t0
         for t in range(t0, (self.epoch + 1) * bpe):
+            if gen != self._generation:  # load_state_dict / set_epoch repositioned the loader
+                return
             self._fill(t + self.depth)
             tq, batch, ev = self._queue.popleft()
             assert tq == t, (tq, t)
@@ -168,6 +178,8 @@ class PrefetchedIndexedLoader:
             self._pending = True
             self.batches += 1
             yield batch
+            if gen != self._generation:
+                return
             self._pending = False
             self.cursor += 1
         self.epoch += 1
@@ -200,6 +212,34 @@ class PrefetchedIndexedLoader:
         self.cursor = int(sd["global_batch_cursor"])
         if self.cursor >= self.order.batches_per_epoch:
             self.epoch, self.cursor = self.epoch + 1, 0
+
+    def _reset_queue(self) -> None:
+        """Drop the prefetched batches (their assembly is drained first) and restart at the cursor."""
+        prep = getattr(self, "prep_stream", None)
+        if prep is not None:
+            prep.synchronize()
+        self._queue.clear()
+        self._next_t = None
+        self._pending = False
+        self._generation += 1  # an iterator started before this point stops instead of yielding stale data
+
+    def load_state_dict(self, sd: dict) -> None:
+        """Restore a ``state_dict()`` on the live loader (any world size with the same global batch);
+        the next ``iter()`` continues exactly after the checkpointed batch."""
+        saved = (self.epoch, self.cursor)
+        try:
+            self._apply_state(sd)
+        except Exception:
+            self.epoch, self.cursor = saved
+            raise
+        self._reset_queue()
+
+    def set_epoch(self, epoch: int) -> None:
+        """torch-style: the next ``iter()`` yields epoch ``epoch`` from its first batch (no-op if already there)."""
+        if int(epoch) == self.epoch and self.cursor == 0 and not self._pending:
+            return
+        self.epoch, self.cursor = int(epoch), 0
+        self._reset_queue()
 
 
 
@@ -262,7 +302,7 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
         else:
             self.shard = self._load_shard(reader, chunk_bytes, host_threads)
         self.load_s = time.perf_counter() - t0
-        self.prep_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        self.prep_stream = streams.batch_stream(self.device) if self.device.type == "cuda" else None
 
     # ----------------------------------------------------------------- load
     def _load_shard(self, reader, chunk_bytes: int, host_threads: int) -> torch.Tensor:

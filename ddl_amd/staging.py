@@ -90,6 +90,7 @@ class WindowStager:
         # w+1 is gathered right behind it: one ring buffer holds that posted window, so give it its
         # own and keep `depth` windows of DMA in flight behind it.
         n_buf = depth + 1 if post_copy is not None and depth >= 2 else depth
+        self.max_window_bytes = int(max_window_bytes)
         self.buffers = [torch.empty(max_window_bytes, dtype=torch.uint8, device=self.device) for _ in range(n_buf)]
         self.ready_events = [torch.cuda.Event() for _ in range(n_buf)]
         self._copy_done = [torch.cuda.Event() for _ in range(n_buf)]
@@ -202,6 +203,9 @@ class WindowStager:
         self._native.close()
         self.copy_stream.synchronize()
         self.stream.synchronize()
+        # drop the ring (a live seek builds a new stager; batches handed out keep their own refs)
+        self._staged.clear()
+        self.buffers = []
 
     @property
     def bytes_h2d(self) -> int:

@@ -93,7 +93,7 @@ class ZeroCopyLoader(PrefetchedIndexedLoader):
                 self._reg_base = base
                 dptr = hip.host_device_pointer(base) + (addr - base)
             self.rows = ops.HostRows(self.cpu, dptr)
-            self.prep_stream = torch.cuda.Stream(self.device)
+            self.prep_stream = streams.batch_stream(self.device)
         else:
             self.rows = self.cpu
 

@@ -126,13 +126,14 @@ def test_column_normalisation_applies_with_owned_batches(auto_mark):
 
 
 def test_host_device_shuffle_uses_feistel_order():
+    from ddl_amd.dataloader import window_perm_key
     from ddl_amd.permutation import FeistelPermutation
 
     with ddl_amd.start(n_producers=2) as (env, conn):
         dl = ddl_amd.DistributedDataLoader(IdProducer(40, 4), 8, conn, 2, env=env, shuffle="device", seed=3)
         eps = _epochs(dl, 2)
     for e, rows in enumerate(eps):
-        perm = FeistelPermutation(40, 3, (0 << 8) | e).full()
+        perm = FeistelPermutation(40, 3, window_perm_key(e, 0)).full()  # window e: producer e, round 0
         assert np.array_equal(rows[:, 2].numpy(), perm)
 
 

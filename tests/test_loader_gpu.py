@@ -6,6 +6,7 @@ import torch
 
 import ddl_amd
 from ddl_amd import Marker
+from ddl_amd.dataloader import window_perm_key
 from ddl_amd.permutation import FeistelPermutation
 from tests.helpers import IdProducer
 
@@ -47,7 +48,7 @@ def test_gpu_device_shuffle_matches_feistel_and_is_deterministic():
     for e in range(3):
         assert torch.equal(seen1[e], seen2[e])
         p = e % 3
-        perm = FeistelPermutation(64, 11, ((e // 3) << 8) | p).full()
+        perm = FeistelPermutation(64, 11, window_perm_key(p, e // 3)).full()
         assert np.array_equal(seen1[e][:, 2].numpy(), perm)
 
 

@@ -130,3 +130,35 @@ def test_resident_augment_needs_gpu_and_known_keys(src):
         ResidentGlobalLoader(src, 48, augment={"size": (4, 4)}, device="cpu")  # CPU, and rows are not images
     with pytest.raises(ValueError):
         ResidentGlobalLoader(src, 48, augment={"bogus": 1}, device="cpu")
+
+
+def _resident_live_reload_rank(rank, world, name, n, gb):
+    import ddl_amd
+    from ddl_amd.models import SharedArraySource
+    from ddl_amd.resident import ResidentGlobalLoader
+
+    src = SharedArraySource(name, n, (3,), "int64")
+    with ddl_amd.start(n_producers=0) as (env, _):
+        dl = ResidentGlobalLoader(src, gb, env, seed=11, depth=2, n_epochs=3)
+        full = [b[:, 0].clone() for e in range(3) for b in dl]
+        dl.set_epoch(0)  # rewind the same loader: epoch 0 again, from its first batch
+        head, sd = [], None
+        for i, b in enumerate(dl):
+            head.append(b[:, 0].clone())
+            if i == 4:
+                sd = dl.state_dict()
+                break
+        for _ in range(2):  # run on into epoch 1 (a stale iterator is abandoned mid-epoch)
+            for b in dl:
+                pass
+        dl.load_state_dict(sd)
+        tail = []
+        while dl.epoch < 3:
+            tail += [b[:, 0].clone() for b in dl]
+        return torch.cat(full).numpy(), torch.cat(head + tail).numpy()
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_resident_live_load_state_dict_and_set_epoch(src, world):
+    for full, resumed in run_ranks(_resident_live_reload_rank, world, src.name, src.n, 48):
+        assert np.array_equal(full, resumed)

@@ -111,6 +111,8 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("trace_dir")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--names", default="bench.phase1,bench.phase2",
+                    help="comma-separated roctx range names to analyse (bench_idle_sweep.py: sweep.p00,...)")
     a = ap.parse_args(argv)
     kernels = [r for p in _find(a.trace_dir, "kernel_trace.csv") for r in _rows(p)]
     copies = [r for p in _find(a.trace_dir, "memory_copy_trace.csv") for r in _rows(p)]
@@ -118,7 +120,7 @@ def main(argv=None) -> int:
     if not kernels or not markers:
         print(f"no kernel/marker trace under {a.trace_dir}", file=sys.stderr)
         return 1
-    res = analyse(kernels, copies, markers)
+    res = analyse(kernels, copies, markers, tuple(n for n in a.names.split(",") if n))
     line = json.dumps(res)
     print(line)
     if a.out:
