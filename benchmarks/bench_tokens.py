@@ -64,7 +64,8 @@ def main(argv=None):
             else:
                 source = src
             n_epochs = (a.warmup + a.steps + a.idle_steps + a.warmup // 2) // (a.n_seqs // gb) + 2
-            dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(source, gb, a.seq_len, a.mode, pack_order=a.pack_order), a.batch, conn,
+            dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(source, gb, a.seq_len, a.mode,
+                                                                  pack_order=a.pack_order if a.mode == "pack" else "in_order"), a.batch, conn,
                                                n_epochs, mode="indexed", env=env, collate="tokens", auto_mark=True)
             dev = torch.device(env.device)
             acc = ops.ChecksumAccumulator(dev)  # one streaming launch per batch

@@ -46,7 +46,7 @@ from .exceptions import ShapeMismatchError
 from .ops import _dtypes
 from .permutation import FeistelPermutation
 from .types import DDLEnv, Marker, MetaData_Consumer_To_Producer, MetaData_Producer_To_Consumer
-from .utils.logging import for_all_methods, logger, with_logging
+from .utils.logging import for_all_methods, with_logging
 from .utils import streams
 from .utils.tracing import LoaderMetrics, trace_range
 

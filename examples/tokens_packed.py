@@ -52,7 +52,8 @@ def main() -> None:
                 offs = SharedArraySource(name + "_off", a.n_seqs + 1, (1,), "int64")
                 n_tok = int(offs.tensor()[-1])
                 src = SharedTokenSource(SharedArraySource(name + "_tok", n_tok, (1,), "int32"), offs, a.seq_len)
-            producer = TokenBatchProducer(src, a.global_batch, a.seq_len, a.mode, pack_order="ffd")
+            producer = TokenBatchProducer(src, a.global_batch, a.seq_len, a.mode,
+                                          pack_order="ffd" if a.mode == "pack" else "in_order")
             dl = ddl_amd.DistributedDataLoader(producer, a.global_batch // env.world_size, conn, a.epochs,
                                                mode="indexed", env=env, collate="tokens", auto_mark=True)
             for epoch in range(a.epochs):

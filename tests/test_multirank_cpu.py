@@ -196,3 +196,40 @@ def test_init_mpi_error_handling_rejects_non_multiple():
     init_mpi_error_handling(DDLEnv(rank=0, world_size=1), 1)  # single rank: warning only
     with pytest.raises(TopologyError):
         init_mpi_error_handling(DDLEnv(rank=0, world_size=6), 4)
+
+
+def _indexed_zero_copy_rank(rank, world, name, n, gb, epochs):
+    import ddl_amd
+    from ddl_amd.models import SharedArraySource
+    from ddl_amd.zerocopy import ZeroCopyLoader
+
+    src = SharedArraySource(name, n, (2,), "int64")
+    with ddl_amd.start(n_producers=0) as (env, _):
+        dl = ZeroCopyLoader(src, gb, env, seed=5, n_epochs=epochs, device="cpu")
+        return [[b[:, 0].clone().numpy() for b in dl] for _ in range(epochs)]
+
+
+def test_indexed_headline_order_is_world_size_invariant():
+    """bench.py's ``indexed`` order (ZeroCopyLoader over a node-shared source): the union of the ranks'
+    slices of every global batch -- in rank order -- is the same batch at W = 1, 2, 4 and 8."""
+    import numpy as np
+
+    from ddl_amd.models import SharedArraySource
+
+    n, gb, epochs = 500, 64, 2
+    data = torch.stack([torch.arange(n), torch.arange(n) * 3], 1).to(torch.int64)
+    src = SharedArraySource.create(f"ddl_amd_inv_{np.random.randint(1 << 30)}", data)
+    try:
+        merged = {}
+        for world in (1, 2, 4, 8):
+            res = run_ranks(_indexed_zero_copy_rank, world, src.name, n, gb, epochs)
+            merged[world] = [[np.concatenate([res[r][e][g] for r in range(world)]) for g in range(len(res[0][e]))]
+                             for e in range(epochs)]
+        for world in (2, 4, 8):
+            for e in range(epochs):
+                assert len(merged[world][e]) == len(merged[1][e]) == n // gb
+                for a, b in zip(merged[world][e], merged[1][e]):
+                    assert np.array_equal(a, b)
+        assert not np.array_equal(np.concatenate(merged[1][0]), np.concatenate(merged[1][1]))  # fresh order per epoch
+    finally:
+        src.close()
