@@ -34,6 +34,10 @@ def main(argv=None) -> None:
     ap.add_argument("--timesteps", type=int, default=10, help="reference nData (10052 rows each)")
     ap.add_argument("--host-shuffle", action="store_true",
                     help="also run the reference's per-round CPU rng.shuffle in the producers")
+    ap.add_argument("--consumer", default="flat", choices=["flat", "groups"],
+                    help="flat: ONE streaming checksum over the batch's three groups (adjacent in one allocation); "
+                         "groups: one checksum launch per group")
+    ap.add_argument("--dispatch", default="native", choices=["native", "python"])
     a = ap.parse_args(argv)
 
     import torch
@@ -46,8 +50,22 @@ def main(argv=None) -> None:
         dev = torch.device(env.device)
         producer = PointwiseProducer(n_timesteps=a.timesteps, host_shuffle=a.host_shuffle)
         dl = ddl_amd.DistributedDataLoader(producer, 4096, conn, 10 ** 6, 0.0, "alltoall", env.rank, env.world_size,
-                                           env=env, shuffle="device", contiguous=True, seed=1)
+                                           env=env, shuffle="device", contiguous=True, seed=1,
+                                           native_dispatch=a.dispatch == "native")
         acc = ops.ChecksumAccumulator(dev)
+
+        def consume(groups):
+            if a.consumer == "groups" or dev.type != "cuda":
+                for g in groups:
+                    acc.add(g)
+                return
+            g0 = groups[0]
+            n = sum(g.numel() for g in groups)
+            off = g0.storage_offset()
+            assert all(g.untyped_storage().data_ptr() == g0.untyped_storage().data_ptr() for g in groups)
+            assert [g.storage_offset() for g in groups] == [off, off + groups[0].numel(),
+                                                             off + groups[0].numel() + groups[1].numel()]
+            acc.add(g0.new_empty(0).set_(g0.untyped_storage(), off, (n,)))
 
         def batches():
             while True:
@@ -63,13 +81,11 @@ def main(argv=None) -> None:
                 torch.cuda.synchronize(dev)
 
         for _ in range(a.warmup):
-            for g in next(it):
-                acc.add(g)
+            consume(next(it))
         sync()
         t0 = time.perf_counter()
         for _ in range(a.steps):
-            for g in next(it):
-                acc.add(g)
+            consume(next(it))
         sync()
         dt = time.perf_counter() - t0
         rows = 4096 * a.steps * env.world_size
@@ -79,7 +95,7 @@ def main(argv=None) -> None:
                               "batches_per_s": round(a.steps / dt, 1), "us_per_batch": round(1e6 * dt / a.steps, 1),
                               "vs_reference_ceiling": round(rows / dt / (REF_ROWS_PER_S * env.world_size), 2),
                               "batches_per_window": len(dl), "producers": a.producers, "host_shuffle": a.host_shuffle,
-                              "device": str(dev)}))
+                              "consumer": a.consumer, "dispatch": a.dispatch, "device": str(dev)}))
 
 
 if __name__ == "__main__":

@@ -15,12 +15,14 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <chrono>
 #include <stdexcept>
 #include <string>
 #include <vector>
 
 #include "common.h"
 #include "launch.h"
+#include "engine.h"
 #include "stager.h"
 
 namespace py = pybind11;
@@ -242,6 +244,188 @@ PYBIND11_MODULE(_ddl_hip, m) {
       .def_property_readonly("windows_landed", &ddl::NativeStager::windows_landed)
       .def_property_readonly("bytes_landed", &ddl::NativeStager::bytes_landed)
       .def_property_readonly("wait_producer_s", &ddl::NativeStager::wait_producer_s);
+
+  // ------------------------------------------------- native batch dispatch
+  py::class_<ddl::BatchEngine>(m, "BatchEngine")
+      .def(py::init([](ddl::NativeStager& stager, int kind, int in_dt, int out_dt, bool shuffle, int64_t batch,
+                       int64_t row_elems, uint64_t seed, std::vector<int64_t> n_data, std::vector<int32_t> widths,
+                       std::vector<float> scale, std::vector<float> bias, int64_t plane, int64_t max_blocks,
+                       int32_t n_producers, std::vector<uintptr_t> buffers, std::vector<uintptr_t> ready,
+                       uintptr_t batch_stream, int device, std::vector<int64_t> token) {
+             ddl::BatchRecipe r;
+             r.kind = kind;
+             r.in_dt = in_dt;
+             r.out_dt = out_dt;
+             r.shuffle = shuffle ? 1 : 0;
+             r.batch = batch;
+             r.row_elems = row_elems;
+             r.seed = seed;
+             r.max_blocks = max_blocks;
+             r.n_data = std::move(n_data);
+             r.widths = std::move(widths);
+             r.aff = make_affine(scale, bias, plane);
+             if (kind == 2) {
+               if (token.size() != 8) throw std::invalid_argument("BatchEngine: token recipe needs 8 values");
+               r.token_mode = static_cast<int32_t>(token[0]);
+               r.pad_id = static_cast<int32_t>(token[1]);
+               r.seq_len = token[2];
+               r.off_offsets = token[3];
+               r.off_row_start = token[4];
+               r.off_row_end = token[5];
+               r.off_seg_offsets = token[6];
+               r.off_tokens = token[7];
+             }
+             std::vector<void*> bufs;
+             for (auto b : buffers) bufs.push_back(as_ptr<void>(b));
+             std::vector<hipEvent_t> rd;
+             for (auto e : ready) rd.push_back(reinterpret_cast<hipEvent_t>(e));
+             return std::make_unique<ddl::BatchEngine>(&stager, std::move(r), n_producers, std::move(bufs),
+                                                       std::move(rd), as_stream(batch_stream), device);
+           }),
+           py::arg("stager"), py::arg("kind"), py::arg("in_dt"), py::arg("out_dt"), py::arg("shuffle"),
+           py::arg("batch"), py::arg("row_elems"), py::arg("seed"), py::arg("n_data"), py::arg("widths"),
+           py::arg("scale"), py::arg("bias"), py::arg("plane"), py::arg("max_blocks"), py::arg("n_producers"),
+           py::arg("buffers"), py::arg("ready"), py::arg("batch_stream"), py::arg("device"),
+           py::arg("token") = std::vector<int64_t>{}, py::keep_alive<1, 2>(),
+           "token = [mode (0 pad, 1 pack), pad_id, seq_len, byte offsets of offsets, row_start, row_end, "
+           "seg_offsets, tokens] for kind 2")
+      .def(
+          "provide",
+          [](ddl::BatchEngine& e, const std::vector<std::vector<uintptr_t>>& slots) {
+            std::vector<std::vector<void*>> v;
+            v.reserve(slots.size());
+            for (const auto& s : slots) {
+              std::vector<void*> o;
+              for (auto p : s) o.push_back(as_ptr<void>(p));
+              v.push_back(std::move(o));
+            }
+            e.provide(v);
+          },
+          py::arg("slots"))
+      .def_property_readonly("slots_left", &ddl::BatchEngine::slots_left)
+      .def(
+          "get",
+          [](ddl::BatchEngine& e, int64_t w, int64_t local, int64_t bpw, bool next_ok, uintptr_t compute,
+             int64_t timeout_ms) {
+            int32_t fp = -1;
+            int64_t slot;
+            int64_t tags[4] = {0, 0, 0, 0};
+            {
+              py::gil_scoped_release nogil;
+              slot = e.get(w, local, bpw, next_ok, as_stream(compute), timeout_ms, &fp, tags);
+            }
+            return py::make_tuple(slot, slot >= 0 ? int32_t{-1} : fp, py::make_tuple(tags[0], tags[1], tags[2], tags[3]));
+          },
+          py::arg("window"), py::arg("local"), py::arg("bpw"), py::arg("next_ok"), py::arg("compute_stream"),
+          py::arg("timeout_ms"),
+          "(slot, -1, window tags) for batch `local` of window `window`, else (code, producer, _): "
+          "-(10 + stager wait code) if the window could not be staged, -1 HIP error, -2 no output slot")
+      .def(
+          "acquire",
+          [](ddl::BatchEngine& e, int64_t w, int64_t timeout_ms) {
+            int32_t fp = -1;
+            int rc;
+            {
+              py::gil_scoped_release nogil;
+              rc = e.acquire(w, timeout_ms, &fp);
+            }
+            return py::make_tuple(rc, fp);
+          },
+          py::arg("window"), py::arg("timeout_ms"))
+      .def("release", &ddl::BatchEngine::release, py::arg("window"))
+      .def("reset", &ddl::BatchEngine::reset)
+      .def_property_readonly("wait_s", &ddl::BatchEngine::wait_s)
+      .def_property_readonly("batches", &ddl::BatchEngine::batches)
+      .def_property_readonly("lookahead_hits", &ddl::BatchEngine::lookahead_hits)
+      .def_property_readonly("timing_ns", &ddl::BatchEngine::timing_ns)
+      .def_property_readonly("compute_waits", &ddl::BatchEngine::compute_waits);
+  m.def(
+      "host_feistel_keys",
+      [](uint64_t seed, uint64_t key, uint64_t n) {
+        const ddl::FeistelKeys k = ddl::host_feistel_keys(seed, key, n);
+        std::vector<uint64_t> keys(k.k, k.k + ddl::kFeistelRounds);
+        return py::make_tuple(keys, k.half_bits);
+      },
+      py::arg("seed"), py::arg("key"), py::arg("n"), "Feistel round keys + half bits of (seed, key) over [0, n)");
+  m.def("host_window_perm_key", &ddl::host_window_perm_key, py::arg("producer"), py::arg("round"));
+  m.def(
+      "bucket_send",
+      [](std::vector<uint64_t> keys, uint64_t n_domain, uint32_t half_bits, int64_t pos0, int64_t count,
+         int64_t shard_rows, int64_t lo, int32_t rank, int32_t world, uintptr_t out, uintptr_t stream) {
+        ddl::BucketSpec sp{};
+        sp.keys = make_keys(keys, n_domain, half_bits);
+        sp.pos0 = pos0;
+        sp.count = count;
+        sp.shard_rows = shard_rows;
+        sp.lo = lo;
+        sp.rank = rank;
+        sp.world = world;
+        check_rc(ddl::bucket_send(sp, as_ptr<int64_t>(out), as_stream(stream)), "bucket_send");
+      },
+      py::arg("keys"), py::arg("n_domain"), py::arg("half_bits"), py::arg("pos0"), py::arg("count"),
+      py::arg("shard_rows"), py::arg("lo"), py::arg("rank"), py::arg("world"), py::arg("out"), py::arg("stream"));
+  m.def(
+      "bucket_recv",
+      [](std::vector<uint64_t> keys, uint64_t n_domain, uint32_t half_bits, int64_t pos0, int64_t count,
+         int64_t shard_rows, int32_t world, std::vector<int64_t> offsets, uintptr_t out, uintptr_t stream) {
+        if (offsets.size() != static_cast<size_t>(world) || world > ddl::kMaxBucketWorld)
+          throw std::invalid_argument("bucket_recv: one offset per rank, world <= 64");
+        ddl::BucketSpec sp{};
+        sp.keys = make_keys(keys, n_domain, half_bits);
+        sp.pos0 = pos0;
+        sp.count = count;
+        sp.shard_rows = shard_rows;
+        sp.world = world;
+        for (int q = 0; q < world; ++q) sp.offsets[q] = offsets[q];
+        check_rc(ddl::bucket_recv(sp, as_ptr<int64_t>(out), as_stream(stream)), "bucket_recv");
+      },
+      py::arg("keys"), py::arg("n_domain"), py::arg("half_bits"), py::arg("pos0"), py::arg("count"),
+      py::arg("shard_rows"), py::arg("world"), py::arg("offsets"), py::arg("out"), py::arg("stream"));
+
+  m.def(
+      "api_costs",
+      [](int iters) {
+        // host cost (us per call) of the HIP calls on the per-batch path, on two fresh streams
+        hipStream_t a, b;
+        hipStreamCreateWithFlags(&a, hipStreamNonBlocking);
+        hipStreamCreateWithFlags(&b, hipStreamNonBlocking);
+        hipEvent_t ev;
+        hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        void* flag = nullptr;
+        hipMalloc(&flag, 64);
+        hipMemsetAsync(flag, 0, 64, a);
+        hipStreamSynchronize(a);
+        auto t = [&](auto fn) {
+          for (int i = 0; i < 50; ++i) fn(i);
+          hipDeviceSynchronize();
+          const auto t0 = std::chrono::steady_clock::now();
+          for (int i = 0; i < iters; ++i) fn(i);
+          const double us =
+              std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / iters;
+          hipDeviceSynchronize();
+          return us;
+        };
+        py::dict d;
+        d["hipEventRecord"] = t([&](int) { hipEventRecord(ev, a); });
+        d["hipStreamWaitEvent"] = t([&](int) { hipStreamWaitEvent(b, ev, 0); });
+        d["hipEventQuery"] = t([&](int) { (void)hipEventQuery(ev); });
+        d["record+wait"] = t([&](int) {
+          hipEventRecord(ev, a);
+          hipStreamWaitEvent(b, ev, 0);
+        });
+        d["hipStreamWriteValue64"] = t([&](int i) { hipStreamWriteValue64(a, flag, static_cast<uint64_t>(i), 0); });
+        d["hipStreamWaitValue64"] = t([&](int i) {
+          hipStreamWaitValue64(b, flag, 0, hipStreamWaitValueGte, 0xFFFFFFFFFFFFFFFFull);
+        });
+        d["hipMemsetAsync 4B"] = t([&](int) { hipMemsetAsync(flag, 0, 4, a); });
+        hipDeviceSynchronize();
+        hipFree(flag);
+        hipEventDestroy(ev);
+        hipStreamDestroy(a);
+        hipStreamDestroy(b);
+        return d;
+      },
+      py::arg("iters") = 20000, "Host microseconds per call of the HIP stream/event APIs on the batch path");
 
   // --------------------------------------------------------------- kernels
   m.def(

@@ -1,0 +1,265 @@
+// See engine.h.
+#include "engine.h"
+
+#include <chrono>
+
+#include "launch.h"
+
+namespace ddl {
+namespace {
+
+uint64_t mix64_host(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+uint32_t half_bits_for(uint64_t n) {
+  uint32_t bl = 0;
+  for (uint64_t v = n - 1; v != 0; v >>= 1) ++bl;  // bit_length(n - 1)
+  const uint32_t h = (bl + 1) / 2;
+  return h < 1 ? 1 : h;
+}
+
+uint64_t clock_ns() {
+  return static_cast<uint64_t>(
+      std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+          .count());
+}
+
+constexpr int kBatchEvents = 16;  // lookahead is 1 batch; a ring this deep never re-records an unwaited event
+constexpr int kFreeEvents = 4;
+
+}  // namespace
+
+FeistelKeys host_feistel_keys(uint64_t seed, uint64_t key, uint64_t n) {
+  FeistelKeys k{};
+  for (int r = 0; r < kFeistelRounds; ++r) {
+    const uint64_t z = seed * 0x9E3779B97F4A7C15ull + key * 0xD1B54A32D192ED03ull +
+                       static_cast<uint64_t>(r + 1) * 0x8CB92BA72F3D8DD7ull;
+    k.k[r] = mix64_host(z);
+  }
+  k.n = n;
+  k.half_bits = half_bits_for(n);
+  return k;
+}
+
+uint64_t host_window_perm_key(uint64_t producer, uint64_t round) {
+  const uint64_t z = producer * 0x9E3779B97F4A7C15ull + round + 0x632BE59BD9B4E019ull;
+  return mix64_host(z) & ((1ull << 63) - 1);
+}
+
+BatchEngine::BatchEngine(NativeStager* stager, BatchRecipe recipe, int32_t n_producers, std::vector<void*> buffers,
+                         std::vector<hipEvent_t> ready, hipStream_t batch_stream, int device)
+    : stager_(stager),
+      r_(std::move(recipe)),
+      P_(n_producers),
+      buffers_(std::move(buffers)),
+      ready_(std::move(ready)),
+      bs_(batch_stream),
+      device_(device) {
+  if (stager_ == nullptr || P_ < 1 || buffers_.empty() || ready_.size() != buffers_.size() ||
+      static_cast<int32_t>(r_.n_data.size()) != P_ || r_.batch < 1 || (r_.kind == 1 && r_.widths.empty()) ||
+      r_.widths.size() > 8 || r_.kind < 0 || r_.kind > 2 || (r_.kind == 2 && r_.seq_len < 1))
+    throw std::invalid_argument("BatchEngine: inconsistent arguments");
+  if (hipSetDevice(device_) != hipSuccess) throw std::runtime_error("BatchEngine: hipSetDevice failed");
+  batch_events_.resize(kBatchEvents);
+  for (auto& e : batch_events_)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+      throw std::runtime_error("BatchEngine: hipEventCreate failed");
+  free_events_.assign(buffers_.size(), std::vector<hipEvent_t>(kFreeEvents, nullptr));
+  for (auto& v : free_events_)
+    for (auto& e : v)
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+        throw std::runtime_error("BatchEngine: hipEventCreate failed");
+  free_next_.assign(buffers_.size(), 0);
+}
+
+BatchEngine::~BatchEngine() {
+  // the owner drains the batch stream before dropping the engine (events may still be waited on)
+  hipStreamSynchronize(bs_);
+  for (auto e : batch_events_) hipEventDestroy(e);
+  for (auto& v : free_events_)
+    for (auto e : v) hipEventDestroy(e);
+}
+
+void BatchEngine::provide(const std::vector<std::vector<void*>>& slots) {
+  for (const auto& s : slots) {
+    const size_t need = r_.kind == 1 ? r_.widths.size() : r_.kind == 2 ? (r_.token_mode == 1 ? 5 : 3) : 1;
+    if (s.size() != need) throw std::invalid_argument("BatchEngine.provide: wrong number of outputs per slot");
+    free_slots_.push_back(static_cast<int64_t>(slots_.size()));
+    slots_.push_back(s);
+  }
+}
+
+const StagedInfo* BatchEngine::acquired(int64_t w) {
+  auto it = windows_.find(w);
+  return it == windows_.end() ? nullptr : &it->second;
+}
+
+int BatchEngine::acquire(int64_t w, int64_t timeout_ms, int32_t* failed_producer) {
+  if (acquired(w) != nullptr) return 0;
+  StagedInfo info;
+  const auto t0 = std::chrono::steady_clock::now();
+  const int rc = stager_->wait(w, timeout_ms, &info, failed_producer);
+  wait_ns_ += static_cast<uint64_t>(
+      std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
+  if (rc != 0) return rc;
+  windows_[w] = info;
+  if (r_.shuffle)
+    keys_[w] = host_feistel_keys(r_.seed, host_window_perm_key(static_cast<uint64_t>(info.producer), info.seq),
+                                 static_cast<uint64_t>(r_.n_data[info.producer]));
+  return 0;
+}
+
+int BatchEngine::enqueue(int64_t w, int64_t local, const StagedInfo& info, Pending* out) {
+  if (free_slots_.empty()) return -2;
+  const int64_t slot = free_slots_.front();
+  free_slots_.pop_front();
+  const auto& dst = slots_[slot];
+  const void* src = buffers_[info.buffer];
+  uint64_t t0 = clock_ns();
+  if (ready_waited_ != w) {  // once per window: every batch of it is on the batch stream behind this wait
+    if (hipStreamWaitEvent(bs_, ready_[info.buffer], 0) != hipSuccess) return -1;
+    ready_waited_ = w;
+  }
+  uint64_t t1 = clock_ns();
+  streamwait_ns_ += t1 - t0;
+  RowIndex ri{};
+  ri.base = local * r_.batch;
+  if (r_.shuffle) {
+    ri.mode = 2;
+    ri.keys = keys_.at(w);
+  } else {
+    ri.mode = 0;
+    ri.keys.n = 1;
+    ri.keys.half_bits = 1;
+  }
+  int rc;
+  if (r_.kind == 2) {  // token window: outputs ids, mask, pos (+ seg, cu)
+    const uint8_t* win = static_cast<const uint8_t*>(src);
+    TokenSpec sp{};
+    sp.tokens = reinterpret_cast<const int32_t*>(win + r_.off_tokens);
+    sp.out_tokens = static_cast<int32_t*>(dst[0]);
+    sp.attn_mask = static_cast<uint8_t*>(dst[1]);
+    sp.position_ids = dst[2];
+    sp.pos_is_i64 = 1;
+    sp.seq_len = r_.seq_len;
+    sp.pad_id = r_.pad_id;
+    sp.mode = r_.token_mode;
+    if (r_.token_mode == 0) {
+      sp.offsets = reinterpret_cast<const int64_t*>(win + r_.off_offsets);
+      sp.rows = r_.batch;
+      rc = pad_pack_tokens(sp, bs_);
+    } else {
+      sp.row_start = reinterpret_cast<const int64_t*>(win + r_.off_row_start);
+      sp.row_end = reinterpret_cast<const int64_t*>(win + r_.off_row_end);
+      sp.seg_offsets = reinterpret_cast<const int64_t*>(win + r_.off_seg_offsets);
+      sp.n_seg = info.tag[2];
+      sp.segment_ids = static_cast<int32_t*>(dst[3]);
+      sp.cu_seqlens_out = static_cast<int32_t*>(dst[4]);
+      sp.rows = info.tag[1];
+      rc = sp.rows > 0 ? pad_pack_tokens(sp, bs_)
+                       : (hipMemsetAsync(dst[4], 0, sizeof(int32_t), bs_) == hipSuccess ? 0 : -1);
+    }
+  } else if (r_.kind == 0) {
+    rc = gather_rows(dst[0], r_.out_dt, src, r_.in_dt, r_.batch, r_.row_elems, ri, r_.aff, 0, r_.max_blocks, bs_);
+  } else {
+    SplitSpec sp{};
+    sp.n_groups = static_cast<int32_t>(r_.widths.size());
+    sp.out_dt = r_.out_dt;
+    for (int g = 0; g < sp.n_groups; ++g) {
+      sp.dst[g] = dst[g];
+      sp.width[g] = r_.widths[g];
+    }
+    rc = split_columns(sp, src, r_.in_dt, r_.batch, r_.row_elems, ri, bs_);
+  }
+  if (rc != 0) return -1;
+  const uint64_t t2 = clock_ns();
+  launch_ns_ += t2 - t1;
+  const int ev = next_event_;
+  next_event_ = (next_event_ + 1) % kBatchEvents;
+  if (hipEventRecord(batch_events_[ev], bs_) != hipSuccess) return -1;
+  record_ns_ += clock_ns() - t2;
+  *out = Pending{w, local, slot, ev};
+  return 0;
+}
+
+int64_t BatchEngine::get(int64_t w, int64_t local, int64_t bpw, bool next_ok, hipStream_t compute,
+                         int64_t timeout_ms, int32_t* failed_producer, int64_t* tags) {
+  const uint64_t g0 = clock_ns();
+  int rc = acquire(w, timeout_ms, failed_producer);
+  if (rc != 0) return -(10 + rc);
+  if (tags != nullptr) {
+    const StagedInfo& wi = windows_.at(w);
+    for (int k = 0; k < 4; ++k) tags[k] = wi.tag[k];
+  }
+  Pending cur{};
+  bool have = false;
+  while (!pending_.empty()) {  // lookahead in schedule order; anything older than (w, local) is stale
+    Pending p = pending_.front();
+    pending_.pop_front();
+    if (p.w == w && p.local == local) {
+      cur = p;
+      have = true;
+      ++hits_;
+      break;
+    }
+  }
+  if (!have) {
+    rc = enqueue(w, local, windows_.at(w), &cur);
+    if (rc != 0) return rc;
+  }
+  const uint64_t s0 = clock_ns();
+  // A batch kernel that already retired needs no cross-stream dependency (its writes are visible to
+  // every later dispatch on the device); only a pending one costs the compute stream a barrier.
+  const hipError_t q = hipEventQuery(batch_events_[cur.ev]);
+  if (q == hipErrorNotReady) {
+    if (hipStreamWaitEvent(compute, batch_events_[cur.ev], 0) != hipSuccess) return -1;
+    ++waits_;
+  } else if (q != hipSuccess) {
+    return -1;
+  }
+  streamwait_ns_ += clock_ns() - s0;
+  ++batches_;
+  // lookahead: the next batch of this window, or the first of the next one if it is already staged
+  Pending nxt{};
+  if (local + 1 < bpw) {
+    if (enqueue(w, local + 1, windows_.at(w), &nxt) == 0) pending_.push_back(nxt);
+  } else if (next_ok) {
+    const StagedInfo* ni = acquired(w + 1);
+    StagedInfo peeked;
+    if (ni == nullptr && stager_->peek(w + 1, &peeked)) {
+      int32_t fp = -1;
+      if (acquire(w + 1, 0, &fp) == 0) ni = acquired(w + 1);
+    }
+    if (ni != nullptr && enqueue(w + 1, 0, *ni, &nxt) == 0) pending_.push_back(nxt);
+  }
+  get_ns_ += clock_ns() - g0;
+  return cur.slot;
+}
+
+int BatchEngine::release(int64_t w) {
+  auto it = windows_.find(w);
+  if (it == windows_.end()) return 0;
+  const int b = it->second.buffer;
+  // a window no batch was built from still has its copy in flight: the free event follows it too
+  if (hipStreamWaitEvent(bs_, ready_[b], 0) != hipSuccess) return -1;
+  hipEvent_t ev = free_events_[b][free_next_[b]];
+  free_next_[b] = (free_next_[b] + 1) % kFreeEvents;
+  if (hipEventRecord(ev, bs_) != hipSuccess) return -1;
+  stager_->release(w, ev);
+  windows_.erase(it);
+  keys_.erase(w);
+  while (!pending_.empty() && pending_.front().w <= w) pending_.pop_front();
+  return 0;
+}
+
+void BatchEngine::reset() {
+  ready_waited_ = -1;
+  pending_.clear();
+  windows_.clear();
+  keys_.clear();
+}
+
+}  // namespace ddl

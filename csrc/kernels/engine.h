@@ -1,0 +1,134 @@
+// Native per-batch dispatch of the window loader (the consumer hot path of the
+// reference, ddl/mpi_dataloader.py:179-227, moved out of Python).
+//
+// The reference hands out zero-copy numpy views per batch (~5.6 us host cost).
+// The MI355X path has more to do per batch: make the compute stream wait for
+// the batch (device side), enqueue the NEXT batch's fused gather/cast/split
+// kernel on the high-priority batch stream behind its window's HBM-ready
+// event, keep the window schedule's lookahead, and hand windows back to the
+// native stager with a free event. In Python that was ~50-80 us per batch;
+// here one call does it:
+//
+//   get(w, local, bpw, next_ok, compute_stream)
+//     acquire window w from the NativeStager (blocks only if not staged yet)
+//     pop batch (w, local) from the lookahead queue, or enqueue it now
+//     hipStreamWaitEvent(compute_stream, batch_event)
+//     enqueue the lookahead batch (w, local+1), or (w+1, 0) if w+1 is staged
+//     -> output slot id
+//   release(w): batch stream waits for w's copy, records a free event, hands
+//     the ring buffer back to the stager (which re-fills it after that event)
+//
+// Outputs are NOT allocated here: Python provides blocks of output slots (one
+// torch.empty per block, amortised over many batches, allocated on the batch
+// stream); a slot is used once and never reused by the engine, so a batch the
+// user keeps stays valid for as long as they keep it.
+//
+// Permutation keys: per window visit (producer p, round seq) the Feistel keys
+// of (seed, window_perm_key(p, seq)) -- bit-identical to ddl_amd/permutation.py
+// and ddl_amd/dataloader.py:window_perm_key (tests compare against the Python
+// path).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <deque>
+#include <map>
+#include <vector>
+
+#include "common.h"
+#include "stager.h"
+
+namespace ddl {
+
+struct BatchRecipe {
+  int32_t kind = 0;       // 0: gather_rows (one output), 1: split_columns (n groups)
+  int32_t in_dt = 0;      // window dtype code
+  int32_t out_dt = 0;     // output dtype code
+  int32_t shuffle = 0;    // 1: per-window-visit Feistel permutation of the rows
+  int64_t batch = 0;      // rows per batch
+  int64_t row_elems = 0;  // elements per row (gather) / n_values (split)
+  uint64_t seed = 0;
+  int64_t max_blocks = 0;
+  std::vector<int64_t> n_data;  // rows per producer window
+  std::vector<int32_t> widths;  // split groups
+  Affine aff{};                 // gather normalisation (aff.enabled = 0: none)
+  // kind 2 (token windows, ddl_amd/models/tokens.py): pad (0) or pack (1) with the
+  // pad_pack_tokens kernel; byte offsets of the window regions; outputs per slot:
+  // input_ids i32, attention_mask u8, position_ids i64 (+ segment_ids i32, cu_seqlens i32)
+  int32_t token_mode = 0;
+  int32_t pad_id = 0;
+  int64_t seq_len = 0;
+  int64_t off_offsets = 0, off_row_start = 0, off_row_end = 0, off_seg_offsets = 0, off_tokens = 0;
+};
+
+class BatchEngine {
+ public:
+  // `stager` outlives the engine; `ready` are the stager's per-ring-buffer events
+  // (recorded when a window's H2D copy retires); `buffers` the ring buffers.
+  BatchEngine(NativeStager* stager, BatchRecipe recipe, int32_t n_producers, std::vector<void*> buffers,
+              std::vector<hipEvent_t> ready, hipStream_t batch_stream, int device);
+  ~BatchEngine();
+  BatchEngine(const BatchEngine&) = delete;
+  BatchEngine& operator=(const BatchEngine&) = delete;
+
+  // Append output slots: one vector of output pointers (one per group) per slot.
+  void provide(const std::vector<std::vector<void*>>& slots);
+  int64_t slots_left() const { return static_cast<int64_t>(free_slots_.size()); }
+
+  // Batch `local` of window `w` (bpw batches; next_ok: a window w+1 follows in this run).
+  // Returns its slot id (>= 0), or a negative code: -(10 + stager wait code) when the window
+  // could not be acquired (see NativeStager::wait; *failed_producer names the producer),
+  // -1 HIP error, -2 no free output slot. `tags` (if not null) receives the window's 4 publish tags.
+  int64_t get(int64_t w, int64_t local, int64_t bpw, bool next_ok, hipStream_t compute, int64_t timeout_ms,
+              int32_t* failed_producer, int64_t* tags = nullptr);
+  // Make window w available without building a batch (skipped windows at a partial epoch end).
+  int acquire(int64_t w, int64_t timeout_ms, int32_t* failed_producer);
+  // The consumer is done with window w: hand its ring buffer back (after every batch kernel
+  // that reads it; no-op if w was never acquired).
+  int release(int64_t w);
+  // Drop the lookahead (seek / shutdown); the batch stream is NOT synchronised here.
+  void reset();
+
+  double wait_s() const { return wait_ns_ * 1e-9; }
+  // host ns spent in get() in total, and inside HIP calls: kernel launches, event records, stream waits
+  std::vector<uint64_t> timing_ns() const { return {get_ns_, launch_ns_, record_ns_, streamwait_ns_}; }
+  uint64_t batches() const { return batches_; }
+  uint64_t lookahead_hits() const { return hits_; }
+  uint64_t compute_waits() const { return waits_; }  // batches the compute stream had to wait for on the device
+
+ private:
+  struct Pending {
+    int64_t w, local, slot;
+    int ev;
+  };
+  int enqueue(int64_t w, int64_t local, const StagedInfo& info, Pending* out);
+  const StagedInfo* acquired(int64_t w);
+
+  NativeStager* stager_;
+  BatchRecipe r_;
+  int32_t P_;
+  std::vector<void*> buffers_;
+  std::vector<hipEvent_t> ready_;
+  hipStream_t bs_;
+  int device_;
+  std::map<int64_t, StagedInfo> windows_;     // acquired, not yet released
+  std::map<int64_t, FeistelKeys> keys_;       // per acquired window (shuffle)
+  std::deque<Pending> pending_;               // lookahead, in enqueue order
+  std::deque<int64_t> free_slots_;
+  std::vector<std::vector<void*>> slots_;     // slot id -> output pointers
+  std::vector<hipEvent_t> batch_events_;      // ring
+  int next_event_ = 0;
+  std::vector<std::vector<hipEvent_t>> free_events_;  // per ring buffer, a small ring of free events
+  std::vector<int> free_next_;
+  uint64_t wait_ns_ = 0, batches_ = 0, hits_ = 0, waits_ = 0;
+  uint64_t get_ns_ = 0, launch_ns_ = 0, record_ns_ = 0, streamwait_ns_ = 0;
+  int64_t ready_waited_ = -1;  // window whose HBM-ready event the batch stream already waits on
+};
+
+// Host derivation of the Feistel round keys of (seed, key) -- ddl_amd/permutation.py round_keys --
+// and of the per-window-visit key (producer, round) -- dataloader.window_perm_key.
+FeistelKeys host_feistel_keys(uint64_t seed, uint64_t key, uint64_t n);
+uint64_t host_window_perm_key(uint64_t producer, uint64_t round);
+
+}  // namespace ddl

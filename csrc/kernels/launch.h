@@ -91,6 +91,27 @@ struct TokenSpec {
 };
 int pad_pack_tokens(const TokenSpec& spec, hipStream_t st);
 
+// bucket.hip ----------------------------------------------------------------
+// Owner bucketing of a global batch for the resident loader's exchange: positions
+// [pos0, pos0 + count) of the Feistel permutation `keys`, sample idx owned by rank
+// idx / shard_rows. bucket_send writes this rank's samples (idx - lo) in position
+// order (count = GB); bucket_recv maps each position of this rank's slice
+// (count = LB) to its row in the all-to-all receive buffer, whose block from
+// source q starts at offsets[q].
+constexpr int kMaxBucketWorld = 64;
+struct BucketSpec {
+  FeistelKeys keys;
+  int64_t pos0;
+  int64_t count;
+  int64_t shard_rows;
+  int64_t lo;
+  int32_t rank;
+  int32_t world;
+  int64_t offsets[kMaxBucketWorld];
+};
+int bucket_send(const BucketSpec& sp, int64_t* send_rows, hipStream_t st);
+int bucket_recv(const BucketSpec& sp, int64_t* inv, hipStream_t st);
+
 // misc.hip ------------------------------------------------------------------
 // Sum of the 32-bit words of [ptr, ptr+bytes) added into *out (u64). Two
 // stages through `scratch` (>= kChecksumMaxBlocks u64). Debug batch checksums

@@ -192,6 +192,31 @@ PYBIND11_MODULE(_ddl_runtime, m) {
       py::arg("keys"), py::arg("half_bits"), py::arg("n"), py::arg("positions"),
       "perm(positions) of the 6-round Feistel permutation (bit-identical to the gfx950 kernels)");
   m.def(
+      "owner_counts",
+      [](std::vector<uint64_t> keys, uint32_t half_bits, uint64_t n, int64_t pos0, int64_t gb, int64_t lb,
+         int64_t shard_rows, int64_t world, int64_t rank) {
+        if (keys.size() != ddl::kHostFeistelRounds) throw std::invalid_argument("owner_counts: need 6 round keys");
+        if (lb <= 0 || shard_rows <= 0 || world < 1 || rank < 0 || rank >= world || pos0 < 0 ||
+            static_cast<uint64_t>(pos0 + gb) > n)
+          throw std::invalid_argument("owner_counts: bad geometry");
+        std::vector<int64_t> send(world, 0), recv(world, 0);
+        {
+          py::gil_scoped_release nogil;
+          for (int64_t i = 0; i < gb; ++i) {
+            const int64_t idx = static_cast<int64_t>(
+                ddl::host_feistel_perm(static_cast<uint64_t>(pos0 + i), keys.data(), half_bits, n));
+            const int64_t owner = idx / shard_rows, dest = i / lb;
+            if (owner == rank) ++send[dest];
+            if (dest == rank) ++recv[owner];
+          }
+        }
+        return py::make_tuple(send, recv);
+      },
+      py::arg("keys"), py::arg("half_bits"), py::arg("n"), py::arg("pos0"), py::arg("gb"), py::arg("lb"),
+      py::arg("shard_rows"), py::arg("world"), py::arg("rank"),
+      "(send_counts, recv_counts) of one global batch: samples this rank sends to / receives from every rank "
+      "(sample idx lives on rank idx / shard_rows, position i goes to rank i / lb)");
+  m.def(
       "parallel_copy",
       [](uintptr_t dst, uintptr_t src, uint64_t bytes, int n_threads) {
         py::gil_scoped_release nogil;

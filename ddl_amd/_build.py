@@ -107,7 +107,8 @@ def build_hip(force: bool = False, jobs: int = 8) -> str:
     binding = os.path.join(CSRC, "kernels", "bindings.cpp")
     # host-only C++ compiled into the HIP module: the native stager and its own copy
     # of the arena implementation (it drives the consumer's Arena object by address)
-    host_srcs = [os.path.join(CSRC, "kernels", "stager.cpp"), os.path.join(CSRC, "runtime", "arena.cpp")]
+    host_srcs = [os.path.join(CSRC, "kernels", "stager.cpp"), os.path.join(CSRC, "kernels", "engine.cpp"),
+                 os.path.join(CSRC, "runtime", "arena.cpp")]
     headers = headers + [os.path.join(CSRC, "runtime", "arena.h")]
 
     jobs_list: list[tuple[list[str], str]] = []

@@ -134,6 +134,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
         copy_batches: bool | None = None,
         collate: str | None = None,
         pad_id: int = 0,
+        native_dispatch: bool = True,
     ):
         if mode not in MODES:
             raise ValueError(f"unknown mode {mode!r}; one of {MODES}")
@@ -172,6 +173,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
         self.debug_checksum = debug_checksum
         self.metrics = LoaderMetrics()
         self.timeout_s = timeout_s if timeout_s is not None else (connection.timeout_s if connection else 600.0)
+        self._timeout_ms = int(self.timeout_s * 1000)
         self.checksums: list[int] = []
         self._pending = False
 
@@ -203,6 +205,8 @@ class DistributedDataLoader(DistributedDataloaderABC):
         self._lookahead: dict = {}
         self._host_window: int | None = None  # host path: window currently held
         self._cur = None                      # device path: StagedWindow of the current window
+        self.native_dispatch = bool(native_dispatch)
+        self._engine = None                   # native per-batch dispatch (csrc/kernels/engine.cpp)
 
         if connection is None or connection.n_producers == 0:
             # Reference behaviour for a single-rank run: nothing to iterate (ddl/mpi_dataloader.py:173-174).
@@ -268,7 +272,170 @@ class DistributedDataLoader(DistributedDataloaderABC):
             connection.add_finalizer(self._stager.close)  # stop the native thread before the arena is unpinned
             if self._produces_copy():
                 self._batch_stream = streams.batch_stream(self.device)
+                self._make_engine()
         self._update_len()
+
+    # ------------------------------------------------------ native dispatch
+    def _engine_recipe(self) -> dict | None:
+        """The batch recipe when the native engine can build batches exactly like ``_batch_from_window``:
+        a fused gather (one output) or a contiguous column split, no exchange / collate / augment."""
+        if (not self.native_dispatch or self._exchange_fn is not None or self.augment is not None
+                or self._batch_stream is None):
+            return None
+        if self.collate == "tokens":
+            return self._token_recipe()
+        if self.collate is not None:
+            return None
+        norm = self.normalize
+        if norm is not None and norm.get("layout", "chw") == "hwc":
+            return None
+        wdt = self.window_dtype
+        out_dtype = self.out_dtype or (torch.float32 if norm is not None else wdt)
+        splits = list(self.splits[0])
+        rec = dict(in_dt=_dtypes.code(wdt), out_dt=_dtypes.code(out_dtype), shuffle=self.shuffle == "device",
+                   batch=self.batch_size, seed=self.seed & ((1 << 64) - 1), max_blocks=0, scale=[], bias=[],
+                   plane=0, n_data=[int(x.nData) for x in self.metadata_from_producer], widths=[])
+        if (self.contiguous or self.copy_batches) and len(splits) > 1 and len(self.sample_shape) == 1 \
+                and norm is None:
+            if out_dtype != wdt and out_dtype not in (torch.bfloat16, torch.float32):
+                return None
+            rec.update(kind=1, row_elems=int(self.sample_shape[0]), widths=[int(w) for w in splits],
+                       out_shapes=[(self.batch_size, int(w)) for w in splits], out_dtype=out_dtype)
+            return rec
+        if len(splits) != 1:
+            return None  # gather + split views: Python path
+        if self.shuffle != "device" and out_dtype == wdt and norm is None and not self.copy_batches:
+            return None  # zero-copy view of the window
+        if out_dtype != wdt and (out_dtype not in (torch.bfloat16, torch.float16, torch.float32)
+                                 or wdt not in (torch.uint8, torch.float32, torch.bfloat16, torch.float16)):
+            return None  # a conversion the gather kernel does not do: the Python path reports it
+        if norm is not None:
+            plane = int(math.prod(self.sample_shape[1:])) if len(self.sample_shape) > 1 else 1
+            c = self.sample_shape[0] if len(self.sample_shape) > 1 else len(norm.get("mean", [0]))
+            sc, bi = ops.norm_affine(c, norm.get("mean"), norm.get("std"), norm.get("scale"), norm.get("bias"),
+                                     ops.pixel_max(wdt))
+            if out_dtype in (torch.uint8, torch.int32, torch.int64):
+                return None
+            rec.update(scale=[float(x) for x in sc], bias=[float(x) for x in bi], plane=plane)
+        rec.update(kind=0, row_elems=int(math.prod(self.sample_shape)) if self.sample_shape else 1,
+                   out_shapes=[(self.batch_size,) + tuple(self.sample_shape)], out_dtype=out_dtype)
+        return rec
+
+    def _token_recipe(self) -> dict | None:
+        """Token windows (models/tokens.py): the pad/pack kernel straight from the staged window."""
+        from .models.tokens import TokenWindowLayout
+
+        ex = [m.extra for m in self.metadata_from_producer]
+        if any(e.get("token_layout") != ex[0].get("token_layout") or e.get("token_mode") != ex[0].get("token_mode")
+               for e in ex):
+            return None
+        lay = TokenWindowLayout(**ex[0]["token_layout"])
+        mode = ex[0]["token_mode"]
+        reg = lay.regions()
+        S = lay.seq_len
+        rows = lay.batch if mode == "pad" else lay.max_segments
+        outs = [((rows, S), torch.int32), ((rows, S), torch.uint8), ((rows, S), torch.int64)]
+        if mode == "pack":
+            outs += [((rows, S), torch.int32), ((lay.max_segments + 1,), torch.int32)]
+        token = [0 if mode == "pad" else 1, int(self.pad_id), S, reg["offsets"][0], reg["row_start"][0],
+                 reg["row_end"][0], reg["seg_offsets"][0], reg["tokens"][0]]
+        return dict(kind=2, in_dt=_dtypes.code(torch.int32), out_dt=_dtypes.code(torch.int32), shuffle=False,
+                    batch=lay.batch, row_elems=1, seed=0, max_blocks=0, scale=[], bias=[], plane=0,
+                    n_data=[int(x.nData) for x in self.metadata_from_producer], widths=[], token=token,
+                    outputs=outs, token_mode=mode)
+
+    def _make_engine(self) -> None:
+        rec = self._engine_recipe()
+        if rec is None:
+            self._engine = None
+            return
+        import collections
+
+        from . import _native
+
+        st = self._stager
+        if "outputs" in rec:
+            self._eng_outputs = rec.pop("outputs")
+        else:
+            dt = rec.pop("out_dtype")
+            self._eng_outputs = [(sh, dt) for sh in rec.pop("out_shapes")]
+        self._eng_tokens = rec.pop("token_mode", None)
+        self._engine = _native.hip().BatchEngine(
+            st._native, n_producers=self.connection.n_producers, buffers=[b.data_ptr() for b in st.buffers],
+            ready=[e.cuda_event for e in st.ready_events], batch_stream=self._batch_stream.cuda_stream,
+            device=self.device.index, **rec)
+        # byte layout of one slot: every output 256-byte aligned (views of one uint8 block)
+        self._eng_layout, off = [], 0
+        for sh, dt in self._eng_outputs:
+            self._eng_layout.append((off, sh, dt))
+            off += -(-math.prod(sh) * _dtypes.itemsize(dt) // 256) * 256
+        self._eng_slot_bytes = max(256, off)
+        self._eng_block = int(min(64, max(4, (512 << 20) // self._eng_slot_bytes)))
+        self._eng_slots: collections.deque = collections.deque()  # (slot id, outputs, block)
+        self._eng_next_id = 0
+        self._eng_rec = (None, None)  # (block, stream) of the last record_stream
+        self._eng_window = None
+
+    def _engine_provide(self) -> None:
+        """One allocation (on the batch stream) for a block of output slots; each slot is used once."""
+        K, sb = self._eng_block, self._eng_slot_bytes
+        with streams.on_stream(self._batch_stream):
+            block = torch.empty(K * sb, dtype=torch.uint8, device=self.device)
+        ptrs = []
+        for k in range(K):
+            outs = tuple(block[k * sb + off:k * sb + off + math.prod(sh) * _dtypes.itemsize(dt)].view(dt).view(sh)
+                         for off, sh, dt in self._eng_layout)
+            ptrs.append([t.data_ptr() for t in outs])
+            self._eng_slots.append((self._eng_next_id + k, outs, block))
+        self._eng_next_id += K
+        self._engine.provide(ptrs)
+
+    def _engine_raise(self, code: int, producer: int, what: str) -> None:
+        from .exceptions import DDLError, DDLTimeoutError, PeerDeathError, ShutdownError
+
+        if code <= -10:
+            rc = -code - 10
+            if rc == 1:
+                raise ShutdownError(f"{what}: loader was shut down")
+            if rc == 2:
+                raise DDLTimeoutError(f"{what}: not staged within {self.timeout_s:.0f}s (producer {producer})")
+            pids = self.connection.producer_pids
+            pid = pids[producer] if 0 <= producer < len(pids) else None
+            if rc in (3, 4):
+                raise PeerDeathError(f"{what}: producer {producer} (pid {pid}) "
+                                     + ("reported a failure" if rc == 4 else "died"), producer, pid)
+            raise DDLError(f"{what}: {self._stager._native.error()}")
+        raise DDLError(f"{what}: native batch engine error {code}")
+
+    def _engine_batch(self, local: int, bpw: int):
+        eng = self._engine
+        if eng.slots_left < 3:
+            self._engine_provide()
+        cur = streams.current(self.device.index)
+        nxt = self.window_in_epoch + 1 < self.windows_per_epoch or self.epoch + 1 < self.n_epochs
+        slot, prod, tags = eng.get(self.window, local, bpw, nxt, cur.cuda_stream, self._timeout_ms)
+        if slot < 0:
+            self._engine_raise(slot, prod, f"batch {local} of window {self.window}")
+        if self._eng_window != self.window:
+            self._eng_window = self.window
+            self.metrics.windows += 1
+        q = self._eng_slots
+        while q[0][0] != slot:  # slots the engine skipped (dropped lookahead)
+            q.popleft()
+        _, out, block = q.popleft()
+        if self._eng_rec[0] is not block or self._eng_rec[1] is not cur:
+            block.record_stream(cur)  # the compute stream uses this block from now on
+            self._eng_rec = (block, cur)
+        if self._eng_tokens is None:
+            return out
+        n_tokens, n_rows, n_seg, max_seg = tags
+        if self._eng_tokens == "pad":
+            return {"input_ids": out[0], "attention_mask": out[1], "position_ids": out[2], "n_tokens": n_tokens}
+        if n_tokens > 0x7FFFFFFF:
+            raise ValueError(f"{n_tokens} tokens in one batch overflow int32 cu_seqlens")
+        return {"input_ids": out[0][:n_rows], "attention_mask": out[1][:n_rows], "position_ids": out[2][:n_rows],
+                "segment_ids": out[3][:n_rows], "cu_seqlens": out[4][:n_seg + 1], "max_seqlen": max_seg,
+                "n_tokens": n_tokens}
 
     # --------------------------------------------------------------- schedule
     def _schedule(self, w: int) -> tuple[int, int]:
@@ -310,6 +477,14 @@ class DistributedDataLoader(DistributedDataloaderABC):
     # ----------------------------------------------------------------- access
     def _window(self):
         """Make the current window available (device: staged; host: acquired)."""
+        if self._engine is not None:
+            if self._eng_window != self.window:
+                rc, prod = self._engine.acquire(self.window, self._timeout_ms)
+                if rc != 0:
+                    self._engine_raise(-(10 + rc), prod, f"staging window {self.window}")
+                self._eng_window = self.window
+                self.metrics.windows += 1
+            return None
         if self._stager is not None:
             if self._cur is None or self._cur.index != self.window:
                 t0 = time.perf_counter()
@@ -344,6 +519,13 @@ class DistributedDataLoader(DistributedDataloaderABC):
         local = idx - first_in_window
         if not 0 <= local < bpw:
             raise IndexError(f"batch {idx} is not in the current window (sequential access only across windows)")
+        if self._engine is not None:
+            out = self._engine_batch(local, bpw)
+            self.metrics.on_batch(self.batch_size)
+            if self.debug_checksum:
+                first = out["input_ids"] if isinstance(out, dict) else out[0]
+                self.checksums.append(int(ops.checksum(first).item()))
+            return out
         sw = self._window()
         if self._batch_stream is not None:
             out = self._device_batch(sw, p, s, local, bpw)
@@ -477,6 +659,14 @@ class DistributedDataLoader(DistributedDataloaderABC):
             raise ValueError(f"Unknown mark {mark}")
 
     def _release_window(self) -> None:
+        if self._engine is not None:
+            if self._engine.release(self.window) != 0:
+                from .exceptions import DDLError
+
+                raise DDLError(f"native batch engine: releasing window {self.window} failed")
+            if self._eng_window == self.window:
+                self._eng_window = None
+            return
         if self._stager is not None:
             stream = None
             if self._batch_stream is not None:
@@ -732,6 +922,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
                 self._batch_stream.synchronize()
             if self._stager is not None:
                 self._stager.close()  # joins the native thread; copies and their slot hand-backs retire
+                self._drop_engine()
             elif self._host_window is not None:
                 self._host_window = None  # seek_producers resets every slot, this one included
             self._cur = None
@@ -755,6 +946,8 @@ class DistributedDataLoader(DistributedDataloaderABC):
                 self.connection.add_finalizer(self._stager.close)
                 self.metrics.bytes_h2d += old.bytes_h2d
                 del old
+                if self._batch_stream is not None:
+                    self._make_engine()
             self._update_len()
             if self.batch == 0:
                 self._begin_window()
@@ -772,14 +965,39 @@ class DistributedDataLoader(DistributedDataloaderABC):
         if self._stager is not None:
             self.metrics.bytes_h2d += self._stager.bytes_h2d
             self._stager.close()
+        self._drop_engine()
         if self.connection is not None:
             self.connection.finalize()
+
+    def _drop_engine(self) -> None:
+        if self._engine is not None:
+            self.metrics.consumer_wait_s += self._engine.wait_s
+            done = getattr(self, "_native_done", {"batches": 0, "lookahead_hits": 0})
+            self._native_done = {"batches": done["batches"] + int(self._engine.batches),
+                                 "lookahead_hits": done["lookahead_hits"] + int(self._engine.lookahead_hits)}
+            self._engine.reset()
+            self._engine = None
+            self._eng_slots.clear()
 
     def close(self) -> None:
         self._finalize()
 
     def stats(self) -> dict:
         d = self.metrics.as_dict()
+        done = getattr(self, "_native_done", None)
+        if self._engine is not None or done is not None:
+            nd = dict(done or {"batches": 0, "lookahead_hits": 0})
+            if self._engine is not None:
+                d["consumer_wait_s"] += self._engine.wait_s
+                nd["batches"] += int(self._engine.batches)
+                nd["lookahead_hits"] += int(self._engine.lookahead_hits)
+                g, la, rec, sw = self._engine.timing_ns
+                n = max(1, int(self._engine.batches))
+                nd["compute_waits"] = int(self._engine.compute_waits)
+                nd["host_us_per_batch"] = {"get": round(g / n / 1e3, 2), "kernel_launch": round(la / n / 1e3, 2),
+                                           "event_record": round(rec / n / 1e3, 2),
+                                           "stream_wait": round(sw / n / 1e3, 2)}
+            d["native_dispatch"] = nd
         if self._stager is not None:
             d.update(self._stager.stats())
         if self.connection is not None:

@@ -303,6 +303,9 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
             self.shard = self._load_shard(reader, chunk_bytes, host_threads)
         self.load_s = time.perf_counter() - t0
         self.prep_stream = streams.batch_stream(self.device) if self.device.type == "cuda" else None
+        if self.device.type == "cuda" and self.W > 1:  # owner-bucketing outputs, reused every step (prep stream)
+            self._send_idx = torch.empty(self.GB, dtype=torch.int64, device=self.device)
+            self._inv_idx = torch.empty(self.LB, dtype=torch.int64, device=self.device)
 
     # ----------------------------------------------------------------- load
     def _load_shard(self, reader, chunk_bytes: int, host_threads: int) -> torch.Tensor:
@@ -342,7 +345,16 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
         """Rank ``src_rank`` streams the dataset H2D chunk by chunk and sends every
         peer the rows of its shard with grouped point-to-point ops (all peers at
         once: on an xGMI-connected node every link carries one peer's slice);
-        the other ranks receive straight into their HBM shard."""
+        the other ranks receive straight into their HBM shard.
+
+        Pipelined on the source rank, double-buffered, with no per-chunk stream
+        synchronisation: while the host reads chunk i+1 into pinned bounce buffer
+        b', the copy stream moves chunk i bounce[b] -> HBM staging[b] and the send
+        stream ships staging[b]'s slices over RCCL. The host blocks only before
+        re-filling a bounce buffer (its previous H2D must have retired); the copy
+        stream waits before re-filling a staging buffer (its previous sends must
+        have completed): read || H2D || P2P.
+        """
         import torch.distributed as dist
 
         rows = self.hi - self.lo
@@ -352,49 +364,66 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
         dist.all_reduce(probe, group=self.group)
         rows_per_chunk = max(1, chunk_bytes // self.row_bytes)
         bounds = [(q * self.S, min(self.N, (q + 1) * self.S)) for q in range(self.W)]
-        staging = None
-        if self.rank == src_rank:
-            staging = torch.empty((rows_per_chunk,) + self.sample_shape, dtype=self.src_dtype, device=self.device)
-            bounce = torch.empty(rows_per_chunk * self.row_bytes, dtype=torch.uint8,
-                                 pin_memory=self.device.type == "cuda")
+        gpu = self.device.type == "cuda"
+        src = self.rank == src_rank
+        if src:
+            staging = [torch.empty((rows_per_chunk,) + self.sample_shape, dtype=self.src_dtype, device=self.device)
+                       for _ in range(2)]
+            bounce = [torch.empty(rows_per_chunk * self.row_bytes, dtype=torch.uint8, pin_memory=gpu)
+                      for _ in range(2)]
+            if gpu:
+                copy_s, send_s = torch.cuda.Stream(self.device), torch.cuda.Stream(self.device)
+                h2d_done = [torch.cuda.Event(), torch.cuda.Event()]
+                sent = [torch.cuda.Event(), torch.cuda.Event()]
+                used = [False, False]
         with trace_range("ddl.resident.scatter"):
-            for c0 in range(0, self.N, rows_per_chunk):
+            for i, c0 in enumerate(range(0, self.N, rows_per_chunk)):
                 c1 = min(self.N, c0 + rows_per_chunk)
                 ops_ = []
-                if self.rank == src_rank:
+                if src:
+                    b = i % 2
                     nbytes = (c1 - c0) * self.row_bytes
-                    reader(c0, c1 - c0, bounce.data_ptr(), host_threads)
-                    stage = staging[: c1 - c0]
-                    stage.view(-1).view(torch.uint8)[:nbytes].copy_(bounce[:nbytes], non_blocking=True)
-                    for q, (lo, hi) in enumerate(bounds):
-                        o0, o1 = max(c0, lo), min(c1, hi)
-                        if o0 >= o1:
-                            continue
-                        piece = stage[o0 - c0:o1 - c0]
-                        if q == self.rank:
-                            shard[o0 - lo:o1 - lo].copy_(piece)
-                        else:
-                            ops_.append(dist.P2POp(dist.isend, piece.contiguous(), q, group=self.group))
-                    self.bytes_exchanged += sum(p.tensor.numel() * p.tensor.element_size() for p in ops_)
+                    if gpu and used[b]:
+                        h2d_done[b].synchronize()  # bounce[b]'s previous H2D retired
+                    reader(c0, c1 - c0, bounce[b].data_ptr(), host_threads)
+                    stage = staging[b][: c1 - c0]
+                    if gpu:
+                        if used[b]:
+                            copy_s.wait_event(sent[b])  # staging[b]'s previous sends completed
+                        with streams.on_stream(copy_s):
+                            stage.view(-1).view(torch.uint8)[:nbytes].copy_(bounce[b][:nbytes], non_blocking=True)
+                        h2d_done[b].record(copy_s)
+                        send_s.wait_event(h2d_done[b])
+                        used[b] = True
+                    else:
+                        stage.view(-1).view(torch.uint8)[:nbytes].copy_(bounce[b][:nbytes])
+                    ctx = streams.on_stream(send_s) if gpu else contextlib.nullcontext()
+                    with ctx:
+                        for q, (lo, hi) in enumerate(bounds):
+                            o0, o1 = max(c0, lo), min(c1, hi)
+                            if o0 >= o1:
+                                continue
+                            piece = stage[o0 - c0:o1 - c0]
+                            if q == self.rank:
+                                shard[o0 - lo:o1 - lo].copy_(piece)
+                            else:
+                                ops_.append(dist.P2POp(dist.isend, piece, q, group=self.group))
+                        self.bytes_exchanged += sum(p.tensor.numel() * p.tensor.element_size() for p in ops_)
+                        if ops_:  # point-to-point (pairwise), not a collective: no ledger entry
+                            for req in dist.batch_isend_irecv(ops_):
+                                req.wait()  # the send stream (not the host) waits for the sends
+                        if gpu:
+                            sent[b].record(send_s)
                 else:
                     o0, o1 = max(c0, self.lo), min(c1, self.hi)
                     if o0 < o1:
                         ops_.append(dist.P2POp(dist.irecv, shard[o0 - self.lo:o1 - self.lo], src_rank,
                                                group=self.group))
-                if ops_:
-                    for req in dist.batch_isend_irecv(ops_):
-                        req.wait()
-                if self.rank == src_rank and self.device.type == "cuda":
-                    torch.cuda.current_stream(self.device).synchronize()  # bounce/staging reuse
-        if self.device.type == "cuda":
+                        for req in dist.batch_isend_irecv(ops_):
+                            req.wait()
+        if gpu:
             torch.cuda.synchronize(self.device)
         return shard
-
-    def _to_dev(self, a: np.ndarray) -> torch.Tensor:
-        t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.int64))
-        if self.device.type == "cuda":
-            return t.pin_memory().to(self.device, non_blocking=True)
-        return t
 
     def _assemble(self, t: int) -> tuple[torch.Tensor, Any]:
         """Enqueue the assembly of global step t = epoch*bpe + g; returns (batch, ready event)."""
@@ -414,30 +443,42 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
                     batch = ops.gather_rows(self.shard, perm=perm, base=g * self.GB, n_rows=self.LB,
                                             out_dtype=self.out_dtype, **kw)
             else:
-                pos = np.arange(g * self.GB, (g + 1) * self.GB, dtype=np.int64)
-                idx_all = perm(pos)
-                owner = idx_all // self.S
-                send_mask = owner == self.rank
-                send_rows = idx_all[send_mask] - self.lo
-                dest = (np.nonzero(send_mask)[0] // self.LB)
-                send_counts = np.bincount(dest, minlength=self.W).tolist()
-                mine = owner[self.rank * self.LB:(self.rank + 1) * self.LB]
-                order_k = np.argsort(mine, kind="stable")
-                recv_counts = np.bincount(mine, minlength=self.W).tolist()
-                inv = np.empty(self.LB, dtype=np.int64)
-                inv[order_k] = np.arange(self.LB)
-                send = ops.gather_rows(self.shard, index=self._to_dev(send_rows)) if len(send_rows) else \
+                # W split counts on the host (native Feistel over the GB positions, no numpy); the send list
+                # and the receive map by the owner-bucketing kernels on the prep stream (csrc/kernels/bucket.hip)
+                pos0 = g * self.GB
+                mine0 = pos0 + self.rank * self.LB
+                send_counts, recv_counts = _native.runtime().owner_counts(
+                    perm.keys, perm.half_bits, self.N, pos0, self.GB, self.LB, self.S, self.W, self.rank)
+                n_send = sum(send_counts)
+                if self.device.type == "cuda":
+                    hip, stream = _native.hip(), self.prep_stream.cuda_stream
+                    hip.bucket_send(perm.keys, self.N, perm.half_bits, pos0, self.GB, self.S, self.lo, self.rank,
+                                    self.W, self._send_idx.data_ptr(), stream)
+                    offsets = np.concatenate([[0], np.cumsum(recv_counts)[:-1]]).tolist()
+                    hip.bucket_recv(perm.keys, self.N, perm.half_bits, mine0, self.LB, self.S, self.W, offsets,
+                                    self._inv_idx.data_ptr(), stream)
+                    send_idx, inv = self._send_idx[:n_send], self._inv_idx
+                else:  # CPU rehearsal: the same maps in numpy
+                    idx_all = perm(np.arange(pos0, pos0 + self.GB, dtype=np.int64))
+                    owner = idx_all // self.S
+                    send_idx = torch.from_numpy(idx_all[owner == self.rank] - self.lo)
+                    mine = owner[self.rank * self.LB:(self.rank + 1) * self.LB]
+                    inv_np = np.empty(self.LB, dtype=np.int64)
+                    inv_np[np.argsort(mine, kind="stable")] = np.arange(self.LB)
+                    inv = torch.from_numpy(inv_np)
+                send = ops.gather_rows(self.shard, index=send_idx) if n_send else \
                     torch.empty((0,) + self.sample_shape, dtype=self.src_dtype, device=self.device)
                 recv = torch.empty((self.LB,) + self.sample_shape, dtype=self.src_dtype, device=self.device)
                 LEDGER.record("resident.all_to_all", t)
                 dist.all_to_all_single(recv.view(self.LB, -1), send.view(send.shape[0], -1), recv_counts,
                                        send_counts, group=self.group)
-                self.bytes_exchanged += (len(send_rows) - send_counts[self.rank]) * self.row_bytes
+                self.bytes_exchanged += (n_send - send_counts[self.rank]) * self.row_bytes
                 if self.augment is not None:  # crop keyed by the global sample id, not the recv row
-                    ids = self._to_dev(idx_all[self.rank * self.LB:(self.rank + 1) * self.LB])
-                    batch = self._crop(recv, e, index=self._to_dev(inv), sample_ids=ids)
+                    ids = ops.feistel_indices(perm, mine0, self.LB, device=self.device) \
+                        if self.device.type == "cuda" else torch.from_numpy(perm(np.arange(mine0, mine0 + self.LB)))
+                    batch = self._crop(recv, e, index=inv, sample_ids=ids)
                 else:
-                    batch = ops.gather_rows(recv, index=self._to_dev(inv), out_dtype=self.out_dtype, **kw)
+                    batch = ops.gather_rows(recv, index=inv, out_dtype=self.out_dtype, **kw)
             ev = None
             if self.prep_stream is not None:
                 ev = torch.cuda.Event()

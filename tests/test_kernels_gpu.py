@@ -373,3 +373,33 @@ def test_random_resized_crop_sample_ids_key_the_crop():
     assert torch.equal(ba, bb) and torch.equal(a, b)
     with pytest.raises(ValueError):
         ops.random_resized_crop(src, index=ids, sample_ids=ids[:4], **kw)
+
+
+@pytest.mark.parametrize("n,gb,world", [(777, 48, 4), (100_000, 2048, 8), (5000, 512, 2), (64, 64, 64)])
+def test_owner_bucketing_kernels_match_numpy(n, gb, world):
+    """bucket_send / bucket_recv (csrc/kernels/bucket.hip) against the numpy maps of the resident exchange,
+    for every rank of the world (the kernels are per-rank; no collective needed)."""
+    from ddl_amd import _native
+    from ddl_amd.permutation import FeistelPermutation
+
+    hip, rt = _native.hip(), _native.runtime()
+    lb, shard = gb // world, -(-n // world)
+    st = torch.cuda.current_stream().cuda_stream
+    for g in range(min(2, n // gb)):
+        px = FeistelPermutation(n, 9, g)
+        idx = px(np.arange(g * gb, (g + 1) * gb))
+        owner = idx // shard
+        for rank in range(world):
+            send_counts, recv_counts = rt.owner_counts(px.keys, px.half_bits, n, g * gb, gb, lb, shard, world, rank)
+            send = torch.full((gb,), -1, dtype=torch.int64, device=_dev())
+            inv = torch.full((lb,), -1, dtype=torch.int64, device=_dev())
+            hip.bucket_send(px.keys, n, px.half_bits, g * gb, gb, shard, rank * shard, rank, world, send.data_ptr(), st)
+            offs = np.concatenate([[0], np.cumsum(recv_counts)[:-1]]).tolist()
+            hip.bucket_recv(px.keys, n, px.half_bits, g * gb + rank * lb, lb, shard, world, offs, inv.data_ptr(), st)
+            ref_send = idx[owner == rank] - rank * shard
+            mine = owner[rank * lb:(rank + 1) * lb]
+            ref_inv = np.empty(lb, dtype=np.int64)
+            ref_inv[np.argsort(mine, kind="stable")] = np.arange(lb)
+            assert sum(send_counts) == len(ref_send)
+            assert np.array_equal(send.cpu().numpy()[:len(ref_send)], ref_send)
+            assert np.array_equal(inv.cpu().numpy(), ref_inv)

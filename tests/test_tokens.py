@@ -255,3 +255,34 @@ def test_cu_seqlens_drive_varlen_attention(corpus, monkeypatch):
             got = _varlen_attention(emb[stream], cu)
             want = torch.cat([_attention(emb[torch.from_numpy(c.astype(np.int64))]) for c in segs])
             torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["pad", "pack"])
+def test_token_native_dispatch_matches_python_path(corpus, mode):
+    """Native batch engine (kind 2: pad/pack kernel straight from the staged window) == the Python collate."""
+    seq_len, gb = 256, 16
+
+    def run(native):
+        out = []
+        with ddl_amd.start(n_producers=2) as (env, conn):
+            dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(corpus, gb, seq_len, mode), gb, conn, 2,
+                                               mode="indexed", env=env, auto_mark=True, collate="tokens", seed=4,
+                                               native_dispatch=native)
+            for _ in range(2):
+                for b in dl:
+                    out.append({k: (v.cpu().clone() if isinstance(v, torch.Tensor) else v) for k, v in b.items()})
+            st = dl.stats()
+        return out, st
+
+    nat, st = run(True)
+    ref, st_ref = run(False)
+    assert st["native_dispatch"]["batches"] == len(nat) and "native_dispatch" not in st_ref
+    assert len(nat) == len(ref) > 0
+    for a, b in zip(nat, ref):
+        assert a.keys() == b.keys()
+        for k in a:
+            if isinstance(a[k], torch.Tensor):
+                assert a[k].dtype == b[k].dtype and torch.equal(a[k], b[k]), k
+            else:
+                assert a[k] == b[k], k
