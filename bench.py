@@ -81,6 +81,8 @@ def parse(argv=None):
                          "next to the headline in the JSON line ('indexed')")
     ap.add_argument("--index-samples", type=int, default=4096,
                     help="indexed order: samples in the node-shared synthetic source")
+    ap.add_argument("--dispatch", default="auto", choices=["auto", "inline", "lookahead", "python"],
+                    help="per-batch dispatch: the native engine (auto / inline / lookahead) or the Python path")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
 
@@ -288,7 +290,8 @@ def main(argv=None) -> int:
         dl = ddl_amd.DistributedDataLoader(
             producer, args.batch, conn, n_epochs, args.exchange, args.exchange_method, env.rank, env.world_size,
             env=env, device=dev, out_dtype=torch.bfloat16, shuffle=args.shuffle, seed=args.seed,
-            n_slots=args.slots, prefetch_depth=args.depth, normalize=norm)
+            n_slots=args.slots, prefetch_depth=args.depth, normalize=norm,
+            native_dispatch=False if args.dispatch == "python" else args.dispatch)
         acc = ops.ChecksumAccumulator(dev)  # one streaming launch per batch
 
         def batches():
@@ -318,10 +321,14 @@ def main(argv=None) -> int:
         w_cur0 = dl.window
         bytes_enq0 = dl._stager.bytes_h2d if dl._stager is not None else 0
         t0 = time.perf_counter()
+        host_log = os.environ.get("DDL_HOST_LOG")
+        ticks = []
         with trace_range("bench.phase1"):  # roctx: lets tools/trace_idle.py find the timed region
             for _ in range(args.steps):
                 (x,) = next(it)
                 acc.add(x)
+                if host_log:
+                    ticks.append(time.perf_counter())
             sync()
         t1 = time.perf_counter()
         w_land1, b_land1 = _landed(dl)
@@ -341,6 +348,12 @@ def main(argv=None) -> int:
             "numa_node": gpu_numa_node(env.local_rank) if dev.type == "cuda" else None,
         }
         stats = dl.stats()
+        if host_log:  # per-iteration host time of the timed loop (debug): the slow iterations
+            dts = [b - a for a, b in zip([t0] + ticks[:-1], ticks)]
+            mine["host_iter_ms_slow"] = [(i, round(1e3 * d, 2)) for i, d in enumerate(dts) if d > 0.002]
+        if os.environ.get("DDL_STAGER_LOG") and dl._stager is not None:  # per-window producer waits (debug)
+            mine["stager_wait_log_us"] = [(w, round(ns / 1e3, 1)) for w, ns in dl._stager._native.wait_log
+                                          if ns > 100_000]
         mine["stager_wait_producer_s"] = round(stats.get("stager_wait_producer_s", 0.0), 4)
         mine["exchange_issue_wait_s"] = stats.get("exchange_issue_wait_s", 0.0)
         mine["consumer_wait_s"] = round(stats["consumer_wait_s"], 4)

@@ -37,7 +37,7 @@ def main(argv=None) -> None:
     ap.add_argument("--consumer", default="flat", choices=["flat", "groups"],
                     help="flat: ONE streaming checksum over the batch's three groups (adjacent in one allocation); "
                          "groups: one checksum launch per group")
-    ap.add_argument("--dispatch", default="native", choices=["native", "python"])
+    ap.add_argument("--dispatch", default="native", choices=["native", "inline", "lookahead", "python"])
     a = ap.parse_args(argv)
 
     import torch
@@ -51,7 +51,7 @@ def main(argv=None) -> None:
         producer = PointwiseProducer(n_timesteps=a.timesteps, host_shuffle=a.host_shuffle)
         dl = ddl_amd.DistributedDataLoader(producer, 4096, conn, 10 ** 6, 0.0, "alltoall", env.rank, env.world_size,
                                            env=env, shuffle="device", contiguous=True, seed=1,
-                                           native_dispatch=a.dispatch == "native")
+                                           native_dispatch={"native": True, "python": False}.get(a.dispatch, a.dispatch))
         acc = ops.ChecksumAccumulator(dev)
 
         def consume(groups):

@@ -243,7 +243,9 @@ PYBIND11_MODULE(_ddl_hip, m) {
       .def_property_readonly("windows_staged", &ddl::NativeStager::windows_staged)
       .def_property_readonly("windows_landed", &ddl::NativeStager::windows_landed)
       .def_property_readonly("bytes_landed", &ddl::NativeStager::bytes_landed)
-      .def_property_readonly("wait_producer_s", &ddl::NativeStager::wait_producer_s);
+      .def_property_readonly("wait_producer_s", &ddl::NativeStager::wait_producer_s)
+      .def_property_readonly("wait_log", &ddl::NativeStager::wait_log,
+                             "[(window, ns waited for its producer)] of the first 4096 staged windows");
 
   // ------------------------------------------------- native batch dispatch
   py::class_<ddl::BatchEngine>(m, "BatchEngine")
@@ -334,6 +336,7 @@ PYBIND11_MODULE(_ddl_hip, m) {
           py::arg("window"), py::arg("timeout_ms"))
       .def("release", &ddl::BatchEngine::release, py::arg("window"))
       .def("reset", &ddl::BatchEngine::reset)
+      .def_property("inline", &ddl::BatchEngine::is_inline, &ddl::BatchEngine::set_inline)
       .def_property_readonly("wait_s", &ddl::BatchEngine::wait_s)
       .def_property_readonly("batches", &ddl::BatchEngine::batches)
       .def_property_readonly("lookahead_hits", &ddl::BatchEngine::lookahead_hits)

@@ -112,16 +112,19 @@ int BatchEngine::acquire(int64_t w, int64_t timeout_ms, int32_t* failed_producer
   return 0;
 }
 
-int BatchEngine::enqueue(int64_t w, int64_t local, const StagedInfo& info, Pending* out) {
+int BatchEngine::enqueue(int64_t w, int64_t local, const StagedInfo& info, Pending* out, bool on_caller,
+                         hipStream_t st, bool last_of_window) {
   if (free_slots_.empty()) return -2;
+  if (!on_caller) st = bs_;  // inline mode: the caller's stream (the null stream is a valid one), no event
   const int64_t slot = free_slots_.front();
   free_slots_.pop_front();
   const auto& dst = slots_[slot];
   const void* src = buffers_[info.buffer];
   uint64_t t0 = clock_ns();
-  if (ready_waited_ != w) {  // once per window: every batch of it is on the batch stream behind this wait
-    if (hipStreamWaitEvent(bs_, ready_[info.buffer], 0) != hipSuccess) return -1;
+  if (ready_waited_ != w || ready_stream_ != st) {  // once per window and stream: its batches queue behind it
+    if (hipStreamWaitEvent(st, ready_[info.buffer], 0) != hipSuccess) return -1;
     ready_waited_ = w;
+    ready_stream_ = st;
   }
   uint64_t t1 = clock_ns();
   streamwait_ns_ += t1 - t0;
@@ -150,7 +153,7 @@ int BatchEngine::enqueue(int64_t w, int64_t local, const StagedInfo& info, Pendi
     if (r_.token_mode == 0) {
       sp.offsets = reinterpret_cast<const int64_t*>(win + r_.off_offsets);
       sp.rows = r_.batch;
-      rc = pad_pack_tokens(sp, bs_);
+      rc = pad_pack_tokens(sp, st);
     } else {
       sp.row_start = reinterpret_cast<const int64_t*>(win + r_.off_row_start);
       sp.row_end = reinterpret_cast<const int64_t*>(win + r_.off_row_end);
@@ -159,11 +162,11 @@ int BatchEngine::enqueue(int64_t w, int64_t local, const StagedInfo& info, Pendi
       sp.segment_ids = static_cast<int32_t*>(dst[3]);
       sp.cu_seqlens_out = static_cast<int32_t*>(dst[4]);
       sp.rows = info.tag[1];
-      rc = sp.rows > 0 ? pad_pack_tokens(sp, bs_)
-                       : (hipMemsetAsync(dst[4], 0, sizeof(int32_t), bs_) == hipSuccess ? 0 : -1);
+      rc = sp.rows > 0 ? pad_pack_tokens(sp, st)
+                       : (hipMemsetAsync(dst[4], 0, sizeof(int32_t), st) == hipSuccess ? 0 : -1);
     }
   } else if (r_.kind == 0) {
-    rc = gather_rows(dst[0], r_.out_dt, src, r_.in_dt, r_.batch, r_.row_elems, ri, r_.aff, 0, r_.max_blocks, bs_);
+    rc = gather_rows(dst[0], r_.out_dt, src, r_.in_dt, r_.batch, r_.row_elems, ri, r_.aff, 0, r_.max_blocks, st);
   } else {
     SplitSpec sp{};
     sp.n_groups = static_cast<int32_t>(r_.widths.size());
@@ -172,14 +175,27 @@ int BatchEngine::enqueue(int64_t w, int64_t local, const StagedInfo& info, Pendi
       sp.dst[g] = dst[g];
       sp.width[g] = r_.widths[g];
     }
-    rc = split_columns(sp, src, r_.in_dt, r_.batch, r_.row_elems, ri, bs_);
+    rc = split_columns(sp, src, r_.in_dt, r_.batch, r_.row_elems, ri, st);
   }
   if (rc != 0) return -1;
   const uint64_t t2 = clock_ns();
   launch_ns_ += t2 - t1;
+  if (on_caller) {  // stream order is the dependency: no event
+    *out = Pending{w, local, slot, -1};
+    return 0;
+  }
   const int ev = next_event_;
   next_event_ = (next_event_ + 1) % kBatchEvents;
   if (hipEventRecord(batch_events_[ev], bs_) != hipSuccess) return -1;
+  if (last_of_window) {
+    // the window's free event, from the buffer's own small ring: the next record into this ring is for the
+    // window that re-uses the buffer, which can only be staged after the stager enqueued its wait on this one
+    const int b = info.buffer;
+    hipEvent_t fe = free_events_[b][free_next_[b]];
+    free_next_[b] = (free_next_[b] + 1) % kFreeEvents;
+    if (hipEventRecord(fe, bs_) != hipSuccess) return -1;
+    done_event_[w] = fe;
+  }
   record_ns_ += clock_ns() - t2;
   *out = Pending{w, local, slot, ev};
   return 0;
@@ -195,6 +211,15 @@ int64_t BatchEngine::get(int64_t w, int64_t local, int64_t bpw, bool next_ok, hi
     for (int k = 0; k < 4; ++k) tags[k] = wi.tag[k];
   }
   Pending cur{};
+  if (inline_) {
+    last_compute_ = compute;
+    have_compute_ = true;
+    rc = enqueue(w, local, windows_.at(w), &cur, true, compute);
+    if (rc != 0) return rc;
+    ++batches_;
+    get_ns_ += clock_ns() - g0;
+    return cur.slot;
+  }
   bool have = false;
   while (!pending_.empty()) {  // lookahead in schedule order; anything older than (w, local) is stale
     Pending p = pending_.front();
@@ -207,7 +232,7 @@ int64_t BatchEngine::get(int64_t w, int64_t local, int64_t bpw, bool next_ok, hi
     }
   }
   if (!have) {
-    rc = enqueue(w, local, windows_.at(w), &cur);
+    rc = enqueue(w, local, windows_.at(w), &cur, false, nullptr, local + 1 == bpw);
     if (rc != 0) return rc;
   }
   const uint64_t s0 = clock_ns();
@@ -225,7 +250,7 @@ int64_t BatchEngine::get(int64_t w, int64_t local, int64_t bpw, bool next_ok, hi
   // lookahead: the next batch of this window, or the first of the next one if it is already staged
   Pending nxt{};
   if (local + 1 < bpw) {
-    if (enqueue(w, local + 1, windows_.at(w), &nxt) == 0) pending_.push_back(nxt);
+    if (enqueue(w, local + 1, windows_.at(w), &nxt, false, nullptr, local + 2 == bpw) == 0) pending_.push_back(nxt);
   } else if (next_ok) {
     const StagedInfo* ni = acquired(w + 1);
     StagedInfo peeked;
@@ -233,6 +258,7 @@ int64_t BatchEngine::get(int64_t w, int64_t local, int64_t bpw, bool next_ok, hi
       int32_t fp = -1;
       if (acquire(w + 1, 0, &fp) == 0) ni = acquired(w + 1);
     }
+    // (w + 1, 0) is the last batch of w + 1 only if it has one batch: its bpw is unknown here, so no done event
     if (ni != nullptr && enqueue(w + 1, 0, *ni, &nxt) == 0) pending_.push_back(nxt);
   }
   get_ns_ += clock_ns() - g0;
@@ -243,11 +269,21 @@ int BatchEngine::release(int64_t w) {
   auto it = windows_.find(w);
   if (it == windows_.end()) return 0;
   const int b = it->second.buffer;
-  // a window no batch was built from still has its copy in flight: the free event follows it too
-  if (hipStreamWaitEvent(bs_, ready_[b], 0) != hipSuccess) return -1;
-  hipEvent_t ev = free_events_[b][free_next_[b]];
-  free_next_[b] = (free_next_[b] + 1) % kFreeEvents;
-  if (hipEventRecord(ev, bs_) != hipSuccess) return -1;
+  // the stream that read the window (inline: the caller's), behind its copy (a window no batch was
+  // built from still has its copy in flight): the free event goes there
+  hipStream_t st = inline_ && have_compute_ ? last_compute_ : bs_;
+  hipEvent_t ev = nullptr;
+  auto de = done_event_.find(w);
+  if (!inline_ && de != done_event_.end()) {
+    ev = de->second;  // right after w's last batch kernel, not behind the next window's lookahead
+  } else {
+    if ((ready_waited_ != w || ready_stream_ != st) && hipStreamWaitEvent(st, ready_[b], 0) != hipSuccess)
+      return -1;
+    ev = free_events_[b][free_next_[b]];
+    free_next_[b] = (free_next_[b] + 1) % kFreeEvents;
+    if (hipEventRecord(ev, st) != hipSuccess) return -1;
+  }
+  if (de != done_event_.end()) done_event_.erase(de);
   stager_->release(w, ev);
   windows_.erase(it);
   keys_.erase(w);
@@ -256,7 +292,9 @@ int BatchEngine::release(int64_t w) {
 }
 
 void BatchEngine::reset() {
+  done_event_.clear();
   ready_waited_ = -1;
+  ready_stream_ = nullptr;
   pending_.clear();
   windows_.clear();
   keys_.clear();

@@ -89,6 +89,12 @@ class BatchEngine {
   int release(int64_t w);
   // Drop the lookahead (seek / shutdown); the batch stream is NOT synchronised here.
   void reset();
+  // Inline mode: the batch kernel is launched at get() time on the CALLER's stream, right before the
+  // step that consumes it -- no batch event, no cross-stream wait per batch (a record + wait pair costs
+  // ~11 us of host time on the box), only one wait per window on its HBM-ready event. For small batches
+  // the host cost is the bottleneck and the kernel's few microseconds on the compute stream are not.
+  void set_inline(bool on) { inline_ = on; }
+  bool is_inline() const { return inline_; }
 
   double wait_s() const { return wait_ns_ * 1e-9; }
   // host ns spent in get() in total, and inside HIP calls: kernel launches, event records, stream waits
@@ -102,7 +108,10 @@ class BatchEngine {
     int64_t w, local, slot;
     int ev;
   };
-  int enqueue(int64_t w, int64_t local, const StagedInfo& info, Pending* out);
+  // on_caller: launch on `st` (the caller's stream, possibly the null stream) without a batch event;
+  // else on the batch stream with one
+  int enqueue(int64_t w, int64_t local, const StagedInfo& info, Pending* out, bool on_caller = false,
+              hipStream_t st = nullptr, bool last_of_window = false);
   const StagedInfo* acquired(int64_t w);
 
   NativeStager* stager_;
@@ -114,6 +123,11 @@ class BatchEngine {
   int device_;
   std::map<int64_t, StagedInfo> windows_;     // acquired, not yet released
   std::map<int64_t, FeistelKeys> keys_;       // per acquired window (shuffle)
+  // per window: a free event recorded right after its LAST batch kernel (from the buffer's free-event ring).
+  // Recording a fresh event at release() time would put it behind the lookahead kernel of the NEXT
+  // window, which waits for that window's copy: the copy after it would then wait for a copy plus a
+  // gather (the ~25-80 us SDMA gaps of the r2 trace).
+  std::map<int64_t, hipEvent_t> done_event_;
   std::deque<Pending> pending_;               // lookahead, in enqueue order
   std::deque<int64_t> free_slots_;
   std::vector<std::vector<void*>> slots_;     // slot id -> output pointers
@@ -123,7 +137,11 @@ class BatchEngine {
   std::vector<int> free_next_;
   uint64_t wait_ns_ = 0, batches_ = 0, hits_ = 0, waits_ = 0;
   uint64_t get_ns_ = 0, launch_ns_ = 0, record_ns_ = 0, streamwait_ns_ = 0;
-  int64_t ready_waited_ = -1;  // window whose HBM-ready event the batch stream already waits on
+  int64_t ready_waited_ = -1;  // window whose HBM-ready event the launch stream already waits on
+  hipStream_t ready_stream_ = nullptr;  // ... and that stream
+  bool inline_ = false;
+  hipStream_t last_compute_ = nullptr;  // inline mode: where the window's reads were enqueued (0 = null stream)
+  bool have_compute_ = false;
 };
 
 // Host derivation of the Feistel round keys of (seed, key) -- ddl_amd/permutation.py round_keys --

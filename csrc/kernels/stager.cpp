@@ -19,23 +19,6 @@ double mono_s() {
   return static_cast<double>(ts.tv_sec) + 1e-9 * static_cast<double>(ts.tv_nsec);
 }
 
-struct SlotRelease {
-  std::atomic<uint32_t>* word;
-  std::atomic<uint64_t>* windows_landed;
-  std::atomic<uint64_t>* bytes_landed;
-  uint64_t bytes;
-};
-
-// Host callback on the copy stream: the DMA out of the slot retired, hand the
-// slot back to its producer (state store + futex wake of the producer).
-void release_slot_cb(void* p) {
-  auto* r = static_cast<SlotRelease*>(p);
-  r->bytes_landed->fetch_add(r->bytes, std::memory_order_relaxed);
-  r->windows_landed->fetch_add(1, std::memory_order_release);
-  r->word->store(kEmpty, std::memory_order_release);
-  syscall(SYS_futex, reinterpret_cast<uint32_t*>(r->word), FUTEX_WAKE, INT32_MAX, nullptr, nullptr, 0);
-  delete r;
-}
 
 }  // namespace
 
@@ -59,14 +42,48 @@ NativeStager::NativeStager(const Arena* arena, int32_t n_producers, int32_t n_sl
       post_copy_(post_copy),
       depth_(static_cast<int>(buffers_.size())),
       free_events_(buffers_.size(), nullptr),
-      released_upto_(first) {
+      released_upto_(first),
+      retired_upto_(first) {
   if (P_ < 1 || n_slots_ < 1 || depth_ < 1 || ready_.size() != buffers_.size() ||
       (post_copy_ && copy_done_.size() != buffers_.size()) || static_cast<int32_t>(peer_pids_.size()) != P_)
     throw std::invalid_argument("NativeStager: inconsistent arguments");
+  if (hipSetDevice(device_) != hipSuccess) throw std::runtime_error("NativeStager: hipSetDevice failed");
+  retire_ev_.resize(kRetireEvents);
+  for (auto& e : retire_ev_)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventBlockingSync) != hipSuccess)
+      throw std::runtime_error("NativeStager: hipEventCreate failed");
   thread_ = std::thread([this] { run(); });
+  retire_thread_ = std::thread([this] { retire_loop(); });
 }
 
-NativeStager::~NativeStager() { close(); }
+NativeStager::~NativeStager() {
+  close();
+  for (auto e : retire_ev_) hipEventDestroy(e);
+}
+
+void NativeStager::retire_loop() {
+  if (hipSetDevice(device_) != hipSuccess) return fail(-1, -1, "hipSetDevice failed in the retire thread");
+  for (;;) {
+    Retire r;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      retire_cv_.wait(lk, [&] { return stop_ || !retire_q_.empty(); });
+      if (retire_q_.empty()) return;  // stopped and drained
+      r = retire_q_.front();
+    }
+    if (hipEventSynchronize(retire_ev_[r.ev]) != hipSuccess) return fail(-1, static_cast<int32_t>(r.producer),
+                                                                         "hipEventSynchronize(retire) failed");
+    bytes_landed_.fetch_add(r.bytes, std::memory_order_relaxed);
+    windows_landed_.fetch_add(1, std::memory_order_release);
+    arena_->set_state(r.producer, r.slot, kEmpty);  // slot back to its producer (release store + futex wake)
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      retire_q_.pop_front();
+      retired_upto_ = r.window + 1;
+    }
+    retire_cv_.notify_all();
+  }
+}
 
 void NativeStager::fail(int code, int32_t producer, const std::string& msg) {
   std::lock_guard<std::mutex> lk(mu_);
@@ -76,6 +93,7 @@ void NativeStager::fail(int code, int32_t producer, const std::string& msg) {
     error_msg_ = msg;
   }
   cv_.notify_all();
+  retire_cv_.notify_all();
 }
 
 void NativeStager::run() {
@@ -107,8 +125,13 @@ void NativeStager::run() {
       }
       if (now_ns() >= deadline_ns) break;
     }
-    wait_producer_ns_ += static_cast<uint64_t>(
+    const uint64_t waited = static_cast<uint64_t>(
         std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
+    wait_producer_ns_ += waited;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (wait_log_.size() < 4096) wait_log_.emplace_back(w, waited);
+    }
     if (rc == kShutdown) {
       std::lock_guard<std::mutex> lk(mu_);
       if (!stop_ && error_code_ == 0) {
@@ -139,11 +162,20 @@ void NativeStager::run() {
         hipMemcpyAsync(buffers_[b], arena_->slot_data(p, s), info.used_bytes, hipMemcpyHostToDevice, copy_stream_) !=
             hipSuccess)
       return fail(-1, static_cast<int32_t>(p), "hipMemcpyAsync H2D failed");
-    auto* req = new SlotRelease{&arena_->slot(p, s)->state, &windows_landed_, &bytes_landed_, info.used_bytes};
-    if (hipLaunchHostFunc(copy_stream_, release_slot_cb, req) != hipSuccess) {
-      delete req;
-      return fail(-1, static_cast<int32_t>(p), "hipLaunchHostFunc(release) failed");
+    // retire event of w: a ring, so window w - kRetireEvents must have been retired before it is re-recorded
+    const int rev = static_cast<int>((w - first_) % kRetireEvents);
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      retire_cv_.wait(lk, [&] { return stop_ || error_code_ != 0 || w - kRetireEvents < retired_upto_; });
+      if (stop_ || error_code_ != 0) return;
     }
+    if (hipEventRecord(retire_ev_[rev], copy_stream_) != hipSuccess)
+      return fail(-1, static_cast<int32_t>(p), "hipEventRecord(retire) failed");
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      retire_q_.push_back(Retire{w, p, s, info.used_bytes, rev});
+    }
+    retire_cv_.notify_all();
     if (hipEventRecord(post_copy_ ? copy_done_[b] : ready_[b], copy_stream_) != hipSuccess)
       return fail(-1, static_cast<int32_t>(p), "hipEventRecord failed");
     info.t_ready_host = mono_s();
@@ -200,7 +232,10 @@ void NativeStager::close() {
     stop_ = true;
   }
   cv_.notify_all();
+  retire_cv_.notify_all();
   if (thread_.joinable()) thread_.join();
+  // the retire thread drains the queue (every enqueued copy's slot goes back to its producer)
+  if (retire_thread_.joinable()) retire_thread_.join();
 }
 
 std::string NativeStager::error() const {

@@ -10,6 +10,7 @@
 
 #include "arena.h"
 #include "feistel.h"
+#include <algorithm>
 #include "fileio.h"
 
 namespace py = pybind11;
@@ -216,6 +217,39 @@ PYBIND11_MODULE(_ddl_runtime, m) {
       py::arg("shard_rows"), py::arg("world"), py::arg("rank"),
       "(send_counts, recv_counts) of one global batch: samples this rank sends to / receives from every rank "
       "(sample idx lives on rank idx / shard_rows, position i goes to rank i / lb)");
+  m.def(
+      "owner_maps",
+      [](std::vector<uint64_t> keys, uint32_t half_bits, uint64_t n, int64_t pos0, int64_t gb, int64_t lb,
+         int64_t shard_rows, int64_t world, int64_t rank, int64_t lo) {
+        // host twin of bucket.hip (CPU rehearsals): send list (own samples in position order, shard-local)
+        // and receive map (row of each local position in the all-to-all receive buffer)
+        if (keys.size() != ddl::kHostFeistelRounds) throw std::invalid_argument("owner_maps: need 6 round keys");
+        if (lb <= 0 || shard_rows <= 0 || world < 1 || rank < 0 || rank >= world || pos0 < 0 ||
+            static_cast<uint64_t>(pos0 + gb) > n)
+          throw std::invalid_argument("owner_maps: bad geometry");
+        std::vector<int64_t> owner(gb), send;
+        std::vector<int64_t> recv_counts(world, 0);
+        auto inv = py::array_t<int64_t>(lb);
+        int64_t* iv = inv.mutable_data();
+        {
+          py::gil_scoped_release nogil;
+          for (int64_t i = 0; i < gb; ++i) {
+            const int64_t idx = static_cast<int64_t>(
+                ddl::host_feistel_perm(static_cast<uint64_t>(pos0 + i), keys.data(), half_bits, n));
+            owner[i] = idx / shard_rows;
+            if (owner[i] == rank) send.push_back(idx - lo);
+          }
+          for (int64_t j = 0; j < lb; ++j) ++recv_counts[owner[rank * lb + j]];
+          std::vector<int64_t> next(world, 0);
+          for (int64_t q = 1; q < world; ++q) next[q] = next[q - 1] + recv_counts[q - 1];
+          for (int64_t j = 0; j < lb; ++j) iv[j] = next[owner[rank * lb + j]]++;
+        }
+        auto sa = py::array_t<int64_t>(static_cast<py::ssize_t>(send.size()));
+        std::copy(send.begin(), send.end(), sa.mutable_data());
+        return py::make_tuple(sa, inv);
+      },
+      py::arg("keys"), py::arg("half_bits"), py::arg("n"), py::arg("pos0"), py::arg("gb"), py::arg("lb"),
+      py::arg("shard_rows"), py::arg("world"), py::arg("rank"), py::arg("lo"));
   m.def(
       "parallel_copy",
       [](uintptr_t dst, uintptr_t src, uint64_t bytes, int n_threads) {

@@ -134,7 +134,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
         copy_batches: bool | None = None,
         collate: str | None = None,
         pad_id: int = 0,
-        native_dispatch: bool = True,
+        native_dispatch: bool | str = True,
     ):
         if mode not in MODES:
             raise ValueError(f"unknown mode {mode!r}; one of {MODES}")
@@ -203,9 +203,14 @@ class DistributedDataLoader(DistributedDataloaderABC):
         self._stager = None
         self._batch_stream = None
         self._lookahead: dict = {}
+        self._win_done: dict = {}  # window -> event after its last batch kernel (Python dispatch path)
         self._host_window: int | None = None  # host path: window currently held
         self._cur = None                      # device path: StagedWindow of the current window
-        self.native_dispatch = bool(native_dispatch)
+        # True / "auto": native engine, inline for small batches (< 16 MB), lookahead on the batch stream
+        # for large ones; "inline" / "lookahead" force the mode; False: the Python dispatch path
+        if native_dispatch not in (True, False, "auto", "inline", "lookahead"):
+            raise ValueError("native_dispatch must be a bool or 'auto' / 'inline' / 'lookahead'")
+        self.native_dispatch = "auto" if native_dispatch is True else native_dispatch
         self._engine = None                   # native per-batch dispatch (csrc/kernels/engine.cpp)
 
         if connection is None or connection.n_producers == 0:
@@ -371,10 +376,19 @@ class DistributedDataLoader(DistributedDataloaderABC):
             off += -(-math.prod(sh) * _dtypes.itemsize(dt) // 256) * 256
         self._eng_slot_bytes = max(256, off)
         self._eng_block = int(min(64, max(4, (512 << 20) // self._eng_slot_bytes)))
+        mode = self.native_dispatch
+        if mode == "auto":
+            mode = "inline" if self._eng_slot_bytes < (16 << 20) else "lookahead"
+        self._engine.inline = mode == "inline"
+        self._eng_mode = mode
         self._eng_slots: collections.deque = collections.deque()  # (slot id, outputs, block)
         self._eng_next_id = 0
         self._eng_rec = (None, None)  # (block, stream) of the last record_stream
         self._eng_window = None
+        # the first blocks are allocated up front, outside any timed loop: >= 24 slots, so that in steady
+        # state every new block reuses a freed one from the caching allocator (no hipMalloc per block)
+        for _ in range(max(2, -(-24 // self._eng_block))):
+            self._engine_provide()
 
     def _engine_provide(self) -> None:
         """One allocation (on the batch stream) for a block of output slots; each slot is used once."""
@@ -550,6 +564,11 @@ class DistributedDataLoader(DistributedDataloaderABC):
             out = self._batch_from_window(sw, p, s, local)
             ev = torch.cuda.Event()
             ev.record(bs)
+        if local + 1 == self.batches_per_window[p]:
+            # the window's free event: right after its last batch kernel, NOT at release time behind the
+            # next window's lookahead kernel (which waits for that window's copy: the copy after it would
+            # then wait for a copy plus a gather)
+            self._win_done[sw.index] = ev
         return out, ev
 
     def _device_batch(self, sw, p: int, s: int, local: int, bpw: int):
@@ -676,6 +695,13 @@ class DistributedDataLoader(DistributedDataloaderABC):
                 for key in [k for k in self._lookahead if k[0] <= self.window]:
                     del self._lookahead[key]
                 stream = self._batch_stream
+                done = self._win_done.pop(self.window, None)
+                for key in [k for k in self._win_done if k < self.window]:
+                    del self._win_done[key]
+                if done is not None and self._stager.post_copy is None:
+                    self._stager.release(self.window, event=done)
+                    self._cur = None
+                    return
                 sw = self._cur
                 if sw is not None and sw.index == self.window:
                     # a window no batch was built from (skipped at a partial epoch end) can still have
@@ -919,6 +945,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
             # 1. stop every reader of the slots / ring buffers
             if self._batch_stream is not None:
                 self._lookahead.clear()
+                self._win_done.clear()
                 self._batch_stream.synchronize()
             if self._stager is not None:
                 self._stager.close()  # joins the native thread; copies and their slot hand-backs retire
@@ -959,6 +986,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
         self._finalized = True
         if self._batch_stream is not None:
             self._lookahead.clear()
+            self._win_done.clear()
             self._batch_stream.synchronize()
         if self.connection is not None:
             self.connection.shutdown_operation()
@@ -997,6 +1025,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
                 nd["host_us_per_batch"] = {"get": round(g / n / 1e3, 2), "kernel_launch": round(la / n / 1e3, 2),
                                            "event_record": round(rec / n / 1e3, 2),
                                            "stream_wait": round(sw / n / 1e3, 2)}
+            nd["mode"] = getattr(self, "_eng_mode", None)
             d["native_dispatch"] = nd
         if self._stager is not None:
             d.update(self._stager.stats())

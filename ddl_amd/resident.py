@@ -39,6 +39,7 @@ from __future__ import annotations
 
 import collections
 import contextlib
+import itertools
 import math
 import time
 from typing import Any, Iterator
@@ -454,18 +455,14 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
                     hip, stream = _native.hip(), self.prep_stream.cuda_stream
                     hip.bucket_send(perm.keys, self.N, perm.half_bits, pos0, self.GB, self.S, self.lo, self.rank,
                                     self.W, self._send_idx.data_ptr(), stream)
-                    offsets = np.concatenate([[0], np.cumsum(recv_counts)[:-1]]).tolist()
+                    offsets = [0, *itertools.accumulate(recv_counts[:-1])]
                     hip.bucket_recv(perm.keys, self.N, perm.half_bits, mine0, self.LB, self.S, self.W, offsets,
                                     self._inv_idx.data_ptr(), stream)
                     send_idx, inv = self._send_idx[:n_send], self._inv_idx
-                else:  # CPU rehearsal: the same maps in numpy
-                    idx_all = perm(np.arange(pos0, pos0 + self.GB, dtype=np.int64))
-                    owner = idx_all // self.S
-                    send_idx = torch.from_numpy(idx_all[owner == self.rank] - self.lo)
-                    mine = owner[self.rank * self.LB:(self.rank + 1) * self.LB]
-                    inv_np = np.empty(self.LB, dtype=np.int64)
-                    inv_np[np.argsort(mine, kind="stable")] = np.arange(self.LB)
-                    inv = torch.from_numpy(inv_np)
+                else:  # CPU rehearsal: the same maps from the native host twin of the kernels
+                    s_np, i_np = _native.runtime().owner_maps(perm.keys, perm.half_bits, self.N, pos0, self.GB,
+                                                              self.LB, self.S, self.W, self.rank, self.lo)
+                    send_idx, inv = torch.from_numpy(s_np), torch.from_numpy(i_np)
                 send = ops.gather_rows(self.shard, index=send_idx) if n_send else \
                     torch.empty((0,) + self.sample_shape, dtype=self.src_dtype, device=self.device)
                 recv = torch.empty((self.LB,) + self.sample_shape, dtype=self.src_dtype, device=self.device)

@@ -181,16 +181,20 @@ class WindowStager:
             raise PeerDeathError(f"{what}: producer {producer} reported a failure", producer, pid)
         raise PeerDeathError(f"{what}: producer {producer} (pid {pid}) died", producer, pid)
 
-    def release(self, w: int, stream: torch.cuda.Stream | None = None) -> None:
+    def release(self, w: int, stream: torch.cuda.Stream | None = None, event: torch.cuda.Event | None = None) -> None:
         """Consumer is done with window ``w`` as of ``stream``'s position (default: the current
-        stream): every kernel that reads the window must be on that stream, before this call."""
+        stream): every kernel that reads the window must be on that stream, before this call.
+        ``event``: an already-recorded event after the last read of the window (used as is)."""
         sw = self._staged.pop(w, None)
         if sw is None:
             return
         self._posted.discard(w)
         self._n_released += 1
-        ev = torch.cuda.Event()
-        ev.record(stream if stream is not None else streams.current(self.device.index))
+        if event is not None:
+            ev = event
+        else:
+            ev = torch.cuda.Event()
+            ev.record(stream if stream is not None else streams.current(self.device.index))
         refs = self._free_refs[sw.buffer]
         refs.append(ev)
         del refs[:-2]  # the stager has enqueued its wait on the older one by now

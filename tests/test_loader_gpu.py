@@ -296,13 +296,14 @@ def test_native_dispatch_matches_python_path(case):
         make = lambda: (ImageWindowProducer(32, (3, 16, 16), "bfloat16", seed=3), 8)  # noqa: E731
         kw = dict(shuffle="none", copy_batches=True)
     partial = {1: 2, 2: 0}
-    nat, st = _collect(True, make, partial=partial, **kw)
     ref, st_ref = _collect(False, make, partial=partial, **kw)
-    assert st.get("native_dispatch") and st["native_dispatch"]["batches"] == len(nat)
     assert st_ref.get("native_dispatch") is None
-    assert len(nat) == len(ref) > 0
-    for a, b in zip(nat, ref):
-        assert torch.equal(a, b)
+    for mode in ("inline", "lookahead"):
+        nat, st = _collect(mode, make, partial=partial, **kw)
+        assert st["native_dispatch"]["batches"] == len(nat) and st["native_dispatch"]["mode"] == mode
+        assert len(nat) == len(ref) > 0
+        for a, b in zip(nat, ref):
+            assert torch.equal(a, b)
 
 
 def test_native_dispatch_held_batches_stay_valid():

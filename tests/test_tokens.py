@@ -275,14 +275,16 @@ def test_token_native_dispatch_matches_python_path(corpus, mode):
             st = dl.stats()
         return out, st
 
-    nat, st = run(True)
     ref, st_ref = run(False)
-    assert st["native_dispatch"]["batches"] == len(nat) and "native_dispatch" not in st_ref
-    assert len(nat) == len(ref) > 0
-    for a, b in zip(nat, ref):
-        assert a.keys() == b.keys()
-        for k in a:
-            if isinstance(a[k], torch.Tensor):
-                assert a[k].dtype == b[k].dtype and torch.equal(a[k], b[k]), k
-            else:
-                assert a[k] == b[k], k
+    assert "native_dispatch" not in st_ref
+    for native in ("inline", "lookahead"):
+        nat, st = run(native)
+        assert st["native_dispatch"]["batches"] == len(nat) and st["native_dispatch"]["mode"] == native
+        assert len(nat) == len(ref) > 0
+        for a, b in zip(nat, ref):
+            assert a.keys() == b.keys()
+            for k in a:
+                if isinstance(a[k], torch.Tensor):
+                    assert a[k].dtype == b[k].dtype and torch.equal(a[k], b[k]), k
+                else:
+                    assert a[k] == b[k], k

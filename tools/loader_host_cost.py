@@ -22,7 +22,7 @@ import time
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 
 
-def run(shape: str, native: bool, steps: int) -> dict:
+def run(shape: str, native, steps: int) -> dict:
     import torch
 
     import ddl_amd
@@ -58,7 +58,7 @@ def run(shape: str, native: bool, steps: int) -> dict:
         st = dl.stats()
         torch.cuda.synchronize()
         dl.close()
-    return {"shape": shape, "dispatch": "native" if native else "python", "batches": steps,
+    return {"shape": shape, "dispatch": native if native else "python", "batches": steps,
             "thread_cpu_us": round(1e6 * (c1 - c0) / steps, 2), "wall_us": round(1e6 * (w1 - w0) / steps, 2),
             "engine": st.get("native_dispatch")}
 
@@ -66,7 +66,7 @@ def run(shape: str, native: bool, steps: int) -> dict:
 def main() -> int:
     steps = int(os.environ.get("STEPS", "3000"))
     for shape in ("pointwise", "images"):
-        for native in (True, False):
+        for native in ("inline", "lookahead", False):
             print(json.dumps(run(shape, native, steps if shape == "pointwise" else steps // 5)), flush=True)
     return 0
 
