@@ -352,8 +352,8 @@ def main(argv=None) -> int:
             dts = [b - a for a, b in zip([t0] + ticks[:-1], ticks)]
             mine["host_iter_ms_slow"] = [(i, round(1e3 * d, 2)) for i, d in enumerate(dts) if d > 0.002]
         if os.environ.get("DDL_STAGER_LOG") and dl._stager is not None:  # per-window producer waits (debug)
-            mine["stager_wait_log_us"] = [(w, round(ns / 1e3, 1)) for w, ns in dl._stager._native.wait_log
-                                          if ns > 100_000]
+            mine["stager_step_log_us"] = [[e[0]] + [round(x / 1e3, 1) for x in e[1:6]]
+                                          for e in dl._stager._native.wait_log if max(e[1:6]) > 500_000]
         mine["stager_wait_producer_s"] = round(stats.get("stager_wait_producer_s", 0.0), 4)
         mine["exchange_issue_wait_s"] = stats.get("exchange_issue_wait_s", 0.0)
         mine["consumer_wait_s"] = round(stats["consumer_wait_s"], 4)

@@ -245,7 +245,8 @@ PYBIND11_MODULE(_ddl_hip, m) {
       .def_property_readonly("bytes_landed", &ddl::NativeStager::bytes_landed)
       .def_property_readonly("wait_producer_s", &ddl::NativeStager::wait_producer_s)
       .def_property_readonly("wait_log", &ddl::NativeStager::wait_log,
-                             "[(window, ns waited for its producer)] of the first 4096 staged windows");
+                             "per staged window (first 4096): [window, ns ring wait, ns free-event wait enqueue, "
+                             "ns producer wait, ns copy enqueue, ns retire slot + event records, t0 ns]");
 
   // ------------------------------------------------- native batch dispatch
   py::class_<ddl::BatchEngine>(m, "BatchEngine")

@@ -98,18 +98,26 @@ void NativeStager::fail(int code, int32_t producer, const std::string& msg) {
 
 void NativeStager::run() {
   if (hipSetDevice(device_) != hipSuccess) return fail(-1, -1, "hipSetDevice failed in the stager thread");
+  auto ns = [] {
+    return static_cast<int64_t>(
+        std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+            .count());
+  };
   for (int64_t w = first_; w < first_ + total_; ++w) {
     const int b = static_cast<int>((w - first_) % depth_);
     hipEvent_t free_ev = nullptr;
+    const int64_t s0 = ns();
     {
       std::unique_lock<std::mutex> lk(mu_);
       cv_.wait(lk, [&] { return stop_ || w - depth_ < released_upto_; });
       if (stop_) return;
       free_ev = free_events_[b];
     }
+    const int64_t s1 = ns();
     // the consumer's kernels reading this ring buffer (window w - depth) finish first
     if (free_ev != nullptr && hipStreamWaitEvent(copy_stream_, free_ev, 0) != hipSuccess)
       return fail(-1, -1, "hipStreamWaitEvent(free) failed");
+    const int64_t s2 = ns();
     const uint32_t p = static_cast<uint32_t>(w % P_);
     const uint32_t s = static_cast<uint32_t>((w / P_) % n_slots_);
     // futex wait in short slices so close() never waits behind a long timeout
@@ -128,10 +136,7 @@ void NativeStager::run() {
     const uint64_t waited = static_cast<uint64_t>(
         std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
     wait_producer_ns_ += waited;
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      if (wait_log_.size() < 4096) wait_log_.emplace_back(w, waited);
-    }
+    const int64_t s3 = ns();
     if (rc == kShutdown) {
       std::lock_guard<std::mutex> lk(mu_);
       if (!stop_ && error_code_ == 0) {
@@ -162,6 +167,7 @@ void NativeStager::run() {
         hipMemcpyAsync(buffers_[b], arena_->slot_data(p, s), info.used_bytes, hipMemcpyHostToDevice, copy_stream_) !=
             hipSuccess)
       return fail(-1, static_cast<int32_t>(p), "hipMemcpyAsync H2D failed");
+    const int64_t s4 = ns();
     // retire event of w: a ring, so window w - kRetireEvents must have been retired before it is re-recorded
     const int rev = static_cast<int>((w - first_) % kRetireEvents);
     {
@@ -181,9 +187,11 @@ void NativeStager::run() {
     info.t_ready_host = mono_s();
     bytes_h2d_ += info.used_bytes;
     windows_staged_ += 1;
+    const int64_t s5 = ns();
     {
       std::lock_guard<std::mutex> lk(mu_);
       staged_[w] = info;
+      if (wait_log_.size() < 4096) wait_log_.push_back({w, s1 - s0, s2 - s1, s3 - s2, s4 - s3, s5 - s4, s0});
     }
     cv_.notify_all();
   }

@@ -88,8 +88,10 @@ class NativeStager {
   uint64_t windows_landed() const { return windows_landed_.load(); }
   uint64_t bytes_landed() const { return bytes_landed_.load(); }
   double wait_producer_s() const { return wait_producer_ns_.load() * 1e-9; }
-  // per staged window (first 4096): ns waited for the producer, and ns from enqueue to retire
-  std::vector<std::pair<int64_t, uint64_t>> wait_log() const {
+  // per staged window (first 4096): ns spent in each step of the stager loop -- waiting for the ring
+  // (consumer release), enqueueing the free-event wait, waiting for the producer, enqueueing the copy,
+  // waiting for a retire-event slot + recording the events
+  std::vector<std::vector<int64_t>> wait_log() const {
     std::lock_guard<std::mutex> lk(mu_);
     return wait_log_;
   }
@@ -136,7 +138,7 @@ class NativeStager {
   std::string error_msg_;
   std::atomic<uint64_t> bytes_h2d_{0}, windows_staged_{0}, wait_producer_ns_{0};
   std::atomic<uint64_t> windows_landed_{0}, bytes_landed_{0};
-  std::vector<std::pair<int64_t, uint64_t>> wait_log_;  // guarded by mu_
+  std::vector<std::vector<int64_t>> wait_log_;  // guarded by mu_
   std::thread thread_;
 };
 

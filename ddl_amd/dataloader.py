@@ -206,8 +206,8 @@ class DistributedDataLoader(DistributedDataloaderABC):
         self._win_done: dict = {}  # window -> event after its last batch kernel (Python dispatch path)
         self._host_window: int | None = None  # host path: window currently held
         self._cur = None                      # device path: StagedWindow of the current window
-        # True / "auto": native engine, inline for small batches (< 16 MB), lookahead on the batch stream
-        # for large ones; "inline" / "lookahead" force the mode; False: the Python dispatch path
+        # True / "auto": native engine in inline mode (batch kernel on the caller's stream at get time);
+        # "lookahead": one batch ahead on the batch stream; False: the Python dispatch path
         if native_dispatch not in (True, False, "auto", "inline", "lookahead"):
             raise ValueError("native_dispatch must be a bool or 'auto' / 'inline' / 'lookahead'")
         self.native_dispatch = "auto" if native_dispatch is True else native_dispatch
@@ -377,8 +377,8 @@ class DistributedDataLoader(DistributedDataloaderABC):
         self._eng_slot_bytes = max(256, off)
         self._eng_block = int(min(64, max(4, (512 << 20) // self._eng_slot_bytes)))
         mode = self.native_dispatch
-        if mode == "auto":
-            mode = "inline" if self._eng_slot_bytes < (16 << 20) else "lookahead"
+        if mode == "auto":  # measured: inline is ahead at every batch size (profiles/r2_native_dispatch)
+            mode = "inline"
         self._engine.inline = mode == "inline"
         self._eng_mode = mode
         self._eng_slots: collections.deque = collections.deque()  # (slot id, outputs, block)

@@ -56,6 +56,41 @@ class StagedWindow:
     tags: tuple = ()
 
 
+_SDMA_WARM: set = set()
+
+
+def warm_copy_engines(device: torch.device, n_engines: int = 4, nbytes: int = 512 << 20) -> float:
+    """Bring up the SDMA copy engines this process's H2D copies will use, once per device.
+
+    The HIP runtime spreads back-to-back async copies over the GPU's SDMA engines: each copy goes to
+    the lowest-numbered engine that is idle at enqueue time. The FIRST copy an engine runs in a
+    process costs the enqueueing thread 6.5-11 ms (engine bring-up, measured with AMD_LOG_LEVEL=4:
+    ``profiles/r2_sdma_warmup``). The stager enqueues copies while earlier ones are still in
+    flight, so its 2nd and 3rd engines came up in the middle of a run -- a 6.5 ms stall of the
+    stager thread each time, i.e. a hole of ~5 windows of H2D in a short benchmark.
+    Here ``n_engines`` copies of ``nbytes`` are enqueued on separate streams back to back, each
+    long enough to keep its engine busy while the next one comes up. Returns the seconds spent.
+    """
+    import os
+    import time
+
+    key = (device.type, device.index)
+    if key in _SDMA_WARM or device.type != "cuda" or os.environ.get("DDL_WARM_SDMA", "1") == "0":
+        return 0.0
+    _SDMA_WARM.add(key)
+    t0 = time.perf_counter()
+    src = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    dsts = [torch.empty(nbytes, dtype=torch.uint8, device=device) for _ in range(n_engines)]
+    ss = [torch.cuda.Stream(device=device) for _ in range(n_engines)]
+    for d, st in zip(dsts, ss):
+        with streams.on_stream(st):
+            d.copy_(src, non_blocking=True)
+    for st in ss:
+        st.synchronize()
+    del src, dsts
+    return time.perf_counter() - t0
+
+
 class WindowStager:
     """Python face of the native stager (``_ddl_hip.NativeStager``).
 
@@ -69,6 +104,7 @@ class WindowStager:
         if depth < 1:
             raise ValueError("prefetch depth must be >= 1")
         hip, rt = _native.hip(), _native.runtime()
+        self.sdma_warm_s = warm_copy_engines(torch.device(device))
         if hip.ARENA_ABI != rt.ARENA_ABI:
             raise NativeExtensionError("_ddl_hip and _ddl_runtime disagree on the Arena layout: rebuild both")
         self.conn = connection
