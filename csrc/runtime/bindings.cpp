@@ -193,6 +193,28 @@ PYBIND11_MODULE(_ddl_runtime, m) {
       py::arg("keys"), py::arg("half_bits"), py::arg("n"), py::arg("positions"),
       "perm(positions) of the 6-round Feistel permutation (bit-identical to the gfx950 kernels)");
   m.def(
+      "in_order_rows",
+      [](py::array_t<int64_t, py::array::c_style> lengths, int64_t seq_len) {
+        if (seq_len < 1) throw std::invalid_argument("in_order_rows: seq_len must be >= 1");
+        const int64_t* l = lengths.data();
+        const py::ssize_t m = lengths.size();
+        int64_t rows = 0, cur = seq_len;  // cur = tokens in the open row (seq_len: no open row)
+        for (py::ssize_t i = 0; i < m; ++i) {
+          for (int64_t n = l[i]; n > 0;) {
+            const int64_t seg = n < seq_len ? n : seq_len;
+            if (cur + seg > seq_len) {
+              ++rows;
+              cur = 0;
+            }
+            cur += seg;
+            n -= seg;
+          }
+        }
+        return rows;
+      },
+      py::arg("lengths"), py::arg("seq_len"),
+      "rows that in-order packing (pack_plan) of sequences of these lengths produces");
+  m.def(
       "owner_counts",
       [](std::vector<uint64_t> keys, uint32_t half_bits, uint64_t n, int64_t pos0, int64_t gb, int64_t lb,
          int64_t shard_rows, int64_t world, int64_t rank) {

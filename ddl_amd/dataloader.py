@@ -102,7 +102,10 @@ class DistributedDataloaderABC(ABC):
 
 
 @for_all_methods(with_logging, exclude=["__getitem__", "__len__", "__iter__", "mark", "_on_batch_end",
-                                        "_window", "_batch_from_window", "_schedule"])
+                                        "_window", "_batch_from_window", "_schedule", "_engine_batch",
+                                        "_engine_provide", "_release_window", "_advance_window",
+                                        "_advance_to_next_producer", "_begin_window", "_update_len",
+                                        "_end_access_epoch", "_device_batch", "_enqueue_batch"])
 class DistributedDataLoader(DistributedDataloaderABC):
     def __init__(
         self,
@@ -206,8 +209,8 @@ class DistributedDataLoader(DistributedDataloaderABC):
         self._win_done: dict = {}  # window -> event after its last batch kernel (Python dispatch path)
         self._host_window: int | None = None  # host path: window currently held
         self._cur = None                      # device path: StagedWindow of the current window
-        # True / "auto": native engine in inline mode (batch kernel on the caller's stream at get time);
-        # "lookahead": one batch ahead on the batch stream; False: the Python dispatch path
+        # True / "auto": native engine, inline (batch kernel on the caller's stream at get time) for batches
+        # under 16 MB, lookahead (one batch ahead on the batch stream) above; False: the Python dispatch path
         if native_dispatch not in (True, False, "auto", "inline", "lookahead"):
             raise ValueError("native_dispatch must be a bool or 'auto' / 'inline' / 'lookahead'")
         self.native_dispatch = "auto" if native_dispatch is True else native_dispatch
@@ -220,6 +223,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
             return
 
         P = connection.n_producers
+        self._n_prod = P
         self._check_resume_layout(P)
         rounds0 = [self._first_round(p, P, self.window) for p in range(P)]
         base_meta = MetaData_Consumer_To_Producer(
@@ -377,14 +381,19 @@ class DistributedDataLoader(DistributedDataloaderABC):
         self._eng_slot_bytes = max(256, off)
         self._eng_block = int(min(64, max(4, (512 << 20) // self._eng_slot_bytes)))
         mode = self.native_dispatch
-        if mode == "auto":  # measured: inline is ahead at every batch size (profiles/r2_native_dispatch)
-            mode = "inline"
+        if mode == "auto":
+            # small batches are host-bound: inline (no batch events, ~3 us of C++ per batch); a large batch
+            # kernel (25 us for 256 images) is worth overlapping with the previous step on the batch stream
+            # (GPU idle behind a train step 0.17% lookahead vs 0.71% inline, profiles/r2_native_dispatch)
+            mode = "inline" if self._eng_slot_bytes < (16 << 20) else "lookahead"
         self._engine.inline = mode == "inline"
         self._eng_mode = mode
         self._eng_slots: collections.deque = collections.deque()  # (slot id, outputs, block)
         self._eng_next_id = 0
         self._eng_rec = (None, None)  # (block, stream) of the last record_stream
         self._eng_window = None
+        self._eng_streams: dict = {}  # torch stream id -> (Stream, raw hipStream_t)
+        self._eng_budget = 0
         # the first blocks are allocated up front, outside any timed loop: >= 24 slots, so that in steady
         # state every new block reuses a freed one from the caching allocator (no hipMalloc per block)
         for _ in range(max(2, -(-24 // self._eng_block))):
@@ -423,15 +432,24 @@ class DistributedDataLoader(DistributedDataloaderABC):
 
     def _engine_batch(self, local: int, bpw: int):
         eng = self._engine
-        if eng.slots_left < 3:
-            self._engine_provide()
-        cur = streams.current(self.device.index)
+        self._eng_budget -= 2  # a get takes at most 2 slots (the batch + a lookahead): query only when low
+        if self._eng_budget < 4:
+            if eng.slots_left < 4:
+                self._engine_provide()
+            self._eng_budget = eng.slots_left
+        sid = torch._C._cuda_getCurrentStream(self.device.index)
+        hit = self._eng_streams.get(sid)
+        if hit is None:
+            st = streams.current(self.device.index)
+            hit = self._eng_streams[sid] = (st, st.cuda_stream)
+        cur, handle = hit
+        w = self.window
         nxt = self.window_in_epoch + 1 < self.windows_per_epoch or self.epoch + 1 < self.n_epochs
-        slot, prod, tags = eng.get(self.window, local, bpw, nxt, cur.cuda_stream, self._timeout_ms)
+        slot, prod, tags = eng.get(w, local, bpw, nxt, handle, self._timeout_ms)
         if slot < 0:
-            self._engine_raise(slot, prod, f"batch {local} of window {self.window}")
-        if self._eng_window != self.window:
-            self._eng_window = self.window
+            self._engine_raise(slot, prod, f"batch {local} of window {w}")
+        if self._eng_window != w:
+            self._eng_window = w
             self.metrics.windows += 1
         q = self._eng_slots
         while q[0][0] != slot:  # slots the engine skipped (dropped lookahead)
@@ -522,6 +540,17 @@ class DistributedDataLoader(DistributedDataloaderABC):
         return None
 
     def __getitem__(self, idx: int):
+        eng = self._engine
+        if eng is not None and 0 <= idx < self._len:  # native dispatch: the lean path
+            bpw = self.batches_per_window[self.window % self._n_prod]
+            local = idx - self.epoch_batch + self.batch
+            if 0 <= local < bpw:
+                out = self._engine_batch(local, bpw)
+                self.metrics.on_batch(self.batch_size)
+                if self.debug_checksum:
+                    first = out["input_ids"] if isinstance(out, dict) else out[0]
+                    self.checksums.append(int(ops.checksum(first).item()))
+                return out
         if idx < 0:
             raise ValueError(f"negative batch index {idx}")
         if idx >= self._len:

@@ -121,7 +121,12 @@ def ffd_order(lengths: np.ndarray, seq_len: int) -> tuple[np.ndarray, int]:
 
 def in_order_rows(lengths: np.ndarray, seq_len: int) -> int:
     """Rows that in-order packing (``pack_plan``) of sequences of these lengths produces:
-    over-long sequences become ``seq_len`` chunks, a row breaks where the next segment does not fit."""
+    over-long sequences become ``seq_len`` chunks, a row breaks where the next segment does not fit.
+    Native (``_ddl_runtime.in_order_rows``); ``in_order_rows_py`` is its reference."""
+    return int(_native.runtime().in_order_rows(np.ascontiguousarray(lengths, dtype=np.int64), int(seq_len)))
+
+
+def in_order_rows_py(lengths: np.ndarray, seq_len: int) -> int:
     S = int(seq_len)
     rows, cur = 0, S  # cur = tokens in the open row (S: no open row)
     for n in np.asarray(lengths, dtype=np.int64).tolist():
@@ -235,7 +240,7 @@ class TokenBatchProducer(ProducerFunctionSkeleton):
             if ffd_rows < in_order_rows(lens, self.seq_len):  # FFD is a heuristic: keep it only if it wins
                 idx = idx[order]
         buf: torch.Tensor = kwargs["my_tensor"].view(-1)
-        v = self.layout.views(buf)
+        v = _cached_views(buf, self.layout)
         toks = self.source.tokens.tensor().view(-1)
         offs = self.source.offsets.tensor().view(-1)
         rt = _native.runtime()

@@ -201,11 +201,14 @@ def test_ffd_never_packs_into_more_rows():
     lens = np.array([5, 3, 2, 4, 3, 3])
     assert in_order_rows(lens, 10) == 2 == len(ops.pack_plan(np.concatenate([[0], np.cumsum(lens)]), 10)[0])
     assert ffd_order(lens, 10)[1] == 3 == ffd_order_py(lens, 10)[1]
+    from ddl_amd.models.tokens import in_order_rows_py
+
     rng = np.random.default_rng(5)
-    for _ in range(200):  # in_order_rows equals the native planner's row count
+    for _ in range(200):  # in_order_rows (native) == its Python reference == the native planner's row count
         S = int(rng.choice([1, 7, 100]))
         ln = rng.integers(0, 3 * S + 1, size=int(rng.integers(0, 40)))
-        assert in_order_rows(ln, S) == len(ops.pack_plan(np.concatenate([[0], np.cumsum(ln)]), S)[0])
+        assert in_order_rows(ln, S) == in_order_rows_py(ln, S) == \
+            len(ops.pack_plan(np.concatenate([[0], np.cumsum(ln)]), S)[0])
 
 
 def test_ffd_requires_pack_mode(corpus):

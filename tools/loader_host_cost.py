@@ -30,6 +30,8 @@ def run(shape: str, native, steps: int) -> dict:
     from ddl_amd.models import PointwiseProducer
     from ddl_amd.models.producers import ImageWindowProducer
 
+    if shape == "tokens":
+        return run_tokens(native, steps)
     with ddl_amd.start(n_producers=3) as (env, conn):
         dev = torch.device(env.device)
         if shape == "pointwise":
@@ -63,11 +65,48 @@ def run(shape: str, native, steps: int) -> dict:
             "engine": st.get("native_dispatch")}
 
 
+def run_tokens(native, steps: int, producers: int = 8) -> dict:
+    """Config 4 shape: 64 sequences (seq_len 4096, mean ~2.2k tokens) per batch, packed, one window per batch."""
+    import torch
+
+    import ddl_amd
+    from ddl_amd.models.tokens import SharedTokenSource, TokenBatchProducer
+
+    src = SharedTokenSource.synthetic(f"ddl_amd_lhc_{os.getpid()}", 8192, 256, 4096, seed=1)
+    try:
+        with ddl_amd.start(n_producers=producers) as (env, conn):
+            dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(src, 64, 4096, "pack", pack_order="ffd"), 64, conn,
+                                               10 ** 4, mode="indexed", env=env, collate="tokens", auto_mark=True,
+                                               native_dispatch=native)
+
+            def gen():
+                while True:
+                    yield from dl
+
+            it = gen()
+            for _ in range(200):
+                next(it)
+            torch.cuda.synchronize()
+            c0, w0 = time.thread_time(), time.perf_counter()
+            for _ in range(steps):
+                next(it)
+            c1, w1 = time.thread_time(), time.perf_counter()
+            st = dl.stats()
+            torch.cuda.synchronize()
+            dl.close()
+    finally:
+        src.close()
+    return {"shape": "tokens (64 seqs packed, 8 producers)", "dispatch": native if native else "python",
+            "batches": steps, "thread_cpu_us": round(1e6 * (c1 - c0) / steps, 2),
+            "wall_us": round(1e6 * (w1 - w0) / steps, 2), "consumer_wait_s": round(st["consumer_wait_s"], 4),
+            "engine": st.get("native_dispatch")}
+
+
 def main() -> int:
     steps = int(os.environ.get("STEPS", "3000"))
-    for shape in ("pointwise", "images"):
+    for shape in ("pointwise", "images", "tokens"):
         for native in ("inline", "lookahead", False):
-            print(json.dumps(run(shape, native, steps if shape == "pointwise" else steps // 5)), flush=True)
+            print(json.dumps(run(shape, native, steps // 5 if shape == "images" else steps)), flush=True)
     return 0
 
 
