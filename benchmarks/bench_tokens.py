@@ -28,6 +28,8 @@ def main(argv=None):
     ap.add_argument("--producers", type=int, default=4)
     ap.add_argument("--slots", type=int, default=1, help="windows per producer (a producer fills one while the "
                                                           "previous is in flight)")
+    ap.add_argument("--batches-per-window", type=int, default=8,
+                    help="global batches per producer window (per-window costs amortised over k batches)")
     ap.add_argument("--dispatch", default="auto", choices=["auto", "inline", "lookahead", "python"])
     ap.add_argument("--mode", default="pack", choices=["pad", "pack"])
     ap.add_argument("--pack-order", default="ffd", choices=["in_order", "ffd"],
@@ -68,7 +70,8 @@ def main(argv=None):
                 source = src
             n_epochs = (a.warmup + a.steps + a.idle_steps + a.warmup // 2) // (a.n_seqs // gb) + 2
             dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(source, gb, a.seq_len, a.mode,
-                                                                  pack_order=a.pack_order if a.mode == "pack" else "in_order"), a.batch, conn,
+                                                                  pack_order=a.pack_order if a.mode == "pack" else "in_order",
+                                                                  batches_per_window=a.batches_per_window), a.batch, conn,
                                                n_epochs, mode="indexed", env=env, collate="tokens", auto_mark=True,
                                                n_slots=a.slots,
                                                native_dispatch=False if a.dispatch == "python" else a.dispatch)
@@ -147,7 +150,7 @@ def main(argv=None):
                     "row_density_est": round(a.batch * mean_len / (rows / a.steps) / a.seq_len, 3),
                     "n_gpus": env.world_size,
                     "steps": a.steps, "ms_per_step": round(1000 * dt / a.steps, 3), "batch_seqs": a.batch,
-                    "producers": a.producers, "slots": a.slots, "dispatch": a.dispatch, "mean_len": round(mean_len, 1),
+                    "producers": a.producers, "slots": a.slots, "batches_per_window": dl.batches_per_window[0], "dispatch": a.dispatch, "mean_len": round(mean_len, 1),
                     "consumer_wait_s": round(st["consumer_wait_s"], 3),
                     "gpu_idle_pct": None if idle is None else round(idle["gpu_idle_pct"], 3),
                     "train_step": None if idle is None else {

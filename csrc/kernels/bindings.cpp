@@ -43,6 +43,7 @@ py::dict staged_dict(const ddl::StagedInfo& i) {
   d["used_bytes"] = i.used_bytes;
   d["tag"] = py::make_tuple(i.tag[0], i.tag[1], i.tag[2], i.tag[3]);
   d["t_ready_host"] = i.t_ready_host;
+  d["meta"] = py::tuple(py::cast(i.meta));
   return d;
 }
 
@@ -191,7 +192,7 @@ PYBIND11_MODULE(_ddl_hip, m) {
       .def(py::init([](uintptr_t arena, int32_t n_producers, int32_t n_slots, int64_t first, int64_t total,
                        std::vector<uintptr_t> buffers, uint64_t buffer_bytes, uintptr_t copy_stream, int device,
                        std::vector<int32_t> peer_pids, int64_t timeout_ms, std::vector<uintptr_t> ready,
-                       std::vector<uintptr_t> copy_done, bool post_copy) {
+                       std::vector<uintptr_t> copy_done, bool post_copy, int64_t meta_bytes) {
              std::vector<void*> bufs;
              for (auto b : buffers) bufs.push_back(as_ptr<void>(b));
              std::vector<hipEvent_t> rd, cd;
@@ -200,12 +201,12 @@ PYBIND11_MODULE(_ddl_hip, m) {
              return std::make_unique<ddl::NativeStager>(
                  reinterpret_cast<const ddl::Arena*>(arena), n_producers, n_slots, first, total, std::move(bufs),
                  buffer_bytes, as_stream(copy_stream), device, std::move(peer_pids), timeout_ms, std::move(rd),
-                 std::move(cd), post_copy);
+                 std::move(cd), post_copy, meta_bytes);
            }),
            py::arg("arena"), py::arg("n_producers"), py::arg("n_slots"), py::arg("first"), py::arg("total"),
            py::arg("buffers"), py::arg("buffer_bytes"), py::arg("copy_stream"), py::arg("device"),
            py::arg("peer_pids"), py::arg("timeout_ms"), py::arg("ready"), py::arg("copy_done"),
-           py::arg("post_copy"))
+           py::arg("post_copy"), py::arg("meta_bytes") = 0)
       .def(
           "wait",
           [](ddl::NativeStager& st, int64_t w, int64_t timeout_ms) {
@@ -268,7 +269,7 @@ PYBIND11_MODULE(_ddl_hip, m) {
              r.widths = std::move(widths);
              r.aff = make_affine(scale, bias, plane);
              if (kind == 2) {
-               if (token.size() != 8) throw std::invalid_argument("BatchEngine: token recipe needs 8 values");
+               if (token.size() != 9) throw std::invalid_argument("BatchEngine: token recipe needs 9 values");
                r.token_mode = static_cast<int32_t>(token[0]);
                r.pad_id = static_cast<int32_t>(token[1]);
                r.seq_len = token[2];
@@ -277,6 +278,7 @@ PYBIND11_MODULE(_ddl_hip, m) {
                r.off_row_end = token[5];
                r.off_seg_offsets = token[6];
                r.off_tokens = token[7];
+               r.header_stride = token[8];
              }
              std::vector<void*> bufs;
              for (auto b : buffers) bufs.push_back(as_ptr<void>(b));

@@ -140,9 +140,13 @@ int BatchEngine::enqueue(int64_t w, int64_t local, const StagedInfo& info, Pendi
   }
   int rc;
   if (r_.kind == 2) {  // token window: outputs ids, mask, pos (+ seg, cu)
-    const uint8_t* win = static_cast<const uint8_t*>(src);
+    // sub-batch `local` of a k-batch window: its header block, its token run (meta: n_tokens, n_rows,
+    // n_seg, max_seg, token start -- copied to the host by the stager at staging time)
+    if (info.meta.size() < static_cast<size_t>(5 * (local + 1))) return -1;  // window head not copied
+    const int64_t* m = token_meta(info, local);
+    const uint8_t* win = static_cast<const uint8_t*>(src) + local * r_.header_stride;
     TokenSpec sp{};
-    sp.tokens = reinterpret_cast<const int32_t*>(win + r_.off_tokens);
+    sp.tokens = reinterpret_cast<const int32_t*>(static_cast<const uint8_t*>(src) + r_.off_tokens) + m[4];
     sp.out_tokens = static_cast<int32_t*>(dst[0]);
     sp.attn_mask = static_cast<uint8_t*>(dst[1]);
     sp.position_ids = dst[2];
@@ -158,10 +162,10 @@ int BatchEngine::enqueue(int64_t w, int64_t local, const StagedInfo& info, Pendi
       sp.row_start = reinterpret_cast<const int64_t*>(win + r_.off_row_start);
       sp.row_end = reinterpret_cast<const int64_t*>(win + r_.off_row_end);
       sp.seg_offsets = reinterpret_cast<const int64_t*>(win + r_.off_seg_offsets);
-      sp.n_seg = info.tag[2];
+      sp.n_seg = m[2];
       sp.segment_ids = static_cast<int32_t*>(dst[3]);
       sp.cu_seqlens_out = static_cast<int32_t*>(dst[4]);
-      sp.rows = info.tag[1];
+      sp.rows = m[1];
       rc = sp.rows > 0 ? pad_pack_tokens(sp, st)
                        : (hipMemsetAsync(dst[4], 0, sizeof(int32_t), st) == hipSuccess ? 0 : -1);
     }
@@ -208,7 +212,12 @@ int64_t BatchEngine::get(int64_t w, int64_t local, int64_t bpw, bool next_ok, hi
   if (rc != 0) return -(10 + rc);
   if (tags != nullptr) {
     const StagedInfo& wi = windows_.at(w);
-    for (int k = 0; k < 4; ++k) tags[k] = wi.tag[k];
+    if (r_.kind == 2) {
+      const int64_t* m = token_meta(wi, local);
+      for (int k = 0; k < 4; ++k) tags[k] = m[k];
+    } else {
+      for (int k = 0; k < 4; ++k) tags[k] = wi.tag[k];
+    }
   }
   Pending cur{};
   if (inline_) {

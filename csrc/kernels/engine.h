@@ -60,6 +60,7 @@ struct BatchRecipe {
   int32_t pad_id = 0;
   int64_t seq_len = 0;
   int64_t off_offsets = 0, off_row_start = 0, off_row_end = 0, off_seg_offsets = 0, off_tokens = 0;
+  int64_t header_stride = 0;  // bytes between the header blocks of consecutive sub-batches of a window
 };
 
 class BatchEngine {
@@ -113,6 +114,12 @@ class BatchEngine {
   int enqueue(int64_t w, int64_t local, const StagedInfo& info, Pending* out, bool on_caller = false,
               hipStream_t st = nullptr, bool last_of_window = false);
   const StagedInfo* acquired(int64_t w);
+  // token windows: the 5 meta fields of sub-batch `local` (the stager's host copy of the window head)
+  static const int64_t* token_meta(const StagedInfo& info, int64_t local) {
+    static const int64_t zero[5] = {0, 0, 0, 0, 0};
+    const size_t at = static_cast<size_t>(local) * 5;
+    return at + 5 <= info.meta.size() ? info.meta.data() + at : zero;
+  }
 
   NativeStager* stager_;
   BatchRecipe r_;

@@ -25,7 +25,7 @@ double mono_s() {
 NativeStager::NativeStager(const Arena* arena, int32_t n_producers, int32_t n_slots, int64_t first, int64_t total,
                            std::vector<void*> buffers, uint64_t buffer_bytes, hipStream_t copy_stream, int device,
                            std::vector<int32_t> peer_pids, int64_t timeout_ms, std::vector<hipEvent_t> ready,
-                           std::vector<hipEvent_t> copy_done, bool post_copy)
+                           std::vector<hipEvent_t> copy_done, bool post_copy, int64_t meta_bytes)
     : arena_(arena),
       P_(n_producers),
       n_slots_(n_slots),
@@ -40,6 +40,7 @@ NativeStager::NativeStager(const Arena* arena, int32_t n_producers, int32_t n_sl
       ready_(std::move(ready)),
       copy_done_(std::move(copy_done)),
       post_copy_(post_copy),
+      meta_bytes_(meta_bytes),
       depth_(static_cast<int>(buffers_.size())),
       free_events_(buffers_.size(), nullptr),
       released_upto_(first),
@@ -160,6 +161,10 @@ void NativeStager::run() {
     info.seq = sh->seq.load(std::memory_order_acquire);
     info.used_bytes = sh->used_bytes.load(std::memory_order_acquire);
     for (int k = 0; k < 4; ++k) info.tag[k] = sh->tag[k].load(std::memory_order_acquire);
+    if (meta_bytes_ > 0) {  // the slot is HELD: its producer cannot touch it until the copy retires
+      const auto* m = reinterpret_cast<const int64_t*>(arena_->slot_data(p, s));
+      info.meta.assign(m, m + meta_bytes_ / static_cast<int64_t>(sizeof(int64_t)));
+    }
     if (info.used_bytes > buffer_bytes_)
       return fail(-1, static_cast<int32_t>(p),
                   "window of " + std::to_string(info.used_bytes) + " B exceeds the staging buffer");

@@ -50,6 +50,9 @@ struct StagedInfo {
   uint64_t used_bytes = 0;
   int64_t tag[4] = {0, 0, 0, 0};
   double t_ready_host = 0.0;  // CLOCK_MONOTONIC seconds when the copy was enqueued
+  // the first meta_bytes of the window, copied on the host at staging time (before the slot goes back
+  // to its producer): per-batch metadata of multi-batch windows (e.g. token counts per sub-batch)
+  std::vector<int64_t> meta;
 };
 
 class NativeStager {
@@ -62,7 +65,7 @@ class NativeStager {
   NativeStager(const Arena* arena, int32_t n_producers, int32_t n_slots, int64_t first, int64_t total,
                std::vector<void*> buffers, uint64_t buffer_bytes, hipStream_t copy_stream, int device,
                std::vector<int32_t> peer_pids, int64_t timeout_ms, std::vector<hipEvent_t> ready,
-               std::vector<hipEvent_t> copy_done, bool post_copy);
+               std::vector<hipEvent_t> copy_done, bool post_copy, int64_t meta_bytes = 0);
   ~NativeStager();
 
   NativeStager(const NativeStager&) = delete;
@@ -125,6 +128,7 @@ class NativeStager {
   const int64_t timeout_ms_;
   const std::vector<hipEvent_t> ready_, copy_done_;
   const bool post_copy_;
+  const int64_t meta_bytes_;
   const int depth_;
 
   mutable std::mutex mu_;

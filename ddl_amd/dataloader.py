@@ -253,10 +253,13 @@ class DistributedDataLoader(DistributedDataloaderABC):
         if len(set(self.splits)) != 1 or len({s[1:] for s in self.shapes}) != 1 or len(set(self.dtypes)) != 1:
             raise ShapeMismatchError(md, "producers disagree on sample shape / splits / dtype")
         if self.mode == "indexed":
-            wpe = {int(x.extra.get("batches_per_epoch", 0)) for x in md}
+            # a window may hold k consecutive global batches (token windows: batches_per_window=k)
+            wpe = {int(x.extra.get("windows_per_epoch", x.extra.get("batches_per_epoch", 0))) for x in md}
             if len(wpe) != 1 or 0 in wpe:
                 raise ShapeMismatchError(md, "indexed producers must announce one batches_per_epoch")
             self.windows_per_epoch = wpe.pop()
+            if len(set(self.batches_per_window)) != 1:
+                raise ShapeMismatchError(md, "indexed producers must agree on batches per window")
             self._check_indexed_resume()
         elif self.mode == "split_along_epoch":
             self.windows_per_epoch = P
@@ -275,9 +278,10 @@ class DistributedDataLoader(DistributedDataloaderABC):
             from .staging import WindowStager
 
             max_bytes = max(math.prod(s) * _dtypes.itemsize(d) for s, d in zip(self.shapes, self.dtypes))
+            meta_bytes = max(int(x.extra.get("meta_bytes", 0)) for x in md)
             self._stager = WindowStager(connection, self.n_slots, self.total_windows, self.prefetch_depth,
                                         self.device, max_bytes, post_copy=self._exchange_fn,
-                                        timeout_s=self.timeout_s, first_window=self.window)
+                                        timeout_s=self.timeout_s, first_window=self.window, meta_bytes=meta_bytes)
             connection.add_finalizer(self._stager.close)  # stop the native thread before the arena is unpinned
             if self._produces_copy():
                 self._batch_stream = streams.batch_stream(self.device)
@@ -347,7 +351,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
         if mode == "pack":
             outs += [((rows, S), torch.int32), ((lay.max_segments + 1,), torch.int32)]
         token = [0 if mode == "pad" else 1, int(self.pad_id), S, reg["offsets"][0], reg["row_start"][0],
-                 reg["row_end"][0], reg["seg_offsets"][0], reg["tokens"][0]]
+                 reg["row_end"][0], reg["seg_offsets"][0], reg["tokens"][0], lay.header_stride]
         return dict(kind=2, in_dt=_dtypes.code(torch.int32), out_dt=_dtypes.code(torch.int32), shuffle=False,
                     batch=lay.batch, row_elems=1, seed=0, max_blocks=0, scale=[], bias=[], plane=0,
                     n_data=[int(x.nData) for x in self.metadata_from_producer], widths=[], token=token,
@@ -373,13 +377,13 @@ class DistributedDataLoader(DistributedDataloaderABC):
             st._native, n_producers=self.connection.n_producers, buffers=[b.data_ptr() for b in st.buffers],
             ready=[e.cuda_event for e in st.ready_events], batch_stream=self._batch_stream.cuda_stream,
             device=self.device.index, **rec)
-        # byte layout of one slot: every output 256-byte aligned (views of one uint8 block)
-        self._eng_layout, off = [], 0
+        # byte layout of one slot: every output 256-byte aligned, in order (a block holds K slots back to back)
+        self._eng_layout, size = [], 0
         for sh, dt in self._eng_outputs:
-            self._eng_layout.append((off, sh, dt))
-            off += -(-math.prod(sh) * _dtypes.itemsize(dt) // 256) * 256
-        self._eng_slot_bytes = max(256, off)
-        self._eng_block = int(min(64, max(4, (512 << 20) // self._eng_slot_bytes)))
+            self._eng_layout.append((sh, dt, size))
+            size += -(-math.prod(sh) * _dtypes.itemsize(dt) // 256) * 256
+        self._eng_slot_bytes = max(256, size)
+        self._eng_block = int(min(128, max(4, (512 << 20) // self._eng_slot_bytes)))
         mode = self.native_dispatch
         if mode == "auto":
             # small batches are host-bound: inline (no batch events, ~3 us of C++ per batch); a large batch
@@ -400,16 +404,23 @@ class DistributedDataLoader(DistributedDataloaderABC):
             self._engine_provide()
 
     def _engine_provide(self) -> None:
-        """One allocation (on the batch stream) for a block of output slots; each slot is used once."""
-        K, sb = self._eng_block, self._eng_slot_bytes
+        """One allocation (on the batch stream) for a block of output slots; each slot is used once.
+        The K slots' views of an output come from ONE strided view + ``unbind`` (per-slot slicing cost
+        ~9 us per batch of host time on the box: three tensor ops per output per slot)."""
+        K = self._eng_block
         with streams.on_stream(self._batch_stream):
-            block = torch.empty(K * sb, dtype=torch.uint8, device=self.device)
-        ptrs = []
-        for k in range(K):
-            outs = tuple(block[k * sb + off:k * sb + off + math.prod(sh) * _dtypes.itemsize(dt)].view(dt).view(sh)
-                         for off, sh, dt in self._eng_layout)
-            ptrs.append([t.data_ptr() for t in outs])
-            self._eng_slots.append((self._eng_next_id + k, outs, block))
+            block = torch.empty(K * self._eng_slot_bytes, dtype=torch.uint8, device=self.device)
+        base, sb, per_group, ptrs = block.data_ptr(), self._eng_slot_bytes, [], [[] for _ in range(K)]
+        for sh, dt, off in self._eng_layout:
+            isz = _dtypes.itemsize(dt)
+            inner = [1] * len(sh)
+            for d in range(len(sh) - 2, -1, -1):
+                inner[d] = inner[d + 1] * sh[d + 1]
+            per_group.append(block[off:].view(dt).as_strided((K,) + tuple(sh), (sb // isz,) + tuple(inner)).unbind(0))
+            for k in range(K):
+                ptrs[k].append(base + k * sb + off)
+        first = self._eng_next_id
+        self._eng_slots.extend(zip(range(first, first + K), zip(*per_group), [block] * K))
         self._eng_next_id += K
         self._engine.provide(ptrs)
 
@@ -537,6 +548,10 @@ class DistributedDataLoader(DistributedDataloaderABC):
             self._host_window = self.window
             self._host_seq = int(info["seq"])
             self._host_tags = tuple(info["tag"])
+            if self.collate == "tokens":  # per-sub-batch sizes live at the head of the window
+                _, t = self.arys[p][s]
+                nb = int(self.metadata_from_producer[p].extra.get("meta_bytes", 0))
+                self._host_meta = tuple(t.reshape(-1).view(torch.uint8)[:nb].view(torch.int64).tolist())
         return None
 
     def __getitem__(self, idx: int):
@@ -635,16 +650,17 @@ class DistributedDataLoader(DistributedDataloaderABC):
         if sw is None:  # host path: zero-copy views of the shm window
             _, win = self.arys[p][s]
             seq, tags = self._host_seq, self._host_tags
+            meta = getattr(self, "_host_meta", ())
         else:
             win = sw.data.view(wdt).view((n_data,) + self.sample_shape) if self.collate is None else sw.data
-            seq, tags = sw.seq, sw.tags
+            seq, tags, meta = sw.seq, sw.tags, sw.meta
         if self.collate == "tokens":
             from .models.tokens import TokenWindowLayout, collate_token_window
 
             ex = self.metadata_from_producer[p].extra
             with trace_range("ddl.consumer.tokens"):
                 return collate_token_window(win.reshape(-1), TokenWindowLayout(**ex["token_layout"]),
-                                            ex["token_mode"], tags, self.pad_id)
+                                            ex["token_mode"], meta, self.pad_id, sub=local)
         perm = self._perm_for(p, seq)
         out_dtype = self.out_dtype or (torch.float32 if self.normalize is not None else wdt)
         if self.augment is not None:
@@ -867,10 +883,12 @@ class DistributedDataLoader(DistributedDataloaderABC):
         }
         if self.mode == "indexed":
             extra = self.metadata_from_producer[0].extra if self.metadata_from_producer else {}
+            k = self.batches_per_window[0] if self.batches_per_window else 1
             base.update({
                 "kind": "indexed",
                 "global_batch_cursor": consumed,
-                "batches_per_epoch": self.windows_per_epoch,
+                "batches_per_epoch": self.windows_per_epoch * k,
+                "batches_per_window": k,
                 "global_batch": extra.get("global_batch"),
                 "n_samples": extra.get("n_samples"),
                 "order_seed": extra.get("order_seed"),
@@ -896,13 +914,14 @@ class DistributedDataLoader(DistributedDataloaderABC):
             self.seed = int(sd["seed"])
         if sd.get("kind") == "indexed":
             bpe = int(sd["batches_per_epoch"])
+            k = int(sd.get("batches_per_window", 1))  # global batches per window (token windows)
             cur = int(sd["global_batch_cursor"])
             if cur >= bpe:
                 self.epoch, cur = self.epoch + 1, 0
-            self.window = self.epoch * bpe + cur
-            self.window_in_epoch = cur
+            self.window = self.epoch * (bpe // k) + cur // k
+            self.window_in_epoch = cur // k
             self.epoch_batch = cur
-            self.batch = 0
+            self.batch = cur % k
             self._resume_check = sd
             return
         # exact resume, also mid-window: the producers restart at this window's round
@@ -962,8 +981,13 @@ class DistributedDataLoader(DistributedDataloaderABC):
             if chk.get(key) is not None and ex.get(key) is not None and chk[key] != ex[key]:
                 raise ShapeMismatchError((key, chk[key], ex[key]),
                                          f"checkpoint {key}={chk[key]} does not match the producers' {ex[key]}")
-        if int(chk["batches_per_epoch"]) != self.windows_per_epoch:
+        k = self.batches_per_window[0]
+        if int(chk["batches_per_epoch"]) != self.windows_per_epoch * k:
             raise ShapeMismatchError(chk, "checkpoint batches_per_epoch does not match")
+        if int(chk.get("batches_per_window", 1)) != k:
+            raise ShapeMismatchError((chk.get("batches_per_window", 1), k),
+                                     "checkpoint batches_per_window differs from the producers' (the window "
+                                     "cursor would not map to the same global batches)")
 
     def _seek(self, window: int, window_in_epoch: int, epoch: int, batch: int, epoch_batch: int) -> None:
         """Live reposition: drain staging, move the producers, rebuild the cursor and the stager."""

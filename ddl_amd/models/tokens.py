@@ -35,25 +35,42 @@ from ..permutation import EpochOrder
 from .datasets import SharedArraySource
 
 
+META_FIELDS = 5  # per sub-batch: n_tokens, n_rows, n_seg, max_seg, token start (elements into the tokens region)
+
+
 @functools.lru_cache(maxsize=64)
-def _regions(batch: int, max_segments: int, max_len: int) -> dict[str, tuple[int, int]]:
-    out, off = {}, 0
-    for name, count, size in (("offsets", batch + 1, 8), ("row_start", max_segments, 8),
-                              ("row_end", max_segments, 8), ("seg_offsets", max_segments + 1, 8),
-                              ("tokens", batch * max_len, 4)):
+def _regions(batch: int, max_segments: int, max_len: int, k: int) -> dict[str, tuple[int, int]]:
+    """name -> (byte offset, element count): the meta table, sub-batch 0's header arrays (sub-batch j's are
+    ``header_stride`` bytes further), the shared tokens region; ``_header_stride`` and ``_total`` bytes."""
+    out, off = {"meta": (0, META_FIELDS * k)}, -(-META_FIELDS * k * 8 // 16) * 16
+    hdr0 = off
+    for name, count in (("offsets", batch + 1), ("row_start", max_segments), ("row_end", max_segments),
+                        ("seg_offsets", max_segments + 1)):
         out[name] = (off, count)
-        off += -(-count * size // 8) * 8
+        off += count * 8
+    stride = -(-(off - hdr0) // 16) * 16
+    off = hdr0 + k * stride
+    out["tokens"] = (off, k * batch * max_len)
+    off += -(-k * batch * max_len * 4 // 16) * 16
+    out["_header_stride"] = (stride, 0)
     out["_total"] = (off, 0)
     return out
 
 
 @dataclasses.dataclass(frozen=True)
 class TokenWindowLayout:
-    """Byte layout of one token window (all regions 8-byte aligned)."""
+    """Byte layout of one token window: ``k`` consecutive local batches (all regions 8-byte aligned).
+
+    ``meta`` [k, 5] int64 (n_tokens, n_rows, n_seg, max_seg, token start of each sub-batch) comes first:
+    the stager copies it on the host at staging time (``meta_bytes``), so the consumer knows every
+    sub-batch's sizes without reading the device copy. Then one header block per sub-batch (sequence
+    offsets, packing plan), then the sub-batches' tokens back to back (only used bytes cross PCIe).
+    """
 
     batch: int      # sequences per (local) batch
     seq_len: int    # S
     max_len: int    # longest sequence in the corpus
+    k: int = 1      # batches per window
 
     @property
     def max_segments(self) -> int:
@@ -61,25 +78,38 @@ class TokenWindowLayout:
 
     def regions(self) -> dict[str, tuple[int, int]]:
         """name -> (byte offset, element count). Computed once per layout (per-batch host path)."""
-        return _regions(self.batch, self.max_segments, self.max_len)
+        return _regions(self.batch, self.max_segments, self.max_len, self.k)
 
     @property
     def nbytes(self) -> int:
         return self.regions()["_total"][0]
 
     @property
-    def row_bytes(self) -> int:
-        return -(-self.nbytes // self.batch // 16) * 16
+    def header_stride(self) -> int:
+        return self.regions()["_header_stride"][0]
 
-    def views(self, buf: torch.Tensor) -> dict[str, torch.Tensor]:
-        """Typed views of a uint8 window buffer (host or device)."""
+    @property
+    def meta_bytes(self) -> int:
+        return META_FIELDS * self.k * 8
+
+    @property
+    def row_bytes(self) -> int:
+        return -(-self.nbytes // (self.batch * self.k) // 16) * 16
+
+    def views(self, buf: torch.Tensor, sub: int = 0) -> dict[str, torch.Tensor]:
+        """Typed views of a uint8 window buffer (host or device): sub-batch ``sub``'s header arrays, the
+        whole tokens region and the meta table [k, 5]."""
         v = {}
+        stride = self.header_stride * sub
         for name, (off, count) in self.regions().items():
-            if name == "_total":
+            if name.startswith("_"):
                 continue
-            dt = torch.int32 if name == "tokens" else torch.int64
-            size = 4 if name == "tokens" else 8
-            v[name] = buf[off:off + count * size].view(dt)
+            if name == "tokens":
+                v[name] = buf[off:off + count * 4].view(torch.int32)
+            elif name == "meta":
+                v[name] = buf[off:off + count * 8].view(torch.int64).view(self.k, META_FIELDS)
+            else:
+                v[name] = buf[stride + off:stride + off + count * 8].view(torch.int64)
         return v
 
 
@@ -198,8 +228,12 @@ class TokenBatchProducer(ProducerFunctionSkeleton):
     """
 
     def __init__(self, source: SharedTokenSource, global_batch: int, seq_len: int = 4096, mode: str = "pad",
-                 seed: int | None = None, host_threads: int = 2, pack_order: str = "in_order"):
+                 seed: int | None = None, host_threads: int = 2, pack_order: str = "in_order",
+                 batches_per_window: int = 1):
         super().__init__()
+        if batches_per_window < 1:
+            raise ValueError("batches_per_window must be >= 1")
+        self.batches_per_window = int(batches_per_window)
         if mode not in ("pad", "pack"):
             raise ValueError("mode must be 'pad' or 'pack'")
         if pack_order not in ("in_order", "ffd"):
@@ -220,71 +254,84 @@ class TokenBatchProducer(ProducerFunctionSkeleton):
             self.seed = int(kwargs.get("seed", 0))
         self.order = EpochOrder(self.source.n, self.global_batch, int(self.seed))
         lb = self.order.local_batch(self.world_size)
-        self.layout = TokenWindowLayout(lb, self.seq_len, self.source.max_len)
+        bpe = self.order.batches_per_epoch
+        # k consecutive global batches per window (per-window costs -- producer round, H2D, stager and
+        # window hand-off -- amortised over k batches); k divides the epoch so windows never straddle it
+        k = max(d for d in range(1, min(self.batches_per_window, bpe) + 1) if bpe % d == 0)
+        self.layout = TokenWindowLayout(lb, self.seq_len, self.source.max_len, k)
         rb = self.layout.row_bytes
-        return DataProducerOnInitReturn(lb, rb, (lb, rb), (rb,), "uint8", extra={
-            "batches_per_epoch": self.order.batches_per_epoch, "global_batch": self.global_batch,
-            "n_samples": self.source.n, "order_seed": int(self.seed), "token_layout": dataclasses.asdict(self.layout),
-            "token_mode": self.mode})
+        return DataProducerOnInitReturn(k * lb, rb, (k * lb, rb), (rb,), "uint8", extra={
+            "batches_per_epoch": bpe, "windows_per_epoch": bpe // k, "batches_per_window": k,
+            "global_batch": self.global_batch, "n_samples": self.source.n, "order_seed": int(self.seed),
+            "token_layout": dataclasses.asdict(self.layout), "token_mode": self.mode,
+            "meta_bytes": self.layout.meta_bytes})
 
     def execute_function(self, *args, **kwargs):
         rnd = int(kwargs.get("round", 0))
-        g_total = rnd * (self.n_producers or 1) + (self.producer_index or 0)
-        epoch, g = divmod(g_total, self.order.batches_per_epoch)
-        idx = self.order.indices(epoch, g, self.rank_global or 0, self.world_size)
-        if self.mode == "pack" and self.pack_order == "ffd":
-            offs_all = self.source.offsets.tensor().view(-1).numpy()
-            idx = np.asarray(idx, dtype=np.int64)
-            lens = offs_all[idx + 1] - offs_all[idx]
-            order, ffd_rows = ffd_order(lens, self.seq_len)
-            if ffd_rows < in_order_rows(lens, self.seq_len):  # FFD is a heuristic: keep it only if it wins
-                idx = idx[order]
+        lay, k = self.layout, self.layout.k
         buf: torch.Tensor = kwargs["my_tensor"].view(-1)
-        v = _cached_views(buf, self.layout)
+        meta = _cached_views(buf, lay)["meta"]
         toks = self.source.tokens.tensor().view(-1)
         offs = self.source.offsets.tensor().view(-1)
+        offs_all = offs.numpy()
+        tok_region = _cached_views(buf, lay)["tokens"]
         rt = _native.runtime()
-        o, dst = v["offsets"], v["tokens"]
-        # native ragged gather (thread pool, GIL released): sequences -> window, offsets alongside
-        n_tokens = int(rt.gather_ragged(dst.data_ptr(), o.data_ptr(), toks.data_ptr(), offs.data_ptr(),
-                                        self.source.n, np.ascontiguousarray(idx, np.int64), 4, dst.numel(),
-                                        self.host_threads))
-        n_rows = n_seg = max_seg = 0
-        if self.mode == "pack":  # packing plan written straight into the window (native)
-            cap = self.layout.max_segments
-            n_rows, n_seg = rt.pack_plan(o.data_ptr(), len(idx), self.seq_len, v["row_start"].data_ptr(),
-                                         v["row_end"].data_ptr(), cap, v["seg_offsets"].data_ptr(), cap)
-            if n_seg:
-                max_seg = int(np.diff(v["seg_offsets"][: n_seg + 1].numpy()).max())
-        tok_off = self.layout.regions()["tokens"][0]
-        return {"tags": [n_tokens, n_rows, n_seg, max_seg], "used_bytes": tok_off + 4 * n_tokens}
+        tok0 = 0
+        for j in range(k):
+            g_total = (rnd * (self.n_producers or 1) + (self.producer_index or 0)) * k + j
+            epoch, g = divmod(g_total, self.order.batches_per_epoch)
+            idx = np.asarray(self.order.indices(epoch, g, self.rank_global or 0, self.world_size), dtype=np.int64)
+            if self.mode == "pack" and self.pack_order == "ffd":
+                lens = offs_all[idx + 1] - offs_all[idx]
+                order, ffd_rows = ffd_order(lens, self.seq_len)
+                if ffd_rows < in_order_rows(lens, self.seq_len):  # FFD is a heuristic: keep it only if it wins
+                    idx = idx[order]
+            v = _cached_views(buf, lay, j)
+            o = v["offsets"]
+            dst = tok_region[tok0:]
+            # native ragged gather (thread pool, GIL released): sequences -> window, offsets alongside
+            n_tokens = int(rt.gather_ragged(dst.data_ptr(), o.data_ptr(), toks.data_ptr(), offs.data_ptr(),
+                                            self.source.n, np.ascontiguousarray(idx, np.int64), 4, dst.numel(),
+                                            self.host_threads))
+            n_rows = n_seg = max_seg = 0
+            if self.mode == "pack":  # packing plan written straight into the window (native)
+                cap = lay.max_segments
+                n_rows, n_seg = rt.pack_plan(o.data_ptr(), len(idx), self.seq_len, v["row_start"].data_ptr(),
+                                             v["row_end"].data_ptr(), cap, v["seg_offsets"].data_ptr(), cap)
+                if n_seg:
+                    max_seg = int(np.diff(v["seg_offsets"][: n_seg + 1].numpy()).max())
+            meta[j, 0], meta[j, 1], meta[j, 2], meta[j, 3], meta[j, 4] = n_tokens, n_rows, n_seg, max_seg, tok0
+            tok0 += n_tokens
+        tok_off = lay.regions()["tokens"][0]
+        return {"tags": [tok0, k, 0, 0], "used_bytes": tok_off + 4 * tok0}
 
 
 _VIEW_CACHE: dict = {}
 
 
-def _cached_views(buf: torch.Tensor, layout: TokenWindowLayout) -> dict[str, torch.Tensor]:
-    """``layout.views(buf)`` memoised per (buffer address, size, layout): the consumer collates out of
-    the same few staging buffers every step, and building five views costs ~9 us per batch. A cached
-    view keeps its (window-sized) buffer alive, so no other allocation can take that address while
-    the entry exists; the cache is bounded."""
-    key = (buf.data_ptr(), buf.numel(), buf.device, layout)
+def _cached_views(buf: torch.Tensor, layout: TokenWindowLayout, sub: int = 0) -> dict[str, torch.Tensor]:
+    """``layout.views(buf, sub)`` memoised per (buffer address, size, layout, sub-batch): the consumer
+    collates out of the same few staging buffers every step, and building the views costs ~9 us per
+    batch. A cached view keeps its (window-sized) buffer alive, so no other allocation can take that
+    address while the entry exists; the cache is bounded."""
+    key = (buf.data_ptr(), buf.numel(), buf.device, layout, sub)
     v = _VIEW_CACHE.get(key)
     if v is None:
-        if len(_VIEW_CACHE) >= 32:
+        if len(_VIEW_CACHE) >= 256:
             _VIEW_CACHE.clear()
-        v = _VIEW_CACHE[key] = layout.views(buf)
+        v = _VIEW_CACHE[key] = layout.views(buf, sub)
     return v
 
 
-def collate_token_window(buf: torch.Tensor, layout: TokenWindowLayout, mode: str, tags, pad_id: int = 0):
-    """Expand one (device or host) token window into model inputs."""
+def collate_token_window(buf: torch.Tensor, layout: TokenWindowLayout, mode: str, meta, pad_id: int = 0,
+                         sub: int = 0):
+    """Expand sub-batch ``sub`` of one (device or host) token window into model inputs; ``meta`` is the
+    window's meta table (flat, META_FIELDS per sub-batch: the stager's host copy, or the host window)."""
     from .. import ops
 
-    v = _cached_views(buf.view(-1), layout)
-    n_tokens, n_rows, n_seg = (int(x) for x in tags[:3])
-    max_seqlen = int(tags[3]) if len(tags) > 3 else 0
-    tokens = v["tokens"][:n_tokens]
+    v = _cached_views(buf.view(-1), layout, sub)
+    n_tokens, n_rows, n_seg, max_seqlen, tok0 = (int(x) for x in meta[META_FIELDS * sub:META_FIELDS * (sub + 1)])
+    tokens = v["tokens"][tok0:tok0 + n_tokens]
     if mode == "pad":
         ids, mask, pos = ops.pad_tokens(tokens, v["offsets"], layout.seq_len, pad_id)
         # n_tokens: tokens shipped (pad mode truncates sequences longer than seq_len: mask.sum() can be less)

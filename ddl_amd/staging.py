@@ -54,6 +54,7 @@ class StagedWindow:
     data: torch.Tensor  # uint8 view [nbytes] of the HBM buffer
     t_ready_host: float
     tags: tuple = ()
+    meta: tuple = ()  # the window's first meta_bytes as int64 (multi-batch windows' per-batch metadata)
 
 
 _SDMA_WARM: set = set()
@@ -100,7 +101,7 @@ class WindowStager:
 
     def __init__(self, connection, n_slots: int, total_windows: int, depth: int, device: torch.device,
                  max_window_bytes: int, post_copy: Callable | None = None, timeout_s: float = 600.0,
-                 first_window: int = 0):
+                 first_window: int = 0, meta_bytes: int = 0):
         if depth < 1:
             raise ValueError("prefetch depth must be >= 1")
         hip, rt = _native.hip(), _native.runtime()
@@ -144,7 +145,8 @@ class WindowStager:
             buffer_bytes=max_window_bytes, copy_stream=self.copy_stream.cuda_stream, device=self.device.index,
             peer_pids=list(connection.producer_pids), timeout_ms=int(timeout_s * 1000),
             ready=[e.cuda_event for e in self.ready_events], copy_done=[e.cuda_event for e in self._copy_done],
-            post_copy=post_copy is not None)
+            post_copy=post_copy is not None, meta_bytes=int(meta_bytes))
+        self.meta_bytes = int(meta_bytes)
 
     # -------------------------------------------------------------- consumer
     def _wrap(self, info: dict) -> StagedWindow:
@@ -153,7 +155,8 @@ class WindowStager:
         if sw is None:
             b, n = int(info["buffer"]), int(info["used_bytes"])
             sw = StagedWindow(w, b, int(info["producer"]), int(info["slot"]), int(info["seq"]), n,
-                              self.buffers[b][:n], float(info["t_ready_host"]), tuple(info["tag"]))
+                              self.buffers[b][:n], float(info["t_ready_host"]), tuple(info["tag"]),
+                              tuple(info["meta"]))
             self._staged[w] = sw
         return sw
 

@@ -17,6 +17,9 @@ batch on the GPU with the pad/pack kernel:
   ``max_seqlen`` (the varlen-attention inputs; one entry per segment).
 * ``pad``: one sequence per row, padded with ``pad_id``.
 
+``batches_per_window=k`` ships k consecutive global batches per producer window
+(one producer round, one H2D copy and one stager hand-off per k batches).
+
 ``state_dict()`` is the indexed-kind cursor (seed, epoch, global batch), so a
 job can resume at another world size.
 """
@@ -37,6 +40,7 @@ def main() -> None:
     ap.add_argument("--seq-len", type=int, default=4096)
     ap.add_argument("--global-batch", type=int, default=32, help="sequences per global step")
     ap.add_argument("--epochs", type=int, default=2)
+    ap.add_argument("--batches-per-window", type=int, default=4)
     a = ap.parse_args()
 
     name = f"ddl_amd_example_tok_{os.environ.get('MASTER_PORT', os.getpid())}"
@@ -53,7 +57,8 @@ def main() -> None:
                 n_tok = int(offs.tensor()[-1])
                 src = SharedTokenSource(SharedArraySource(name + "_tok", n_tok, (1,), "int32"), offs, a.seq_len)
             producer = TokenBatchProducer(src, a.global_batch, a.seq_len, a.mode,
-                                          pack_order="ffd" if a.mode == "pack" else "in_order")
+                                          pack_order="ffd" if a.mode == "pack" else "in_order",
+                                          batches_per_window=a.batches_per_window)
             dl = ddl_amd.DistributedDataLoader(producer, a.global_batch // env.world_size, conn, a.epochs,
                                                mode="indexed", env=env, collate="tokens", auto_mark=True)
             for epoch in range(a.epochs):

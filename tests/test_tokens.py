@@ -26,14 +26,18 @@ def _check_pad(batch, source, idx, seq_len):
         assert torch.equal(pos[r, :n], torch.arange(n))
 
 
+@pytest.mark.parametrize("k", [1, 5])
 @pytest.mark.parametrize("mode", ["pad", "pack"])
-def test_token_batches_cpu(corpus, mode, monkeypatch):
+def test_token_batches_cpu(corpus, mode, k, monkeypatch):
+    """k=5 asks for 5 batches per window: 12 batches per epoch -> 4 (the largest divisor <= 5)."""
     monkeypatch.setenv("DDL_DEVICE", "cpu")  # host collate path, even on a GPU box
     seq_len, gb = 256, 16
     order = EpochOrder(corpus.n, gb, 4)
     with ddl_amd.start(n_producers=2) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(corpus, gb, seq_len, mode), gb, conn, 2,
-                                           mode="indexed", env=env, auto_mark=True, collate="tokens", seed=4)
+        dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(corpus, gb, seq_len, mode, batches_per_window=k), gb,
+                                           conn, 2, mode="indexed", env=env, auto_mark=True, collate="tokens", seed=4)
+        assert dl.batches_per_window == [1 if k == 1 else 4] * 2
+        assert len(dl) == order.batches_per_epoch
         for e in range(2):
             for g, batch in enumerate(dl):
                 idx = order.indices(e, g)
@@ -51,12 +55,14 @@ def test_token_batches_cpu(corpus, mode, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("k", [1, 4])
 @pytest.mark.parametrize("mode", ["pad", "pack"])
-def test_token_batches_gpu(corpus, mode):
+def test_token_batches_gpu(corpus, mode, k):
     seq_len, gb = 256, 16
     order = EpochOrder(corpus.n, gb, 4)
     with ddl_amd.start(n_producers=2) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(corpus, gb, seq_len, mode), gb, conn, 1,
+        dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(corpus, gb, seq_len, mode, batches_per_window=k), gb,
+                                           conn, 1,
                                            mode="indexed", env=env, auto_mark=True, collate="tokens", seed=4)
         held = None
         for g, batch in enumerate(dl):
@@ -261,15 +267,18 @@ def test_cu_seqlens_drive_varlen_attention(corpus, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("bpw", [1, 4])
 @pytest.mark.parametrize("mode", ["pad", "pack"])
-def test_token_native_dispatch_matches_python_path(corpus, mode):
-    """Native batch engine (kind 2: pad/pack kernel straight from the staged window) == the Python collate."""
+def test_token_native_dispatch_matches_python_path(corpus, mode, bpw):
+    """Native batch engine (kind 2: pad/pack kernel straight from the staged window) == the Python collate,
+    also for k-batch windows (per-sub-batch header + token run from the stager's host copy of the meta)."""
     seq_len, gb = 256, 16
 
     def run(native):
         out = []
         with ddl_amd.start(n_producers=2) as (env, conn):
-            dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(corpus, gb, seq_len, mode), gb, conn, 2,
+            dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(corpus, gb, seq_len, mode, batches_per_window=bpw),
+                                               gb, conn, 2,
                                                mode="indexed", env=env, auto_mark=True, collate="tokens", seed=4,
                                                native_dispatch=native)
             for _ in range(2):
@@ -291,3 +300,40 @@ def test_token_native_dispatch_matches_python_path(corpus, mode):
                     assert a[k].dtype == b[k].dtype and torch.equal(a[k], b[k]), k
                 else:
                     assert a[k] == b[k], k
+
+
+@pytest.mark.parametrize("live", [False, True])
+def test_multi_batch_window_resume_mid_window(corpus, live, monkeypatch):
+    """Indexed checkpoint of a k-batch-window loader: the cursor counts global batches; resume lands
+    mid-window (window 1, sub-batch 2) and continues with exactly the next global batch."""
+    monkeypatch.setenv("DDL_DEVICE", "cpu")
+    seq_len, gb, k = 256, 16, 4
+    order = EpochOrder(corpus.n, gb, 4)
+
+    def make(conn, env, sd=None):
+        return ddl_amd.DistributedDataLoader(TokenBatchProducer(corpus, gb, seq_len, "pad", batches_per_window=k), gb,
+                                             conn, 2, mode="indexed", env=env, auto_mark=True, collate="tokens",
+                                             seed=4, resume_state=sd)
+
+    with ddl_amd.start(n_producers=2) as (env, conn):
+        dl = make(conn, env)
+        it = iter(dl)
+        for _ in range(6):
+            next(it)
+        sd = dl.state_dict()
+        assert sd["global_batch_cursor"] == 6 and sd["batches_per_window"] == k
+        assert sd["batches_per_epoch"] == order.batches_per_epoch
+        if live:
+            next(it)
+            next(it)
+            dl.load_state_dict(sd)
+            got = [b for _, b in zip(range(3), iter(dl))]
+        else:
+            dl.close()
+    if not live:
+        with ddl_amd.start(n_producers=2) as (env, conn):
+            dl = make(conn, env, sd)
+            got = [b for _, b in zip(range(3), iter(dl))]
+            dl.close()
+    for j, b in enumerate(got):
+        _check_pad(b, corpus, order.indices(0, 6 + j), seq_len)

@@ -65,8 +65,8 @@ def run(shape: str, native, steps: int) -> dict:
             "engine": st.get("native_dispatch")}
 
 
-def run_tokens(native, steps: int, producers: int = 8) -> dict:
-    """Config 4 shape: 64 sequences (seq_len 4096, mean ~2.2k tokens) per batch, packed, one window per batch."""
+def run_tokens(native, steps: int, producers: int = 4, k: int = 8) -> dict:
+    """Config 4 shape: 64 sequences (seq_len 4096, mean ~2.2k tokens) per batch, packed, k batches per window."""
     import torch
 
     import ddl_amd
@@ -75,7 +75,8 @@ def run_tokens(native, steps: int, producers: int = 8) -> dict:
     src = SharedTokenSource.synthetic(f"ddl_amd_lhc_{os.getpid()}", 8192, 256, 4096, seed=1)
     try:
         with ddl_amd.start(n_producers=producers) as (env, conn):
-            dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(src, 64, 4096, "pack", pack_order="ffd"), 64, conn,
+            dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(src, 64, 4096, "pack", pack_order="ffd",
+                                                                  batches_per_window=k), 64, conn,
                                                10 ** 4, mode="indexed", env=env, collate="tokens", auto_mark=True,
                                                native_dispatch=native)
 
@@ -96,7 +97,7 @@ def run_tokens(native, steps: int, producers: int = 8) -> dict:
             dl.close()
     finally:
         src.close()
-    return {"shape": "tokens (64 seqs packed, 8 producers)", "dispatch": native if native else "python",
+    return {"shape": f"tokens (64 seqs packed, {producers} producers, {k} batches per window)", "dispatch": native if native else "python",
             "batches": steps, "thread_cpu_us": round(1e6 * (c1 - c0) / steps, 2),
             "wall_us": round(1e6 * (w1 - w0) / steps, 2), "consumer_wait_s": round(st["consumer_wait_s"], 4),
             "engine": st.get("native_dispatch")}
