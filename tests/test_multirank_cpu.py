@@ -233,3 +233,73 @@ def test_indexed_headline_order_is_world_size_invariant():
         assert not np.array_equal(np.concatenate(merged[1][0]), np.concatenate(merged[1][1]))  # fresh order per epoch
     finally:
         src.close()
+
+
+def _token_rank(rank, world, name, n, max_len, gb, k, resume=None, stop_after=None):
+    """Pad-mode token loader with k-batch windows: each rank's batches as lists of sequence ids
+    (the first token of every synthetic sequence is checked against the corpus instead)."""
+    import ddl_amd
+    from ddl_amd.models import SharedArraySource
+    from ddl_amd.models.tokens import SharedTokenSource, TokenBatchProducer
+
+    offs = SharedArraySource(name + "_off", n + 1, (1,), "int64")
+    n_tok = int(offs.tensor()[-1])
+    src = SharedTokenSource(SharedArraySource(name + "_tok", n_tok, (1,), "int32"), offs, max_len)
+    starts = offs.tensor().view(-1).numpy()
+    toks = src.tokens.tensor().view(-1).numpy()
+    out = []
+    with ddl_amd.start(n_producers=2) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(src, gb, max_len, "pad", batches_per_window=k),
+                                           gb // world, conn, 1, mode="indexed", env=env, collate="tokens",
+                                           auto_mark=True, seed=5, resume_state=resume)
+        for i, b in enumerate(dl):
+            ids = b["input_ids"]
+            # identify each row's sequence by its tokens (synthetic corpus: rows are distinct)
+            seqs = []
+            for r in range(ids.shape[0]):
+                n_r = int(b["attention_mask"][r].sum())
+                hit = [j for j in range(n) if starts[j + 1] - starts[j] == n_r
+                       and np.array_equal(toks[starts[j]:starts[j + 1]], ids[r, :n_r].numpy())]
+                seqs.append(hit[0] if len(hit) == 1 else -1)
+            out.append(seqs)
+            if stop_after is not None and i + 1 == stop_after:
+                sd = dl.state_dict()
+                dl.close()
+                return out, sd
+    return out, None
+
+
+@pytest.fixture
+def token_corpus():
+    from ddl_amd.models.tokens import SharedTokenSource
+
+    src = SharedTokenSource.synthetic(f"ddl_amd_mrtok_{np.random.randint(1 << 30)}", 96, 4, 64, seed=2)
+    yield src
+    src.close()
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_token_windows_world_size_invariant(token_corpus, world):
+    """k-batch token windows keep the indexed order: global batch g = concat of rank slices, at any W."""
+    from ddl_amd.permutation import EpochOrder
+
+    src, gb, k = token_corpus, 8, 4
+    res = run_ranks(_token_rank, world, src.tokens.name[:-4], src.n, src.max_len, gb, k, env={"DDL_DEVICE": "cpu"})
+    order = EpochOrder(src.n, gb, 5)
+    for g in range(order.batches_per_epoch):
+        merged = sum((r[0][g] for r in res), [])
+        assert merged == [int(x) for x in order.indices(0, g)]
+
+
+def test_token_windows_resume_mid_window_at_other_world_size(token_corpus):
+    from ddl_amd.permutation import EpochOrder
+
+    src, gb, k = token_corpus, 8, 4
+    res = run_ranks(_token_rank, 2, src.tokens.name[:-4], src.n, src.max_len, gb, k, None, 6,
+                    env={"DDL_DEVICE": "cpu"})
+    sd = res[0][1]
+    assert sd["global_batch_cursor"] == 6 and sd["batches_per_window"] == k
+    (out, _), = run_ranks(_token_rank, 1, src.tokens.name[:-4], src.n, src.max_len, gb, k, sd,
+                          env={"DDL_DEVICE": "cpu"})
+    order = EpochOrder(src.n, gb, 5)
+    assert out == [[int(x) for x in order.indices(0, g)] for g in range(6, order.batches_per_epoch)]
