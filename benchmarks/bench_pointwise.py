@@ -37,7 +37,7 @@ def main(argv=None) -> None:
     ap.add_argument("--consumer", default="flat", choices=["flat", "groups"],
                     help="flat: ONE streaming checksum over the batch's three groups (adjacent in one allocation); "
                          "groups: one checksum launch per group")
-    ap.add_argument("--dispatch", default="native", choices=["native", "inline", "lookahead", "python"])
+    ap.add_argument("--dispatch", default="native", choices=["native", "inline", "lookahead", "window", "python"])
     a = ap.parse_args(argv)
 
     import torch
@@ -89,13 +89,15 @@ def main(argv=None) -> None:
         sync()
         dt = time.perf_counter() - t0
         rows = 4096 * a.steps * env.world_size
+        mode = (dl.stats().get("native_dispatch") or {}).get("mode")
         dl.close()
         if env.rank == 0:
             print(json.dumps({"bench": "pointwise (reference CI shape)", "rows_per_s": round(rows / dt),
                               "batches_per_s": round(a.steps / dt, 1), "us_per_batch": round(1e6 * dt / a.steps, 1),
                               "vs_reference_ceiling": round(rows / dt / (REF_ROWS_PER_S * env.world_size), 2),
                               "batches_per_window": len(dl), "producers": a.producers, "host_shuffle": a.host_shuffle,
-                              "consumer": a.consumer, "dispatch": a.dispatch, "device": str(dev)}))
+                              "consumer": a.consumer, "dispatch": a.dispatch, "mode": mode,
+                              "device": str(dev)}))
 
 
 if __name__ == "__main__":

@@ -223,11 +223,13 @@ __global__ void __launch_bounds__(kThreads) split_columns_kernel(SplitSpec spec,
       col -= spec.width[g];
       ++g;
     }
-    const int64_t off = row * spec.width[g] + col;
+    const int64_t slot = spec.slot_rows > 0 ? div_small(row, spec.slot_rows, n_rows) : 0;
+    const int64_t off = (row - slot * spec.slot_rows) * spec.width[g] + col;
+    char* out = static_cast<char*>(spec.dst[g]) + slot * spec.slot_stride;
     if constexpr (OUT == kBF16)
-      static_cast<uint16_t*>(spec.dst[g])[off] = f32_to_bf16_bits(v);
+      reinterpret_cast<uint16_t*>(out)[off] = f32_to_bf16_bits(v);
     else
-      static_cast<float*>(spec.dst[g])[off] = v;
+      reinterpret_cast<float*>(out)[off] = v;
   }
 }
 
@@ -246,7 +248,9 @@ __global__ void __launch_bounds__(kThreads) split_columns_raw_kernel(SplitSpec s
       col -= spec.width[g];
       ++g;
     }
-    static_cast<T*>(spec.dst[g])[row * spec.width[g] + col] = v;
+    const int64_t slot = spec.slot_rows > 0 ? div_small(row, spec.slot_rows, n_rows) : 0;
+    reinterpret_cast<T*>(static_cast<char*>(spec.dst[g]) + slot * spec.slot_stride)
+        [(row - slot * spec.slot_rows) * spec.width[g] + col] = v;
   }
 }
 

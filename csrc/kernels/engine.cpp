@@ -73,6 +73,8 @@ BatchEngine::BatchEngine(NativeStager* stager, BatchRecipe recipe, int32_t n_pro
       if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
         throw std::runtime_error("BatchEngine: hipEventCreate failed");
   free_next_.assign(buffers_.size(), 0);
+  if (hipEventCreateWithFlags(&ww_ev_, hipEventDisableTiming) != hipSuccess)
+    throw std::runtime_error("BatchEngine: hipEventCreate failed");
 }
 
 BatchEngine::~BatchEngine() {
@@ -81,6 +83,7 @@ BatchEngine::~BatchEngine() {
   for (auto e : batch_events_) hipEventDestroy(e);
   for (auto& v : free_events_)
     for (auto e : v) hipEventDestroy(e);
+  hipEventDestroy(ww_ev_);
 }
 
 void BatchEngine::provide(const std::vector<std::vector<void*>>& slots) {
@@ -89,7 +92,9 @@ void BatchEngine::provide(const std::vector<std::vector<void*>>& slots) {
     if (s.size() != need) throw std::invalid_argument("BatchEngine.provide: wrong number of outputs per slot");
     free_slots_.push_back(static_cast<int64_t>(slots_.size()));
     slots_.push_back(s);
+    slot_block_.push_back(next_block_);
   }
+  ++next_block_;
 }
 
 const StagedInfo* BatchEngine::acquired(int64_t w) {
@@ -118,6 +123,58 @@ int BatchEngine::enqueue(int64_t w, int64_t local, const StagedInfo& info, Pendi
   if (!on_caller) st = bs_;  // inline mode: the caller's stream (the null stream is a valid one), no event
   const int64_t slot = free_slots_.front();
   free_slots_.pop_front();
+  if (launch(w, local, 1, info, slot, st) != 0) return -1;
+  const uint64_t t2 = clock_ns();
+  if (on_caller) {  // stream order is the dependency: no event
+    *out = Pending{w, local, slot, -1};
+    return 0;
+  }
+  const int ev = next_event_;
+  next_event_ = (next_event_ + 1) % kBatchEvents;
+  if (hipEventRecord(batch_events_[ev], bs_) != hipSuccess) return -1;
+  if (last_of_window) {
+    // the window's free event, from the buffer's own small ring: the next record into this ring is for the
+    // window that re-uses the buffer, which can only be staged after the stager enqueued its wait on this one
+    const int b = info.buffer;
+    hipEvent_t fe = free_events_[b][free_next_[b]];
+    free_next_[b] = (free_next_[b] + 1) % kFreeEvents;
+    if (hipEventRecord(fe, bs_) != hipSuccess) return -1;
+    done_event_[w] = fe;
+  }
+  record_ns_ += clock_ns() - t2;
+  *out = Pending{w, local, slot, ev};
+  return 0;
+}
+
+int BatchEngine::enqueue_window(int64_t w, int64_t bpw, const StagedInfo& info, hipStream_t st) {
+  // bpw consecutive slots of one provide() block (a block's slots are slot_stride_ bytes apart); the
+  // remainder of a block too short for the window is skipped (the caller drops skipped slot ids)
+  while (true) {
+    if (static_cast<int64_t>(free_slots_.size()) < bpw) return -2;
+    const int64_t s0 = free_slots_.front(), last = free_slots_[static_cast<size_t>(bpw - 1)];
+    if (last - s0 == bpw - 1 && slot_block_[s0] == slot_block_[last]) break;
+    const int64_t blk = slot_block_[s0];
+    while (!free_slots_.empty() && slot_block_[free_slots_.front()] == blk) free_slots_.pop_front();
+  }
+  const int64_t s0 = free_slots_.front();
+  for (int64_t j = 0; j < bpw; ++j) free_slots_.pop_front();
+  if (launch(w, 0, bpw, info, s0, st) != 0) return -1;
+  const uint64_t t2 = clock_ns();
+  // the launch is the window buffer's only reader: its free event goes right behind it
+  const int b = info.buffer;
+  hipEvent_t fe = free_events_[b][free_next_[b]];
+  free_next_[b] = (free_next_[b] + 1) % kFreeEvents;
+  if (hipEventRecord(fe, st) != hipSuccess) return -1;
+  done_event_[w] = fe;
+  record_ns_ += clock_ns() - t2;
+  ww_w_ = w;
+  ww_slot0_ = s0;
+  ww_stream_ = st;
+  return 0;
+}
+
+int BatchEngine::launch(int64_t w, int64_t local, int64_t n_batches, const StagedInfo& info, int64_t slot,
+                        hipStream_t st) {
   const auto& dst = slots_[slot];
   const void* src = buffers_[info.buffer];
   uint64_t t0 = clock_ns();
@@ -170,7 +227,10 @@ int BatchEngine::enqueue(int64_t w, int64_t local, const StagedInfo& info, Pendi
                        : (hipMemsetAsync(dst[4], 0, sizeof(int32_t), st) == hipSuccess ? 0 : -1);
     }
   } else if (r_.kind == 0) {
-    rc = gather_rows(dst[0], r_.out_dt, src, r_.in_dt, r_.batch, r_.row_elems, ri, r_.aff, 0, r_.max_blocks, st);
+    // n_batches > 1: consecutive slots are contiguous for this kind (the caller enables whole-window mode
+    // only when a slot is exactly one batch of output)
+    rc = gather_rows(dst[0], r_.out_dt, src, r_.in_dt, n_batches * r_.batch, r_.row_elems, ri, r_.aff, 0,
+                     r_.max_blocks, st);
   } else {
     SplitSpec sp{};
     sp.n_groups = static_cast<int32_t>(r_.widths.size());
@@ -179,29 +239,14 @@ int BatchEngine::enqueue(int64_t w, int64_t local, const StagedInfo& info, Pendi
       sp.dst[g] = dst[g];
       sp.width[g] = r_.widths[g];
     }
-    rc = split_columns(sp, src, r_.in_dt, r_.batch, r_.row_elems, ri, st);
+    if (n_batches > 1) {
+      sp.slot_rows = r_.batch;
+      sp.slot_stride = slot_stride_;
+    }
+    rc = split_columns(sp, src, r_.in_dt, n_batches * r_.batch, r_.row_elems, ri, st);
   }
   if (rc != 0) return -1;
-  const uint64_t t2 = clock_ns();
-  launch_ns_ += t2 - t1;
-  if (on_caller) {  // stream order is the dependency: no event
-    *out = Pending{w, local, slot, -1};
-    return 0;
-  }
-  const int ev = next_event_;
-  next_event_ = (next_event_ + 1) % kBatchEvents;
-  if (hipEventRecord(batch_events_[ev], bs_) != hipSuccess) return -1;
-  if (last_of_window) {
-    // the window's free event, from the buffer's own small ring: the next record into this ring is for the
-    // window that re-uses the buffer, which can only be staged after the stager enqueued its wait on this one
-    const int b = info.buffer;
-    hipEvent_t fe = free_events_[b][free_next_[b]];
-    free_next_[b] = (free_next_[b] + 1) % kFreeEvents;
-    if (hipEventRecord(fe, bs_) != hipSuccess) return -1;
-    done_event_[w] = fe;
-  }
-  record_ns_ += clock_ns() - t2;
-  *out = Pending{w, local, slot, ev};
+  launch_ns_ += clock_ns() - t1;
   return 0;
 }
 
@@ -220,6 +265,23 @@ int64_t BatchEngine::get(int64_t w, int64_t local, int64_t bpw, bool next_ok, hi
     }
   }
   Pending cur{};
+  if (inline_ && whole_ && bpw > 1 && r_.kind != 2) {
+    if (ww_w_ != w) {
+      rc = enqueue_window(w, bpw, windows_.at(w), compute);
+      if (rc != 0) return rc;
+    } else if (compute != ww_stream_) {  // a later batch consumed on another stream: behind the launch
+      const uint64_t s0 = clock_ns();
+      if (hipEventRecord(ww_ev_, ww_stream_) != hipSuccess || hipStreamWaitEvent(compute, ww_ev_, 0) != hipSuccess)
+        return -1;
+      ww_stream_ = compute;
+      streamwait_ns_ += clock_ns() - s0;
+    }
+    last_compute_ = compute;
+    have_compute_ = true;
+    ++batches_;
+    get_ns_ += clock_ns() - g0;
+    return ww_slot0_ + local;
+  }
   if (inline_) {
     last_compute_ = compute;
     have_compute_ = true;
@@ -283,7 +345,7 @@ int BatchEngine::release(int64_t w) {
   hipStream_t st = inline_ && have_compute_ ? last_compute_ : bs_;
   hipEvent_t ev = nullptr;
   auto de = done_event_.find(w);
-  if (!inline_ && de != done_event_.end()) {
+  if (de != done_event_.end()) {
     ev = de->second;  // right after w's last batch kernel, not behind the next window's lookahead
   } else {
     if ((ready_waited_ != w || ready_stream_ != st) && hipStreamWaitEvent(st, ready_[b], 0) != hipSuccess)
@@ -302,6 +364,8 @@ int BatchEngine::release(int64_t w) {
 
 void BatchEngine::reset() {
   done_event_.clear();
+  ww_w_ = -1;
+  ww_slot0_ = -1;
   ready_waited_ = -1;
   ready_stream_ = nullptr;
   pending_.clear();

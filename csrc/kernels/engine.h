@@ -96,6 +96,15 @@ class BatchEngine {
   // the host cost is the bottleneck and the kernel's few microseconds on the compute stream are not.
   void set_inline(bool on) { inline_ = on; }
   bool is_inline() const { return inline_; }
+  // Whole-window mode (inline only; gather/split kinds): the first get() of a window launches ONE kernel
+  // that builds all of its bpw batches into bpw consecutive output slots (slot_stride bytes apart, one
+  // provide() block); the other gets of the window make no HIP call. The window's free event follows that
+  // kernel, so its ring buffer goes back to the stager before the window's batches are consumed.
+  void set_window_mode(bool on, int64_t slot_stride) {
+    whole_ = on;
+    slot_stride_ = slot_stride;
+  }
+  bool window_mode() const { return whole_; }
 
   double wait_s() const { return wait_ns_ * 1e-9; }
   // host ns spent in get() in total, and inside HIP calls: kernel launches, event records, stream waits
@@ -113,6 +122,9 @@ class BatchEngine {
   // else on the batch stream with one
   int enqueue(int64_t w, int64_t local, const StagedInfo& info, Pending* out, bool on_caller = false,
               hipStream_t st = nullptr, bool last_of_window = false);
+  // the batch kernel(s): n_batches batches from `local` on into slot `slot` (and the following slots)
+  int launch(int64_t w, int64_t local, int64_t n_batches, const StagedInfo& info, int64_t slot, hipStream_t st);
+  int enqueue_window(int64_t w, int64_t bpw, const StagedInfo& info, hipStream_t st);
   const StagedInfo* acquired(int64_t w);
   // token windows: the 5 meta fields of sub-batch `local` (the stager's host copy of the window head)
   static const int64_t* token_meta(const StagedInfo& info, int64_t local) {
@@ -147,6 +159,13 @@ class BatchEngine {
   int64_t ready_waited_ = -1;  // window whose HBM-ready event the launch stream already waits on
   hipStream_t ready_stream_ = nullptr;  // ... and that stream
   bool inline_ = false;
+  bool whole_ = false;                 // whole-window mode
+  int64_t slot_stride_ = 0;            // bytes between consecutive slots of a provide() block
+  std::vector<int64_t> slot_block_;    // slot id -> provide() block
+  int64_t next_block_ = 0;
+  int64_t ww_w_ = -1, ww_slot0_ = -1;  // window built by the last whole-window launch, its first slot
+  hipStream_t ww_stream_ = nullptr;    // ... and the stream it ran on
+  hipEvent_t ww_ev_ = nullptr;         // orders a later batch of that window on another stream
   hipStream_t last_compute_ = nullptr;  // inline mode: where the window's reads were enqueued (0 = null stream)
   bool have_compute_ = false;
 };

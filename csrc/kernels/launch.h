@@ -33,6 +33,10 @@ struct SplitSpec {
   int32_t width[8];
   int32_t n_groups;
   int32_t out_dt;
+  // split only: rows land in consecutive output slots of slot_rows rows, slot_stride bytes apart
+  // (a whole window's batches in one launch); 0 = one contiguous [n_rows, width] block per group
+  int64_t slot_rows;
+  int64_t slot_stride;
 };
 int split_columns(const SplitSpec& spec, const void* src, int32_t in_dt, int64_t n_rows, int64_t n_values,
                   const RowIndex& ri, hipStream_t st);

@@ -210,9 +210,11 @@ class DistributedDataLoader(DistributedDataloaderABC):
         self._host_window: int | None = None  # host path: window currently held
         self._cur = None                      # device path: StagedWindow of the current window
         # True / "auto": native engine, inline (batch kernel on the caller's stream at get time) for batches
-        # under 16 MB, lookahead (one batch ahead on the batch stream) above; False: the Python dispatch path
-        if native_dispatch not in (True, False, "auto", "inline", "lookahead"):
-            raise ValueError("native_dispatch must be a bool or 'auto' / 'inline' / 'lookahead'")
+        # under 16 MB -- "window" (one kernel builds all of a window's batches at its first get) when a
+        # window holds several small gather/split batches -- and lookahead (one batch ahead on the batch
+        # stream) above 16 MB; False: the Python dispatch path
+        if native_dispatch not in (True, False, "auto", "inline", "lookahead", "window"):
+            raise ValueError("native_dispatch must be a bool or 'auto' / 'inline' / 'lookahead' / 'window'")
         self.native_dispatch = "auto" if native_dispatch is True else native_dispatch
         self._engine = None                   # native per-batch dispatch (csrc/kernels/engine.cpp)
 
@@ -385,12 +387,27 @@ class DistributedDataLoader(DistributedDataloaderABC):
         self._eng_slot_bytes = max(256, size)
         self._eng_block = int(min(128, max(4, (512 << 20) // self._eng_slot_bytes)))
         mode = self.native_dispatch
+        bpw_max = max(self.batches_per_window)
+        # whole-window launches: gather/split kinds, every window holds >= 2 batches, and consecutive slots
+        # of a block are one contiguous run per output where the kernel needs that (gather: no slot padding)
+        whole_ok = (rec["kind"] in (0, 1) and min(self.batches_per_window) > 1
+                    and (rec["kind"] == 1 or self._eng_slot_bytes == math.prod(self._eng_outputs[0][0])
+                         * _dtypes.itemsize(self._eng_outputs[0][1])))
         if mode == "auto":
-            # small batches are host-bound: inline (no batch events, ~3 us of C++ per batch); a large batch
-            # kernel (25 us for 256 images) is worth overlapping with the previous step on the batch stream
-            # (GPU idle behind a train step 0.17% lookahead vs 0.71% inline, profiles/r2_native_dispatch)
+            # small batches are host-bound: inline (no batch events, ~3 us of C++ per batch), or one launch per
+            # window when a window holds several small batches; a large batch kernel (25 us for 256 images) is
+            # worth overlapping with the previous step on the batch stream (GPU idle behind a train step 0.17%
+            # lookahead vs 0.71% inline, profiles/r2_native_dispatch)
             mode = "inline" if self._eng_slot_bytes < (16 << 20) else "lookahead"
-        self._engine.inline = mode == "inline"
+            if mode == "inline" and whole_ok and self._eng_slot_bytes * bpw_max <= (64 << 20):
+                mode = "window"
+        if mode == "window" and not whole_ok:
+            mode = "inline"
+        self._eng_whole = mode == "window"
+        if self._eng_whole:
+            self._eng_block = max(self._eng_block, bpw_max)  # a window's slots come from one block
+            self._engine.set_window_mode(True, self._eng_slot_bytes)
+        self._engine.inline = mode in ("inline", "window")
         self._eng_mode = mode
         self._eng_slots: collections.deque = collections.deque()  # (slot id, outputs, block)
         self._eng_next_id = 0
@@ -443,11 +460,16 @@ class DistributedDataLoader(DistributedDataloaderABC):
 
     def _engine_batch(self, local: int, bpw: int):
         eng = self._engine
-        self._eng_budget -= 2  # a get takes at most 2 slots (the batch + a lookahead): query only when low
-        if self._eng_budget < 4:
-            if eng.slots_left < 4:
-                self._engine_provide()
-            self._eng_budget = eng.slots_left
+        if self._eng_whole:
+            if local == 0:  # the window's bpw slots, after at most the skipped tail of a block
+                while eng.slots_left < bpw + self._eng_block:
+                    self._engine_provide()
+        else:
+            self._eng_budget -= 2  # a get takes at most 2 slots (the batch + a lookahead): query only when low
+            if self._eng_budget < 4:
+                if eng.slots_left < 4:
+                    self._engine_provide()
+                self._eng_budget = eng.slots_left
         sid = torch._C._cuda_getCurrentStream(self.device.index)
         hit = self._eng_streams.get(sid)
         if hit is None:

@@ -298,9 +298,12 @@ def test_native_dispatch_matches_python_path(case):
     partial = {1: 2, 2: 0}
     ref, st_ref = _collect(False, make, partial=partial, **kw)
     assert st_ref.get("native_dispatch") is None
-    for mode in ("inline", "lookahead"):
+    for mode in ("inline", "lookahead", "window"):
         nat, st = _collect(mode, make, partial=partial, **kw)
-        assert st["native_dispatch"]["batches"] == len(nat) and st["native_dispatch"]["mode"] == mode
+        # whole-window launches need contiguous slots: a gather whose batch is not a multiple of 256 bytes
+        # (gather_cast_bf16: 32 B) falls back to inline
+        expect = "inline" if (mode == "window" and case == "gather_cast_bf16") else mode
+        assert st["native_dispatch"]["batches"] == len(nat) and st["native_dispatch"]["mode"] == expect
         assert len(nat) == len(ref) > 0
         for a, b in zip(nat, ref):
             assert torch.equal(a, b)
@@ -326,3 +329,27 @@ def test_native_dispatch_held_batches_stay_valid():
         assert dl.stats()["native_dispatch"]["batches"] == 30 * 4
     for x, s in zip(held, snap):
         assert torch.equal(x.cpu(), s)
+
+
+def test_window_dispatch_batches_on_other_streams():
+    """Whole-window mode builds a window's batches at its first get on that stream; a later batch of the
+    window consumed on another stream is ordered behind that launch (event + wait), values unchanged."""
+    make = lambda: (IdProducer(64, 8), 16)  # noqa: E731
+    kw = dict(shuffle="device", seed=5, contiguous=True)
+    ref, _ = _collect(False, make, epochs=2, **kw)
+    side = [torch.cuda.Stream() for _ in range(2)]
+    out = []
+    with ddl_amd.start(n_producers=3) as (env, conn):
+        prod, bs = make()
+        dl = ddl_amd.DistributedDataLoader(prod, bs, conn, 2, env=env, native_dispatch="window", **kw)
+        for e in range(2):
+            for i in range(len(dl)):
+                with torch.cuda.stream(side[i % 2]):
+                    b = dl[i]
+                    out.append(torch.cat([t.reshape(t.shape[0], -1).float() for t in b], 1).cpu())
+                dl.mark(Marker.END_OF_BATCH)
+            dl.mark(Marker.END_OF_EPOCH)
+        assert dl.stats()["native_dispatch"]["mode"] == "window"
+    assert len(out) == len(ref) > 0
+    for a, b in zip(out, ref):
+        assert torch.equal(a, b)

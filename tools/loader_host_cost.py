@@ -106,7 +106,7 @@ def run_tokens(native, steps: int, producers: int = 4, k: int = 8) -> dict:
 def main() -> int:
     steps = int(os.environ.get("STEPS", "3000"))
     for shape in ("pointwise", "images", "tokens"):
-        for native in ("inline", "lookahead", False):
+        for native in ("window", "inline", "lookahead", False):
             print(json.dumps(run(shape, native, steps // 5 if shape == "images" else steps)), flush=True)
     return 0
 
