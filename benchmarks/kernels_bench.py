@@ -127,6 +127,28 @@ def main():
     pp = FeistelPermutation(100_520, 5, 5)
     t = bench(lambda: ops.split_columns(pw, (3, 5, 1), perm=pp, base=0, n_rows=4096))
     report("split_columns 4096x(3,5,1) f32", t, 2 * 4096 * 36)
+    # whole-window dispatch: the window's 24 batches in one launch (same kernel, 24x the rows)
+    t = bench(lambda: ops.split_columns(pw, (3, 5, 1), perm=pp, base=0, n_rows=24 * 4096))
+    report("split_columns 24x4096x(3,5,1) f32 (one launch per window)", t, 2 * 24 * 4096 * 36)
+    # resident exchange bucketing (W=8, global batch 2048): send list + receive map, one workgroup each
+    from ddl_amd import _native
+
+    hip = _native.hip()
+    pr = FeistelPermutation(1 << 20, 7, 1)
+    S, W, GB, LB, rank = (1 << 20) // 8, 8, 2048, 256, 1
+    send_idx = torch.empty(GB, dtype=torch.int64, device=dev)
+    inv_idx = torch.empty(LB, dtype=torch.int64, device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    send_c, recv_c = _native.runtime().owner_counts(pr.keys, pr.half_bits, pr.n, 0, GB, LB, S, W, rank)
+    t = bench(lambda: hip.bucket_send(pr.keys, pr.n, pr.half_bits, 0, GB, S, S * rank, rank, W,
+                                      send_idx.data_ptr(), st))
+    report("bucket_send W=8 GB=2048", t, GB * 8, sent=sum(send_c))
+    offs = [0]
+    for c in recv_c[:-1]:
+        offs.append(offs[-1] + c)
+    t = bench(lambda: hip.bucket_recv(pr.keys, pr.n, pr.half_bits, rank * LB, LB, S, W, offs,
+                                      inv_idx.data_ptr(), st))
+    report("bucket_recv W=8 slice 256", t, LB * 8)
     grp = [pw[:, :3].contiguous(), pw[:, 3:8].contiguous(), pw[:, 8:].contiguous()]
     t = bench(lambda: ops.pack_columns(grp))
     report("pack_columns window 100520x(3,5,1) f32", t, 2 * 100_520 * 36)

@@ -206,80 +206,139 @@ int launch_hwc(void* dst, int32_t out_dt, const void* src, int64_t batch, int64_
 }
 
 // ------------------------------------------------------------------ split ---
+// Row tiles of one wavefront: rows are short (the reference's CI rows are 9
+// floats), so a lane per (row, column) element would evaluate the row's
+// Feistel permutation once per element -- 9x the 64-bit hash work per row,
+// which made these kernels ALU-bound at ~0.2 TB/s. Instead each wave owns R
+// (<= 64, tile_rows) consecutive output rows, lane l computes source_row() of
+// row l of the tile ONCE, and the tile's rows*n_values elements are walked lane-contiguously
+// (coalesced reads of each source row, coalesced per-group writes) with the
+// source row fetched from its owner lane by a cross-lane shuffle. The shuffle
+// is executed by all 64 lanes every iteration (uniform loop), so it never
+// reads from a lane that has left the loop.
+// Rows per wave tile: ~128 elements, so a lane walks at most 2 of them -- the dependent
+// load -> store chain per wave stays short and a 4096-row batch still spreads over ~300 waves.
+__host__ __device__ __forceinline__ int64_t tile_rows(int64_t n_values) {
+  const int64_t r = 128 / (n_values > 0 ? n_values : 1);
+  return r < 1 ? 1 : (r > 64 ? 64 : r);
+}
+
+template <typename F>
+__device__ __forceinline__ void for_row_tiles(int64_t n_rows, int64_t n_values, const RowIndex& ri, F&& f) {
+  const int lane = threadIdx.x & 63;
+  const int64_t waves = static_cast<int64_t>(gridDim.x) * (kThreads / 64);
+  const int64_t R = tile_rows(n_values);
+  const int64_t n_tiles = (n_rows + R - 1) / R;
+  const uint32_t nv = static_cast<uint32_t>(n_values);
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * (kThreads / 64) + (threadIdx.x >> 6); t < n_tiles;
+       t += waves) {
+    const int64_t r0 = t * R;
+    const int64_t rows = n_rows - r0 < R ? n_rows - r0 : R;
+    const int64_t mine = lane < rows ? source_row(ri, r0 + lane) : 0;
+    const uint32_t total = static_cast<uint32_t>(rows) * nv;  // <= 64 * n_values
+    for (uint32_t base = 0; base < total; base += 64) {
+      const uint32_t e = base + static_cast<uint32_t>(lane);
+      const uint32_t rr = e < total ? e / nv : 0;
+      const int64_t src_row = __shfl(mine, static_cast<int>(rr), 64);
+      if (e < total) f(r0 + rr, static_cast<int>(e - rr * nv), src_row);
+    }
+  }
+}
+
+// Long rows (n_values > kTileMaxValues): a wave per (row, chunk of kRowChunk elements); the row's source
+// is evaluated once per chunk (the same value in every lane) instead of once per element.
+constexpr int64_t kTileMaxValues = 256;
+constexpr int64_t kRowChunk = 4096;
+
+template <typename F>
+__device__ __forceinline__ void for_row_chunks(int64_t n_rows, int64_t n_values, const RowIndex& ri, F&& f) {
+  const int lane = threadIdx.x & 63;
+  const int64_t waves = static_cast<int64_t>(gridDim.x) * (kThreads / 64);
+  const int64_t chunks = (n_values + kRowChunk - 1) / kRowChunk;
+  for (int64_t item = static_cast<int64_t>(blockIdx.x) * (kThreads / 64) + (threadIdx.x >> 6);
+       item < n_rows * chunks; item += waves) {
+    const int64_t row = item / chunks;
+    const int64_t c0 = (item - row * chunks) * kRowChunk;
+    const int64_t c1 = c0 + kRowChunk < n_values ? c0 + kRowChunk : n_values;
+    const int64_t src_row = source_row(ri, row);
+    for (int64_t c = c0 + lane; c < c1; c += 64) f(row, static_cast<int>(c), src_row);
+  }
+}
+
+template <typename F>
+__device__ __forceinline__ void for_rows(int64_t n_rows, int64_t n_values, const RowIndex& ri, F&& f) {
+  if (n_values <= kTileMaxValues)
+    for_row_tiles(n_rows, n_values, ri, f);
+  else
+    for_row_chunks(n_rows, n_values, ri, f);
+}
+
+// waves the row walk of (n_rows, n_values) can use
+inline int64_t row_walk_waves(int64_t n_rows, int64_t n_values) {
+  return n_values <= kTileMaxValues ? (n_rows + tile_rows(n_values) - 1) / tile_rows(n_values)
+                                    : n_rows * ((n_values + kRowChunk - 1) / kRowChunk);
+}
+
+__device__ __forceinline__ int group_of(const SplitSpec& spec, int* col) {
+  int g = 0;
+  while (g < spec.n_groups - 1 && *col >= spec.width[g]) {
+    *col -= spec.width[g];
+    ++g;
+  }
+  return g;
+}
+
+// output element of group g, row `row` (slotted: whole-window launches, see SplitSpec)
+template <typename T>
+__device__ __forceinline__ T* split_out(const SplitSpec& spec, int g, int64_t row, int col, int64_t n_rows) {
+  const int64_t slot = spec.slot_rows > 0 ? div_small(row, spec.slot_rows, n_rows) : 0;
+  return reinterpret_cast<T*>(static_cast<char*>(spec.dst[g]) + slot * spec.slot_stride) +
+         (row - slot * spec.slot_rows) * spec.width[g] + col;
+}
+
 template <typename Tin, int OUT>
 __global__ void __launch_bounds__(kThreads) split_columns_kernel(SplitSpec spec, const Tin* __restrict__ src,
                                                                  int64_t n_rows, int64_t n_values, RowIndex ri) {
-  // One lane per (row, column): rows are short (the reference's CI rows are
-  // 9 floats); consecutive lanes cover consecutive columns of consecutive
-  // rows, so both the read and the per-group writes stay coalesced.
-  const int64_t total = n_rows * n_values;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
-  for (int64_t e = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; e < total; e += stride) {
-    const int64_t row = div_small(e, n_values, total);
-    int col = static_cast<int>(e - row * n_values);
-    const float v = Px<Tin>::get(src + source_row(ri, row) * n_values, col);
-    int g = 0;
-    while (g < spec.n_groups - 1 && col >= spec.width[g]) {
-      col -= spec.width[g];
-      ++g;
-    }
-    const int64_t slot = spec.slot_rows > 0 ? div_small(row, spec.slot_rows, n_rows) : 0;
-    const int64_t off = (row - slot * spec.slot_rows) * spec.width[g] + col;
-    char* out = static_cast<char*>(spec.dst[g]) + slot * spec.slot_stride;
+  for_rows(n_rows, n_values, ri, [&](int64_t row, int col, int64_t src_row) {
+    const float v = Px<Tin>::get(src + src_row * n_values, col);
+    const int g = group_of(spec, &col);
     if constexpr (OUT == kBF16)
-      reinterpret_cast<uint16_t*>(out)[off] = f32_to_bf16_bits(v);
+      *split_out<uint16_t>(spec, g, row, col, n_rows) = f32_to_bf16_bits(v);
     else
-      reinterpret_cast<float*>(out)[off] = v;
-  }
+      *split_out<float>(spec, g, row, col, n_rows) = v;
+  });
 }
 
 // Same-dtype split: raw element copies (any 1/2/4/8-byte dtype, no rounding).
 template <typename T>
 __global__ void __launch_bounds__(kThreads) split_columns_raw_kernel(SplitSpec spec, const T* __restrict__ src,
                                                                      int64_t n_rows, int64_t n_values, RowIndex ri) {
-  const int64_t total = n_rows * n_values;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
-  for (int64_t e = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; e < total; e += stride) {
-    const int64_t row = div_small(e, n_values, total);
-    int col = static_cast<int>(e - row * n_values);
-    const T v = src[source_row(ri, row) * n_values + col];
-    int g = 0;
-    while (g < spec.n_groups - 1 && col >= spec.width[g]) {
-      col -= spec.width[g];
-      ++g;
-    }
-    const int64_t slot = spec.slot_rows > 0 ? div_small(row, spec.slot_rows, n_rows) : 0;
-    reinterpret_cast<T*>(static_cast<char*>(spec.dst[g]) + slot * spec.slot_stride)
-        [(row - slot * spec.slot_rows) * spec.width[g] + col] = v;
-  }
+  for_rows(n_rows, n_values, ri, [&](int64_t row, int col, int64_t src_row) {
+    const T v = src[src_row * n_values + col];
+    const int g = group_of(spec, &col);
+    *split_out<T>(spec, g, row, col, n_rows) = v;
+  });
 }
 
 // ------------------------------------------------------------------- pack ---
 // Inverse of split: k [n_src, w_g] groups -> one [n_rows, n_values] row block,
 // row r taking source row source_row(ri, r) of every group (gather + concat +
-// cast in one pass). Lane e covers output element e, so the (wide) output
-// write is coalesced; each group's reads are contiguous runs of w_g.
+// cast in one pass), in the same 64-row wave tiles: the output write is
+// lane-contiguous, each group's reads are contiguous runs of w_g.
 template <typename Tin, int OUT>
 __global__ void __launch_bounds__(kThreads) pack_columns_kernel(SplitSpec spec, void* __restrict__ dst,
                                                                 int64_t n_rows, int64_t n_values, RowIndex ri) {
-  const int64_t total = n_rows * n_values;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
-  for (int64_t e = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; e < total; e += stride) {
-    const int64_t row = div_small(e, n_values, total);
-    int col = static_cast<int>(e - row * n_values);
-    int g = 0;
-    while (g < spec.n_groups - 1 && col >= spec.width[g]) {
-      col -= spec.width[g];
-      ++g;
-    }
-    const Tin* s = static_cast<const Tin*>(spec.dst[g]) + source_row(ri, row) * spec.width[g];
+  for_rows(n_rows, n_values, ri, [&](int64_t row, int col, int64_t src_row) {
+    const int64_t e = row * n_values + col;
+    const int g = group_of(spec, &col);
+    const Tin* s = static_cast<const Tin*>(spec.dst[g]) + src_row * spec.width[g];
     if constexpr (OUT == kBF16)
       static_cast<uint16_t*>(dst)[e] = f32_to_bf16_bits(Px<Tin>::get(s, col));
     else if constexpr (OUT == kF32)
       static_cast<float*>(dst)[e] = Px<Tin>::get(s, col);
     else
       static_cast<Tin*>(dst)[e] = s[col];  // raw (same dtype)
-  }
+  });
 }
 
 constexpr int kRaw = -1;
@@ -302,8 +361,8 @@ int split_columns(const SplitSpec& spec, const void* src, int32_t in_dt, int64_t
                   const RowIndex& ri, hipStream_t st) {
   if (n_rows <= 0) return 0;
   if (spec.n_groups < 1 || spec.n_groups > 8) return -2;
-  const int64_t total = n_rows * n_values;
-  int64_t blocks = (total + kThreads - 1) / kThreads;
+  if (n_values < 1 || n_values > (1 << 24)) return -2;  // 64 rows x n_values fits the tile's 32-bit walk
+  int64_t blocks = (row_walk_waves(n_rows, n_values) + kThreads / 64 - 1) / (kThreads / 64);
   if (blocks > 8192) blocks = 8192;
   const dim3 grid(static_cast<uint32_t>(blocks));
   if (spec.out_dt == in_dt) {
@@ -345,8 +404,8 @@ int pack_columns(const SplitSpec& spec, void* dst, int32_t in_dt, int64_t n_rows
                  const RowIndex& ri, hipStream_t st) {
   if (n_rows <= 0) return 0;
   if (spec.n_groups < 1 || spec.n_groups > 8) return -2;
-  const int64_t total = n_rows * n_values;
-  int64_t blocks = (total + kThreads - 1) / kThreads;
+  if (n_values < 1 || n_values > (1 << 24)) return -2;  // 64 rows x n_values fits the tile's 32-bit walk
+  int64_t blocks = (row_walk_waves(n_rows, n_values) + kThreads / 64 - 1) / (kThreads / 64);
   if (blocks > 8192) blocks = 8192;
   const dim3 grid(static_cast<uint32_t>(blocks));
 #define DDL_PACK(TIN, OUT)                                                                                        \

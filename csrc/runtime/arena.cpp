@@ -386,7 +386,7 @@ uint64_t gather_ragged(uint8_t* dst, int64_t* dst_offsets, const uint8_t* src, c
                        int n_threads) {
   // Token windows of the north-star LM config: one producer round = one local
   // batch of ragged sequences. Offsets first (serial prefix sum, n is a batch),
-  // then the copies on the pool, ~1 MiB per task.
+  // then the copies on the pool, ~256 KiB per task.
   dst_offsets[0] = 0;
   for (uint64_t i = 0; i < n; ++i) {
     if (idx[i] < 0 || static_cast<uint64_t>(idx[i]) >= n_src)
@@ -400,9 +400,10 @@ uint64_t gather_ragged(uint8_t* dst, int64_t* dst_offsets, const uint8_t* src, c
     throw std::length_error("gather_ragged: " + std::to_string(total) + " elements exceed the window capacity " +
                             std::to_string(dst_capacity));
   if (total == 0) return 0;
-  // tasks = contiguous runs of sequences holding ~1 MiB each
+  // tasks = contiguous runs of sequences holding ~256 KiB each (a 64-sequence LM batch is ~0.5 MiB:
+  // two or more tasks, so the pool's threads share it)
   std::vector<uint64_t> cuts{0};
-  const uint64_t target = std::max<uint64_t>(1, (1ull << 20) / std::max<uint64_t>(elem_bytes, 1));
+  const uint64_t target = std::max<uint64_t>(1, (256ull << 10) / std::max<uint64_t>(elem_bytes, 1));
   uint64_t acc = 0;
   for (uint64_t i = 0; i < n; ++i) {
     acc += static_cast<uint64_t>(dst_offsets[i + 1] - dst_offsets[i]);

@@ -246,6 +246,7 @@ class TokenBatchProducer(ProducerFunctionSkeleton):
         self.host_threads = host_threads
         self.order = None
         self.layout = None
+        self._views: dict = {}
 
     def on_init(self, *args, **kwargs):
         super().on_init(*args, **kwargs)
@@ -266,41 +267,58 @@ class TokenBatchProducer(ProducerFunctionSkeleton):
             "token_layout": dataclasses.asdict(self.layout), "token_mode": self.mode,
             "meta_bytes": self.layout.meta_bytes})
 
+    def _window_views(self, buf: torch.Tensor):
+        """Per staging buffer (cached): raw addresses of every sub-batch's header arrays and of the tokens
+        region, and numpy views of the meta table and of the seg_offsets arrays (the producer loop below
+        makes no tensor op per batch)."""
+        key = (buf.data_ptr(), buf.numel())
+        hit = self._views.get(key)
+        if hit is None:
+            lay = self.layout
+            subs = []
+            for j in range(lay.k):
+                v = lay.views(buf, j)
+                subs.append((v["offsets"].data_ptr(), v["row_start"].data_ptr(), v["row_end"].data_ptr(),
+                             v["seg_offsets"].data_ptr(), v["seg_offsets"].numpy()))
+            v0 = lay.views(buf, 0)
+            hit = (subs, v0["meta"].numpy(), v0["tokens"].data_ptr(), v0["tokens"].numel(), buf)
+            if len(self._views) >= 8:  # a producer cycles through its n_slots buffers
+                self._views.clear()
+            self._views[key] = hit
+        return hit
+
     def execute_function(self, *args, **kwargs):
         rnd = int(kwargs.get("round", 0))
         lay, k = self.layout, self.layout.k
-        buf: torch.Tensor = kwargs["my_tensor"].view(-1)
-        meta = _cached_views(buf, lay)["meta"]
+        subs, meta, tok_ptr, tok_cap, _ = self._window_views(kwargs["my_tensor"].view(-1))
         toks = self.source.tokens.tensor().view(-1)
         offs = self.source.offsets.tensor().view(-1)
         offs_all = offs.numpy()
-        tok_region = _cached_views(buf, lay)["tokens"]
+        toks_ptr, offs_ptr, n_src = toks.data_ptr(), offs.data_ptr(), self.source.n
         rt = _native.runtime()
+        base = (rnd * (self.n_producers or 1) + (self.producer_index or 0)) * k
+        rank, world, bpe, S = self.rank_global or 0, self.world_size, self.order.batches_per_epoch, self.seq_len
+        pack, ffd, cap = self.mode == "pack", self.pack_order == "ffd", lay.max_segments
         tok0 = 0
         for j in range(k):
-            g_total = (rnd * (self.n_producers or 1) + (self.producer_index or 0)) * k + j
-            epoch, g = divmod(g_total, self.order.batches_per_epoch)
-            idx = np.asarray(self.order.indices(epoch, g, self.rank_global or 0, self.world_size), dtype=np.int64)
-            if self.mode == "pack" and self.pack_order == "ffd":
+            epoch, g = divmod(base + j, bpe)
+            idx = np.asarray(self.order.indices(epoch, g, rank, world), dtype=np.int64)
+            if pack and ffd:
                 lens = offs_all[idx + 1] - offs_all[idx]
-                order, ffd_rows = ffd_order(lens, self.seq_len)
-                if ffd_rows < in_order_rows(lens, self.seq_len):  # FFD is a heuristic: keep it only if it wins
+                order, ffd_rows = ffd_order(lens, S)
+                if ffd_rows < in_order_rows(lens, S):  # FFD is a heuristic: keep it only if it wins
                     idx = idx[order]
-            v = _cached_views(buf, lay, j)
-            o = v["offsets"]
-            dst = tok_region[tok0:]
+            o_ptr, rs_ptr, re_ptr, so_ptr, so_np = subs[j]
             # native ragged gather (thread pool, GIL released): sequences -> window, offsets alongside
-            n_tokens = int(rt.gather_ragged(dst.data_ptr(), o.data_ptr(), toks.data_ptr(), offs.data_ptr(),
-                                            self.source.n, np.ascontiguousarray(idx, np.int64), 4, dst.numel(),
+            n_tokens = int(rt.gather_ragged(tok_ptr + 4 * tok0, o_ptr, toks_ptr, offs_ptr, n_src,
+                                            np.ascontiguousarray(idx, np.int64), 4, tok_cap - tok0,
                                             self.host_threads))
             n_rows = n_seg = max_seg = 0
-            if self.mode == "pack":  # packing plan written straight into the window (native)
-                cap = lay.max_segments
-                n_rows, n_seg = rt.pack_plan(o.data_ptr(), len(idx), self.seq_len, v["row_start"].data_ptr(),
-                                             v["row_end"].data_ptr(), cap, v["seg_offsets"].data_ptr(), cap)
+            if pack:  # packing plan written straight into the window (native)
+                n_rows, n_seg = rt.pack_plan(o_ptr, len(idx), S, rs_ptr, re_ptr, cap, so_ptr, cap)
                 if n_seg:
-                    max_seg = int(np.diff(v["seg_offsets"][: n_seg + 1].numpy()).max())
-            meta[j, 0], meta[j, 1], meta[j, 2], meta[j, 3], meta[j, 4] = n_tokens, n_rows, n_seg, max_seg, tok0
+                    max_seg = int(np.diff(so_np[: n_seg + 1]).max())
+            meta[j] = (n_tokens, n_rows, n_seg, max_seg, tok0)
             tok0 += n_tokens
         tok_off = lay.regions()["tokens"][0]
         return {"tags": [tok0, k, 0, 0], "used_bytes": tok_off + 4 * tok0}

@@ -132,6 +132,23 @@ def test_split_columns(src_dtype, out_dtype):
         assert torch.equal(a.cpu(), b)
 
 
+@pytest.mark.parametrize("widths,n_rows", [((3, 5, 1), 1000), ((1,), 77), ((100, 150, 6), 300), ((4000, 1000, 9), 70)])
+def test_split_pack_row_walks(widths, n_rows):
+    """Both row walks of the split/pack kernels (64-row wave tiles for rows <= 256 values, (row, 4096-value
+    chunk) items above), with tails: n_rows not a multiple of 64, rows spanning several chunks."""
+    nv = sum(widths)
+    src = torch.randn(2 * n_rows + 5, nv)
+    p = FeistelPermutation(src.shape[0], 1, 9)
+    ref = ops.ref_split_columns(src, widths, perm=p, base=3, n_rows=n_rows, out_dtype=torch.bfloat16)
+    out = ops.split_columns(src.to(_dev()), widths, perm=p, base=3, n_rows=n_rows, out_dtype=torch.bfloat16)
+    for a, b in zip(out, ref):
+        assert torch.equal(a.cpu(), b)
+    groups = [t.contiguous() for t in torch.split(src, list(widths), dim=1)]
+    ref = ops.ref_pack_columns(groups, perm=p, base=3, n_rows=n_rows, out_dtype=torch.float32)
+    out = ops.pack_columns([g.to(_dev()) for g in groups], perm=p, base=3, n_rows=n_rows, out_dtype=torch.float32)
+    assert torch.equal(out.cpu(), ref)
+
+
 @pytest.mark.parametrize("src_dtype,out_dtype", [(torch.float32, torch.float32), (torch.float32, torch.bfloat16),
                                                  (torch.uint8, torch.bfloat16), (torch.int64, torch.int64),
                                                  (torch.bfloat16, torch.float32)])
