@@ -216,18 +216,21 @@ int launch_hwc(void* dst, int32_t out_dt, const void* src, int64_t batch, int64_
 // source row fetched from its owner lane by a cross-lane shuffle. The shuffle
 // is executed by all 64 lanes every iteration (uniform loop), so it never
 // reads from a lane that has left the loop.
-// Rows per wave tile: ~128 elements, so a lane walks at most 2 of them -- the dependent
-// load -> store chain per wave stays short and a 4096-row batch still spreads over ~300 waves.
-__host__ __device__ __forceinline__ int64_t tile_rows(int64_t n_values) {
-  const int64_t r = 128 / (n_values > 0 ? n_values : 1);
-  return r < 1 ? 1 : (r > 64 ? 64 : r);
+// Rows per wave tile. The Feistel cycle walk diverges: a wave runs until its slowest lane's row is
+// placed (~10 rounds for 64 rows at the pointwise shape's n / 2^(2h) = 0.38), so the total ALU work
+// is lowest with 64-row tiles. A small launch (one 4096-row batch = 64 such waves) is instead
+// latency-bound on that chain: there the tile shrinks (down to 8 rows) until ~512 waves share it.
+__host__ __device__ __forceinline__ int64_t tile_rows(int64_t n_rows) {
+  int64_t r = 64;
+  while (r > 8 && n_rows / r < 512) r >>= 1;
+  return r;
 }
 
 template <typename F>
 __device__ __forceinline__ void for_row_tiles(int64_t n_rows, int64_t n_values, const RowIndex& ri, F&& f) {
   const int lane = threadIdx.x & 63;
   const int64_t waves = static_cast<int64_t>(gridDim.x) * (kThreads / 64);
-  const int64_t R = tile_rows(n_values);
+  const int64_t R = tile_rows(n_rows);
   const int64_t n_tiles = (n_rows + R - 1) / R;
   const uint32_t nv = static_cast<uint32_t>(n_values);
   for (int64_t t = static_cast<int64_t>(blockIdx.x) * (kThreads / 64) + (threadIdx.x >> 6); t < n_tiles;
@@ -275,7 +278,7 @@ __device__ __forceinline__ void for_rows(int64_t n_rows, int64_t n_values, const
 
 // waves the row walk of (n_rows, n_values) can use
 inline int64_t row_walk_waves(int64_t n_rows, int64_t n_values) {
-  return n_values <= kTileMaxValues ? (n_rows + tile_rows(n_values) - 1) / tile_rows(n_values)
+  return n_values <= kTileMaxValues ? (n_rows + tile_rows(n_rows) - 1) / tile_rows(n_rows)
                                     : n_rows * ((n_values + kRowChunk - 1) / kRowChunk);
 }
 
