@@ -25,7 +25,8 @@ double mono_s() {
 NativeStager::NativeStager(const Arena* arena, int32_t n_producers, int32_t n_slots, int64_t first, int64_t total,
                            std::vector<void*> buffers, uint64_t buffer_bytes, hipStream_t copy_stream, int device,
                            std::vector<int32_t> peer_pids, int64_t timeout_ms, std::vector<hipEvent_t> ready,
-                           std::vector<hipEvent_t> copy_done, bool post_copy, int64_t meta_bytes)
+                           std::vector<hipEvent_t> copy_done, bool post_copy, int64_t meta_bytes,
+                           hipStream_t copy_stream2)
     : arena_(arena),
       P_(n_producers),
       n_slots_(n_slots),
@@ -34,6 +35,7 @@ NativeStager::NativeStager(const Arena* arena, int32_t n_producers, int32_t n_sl
       buffers_(std::move(buffers)),
       buffer_bytes_(buffer_bytes),
       copy_stream_(copy_stream),
+      copy_stream2_(copy_stream2),
       device_(device),
       peer_pids_(std::move(peer_pids)),
       timeout_ms_(timeout_ms),
@@ -106,6 +108,7 @@ void NativeStager::run() {
   };
   for (int64_t w = first_; w < first_ + total_; ++w) {
     const int b = static_cast<int>((w - first_) % depth_);
+    hipStream_t cs = copy_stream2_ != nullptr && ((w - first_) & 1) ? copy_stream2_ : copy_stream_;
     hipEvent_t free_ev = nullptr;
     const int64_t s0 = ns();
     {
@@ -116,7 +119,7 @@ void NativeStager::run() {
     }
     const int64_t s1 = ns();
     // the consumer's kernels reading this ring buffer (window w - depth) finish first
-    if (free_ev != nullptr && hipStreamWaitEvent(copy_stream_, free_ev, 0) != hipSuccess)
+    if (free_ev != nullptr && hipStreamWaitEvent(cs, free_ev, 0) != hipSuccess)
       return fail(-1, -1, "hipStreamWaitEvent(free) failed");
     const int64_t s2 = ns();
     const uint32_t p = static_cast<uint32_t>(w % P_);
@@ -169,7 +172,7 @@ void NativeStager::run() {
       return fail(-1, static_cast<int32_t>(p),
                   "window of " + std::to_string(info.used_bytes) + " B exceeds the staging buffer");
     if (info.used_bytes > 0 &&
-        hipMemcpyAsync(buffers_[b], arena_->slot_data(p, s), info.used_bytes, hipMemcpyHostToDevice, copy_stream_) !=
+        hipMemcpyAsync(buffers_[b], arena_->slot_data(p, s), info.used_bytes, hipMemcpyHostToDevice, cs) !=
             hipSuccess)
       return fail(-1, static_cast<int32_t>(p), "hipMemcpyAsync H2D failed");
     const int64_t s4 = ns();
@@ -180,14 +183,14 @@ void NativeStager::run() {
       retire_cv_.wait(lk, [&] { return stop_ || error_code_ != 0 || w - kRetireEvents < retired_upto_; });
       if (stop_ || error_code_ != 0) return;
     }
-    if (hipEventRecord(retire_ev_[rev], copy_stream_) != hipSuccess)
+    if (hipEventRecord(retire_ev_[rev], cs) != hipSuccess)
       return fail(-1, static_cast<int32_t>(p), "hipEventRecord(retire) failed");
     {
       std::lock_guard<std::mutex> lk(mu_);
       retire_q_.push_back(Retire{w, p, s, info.used_bytes, rev});
     }
     retire_cv_.notify_all();
-    if (hipEventRecord(post_copy_ ? copy_done_[b] : ready_[b], copy_stream_) != hipSuccess)
+    if (hipEventRecord(post_copy_ ? copy_done_[b] : ready_[b], cs) != hipSuccess)
       return fail(-1, static_cast<int32_t>(p), "hipEventRecord failed");
     info.t_ready_host = mono_s();
     bytes_h2d_ += info.used_bytes;

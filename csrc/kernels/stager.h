@@ -65,7 +65,8 @@ class NativeStager {
   NativeStager(const Arena* arena, int32_t n_producers, int32_t n_slots, int64_t first, int64_t total,
                std::vector<void*> buffers, uint64_t buffer_bytes, hipStream_t copy_stream, int device,
                std::vector<int32_t> peer_pids, int64_t timeout_ms, std::vector<hipEvent_t> ready,
-               std::vector<hipEvent_t> copy_done, bool post_copy, int64_t meta_bytes = 0);
+               std::vector<hipEvent_t> copy_done, bool post_copy, int64_t meta_bytes = 0,
+               hipStream_t copy_stream2 = nullptr);
   ~NativeStager();
 
   NativeStager(const NativeStager&) = delete;
@@ -123,6 +124,9 @@ class NativeStager {
   const std::vector<void*> buffers_;
   const uint64_t buffer_bytes_;
   hipStream_t copy_stream_;
+  // optional second copy stream: windows alternate between the two, so the next window's copy is
+  // already running on another SDMA engine when one finishes (no per-copy gap on the link)
+  hipStream_t copy_stream2_;
   const int device_;
   const std::vector<int32_t> peer_pids_;
   const int64_t timeout_ms_;

@@ -32,6 +32,7 @@ two ring buffers for the exchange lookahead when the exchange is on.
 from __future__ import annotations
 
 import dataclasses
+import os
 import time
 from typing import Callable
 
@@ -121,6 +122,11 @@ class WindowStager:
         # exchange) on a second stream, so window w's exchange overlaps window
         # w+1's DMA instead of idling the copy engine.
         self.copy_stream = torch.cuda.Stream(device=self.device)
+        # windows alternate between two copy streams (two SDMA engines): the next copy is already
+        # running when one finishes, so the ~25 us gap per copy on one engine is gone (+1.8%,
+        # profiles/r2_copy_streams); DDL_COPY_STREAMS=1 restores one stream
+        n_cs = int(os.environ.get("DDL_COPY_STREAMS", "2"))
+        self.copy_stream2 = torch.cuda.Stream(device=self.device) if n_cs >= 2 else None
         self.stream = torch.cuda.Stream(device=self.device) if post_copy is not None else self.copy_stream
         # The consumer posts window w+1's exchange when it hands window w back (the fixed,
         # rank-identical issue point of the collective, parallel/order.py), and the first batch of
@@ -145,7 +151,8 @@ class WindowStager:
             buffer_bytes=max_window_bytes, copy_stream=self.copy_stream.cuda_stream, device=self.device.index,
             peer_pids=list(connection.producer_pids), timeout_ms=int(timeout_s * 1000),
             ready=[e.cuda_event for e in self.ready_events], copy_done=[e.cuda_event for e in self._copy_done],
-            post_copy=post_copy is not None, meta_bytes=int(meta_bytes))
+            post_copy=post_copy is not None, meta_bytes=int(meta_bytes),
+            copy_stream2=self.copy_stream2.cuda_stream if self.copy_stream2 is not None else 0)
         self.meta_bytes = int(meta_bytes)
 
     # -------------------------------------------------------------- consumer
@@ -245,6 +252,8 @@ class WindowStager:
         self._closed = True
         self._native.close()
         self.copy_stream.synchronize()
+        if self.copy_stream2 is not None:
+            self.copy_stream2.synchronize()
         self.stream.synchronize()
         # drop the ring (a live seek builds a new stager; batches handed out keep their own refs)
         self._staged.clear()
