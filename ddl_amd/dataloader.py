@@ -217,6 +217,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
             raise ValueError("native_dispatch must be a bool or 'auto' / 'inline' / 'lookahead' / 'window'")
         self.native_dispatch = "auto" if native_dispatch is True else native_dispatch
         self._engine = None                   # native per-batch dispatch (csrc/kernels/engine.cpp)
+        self._fields = None                   # MapDatasetSource rows: (fields, kind) to unpack batches into
 
         if connection is None or connection.n_producers == 0:
             # Reference behaviour for a single-rank run: nothing to iterate (ddl/mpi_dataloader.py:173-174).
@@ -269,6 +270,13 @@ class DistributedDataLoader(DistributedDataloaderABC):
             self.windows_per_epoch = 1
         self.sample_shape = self.shapes[0][1:]
         self.window_dtype = self.dtypes[0]
+        # MapDatasetSource rows: batches come back in the dataset's sample structure (typed views)
+        ex0 = md[0].extra if md else {}
+        self._fields = (ex0.get("fields"), ex0.get("fields_kind")) if ex0.get("fields") else None
+        if self._fields is not None and (self.window_dtype != torch.uint8 or len(self.sample_shape) != 1
+                                         or self.normalize is not None or self.augment is not None
+                                         or self.out_dtype not in (None, torch.uint8)):
+            raise ValueError("dataset-field rows are raw bytes: no normalize / augment / out_dtype")
 
         views = connection.init_windows(self.shapes, self.dtypes, self.n_slots,
                                         pin=self.device.type == "cuda")
@@ -587,7 +595,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
                 if self.debug_checksum:
                     first = out["input_ids"] if isinstance(out, dict) else out[0]
                     self.checksums.append(int(ops.checksum(first).item()))
-                return out
+                return out if self._fields is None else self._unpack(out)
         if idx < 0:
             raise ValueError(f"negative batch index {idx}")
         if idx >= self._len:
@@ -605,7 +613,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
             if self.debug_checksum:
                 first = out["input_ids"] if isinstance(out, dict) else out[0]
                 self.checksums.append(int(ops.checksum(first).item()))
-            return out
+            return out if self._fields is None else self._unpack(out)
         sw = self._window()
         if self._batch_stream is not None:
             out = self._device_batch(sw, p, s, local, bpw)
@@ -614,7 +622,13 @@ class DistributedDataLoader(DistributedDataloaderABC):
         self.metrics.on_batch(self.batch_size)
         if self.debug_checksum:
             self.checksums.append(int(ops.checksum(out[0] if isinstance(out, tuple) else out).item()))
-        return out
+        return out if self._fields is None else self._unpack(out)
+
+    def _unpack(self, out):
+        from .models.datasets import unpack_fields
+
+        rows = out[0] if isinstance(out, (tuple, list)) else out
+        return unpack_fields(rows, *self._fields)
 
     # ---------------------------------------------------------- batch stream
     def _produces_copy(self) -> bool:

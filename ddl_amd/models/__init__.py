@@ -3,22 +3,26 @@
 from .datasets import (
     DummyDataset,
     FileRowsSource,
+    MapDatasetSource,
     NpyMemmapSource,
     PointWiseData,
     SharedArraySource,
     SyntheticTokens,
     synthetic_images,
+    unpack_fields,
 )
 from .producers import ImageWindowProducer, IndexedProducer, PointwiseProducer
 
 __all__ = [
     "DummyDataset",
     "FileRowsSource",
+    "MapDatasetSource",
     "NpyMemmapSource",
     "PointWiseData",
     "SharedArraySource",
     "SyntheticTokens",
     "synthetic_images",
+    "unpack_fields",
     "ImageWindowProducer",
     "IndexedProducer",
     "PointwiseProducer",

@@ -301,3 +301,140 @@ class SyntheticTokens:
         seqs = [self.sequence(int(i)) for i in indices]
         offs = np.concatenate([[0], np.cumsum([len(s) for s in seqs])]).astype(np.int64)
         return (np.concatenate(seqs) if seqs else np.zeros(0, np.int32)), offs
+
+
+class MapDatasetSource:
+    """Any map-style dataset (``len(ds)``, ``ds[i]`` -- a ``torch.utils.data.Dataset``) as a row source
+    for ``IndexedProducer``: the drop-in path for existing Dataset code.
+
+    A sample is a tensor / ndarray / number, or a flat tuple, list or dict of them, with the same
+    shapes and dtypes for every index (probed on ``ds[0]``). Each sample is packed into one byte row:
+    field k at a 16-byte aligned offset. The loader turns a batch of rows back into the sample's
+    structure with zero-copy typed views (``DistributedDataLoader`` does it by itself when the
+    producers announce ``fields``): a tuple / dict / tensor of ``[B, *shape]`` tensors, like torch's
+    ``default_collate``.
+
+    Producers call ``ds[i]`` for their share of each global batch (``EpochOrder``: the world-size-
+    invariant order, checkpointable by global batch), on ``n_threads`` threads per producer; the
+    dataset object is pickled to every producer process, as with torch DataLoader workers.
+    """
+
+    ALIGN = 16
+
+    def __init__(self, dataset, name: str | None = None):
+        self.dataset = dataset
+        self.n = len(dataset)
+        if self.n < 1:
+            raise ValueError("MapDatasetSource: empty dataset")
+        self.name = name or type(dataset).__name__
+        self.kind, fields = self._describe(dataset[0])
+        off, self.fields = 0, []
+        for key, shape, dt, nbytes in fields:
+            self.fields.append((key, tuple(shape), dt, off, nbytes))
+            off += -(-nbytes // self.ALIGN) * self.ALIGN
+        self.row_bytes = max(self.ALIGN, off)
+        self.sample_shape = (self.row_bytes,)
+        self.dtype = torch.uint8
+        self._pool = None
+
+    # sample structure ---------------------------------------------------------------------------
+    @staticmethod
+    def _leaf(v):
+        """(shape, dtype name, bytes as a flat uint8 ndarray) of one field value."""
+        if isinstance(v, torch.Tensor):
+            t = v.detach().cpu().contiguous()
+            return tuple(t.shape), str(t.dtype).replace("torch.", ""), t.view(-1).view(torch.uint8).numpy()
+        if isinstance(v, (bool, np.bool_)):
+            a = np.asarray(v, dtype=np.bool_)
+        elif isinstance(v, int):
+            a = np.asarray(v, dtype=np.int64)
+        elif isinstance(v, float):
+            a = np.asarray(v, dtype=np.float64)
+        elif isinstance(v, (np.ndarray, np.generic)):
+            a = np.asarray(v)  # (np.ascontiguousarray would turn a 0-d scalar into shape (1,))
+            if not a.flags.c_contiguous:
+                a = a.copy()
+        else:
+            raise TypeError(f"MapDatasetSource: unsupported field type {type(v).__name__} (tensor, ndarray or number)")
+        if a.dtype == object:
+            raise TypeError("MapDatasetSource: object arrays are not fixed-size")
+        return tuple(a.shape), str(a.dtype), a.reshape(-1).view(np.uint8)
+
+    def _items(self, sample):
+        if isinstance(sample, dict):
+            return "dict", list(sample.items())
+        if isinstance(sample, (tuple, list)):
+            return "tuple", list(enumerate(sample))
+        return "tensor", [(0, sample)]
+
+    def _describe(self, sample):
+        kind, items = self._items(sample)
+        fields = []
+        for key, v in items:
+            if isinstance(v, (dict, tuple, list)):
+                raise TypeError("MapDatasetSource: nested samples are not supported; flatten them")
+            shape, dt, raw = self._leaf(v)
+            _field_dtype(dt)  # a dtype the loader can view
+            fields.append((key, shape, dt, int(raw.nbytes)))
+        return kind, fields
+
+    # producer side --------------------------------------------------------------------------------
+    def __getstate__(self):
+        st = dict(self.__dict__)
+        st["_pool"] = None
+        return st
+
+    def _write(self, rows: np.ndarray, j: int, i: int) -> None:
+        kind, items = self._items(self.dataset[i])
+        if len(items) != len(self.fields):
+            raise ValueError(f"MapDatasetSource: sample {i} has {len(items)} fields, sample 0 has {len(self.fields)}")
+        for (key, v), (key0, shape, dt, off, nbytes) in zip(items, self.fields):
+            s, d, raw = self._leaf(v)
+            if key != key0 or s != shape or d != dt:
+                raise ValueError(f"MapDatasetSource: sample {i} field {key!r} is {d}{list(s)}, "
+                                 f"sample 0 has {dt}{list(shape)}")
+            rows[j, off:off + nbytes] = raw
+
+    def gather(self, indices: np.ndarray, dst_address: int, n_threads: int = 4) -> None:
+        import ctypes
+
+        idx = np.asarray(indices, dtype=np.int64)
+        if len(idx) == 0:
+            return
+        rows = np.ctypeslib.as_array((ctypes.c_uint8 * (len(idx) * self.row_bytes)).from_address(dst_address))
+        rows = rows.reshape(len(idx), self.row_bytes)
+        if n_threads <= 1 or len(idx) < 2 * n_threads:
+            for j, i in enumerate(idx):
+                self._write(rows, j, int(i))
+            return
+        if self._pool is None:
+            from concurrent.futures import ThreadPoolExecutor
+
+            self._pool = ThreadPoolExecutor(max_workers=n_threads, thread_name_prefix="ddl-dataset")
+        chunks = np.array_split(np.arange(len(idx)), n_threads)
+        list(self._pool.map(lambda js: [self._write(rows, int(j), int(idx[j])) for j in js], chunks))
+
+
+def _field_dtype(name: str) -> torch.dtype:
+    dt = getattr(torch, name, None)
+    if not isinstance(dt, torch.dtype):
+        raise TypeError(f"MapDatasetSource: dtype {name!r} has no torch equivalent")
+    return dt
+
+
+def unpack_fields(rows: torch.Tensor, fields, kind: str):
+    """Typed zero-copy views of a batch of packed rows [B, row_bytes] (``MapDatasetSource`` layout):
+    a tensor, a tuple or a dict of ``[B, *shape]`` tensors, following the dataset's sample structure."""
+    B = rows.shape[0]
+    out = []
+    for key, shape, dt, off, nbytes in fields:
+        tdt = _field_dtype(dt)
+        v = rows[:, off:off + nbytes]
+        if tdt != torch.uint8:
+            v = v.view(tdt)
+        out.append((key, v.view((B,) + tuple(shape))))
+    if kind == "tensor":
+        return out[0][1]
+    if kind == "dict":
+        return {k: v for k, v in out}
+    return tuple(v for _, v in out)

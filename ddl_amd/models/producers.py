@@ -142,7 +142,10 @@ class IndexedProducer(ProducerFunctionSkeleton):
         return DataProducerOnInitReturn(lb, nv, (lb, *self.source.sample_shape), (nv,), self.source.dtype,
                                         extra={"batches_per_epoch": self.order.batches_per_epoch,
                                                "global_batch": self.global_batch, "n_samples": self.source.n,
-                                               "order_seed": int(self.seed)})
+                                               "order_seed": int(self.seed),
+                                               # MapDatasetSource: the loader rebuilds the sample structure
+                                               "fields": getattr(self.source, "fields", None),
+                                               "fields_kind": getattr(self.source, "kind", None)})
 
     def post_init(self, *args, **kwargs):
         super().post_init(*args, **kwargs)

@@ -1,0 +1,125 @@
+"""Map-style Dataset drop-in: ``IndexedProducer(MapDatasetSource(ds))`` delivers batches in the
+dataset's own sample structure, in the world-size-invariant global order."""
+
+import numpy as np
+import pytest
+import torch
+
+import ddl_amd
+from ddl_amd.models import IndexedProducer, MapDatasetSource, unpack_fields
+from ddl_amd.permutation import EpochOrder
+from tests.mp_harness import run_ranks
+
+
+class TupleDataset(torch.utils.data.Dataset):
+    """image uint8 [3, 5, 7], label int, weight float32, bf16 feature [4], flag bool."""
+
+    def __init__(self, n):
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        g = torch.Generator().manual_seed(i)
+        img = torch.randint(0, 256, (3, 5, 7), generator=g, dtype=torch.uint8)
+        return (img, i * 7, np.float32(i) / 3, torch.full((4,), float(i), dtype=torch.bfloat16), bool(i % 2))
+
+
+class DictDataset(TupleDataset):
+    def __getitem__(self, i):
+        img, label, w, feat, flag = super().__getitem__(i)
+        return {"image": img, "label": label, "weight": w}
+
+
+def _expected(ds, idx):
+    return torch.utils.data.default_collate([ds[int(i)] for i in idx])
+
+
+def _check(batch, ref):
+    if isinstance(ref, dict):
+        assert set(batch) == set(ref)
+        pairs = [(batch[k], ref[k]) for k in ref]
+    else:
+        pairs = list(zip(batch, ref))
+    for got, want in pairs:
+        want = torch.as_tensor(want)
+        assert got.shape == want.shape and got.dtype == want.dtype, (got.shape, want.shape, got.dtype, want.dtype)
+        assert torch.equal(got.cpu(), want)
+
+
+def test_layout_and_unpack_roundtrip():
+    ds = TupleDataset(10)
+    src = MapDatasetSource(ds)
+    assert src.kind == "tuple" and len(src.fields) == 5
+    assert all(off % 16 == 0 for _, _, _, off, _ in src.fields) and src.row_bytes % 16 == 0
+    rows = np.zeros((4, src.row_bytes), dtype=np.uint8)
+    src.gather(np.array([3, 1, 4, 1]), rows.ctypes.data, n_threads=1)
+    _check(unpack_fields(torch.from_numpy(rows), src.fields, src.kind), _expected(ds, [3, 1, 4, 1]))
+
+
+def test_inconsistent_sample_is_rejected():
+    class Bad(TupleDataset):
+        def __getitem__(self, i):
+            out = super().__getitem__(i)
+            return out if i == 0 else out[:4]
+
+    src = MapDatasetSource(Bad(4))
+    rows = np.zeros((2, src.row_bytes), dtype=np.uint8)
+    with pytest.raises(ValueError, match="fields"):
+        src.gather(np.array([0, 1]), rows.ctypes.data, n_threads=1)
+
+
+@pytest.mark.parametrize("ds_cls", [TupleDataset, DictDataset])
+def test_map_dataset_loader_cpu(ds_cls, monkeypatch):
+    monkeypatch.setenv("DDL_DEVICE", "cpu")
+    ds, gb = ds_cls(50), 8
+    order = EpochOrder(len(ds), gb, 3)
+    with ddl_amd.start(n_producers=2) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(IndexedProducer(MapDatasetSource(ds), gb, host_threads=2), gb, conn, 2,
+                                           mode="indexed", env=env, auto_mark=True, seed=3)
+        for e in range(2):
+            n = 0
+            for g, b in enumerate(dl):
+                _check(b, _expected(ds, order.indices(e, g)))
+                n += 1
+            assert n == order.batches_per_epoch
+
+
+def _rank(rank, world, n, gb):
+    import ddl_amd
+
+    out = []
+    ds = TupleDataset(n)
+    with ddl_amd.start(n_producers=2) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(IndexedProducer(MapDatasetSource(ds), gb), gb // world, conn, 1,
+                                           mode="indexed", env=env, auto_mark=True, seed=3)
+        for b in dl:
+            out.append(b[1].tolist())  # labels = 7 * sample id
+    return out
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_map_dataset_world_size_invariant(world):
+    n, gb = 40, 8
+    res = run_ranks(_rank, world, n, gb, env={"DDL_DEVICE": "cpu"})
+    order = EpochOrder(n, gb, 3)
+    for g in range(order.batches_per_epoch):
+        merged = sum((r[g] for r in res), [])
+        assert merged == [7 * int(i) for i in order.indices(0, g)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("native", [True, False])
+def test_map_dataset_loader_gpu(native):
+    ds, gb = TupleDataset(64), 16
+    order = EpochOrder(len(ds), gb, 3)
+    with ddl_amd.start(n_producers=2) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(IndexedProducer(MapDatasetSource(ds), gb), gb, conn, 2, mode="indexed",
+                                           env=env, auto_mark=True, seed=3, native_dispatch=native)
+        for e in range(2):
+            for g, b in enumerate(dl):
+                assert all(t.is_cuda for t in b)
+                _check(b, _expected(ds, order.indices(e, g)))
+        st = dl.stats()
+    assert (st.get("native_dispatch") is not None) == native
