@@ -30,7 +30,7 @@ def main(argv=None):
                                                           "previous is in flight)")
     ap.add_argument("--batches-per-window", type=int, default=8,
                     help="global batches per producer window (per-window costs amortised over k batches)")
-    ap.add_argument("--dispatch", default="auto", choices=["auto", "inline", "lookahead", "python"])
+    ap.add_argument("--dispatch", default="auto", choices=["auto", "inline", "lookahead", "window", "python"])
     ap.add_argument("--mode", default="pack", choices=["pad", "pack"])
     ap.add_argument("--pack-order", default="ffd", choices=["in_order", "ffd"],
                     help="pack mode: first-fit-decreasing rows (measured 93%% dense) or in-order (~75%%)")
@@ -150,7 +150,7 @@ def main(argv=None):
                     "row_density_est": round(a.batch * mean_len / (rows / a.steps) / a.seq_len, 3),
                     "n_gpus": env.world_size,
                     "steps": a.steps, "ms_per_step": round(1000 * dt / a.steps, 3), "batch_seqs": a.batch,
-                    "producers": a.producers, "slots": a.slots, "batches_per_window": dl.batches_per_window[0], "dispatch": a.dispatch, "mean_len": round(mean_len, 1),
+                    "producers": a.producers, "slots": a.slots, "batches_per_window": dl.batches_per_window[0], "dispatch": a.dispatch, "dispatch_mode": (st.get("native_dispatch") or {}).get("mode"), "mean_len": round(mean_len, 1),
                     "consumer_wait_s": round(st["consumer_wait_s"], 3),
                     "gpu_idle_pct": None if idle is None else round(idle["gpu_idle_pct"], 3),
                     "train_step": None if idle is None else {

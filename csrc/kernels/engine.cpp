@@ -173,6 +173,35 @@ int BatchEngine::enqueue_window(int64_t w, int64_t bpw, const StagedInfo& info, 
   return 0;
 }
 
+TokenSpec BatchEngine::token_spec(const StagedInfo& info, int64_t sub, const std::vector<void*>& dst,
+                                  const void* src) const {
+  // sub-batch `sub`: its header block, its token run (meta: n_tokens, n_rows, n_seg, max_seg, token start)
+  const int64_t* m = token_meta(info, sub);
+  const uint8_t* win = static_cast<const uint8_t*>(src) + sub * r_.header_stride;
+  TokenSpec sp{};
+  sp.tokens = reinterpret_cast<const int32_t*>(static_cast<const uint8_t*>(src) + r_.off_tokens) + m[4];
+  sp.out_tokens = static_cast<int32_t*>(dst[0]);
+  sp.attn_mask = static_cast<uint8_t*>(dst[1]);
+  sp.position_ids = dst[2];
+  sp.pos_is_i64 = 1;
+  sp.seq_len = r_.seq_len;
+  sp.pad_id = r_.pad_id;
+  sp.mode = r_.token_mode;
+  if (r_.token_mode == 0) {
+    sp.offsets = reinterpret_cast<const int64_t*>(win + r_.off_offsets);
+    sp.rows = r_.batch;
+  } else {
+    sp.row_start = reinterpret_cast<const int64_t*>(win + r_.off_row_start);
+    sp.row_end = reinterpret_cast<const int64_t*>(win + r_.off_row_end);
+    sp.seg_offsets = reinterpret_cast<const int64_t*>(win + r_.off_seg_offsets);
+    sp.n_seg = m[2];
+    sp.segment_ids = static_cast<int32_t*>(dst[3]);
+    sp.cu_seqlens_out = static_cast<int32_t*>(dst[4]);
+    sp.rows = m[1];
+  }
+  return sp;
+}
+
 int BatchEngine::launch(int64_t w, int64_t local, int64_t n_batches, const StagedInfo& info, int64_t slot,
                         hipStream_t st) {
   const auto& dst = slots_[slot];
@@ -197,34 +226,17 @@ int BatchEngine::launch(int64_t w, int64_t local, int64_t n_batches, const Stage
   }
   int rc;
   if (r_.kind == 2) {  // token window: outputs ids, mask, pos (+ seg, cu)
-    // sub-batch `local` of a k-batch window: its header block, its token run (meta: n_tokens, n_rows,
-    // n_seg, max_seg, token start -- copied to the host by the stager at staging time)
-    if (info.meta.size() < static_cast<size_t>(5 * (local + 1))) return -1;  // window head not copied
-    const int64_t* m = token_meta(info, local);
-    const uint8_t* win = static_cast<const uint8_t*>(src) + local * r_.header_stride;
-    TokenSpec sp{};
-    sp.tokens = reinterpret_cast<const int32_t*>(static_cast<const uint8_t*>(src) + r_.off_tokens) + m[4];
-    sp.out_tokens = static_cast<int32_t*>(dst[0]);
-    sp.attn_mask = static_cast<uint8_t*>(dst[1]);
-    sp.position_ids = dst[2];
-    sp.pos_is_i64 = 1;
-    sp.seq_len = r_.seq_len;
-    sp.pad_id = r_.pad_id;
-    sp.mode = r_.token_mode;
-    if (r_.token_mode == 0) {
-      sp.offsets = reinterpret_cast<const int64_t*>(win + r_.off_offsets);
-      sp.rows = r_.batch;
-      rc = pad_pack_tokens(sp, st);
+    // sub-batches local .. local + n_batches - 1 of a k-batch window (their meta rows were copied to the
+    // host by the stager at staging time) into slots slot .. slot + n_batches - 1
+    if (info.meta.size() < static_cast<size_t>(5 * (local + n_batches))) return -1;  // window head not copied
+    token_specs_.clear();
+    for (int64_t j = 0; j < n_batches; ++j) token_specs_.push_back(token_spec(info, local + j, slots_[slot + j], src));
+    if (n_batches > 1) {
+      rc = pad_pack_tokens_multi(token_specs_.data(), static_cast<int>(n_batches), st);
     } else {
-      sp.row_start = reinterpret_cast<const int64_t*>(win + r_.off_row_start);
-      sp.row_end = reinterpret_cast<const int64_t*>(win + r_.off_row_end);
-      sp.seg_offsets = reinterpret_cast<const int64_t*>(win + r_.off_seg_offsets);
-      sp.n_seg = m[2];
-      sp.segment_ids = static_cast<int32_t*>(dst[3]);
-      sp.cu_seqlens_out = static_cast<int32_t*>(dst[4]);
-      sp.rows = m[1];
+      const TokenSpec& sp = token_specs_[0];
       rc = sp.rows > 0 ? pad_pack_tokens(sp, st)
-                       : (hipMemsetAsync(dst[4], 0, sizeof(int32_t), st) == hipSuccess ? 0 : -1);
+                       : (hipMemsetAsync(sp.cu_seqlens_out, 0, sizeof(int32_t), st) == hipSuccess ? 0 : -1);
     }
   } else if (r_.kind == 0) {
     // n_batches > 1: consecutive slots are contiguous for this kind (the caller enables whole-window mode
@@ -265,7 +277,7 @@ int64_t BatchEngine::get(int64_t w, int64_t local, int64_t bpw, bool next_ok, hi
     }
   }
   Pending cur{};
-  if (inline_ && whole_ && bpw > 1 && r_.kind != 2) {
+  if (inline_ && whole_ && bpw > 1) {
     if (ww_w_ != w) {
       rc = enqueue_window(w, bpw, windows_.at(w), compute);
       if (rc != 0) return rc;

@@ -37,6 +37,7 @@
 #include <vector>
 
 #include "common.h"
+#include "launch.h"
 #include "stager.h"
 
 namespace ddl {
@@ -96,9 +97,9 @@ class BatchEngine {
   // the host cost is the bottleneck and the kernel's few microseconds on the compute stream are not.
   void set_inline(bool on) { inline_ = on; }
   bool is_inline() const { return inline_; }
-  // Whole-window mode (inline only; gather/split kinds): the first get() of a window launches ONE kernel
-  // that builds all of its bpw batches into bpw consecutive output slots (slot_stride bytes apart, one
-  // provide() block); the other gets of the window make no HIP call. The window's free event follows that
+  // Whole-window mode (inline only): the first get() of a window launches ONE kernel that builds all of
+  // its bpw batches into bpw consecutive output slots (slot_stride bytes apart, one provide() block;
+  // token windows: one pad/pack launch per 16 sub-batches); the other gets of the window make no HIP call. The window's free event follows that
   // kernel, so its ring buffer goes back to the stager before the window's batches are consumed.
   void set_window_mode(bool on, int64_t slot_stride) {
     whole_ = on;
@@ -125,6 +126,8 @@ class BatchEngine {
   // the batch kernel(s): n_batches batches from `local` on into slot `slot` (and the following slots)
   int launch(int64_t w, int64_t local, int64_t n_batches, const StagedInfo& info, int64_t slot, hipStream_t st);
   int enqueue_window(int64_t w, int64_t bpw, const StagedInfo& info, hipStream_t st);
+  TokenSpec token_spec(const StagedInfo& info, int64_t sub, const std::vector<void*>& dst, const void* src) const;
+  std::vector<TokenSpec> token_specs_;  // scratch (kind 2)
   const StagedInfo* acquired(int64_t w);
   // token windows: the 5 meta fields of sub-batch `local` (the stager's host copy of the window head)
   static const int64_t* token_meta(const StagedInfo& info, int64_t local) {

@@ -94,6 +94,10 @@ struct TokenSpec {
   int32_t pad;
 };
 int pad_pack_tokens(const TokenSpec& spec, hipStream_t st);
+// Several independent token batches (the sub-batches of one multi-batch window) in one launch per
+// kMaxTokenSubs of them: grid.y = sub-batch.
+constexpr int kMaxTokenSubs = 16;
+int pad_pack_tokens_multi(const TokenSpec* specs, int n, hipStream_t st);
 
 // bucket.hip ----------------------------------------------------------------
 // Owner bucketing of a global batch for the resident loader's exchange: positions

@@ -101,33 +101,51 @@ __device__ __forceinline__ void emit4(const TokenSpec& sp, int64_t row, int64_t 
   }
 }
 
-__global__ void __launch_bounds__(kThreads) pad_pack_kernel(TokenSpec sp, int32_t chunks) {
-  __shared__ int64_t seg_lds[kSegCap];
-  const uint32_t row = blockIdx.x / static_cast<uint32_t>(chunks);
-  const int64_t p0 = static_cast<int64_t>(blockIdx.x - row * static_cast<uint32_t>(chunks)) * kSpan +
+// One workgroup = (row, chunk) `bx` of batch `sp`. Blocks past the batch's rows (a multi-batch launch is
+// sized for its largest sub-batch) only do block 0's cu_seqlens copy; the exit is block-uniform.
+__device__ __forceinline__ void pad_pack_block(const TokenSpec& sp, uint32_t bx, int32_t chunks, int64_t* seg_lds) {
+  const uint32_t row = bx / static_cast<uint32_t>(chunks);
+  const bool live = row < sp.rows;
+  const int64_t p0 = static_cast<int64_t>(bx - row * static_cast<uint32_t>(chunks)) * kSpan +
                      static_cast<int64_t>(threadIdx.x) * 4;
-  int64_t start, len;
-  if (sp.mode == 0) {
-    start = sp.offsets[row];
-    len = sp.offsets[row + 1] - start;
-  } else {
-    start = sp.row_start[row];
-    len = sp.row_end[row] - start;
+  int64_t start = 0, len = 0;
+  if (live) {
+    if (sp.mode == 0) {
+      start = sp.offsets[row];
+      len = sp.offsets[row + 1] - start;
+    } else {
+      start = sp.row_start[row];
+      len = sp.row_end[row] - start;
+    }
   }
   if (len > sp.seq_len) len = sp.seq_len;
   if (len < 0) len = 0;
-  const bool staged = sp.mode == 1 && sp.n_seg + 1 <= kSegCap;  // kernel-uniform
-  if (staged)
+  const bool staged = sp.mode == 1 && sp.n_seg + 1 <= kSegCap;  // batch-uniform
+  if (staged && live)
     for (int64_t i = threadIdx.x; i <= sp.n_seg; i += kThreads) seg_lds[i] = sp.seg_offsets[i];
-  if (sp.cu_seqlens_out != nullptr && blockIdx.x == 0)  // owned copy of the sequence starts (cu_seqlens)
+  if (sp.cu_seqlens_out != nullptr && bx == 0)  // owned copy of the sequence starts (cu_seqlens)
     for (int64_t i = threadIdx.x; i <= sp.n_seg; i += kThreads)
       sp.cu_seqlens_out[i] = static_cast<int32_t>(sp.seg_offsets[i]);
   __syncthreads();
-  if (p0 >= sp.seq_len) return;
+  if (!live || p0 >= sp.seq_len) return;
   if (staged)
     emit4(sp, row, p0, start, len, [&](int64_t i) { return seg_lds[i]; });
   else
     emit4(sp, row, p0, start, len, [&](int64_t i) { return sp.seg_offsets[i]; });
+}
+
+__global__ void __launch_bounds__(kThreads) pad_pack_kernel(TokenSpec sp, int32_t chunks) {
+  __shared__ int64_t seg_lds[kSegCap];
+  pad_pack_block(sp, blockIdx.x, chunks, seg_lds);
+}
+
+struct TokenMulti {
+  TokenSpec sub[kMaxTokenSubs];
+};
+
+__global__ void __launch_bounds__(kThreads) pad_pack_multi_kernel(TokenMulti m, int32_t chunks) {
+  __shared__ int64_t seg_lds[kSegCap];
+  pad_pack_block(m.sub[blockIdx.y], blockIdx.x, chunks, seg_lds);
 }
 
 }  // namespace
@@ -141,6 +159,31 @@ int pad_pack_tokens(const TokenSpec& spec, hipStream_t st) {
   hipLaunchKernelGGL(pad_pack_kernel, dim3(static_cast<uint32_t>(spec.rows * chunks)), dim3(kThreads), 0, st, spec,
                      static_cast<int32_t>(chunks));
   return static_cast<int>(hipGetLastError());
+}
+
+int pad_pack_tokens_multi(const TokenSpec* specs, int n, hipStream_t st) {
+  for (int g = 0; g < n; g += kMaxTokenSubs) {
+    TokenMulti m{};
+    const int cnt = n - g < kMaxTokenSubs ? n - g : kMaxTokenSubs;
+    int64_t max_rows = 1, seq_len = 0;  // >= 1 block per sub-batch: block 0 writes its cu_seqlens
+    for (int j = 0; j < cnt; ++j) {
+      const TokenSpec& sp = specs[g + j];
+      if (sp.seq_len <= 0 || (sp.mode == 0 && !sp.offsets) ||
+          (sp.mode == 1 && (!sp.row_start || !sp.row_end || !sp.seg_offsets)))
+        return -2;
+      if (j > 0 && sp.seq_len != seq_len) return -2;  // one chunking for the launch
+      seq_len = sp.seq_len;
+      if (sp.rows > max_rows) max_rows = sp.rows;
+      m.sub[j] = sp;
+    }
+    const int64_t chunks = (seq_len + kSpan - 1) / kSpan;
+    if (max_rows * chunks >= (int64_t{1} << 31)) return -4;
+    hipLaunchKernelGGL(pad_pack_multi_kernel, dim3(static_cast<uint32_t>(max_rows * chunks), static_cast<uint32_t>(cnt)),
+                       dim3(kThreads), 0, st, m, static_cast<int32_t>(chunks));
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return static_cast<int>(e);
+  }
+  return 0;
 }
 
 }  // namespace ddl

@@ -396,10 +396,11 @@ class DistributedDataLoader(DistributedDataloaderABC):
         self._eng_block = int(min(128, max(4, (512 << 20) // self._eng_slot_bytes)))
         mode = self.native_dispatch
         bpw_max = max(self.batches_per_window)
-        # whole-window launches: gather/split kinds, every window holds >= 2 batches, and consecutive slots
-        # of a block are one contiguous run per output where the kernel needs that (gather: no slot padding)
-        whole_ok = (rec["kind"] in (0, 1) and min(self.batches_per_window) > 1
-                    and (rec["kind"] == 1 or self._eng_slot_bytes == math.prod(self._eng_outputs[0][0])
+        # whole-window launches: every window holds >= 2 batches, and consecutive slots of a block are one
+        # contiguous run per output where the kernel needs that (gather: no slot padding; split takes a slot
+        # stride; token windows get one pad/pack launch with a grid row per sub-batch)
+        whole_ok = (min(self.batches_per_window) > 1
+                    and (rec["kind"] != 0 or self._eng_slot_bytes == math.prod(self._eng_outputs[0][0])
                          * _dtypes.itemsize(self._eng_outputs[0][1])))
         if mode == "auto":
             # small batches are host-bound: inline (no batch events, ~3 us of C++ per batch), or one launch per
@@ -407,7 +408,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
             # worth overlapping with the previous step on the batch stream (GPU idle behind a train step 0.17%
             # lookahead vs 0.71% inline, profiles/r2_native_dispatch)
             mode = "inline" if self._eng_slot_bytes < (16 << 20) else "lookahead"
-            if mode == "inline" and whole_ok and self._eng_slot_bytes * bpw_max <= (64 << 20):
+            if mode == "inline" and whole_ok and self._eng_slot_bytes * bpw_max <= (256 << 20):
                 mode = "window"
         if mode == "window" and not whole_ok:
             mode = "inline"

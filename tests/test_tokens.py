@@ -289,9 +289,11 @@ def test_token_native_dispatch_matches_python_path(corpus, mode, bpw):
 
     ref, st_ref = run(False)
     assert "native_dispatch" not in st_ref
-    for native in ("inline", "lookahead"):
+    for native in ("inline", "lookahead", "window"):
         nat, st = run(native)
-        assert st["native_dispatch"]["batches"] == len(nat) and st["native_dispatch"]["mode"] == native
+        # window: one multi-batch pad/pack launch per window (k > 1); a 1-batch window falls back to inline
+        expect = "inline" if (native == "window" and bpw == 1) else native
+        assert st["native_dispatch"]["batches"] == len(nat) and st["native_dispatch"]["mode"] == expect
         assert len(nat) == len(ref) > 0
         for a, b in zip(nat, ref):
             assert a.keys() == b.keys()
