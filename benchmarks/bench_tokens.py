@@ -30,6 +30,8 @@ def main(argv=None):
                                                           "previous is in flight)")
     ap.add_argument("--batches-per-window", type=int, default=8,
                     help="global batches per producer window (per-window costs amortised over k batches)")
+    ap.add_argument("--token-rows", default="exact", choices=["exact", "fixed"],
+                    help="pack mode: exact packed rows per batch, or the window layout's fixed max rows (padding)")
     ap.add_argument("--dispatch", default="auto", choices=["auto", "inline", "lookahead", "window", "python"])
     ap.add_argument("--mode", default="pack", choices=["pad", "pack"])
     ap.add_argument("--pack-order", default="ffd", choices=["in_order", "ffd"],
@@ -73,7 +75,7 @@ def main(argv=None):
                                                                   pack_order=a.pack_order if a.mode == "pack" else "in_order",
                                                                   batches_per_window=a.batches_per_window), a.batch, conn,
                                                n_epochs, mode="indexed", env=env, collate="tokens", auto_mark=True,
-                                               n_slots=a.slots,
+                                               n_slots=a.slots, token_rows=a.token_rows,
                                                native_dispatch=False if a.dispatch == "python" else a.dispatch)
             dev = torch.device(env.device)
             acc = ops.ChecksumAccumulator(dev)  # one streaming launch per batch
@@ -95,7 +97,7 @@ def main(argv=None):
             for _ in range(a.steps):
                 b = next(it)
                 acc.add(b["input_ids"])
-                rows += b["input_ids"].shape[0]
+                rows += b.get("n_rows", b["input_ids"].shape[0])
                 real += b["n_tokens"]  # counted from the delivered batches (producer tag), not estimated
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
@@ -150,7 +152,7 @@ def main(argv=None):
                     "row_density_est": round(a.batch * mean_len / (rows / a.steps) / a.seq_len, 3),
                     "n_gpus": env.world_size,
                     "steps": a.steps, "ms_per_step": round(1000 * dt / a.steps, 3), "batch_seqs": a.batch,
-                    "producers": a.producers, "slots": a.slots, "batches_per_window": dl.batches_per_window[0], "dispatch": a.dispatch, "dispatch_mode": (st.get("native_dispatch") or {}).get("mode"), "mean_len": round(mean_len, 1),
+                    "producers": a.producers, "slots": a.slots, "batches_per_window": dl.batches_per_window[0], "dispatch": a.dispatch, "dispatch_mode": (st.get("native_dispatch") or {}).get("mode"), "token_rows": a.token_rows, "mean_len": round(mean_len, 1),
                     "consumer_wait_s": round(st["consumer_wait_s"], 3),
                     "gpu_idle_pct": None if idle is None else round(idle["gpu_idle_pct"], 3),
                     "train_step": None if idle is None else {

@@ -269,7 +269,7 @@ PYBIND11_MODULE(_ddl_hip, m) {
              r.widths = std::move(widths);
              r.aff = make_affine(scale, bias, plane);
              if (kind == 2) {
-               if (token.size() != 9) throw std::invalid_argument("BatchEngine: token recipe needs 9 values");
+               if (token.size() != 10) throw std::invalid_argument("BatchEngine: token recipe needs 10 values");
                r.token_mode = static_cast<int32_t>(token[0]);
                r.pad_id = static_cast<int32_t>(token[1]);
                r.seq_len = token[2];
@@ -279,6 +279,7 @@ PYBIND11_MODULE(_ddl_hip, m) {
                r.off_seg_offsets = token[6];
                r.off_tokens = token[7];
                r.header_stride = token[8];
+               r.token_fill_rows = token[9];
              }
              std::vector<void*> bufs;
              for (auto b : buffers) bufs.push_back(as_ptr<void>(b));
@@ -562,8 +563,9 @@ PYBIND11_MODULE(_ddl_hip, m) {
       [](uintptr_t tokens, uintptr_t offsets, uintptr_t row_start, uintptr_t row_end, uintptr_t seg_offsets,
          int64_t n_seg, uintptr_t out_tokens, uintptr_t attn_mask, uintptr_t position_ids, bool pos_is_i64,
          uintptr_t segment_ids, uintptr_t cu_seqlens_out, int64_t rows, int64_t seq_len, int pad_id, int mode,
-         uintptr_t stream) {
+         uintptr_t stream, int64_t fill_rows) {
         ddl::TokenSpec sp{};
+        sp.fill_rows = fill_rows;
         sp.tokens = as_ptr<const int32_t>(tokens);
         sp.offsets = as_ptr<const int64_t>(offsets);
         sp.row_start = as_ptr<const int64_t>(row_start);
@@ -585,7 +587,7 @@ PYBIND11_MODULE(_ddl_hip, m) {
       py::arg("tokens"), py::arg("offsets"), py::arg("row_start"), py::arg("row_end"), py::arg("seg_offsets"),
       py::arg("n_seg"), py::arg("out_tokens"), py::arg("attn_mask"), py::arg("position_ids"), py::arg("pos_is_i64"),
       py::arg("segment_ids"), py::arg("cu_seqlens_out"), py::arg("rows"), py::arg("seq_len"), py::arg("pad_id"),
-      py::arg("mode"), py::arg("stream"));
+      py::arg("mode"), py::arg("stream"), py::arg("fill_rows") = 0);
   m.def(
       "stream_copy",
       [](uintptr_t src, uintptr_t dst, int64_t bytes, int blocks, uintptr_t stream) {

@@ -198,6 +198,7 @@ TokenSpec BatchEngine::token_spec(const StagedInfo& info, int64_t sub, const std
     sp.segment_ids = static_cast<int32_t*>(dst[3]);
     sp.cu_seqlens_out = static_cast<int32_t*>(dst[4]);
     sp.rows = m[1];
+    sp.fill_rows = r_.token_fill_rows;
   }
   return sp;
 }
@@ -235,8 +236,9 @@ int BatchEngine::launch(int64_t w, int64_t local, int64_t n_batches, const Stage
       rc = pad_pack_tokens_multi(token_specs_.data(), static_cast<int>(n_batches), st);
     } else {
       const TokenSpec& sp = token_specs_[0];
-      rc = sp.rows > 0 ? pad_pack_tokens(sp, st)
-                       : (hipMemsetAsync(sp.cu_seqlens_out, 0, sizeof(int32_t), st) == hipSuccess ? 0 : -1);
+      rc = sp.rows > 0 || sp.fill_rows > 0
+               ? pad_pack_tokens(sp, st)
+               : (hipMemsetAsync(sp.cu_seqlens_out, 0, sizeof(int32_t), st) == hipSuccess ? 0 : -1);
     }
   } else if (r_.kind == 0) {
     // n_batches > 1: consecutive slots are contiguous for this kind (the caller enables whole-window mode

@@ -92,6 +92,9 @@ struct TokenSpec {
   int32_t pos_is_i64;
   int32_t mode;  // 0 pad, 1 pack
   int32_t pad;
+  // > rows: rows [rows, fill_rows) are written as padding (pad_id, mask 0, position 0, segment -1), so a
+  // packed batch has a fixed shape [fill_rows, seq_len] (static shapes for graphs / compiled steps)
+  int64_t fill_rows;
 };
 int pad_pack_tokens(const TokenSpec& spec, hipStream_t st);
 // Several independent token batches (the sub-batches of one multi-batch window) in one launch per

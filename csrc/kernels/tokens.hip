@@ -105,11 +105,11 @@ __device__ __forceinline__ void emit4(const TokenSpec& sp, int64_t row, int64_t 
 // sized for its largest sub-batch) only do block 0's cu_seqlens copy; the exit is block-uniform.
 __device__ __forceinline__ void pad_pack_block(const TokenSpec& sp, uint32_t bx, int32_t chunks, int64_t* seg_lds) {
   const uint32_t row = bx / static_cast<uint32_t>(chunks);
-  const bool live = row < sp.rows;
+  const bool live = row < (sp.fill_rows > sp.rows ? sp.fill_rows : sp.rows);  // data row or padding row
   const int64_t p0 = static_cast<int64_t>(bx - row * static_cast<uint32_t>(chunks)) * kSpan +
                      static_cast<int64_t>(threadIdx.x) * 4;
-  int64_t start = 0, len = 0;
-  if (live) {
+  int64_t start = 0, len = 0;  // a padding row: len 0, every position written as padding
+  if (row < sp.rows) {
     if (sp.mode == 0) {
       start = sp.offsets[row];
       len = sp.offsets[row + 1] - start;
@@ -151,12 +151,13 @@ __global__ void __launch_bounds__(kThreads) pad_pack_multi_kernel(TokenMulti m, 
 }  // namespace
 
 int pad_pack_tokens(const TokenSpec& spec, hipStream_t st) {
-  if (spec.rows <= 0 || spec.seq_len <= 0) return 0;
+  const int64_t rows = spec.fill_rows > spec.rows ? spec.fill_rows : spec.rows;
+  if (rows <= 0 || spec.seq_len <= 0) return 0;
   if (spec.mode == 0 && !spec.offsets) return -2;
   if (spec.mode == 1 && (!spec.row_start || !spec.row_end || !spec.seg_offsets)) return -2;
   const int64_t chunks = (spec.seq_len + kSpan - 1) / kSpan;
-  if (spec.rows * chunks >= (int64_t{1} << 31)) return -4;
-  hipLaunchKernelGGL(pad_pack_kernel, dim3(static_cast<uint32_t>(spec.rows * chunks)), dim3(kThreads), 0, st, spec,
+  if (rows * chunks >= (int64_t{1} << 31)) return -4;
+  hipLaunchKernelGGL(pad_pack_kernel, dim3(static_cast<uint32_t>(rows * chunks)), dim3(kThreads), 0, st, spec,
                      static_cast<int32_t>(chunks));
   return static_cast<int>(hipGetLastError());
 }
@@ -174,6 +175,7 @@ int pad_pack_tokens_multi(const TokenSpec* specs, int n, hipStream_t st) {
       if (j > 0 && sp.seq_len != seq_len) return -2;  // one chunking for the launch
       seq_len = sp.seq_len;
       if (sp.rows > max_rows) max_rows = sp.rows;
+      if (sp.fill_rows > max_rows) max_rows = sp.fill_rows;
       m.sub[j] = sp;
     }
     const int64_t chunks = (seq_len + kSpan - 1) / kSpan;

@@ -138,6 +138,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
         collate: str | None = None,
         pad_id: int = 0,
         native_dispatch: bool | str = True,
+        token_rows: str = "exact",
     ):
         if mode not in MODES:
             raise ValueError(f"unknown mode {mode!r}; one of {MODES}")
@@ -173,6 +174,12 @@ class DistributedDataLoader(DistributedDataloaderABC):
             raise ValueError("collate must be None or 'tokens'")
         self.collate = collate
         self.pad_id = pad_id
+        # collate="tokens", pack mode: "exact" -> [packed rows, S] per batch; "fixed" -> every batch has the
+        # window layout's max rows (padding rows past the packed ones): static shapes, and no per-batch
+        # slicing of four [R, S] outputs on the host (~2 us per tensor view)
+        if token_rows not in ("exact", "fixed"):
+            raise ValueError("token_rows must be 'exact' or 'fixed'")
+        self.token_rows = token_rows
         self.debug_checksum = debug_checksum
         self.metrics = LoaderMetrics()
         self.timeout_s = timeout_s if timeout_s is not None else (connection.timeout_s if connection else 600.0)
@@ -360,8 +367,9 @@ class DistributedDataLoader(DistributedDataloaderABC):
         outs = [((rows, S), torch.int32), ((rows, S), torch.uint8), ((rows, S), torch.int64)]
         if mode == "pack":
             outs += [((rows, S), torch.int32), ((lay.max_segments + 1,), torch.int32)]
+        fill = lay.max_segments if (mode == "pack" and self.token_rows == "fixed") else 0
         token = [0 if mode == "pad" else 1, int(self.pad_id), S, reg["offsets"][0], reg["row_start"][0],
-                 reg["row_end"][0], reg["seg_offsets"][0], reg["tokens"][0], lay.header_stride]
+                 reg["row_end"][0], reg["seg_offsets"][0], reg["tokens"][0], lay.header_stride, fill]
         return dict(kind=2, in_dt=_dtypes.code(torch.int32), out_dt=_dtypes.code(torch.int32), shuffle=False,
                     batch=lay.batch, row_elems=1, seed=0, max_blocks=0, scale=[], bias=[], plane=0,
                     n_data=[int(x.nData) for x in self.metadata_from_producer], widths=[], token=token,
@@ -507,6 +515,9 @@ class DistributedDataLoader(DistributedDataloaderABC):
             return {"input_ids": out[0], "attention_mask": out[1], "position_ids": out[2], "n_tokens": n_tokens}
         if n_tokens > 0x7FFFFFFF:
             raise ValueError(f"{n_tokens} tokens in one batch overflow int32 cu_seqlens")
+        if self.token_rows == "fixed":
+            return {"input_ids": out[0], "attention_mask": out[1], "position_ids": out[2], "segment_ids": out[3],
+                    "cu_seqlens": out[4][:n_seg + 1], "max_seqlen": max_seg, "n_tokens": n_tokens, "n_rows": n_rows}
         return {"input_ids": out[0][:n_rows], "attention_mask": out[1][:n_rows], "position_ids": out[2][:n_rows],
                 "segment_ids": out[3][:n_rows], "cu_seqlens": out[4][:n_seg + 1], "max_seqlen": max_seg,
                 "n_tokens": n_tokens}
@@ -697,7 +708,8 @@ class DistributedDataLoader(DistributedDataloaderABC):
             ex = self.metadata_from_producer[p].extra
             with trace_range("ddl.consumer.tokens"):
                 return collate_token_window(win.reshape(-1), TokenWindowLayout(**ex["token_layout"]),
-                                            ex["token_mode"], meta, self.pad_id, sub=local)
+                                            ex["token_mode"], meta, self.pad_id, sub=local,
+                                            fixed_rows=self.token_rows == "fixed")
         perm = self._perm_for(p, seq)
         out_dtype = self.out_dtype or (torch.float32 if self.normalize is not None else wdt)
         if self.augment is not None:

@@ -342,9 +342,11 @@ def _cached_views(buf: torch.Tensor, layout: TokenWindowLayout, sub: int = 0) ->
 
 
 def collate_token_window(buf: torch.Tensor, layout: TokenWindowLayout, mode: str, meta, pad_id: int = 0,
-                         sub: int = 0):
+                         sub: int = 0, fixed_rows: bool = False):
     """Expand sub-batch ``sub`` of one (device or host) token window into model inputs; ``meta`` is the
-    window's meta table (flat, META_FIELDS per sub-batch: the stager's host copy, or the host window)."""
+    window's meta table (flat, META_FIELDS per sub-batch: the stager's host copy, or the host window).
+    ``fixed_rows`` (pack mode): every batch has ``layout.max_segments`` rows, the rows past the packed
+    ones are padding (static shapes), and ``n_rows`` gives the packed count."""
     from .. import ops
 
     v = _cached_views(buf.view(-1), layout, sub)
@@ -354,36 +356,39 @@ def collate_token_window(buf: torch.Tensor, layout: TokenWindowLayout, mode: str
         ids, mask, pos = ops.pad_tokens(tokens, v["offsets"], layout.seq_len, pad_id)
         # n_tokens: tokens shipped (pad mode truncates sequences longer than seq_len: mask.sum() can be less)
         return {"input_ids": ids, "attention_mask": mask, "position_ids": pos, "n_tokens": n_tokens}
+    fill = layout.max_segments if fixed_rows else 0
+    extra = {"n_rows": n_rows} if fixed_rows else {}
     if not tokens.is_cuda:
         ids, mask, pos, seg = ops.ref_pack_tokens(tokens, v["row_start"][:n_rows].numpy(),
                                                   v["row_end"][:n_rows].numpy(), v["seg_offsets"][: n_seg + 1].numpy(),
-                                                  layout.seq_len, pad_id)
+                                                  layout.seq_len, pad_id, fill_rows=fill)
         return {"input_ids": ids, "attention_mask": mask, "position_ids": pos, "segment_ids": seg,
                 "cu_seqlens": v["seg_offsets"][: n_seg + 1].to(torch.int32), "max_seqlen": max_seqlen,
-                "n_tokens": n_tokens}
+                "n_tokens": n_tokens, **extra}
     dev = tokens.device
     s = layout.seq_len
     # one allocation for all five outputs (aligned regions: position_ids i64, cu_seqlens i32,
     # input_ids i32, segment_ids i32, attention_mask u8). cu_seqlens is written by the kernel into
     # memory of its own: a view of the staging buffer would be overwritten when it is re-staged
-    n = n_rows * s
+    R = max(n_rows, fill)
+    n = R * s
     cu_n = -(-(n_seg + 1) // 4) * 4  # i32 count rounded so the following regions stay 16-byte aligned
     whole = torch.empty(8 * n + 4 * cu_n + 4 * n + 4 * n + n, dtype=torch.uint8, device=dev)
     o = 0
-    pos = whole[o:o + 8 * n].view(torch.int64).view(n_rows, s)
+    pos = whole[o:o + 8 * n].view(torch.int64).view(R, s)
     o += 8 * n
     cu = whole[o:o + 4 * (n_seg + 1)].view(torch.int32)
     o += 4 * cu_n
-    ids = whole[o:o + 4 * n].view(torch.int32).view(n_rows, s)
+    ids = whole[o:o + 4 * n].view(torch.int32).view(R, s)
     o += 4 * n
-    seg = whole[o:o + 4 * n].view(torch.int32).view(n_rows, s)
+    seg = whole[o:o + 4 * n].view(torch.int32).view(R, s)
     o += 4 * n
-    mask = whole[o:o + n].view(n_rows, s)
+    mask = whole[o:o + n].view(R, s)
     from ..ops.kernels import _stream_handle
 
     if n_tokens > 0x7FFFFFFF:
         raise ValueError(f"{n_tokens} tokens in one batch overflow int32 cu_seqlens")
-    if n_rows == 0:
+    if R == 0:
         cu.copy_(v["seg_offsets"][: n_seg + 1])
     else:
         _native.hip().pad_pack_tokens(
@@ -391,9 +396,9 @@ def collate_token_window(buf: torch.Tensor, layout: TokenWindowLayout, mode: str
             row_end=v["row_end"].data_ptr(), seg_offsets=v["seg_offsets"].data_ptr(), n_seg=n_seg,
             out_tokens=ids.data_ptr(), attn_mask=mask.data_ptr(), position_ids=pos.data_ptr(), pos_is_i64=True,
             segment_ids=seg.data_ptr(), cu_seqlens_out=cu.data_ptr(), rows=n_rows, seq_len=s, pad_id=pad_id, mode=1,
-            stream=_stream_handle(None))
+            stream=_stream_handle(None), fill_rows=fill)
     return {"input_ids": ids, "attention_mask": mask, "position_ids": pos, "segment_ids": seg, "cu_seqlens": cu,
-            "max_seqlen": max_seqlen, "n_tokens": n_tokens}
+            "max_seqlen": max_seqlen, "n_tokens": n_tokens, **extra}
 
 
 def expected_tokens(source: SharedTokenSource, idx) -> list[np.ndarray]:

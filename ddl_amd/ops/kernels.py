@@ -575,15 +575,17 @@ def ref_pack_plan(seq_offsets: np.ndarray, seq_len: int, max_rows: int | None = 
     return np.array(row_start, dtype=np.int64), np.array(row_end, dtype=np.int64), seg_offsets
 
 
-def ref_pack_tokens(tokens, row_start, row_end, seg_offsets, seq_len, pad_id=0, position_dtype=torch.int64):
+def ref_pack_tokens(tokens, row_start, row_end, seg_offsets, seq_len, pad_id=0, position_dtype=torch.int64,
+                    fill_rows: int = 0):
+    """CPU reference of pack mode; ``fill_rows`` > packed rows: padding rows up to that fixed row count."""
     t = tokens.to("cpu", torch.int32)
     rs, re_, so = (np.asarray(a) for a in (row_start, row_end, seg_offsets))
-    r = len(rs)
+    r = max(len(rs), int(fill_rows))
     out = torch.full((r, seq_len), pad_id, dtype=torch.int32)
     mask = torch.zeros((r, seq_len), dtype=torch.uint8)
     pos = torch.zeros((r, seq_len), dtype=position_dtype)
     seg = torch.full((r, seq_len), -1, dtype=torch.int32)
-    for i in range(r):
+    for i in range(len(rs)):
         n = min(int(re_[i] - rs[i]), seq_len)
         g = np.arange(rs[i], rs[i] + n)
         sidx = np.searchsorted(so, g, side="right") - 1

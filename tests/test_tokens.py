@@ -339,3 +339,70 @@ def test_multi_batch_window_resume_mid_window(corpus, live, monkeypatch):
             dl.close()
     for j, b in enumerate(got):
         _check_pad(b, corpus, order.indices(0, 6 + j), seq_len)
+
+
+def _check_fixed_against_exact(fixed, exact, max_rows, seq_len, pad_id=0):
+    n = exact["input_ids"].shape[0]
+    assert fixed["n_rows"] == n and fixed["input_ids"].shape == (max_rows, seq_len)
+    for k in ("input_ids", "attention_mask", "position_ids", "segment_ids"):
+        assert fixed[k].dtype == exact[k].dtype and torch.equal(fixed[k][:n].cpu(), exact[k].cpu()), k
+    pad = {"input_ids": pad_id, "attention_mask": 0, "position_ids": 0, "segment_ids": -1}
+    for k, v in pad.items():
+        assert bool((fixed[k][n:].cpu() == v).all()), k
+    assert torch.equal(fixed["cu_seqlens"].cpu(), exact["cu_seqlens"].cpu())
+    assert fixed["n_tokens"] == exact["n_tokens"] and fixed["max_seqlen"] == exact["max_seqlen"]
+
+
+def _token_run(corpus, gb, seq_len, k, epochs=1, **kw):
+    out = []
+    with ddl_amd.start(n_producers=2) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(corpus, gb, seq_len, "pack", batches_per_window=k), gb,
+                                           conn, epochs, mode="indexed", env=env, auto_mark=True, collate="tokens",
+                                           seed=4, **kw)
+        for _ in range(epochs):
+            for b in dl:
+                out.append({x: (v.cpu().clone() if isinstance(v, torch.Tensor) else v) for x, v in b.items()})
+        st = dl.stats()
+        layout = dl.metadata_from_producer[0].extra["token_layout"]
+    return out, st, layout
+
+
+def test_fixed_token_rows_cpu(corpus, monkeypatch):
+    """token_rows="fixed": every packed batch has the layout's max rows; the packed rows equal the exact
+    batch and the rest are padding (static shapes for graph-captured steps)."""
+    monkeypatch.setenv("DDL_DEVICE", "cpu")
+    from ddl_amd.models.tokens import TokenWindowLayout
+
+    exact, _, _ = _token_run(corpus, 16, 256, 4)
+    fixed, _, lay = _token_run(corpus, 16, 256, 4, token_rows="fixed")
+    max_rows = TokenWindowLayout(**lay).max_segments
+    assert len(exact) == len(fixed) > 0
+    for f, e in zip(fixed, exact):
+        _check_fixed_against_exact(f, e, max_rows, 256)
+
+
+@pytest.mark.gpu
+def test_fixed_token_rows_gpu_native_and_python():
+    """Fixed-row packed batches from the native engine (inline and whole-window) == the Python collate
+    == the exact batches padded."""
+    from ddl_amd.models.tokens import TokenWindowLayout
+
+    src = SharedTokenSource.synthetic(f"ddl_amd_tokfix_{np.random.randint(1 << 30)}", 200, 5, 300, seed=3)
+    try:
+        exact, _, _ = _token_run(src, 16, 256, 4, native_dispatch=False)
+        ref, _, lay = _token_run(src, 16, 256, 4, native_dispatch=False, token_rows="fixed")
+        max_rows = TokenWindowLayout(**lay).max_segments
+        for f, e in zip(ref, exact):
+            _check_fixed_against_exact(f, e, max_rows, 256)
+        for native in ("inline", "window"):
+            nat, st, _ = _token_run(src, 16, 256, 4, native_dispatch=native, token_rows="fixed")
+            assert st["native_dispatch"]["mode"] == native and len(nat) == len(ref)
+            for a, b in zip(nat, ref):
+                assert a.keys() == b.keys()
+                for x in a:
+                    if isinstance(a[x], torch.Tensor):
+                        assert torch.equal(a[x], b[x]), (native, x)
+                    else:
+                        assert a[x] == b[x], (native, x)
+    finally:
+        src.close()
