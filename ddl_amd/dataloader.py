@@ -44,7 +44,7 @@ from .connection import Connection
 from .datasetwrapper import ProducerFunctionSkeleton
 from .exceptions import ShapeMismatchError
 from .ops import _dtypes
-from .permutation import FeistelPermutation
+from .permutation import FeistelPermutation, batch_cursor
 from .types import DDLEnv, Marker, MetaData_Consumer_To_Producer, MetaData_Producer_To_Consumer
 from .utils.logging import for_all_methods, with_logging
 from .utils import streams
@@ -936,6 +936,8 @@ class DistributedDataLoader(DistributedDataloaderABC):
             base.update({
                 "kind": "indexed",
                 "global_batch_cursor": consumed,
+                # the same position in samples of the epoch order (the epoch/sample-index format)
+                "global_sample_cursor": consumed * int(extra.get("global_batch") or 0),
                 "batches_per_epoch": self.windows_per_epoch * k,
                 "batches_per_window": k,
                 "global_batch": extra.get("global_batch"),
@@ -964,7 +966,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
         if sd.get("kind") == "indexed":
             bpe = int(sd["batches_per_epoch"])
             k = int(sd.get("batches_per_window", 1))  # global batches per window (token windows)
-            cur = int(sd["global_batch_cursor"])
+            cur = batch_cursor(sd, sd.get("global_batch"))
             if cur >= bpe:
                 self.epoch, cur = self.epoch + 1, 0
             self.window = self.epoch * (bpe // k) + cur // k

@@ -168,3 +168,17 @@ class EpochOrder:
     def indices(self, epoch: int, g: int, rank: int = 0, world_size: int = 1) -> np.ndarray:
         """Sample indices of rank ``rank``'s share of global batch ``g`` in ``epoch``."""
         return self.perm(epoch)(self.positions(g, rank, world_size))
+
+
+def batch_cursor(sd: dict, global_batch) -> int:
+    """The global-batch cursor of an indexed checkpoint: ``global_batch_cursor``, or derived from
+    ``global_sample_cursor`` (epoch/sample-index checkpoints) when only that is given."""
+    if "global_batch_cursor" in sd:
+        return int(sd["global_batch_cursor"])
+    if "global_sample_cursor" not in sd:
+        raise KeyError("indexed checkpoint without global_batch_cursor / global_sample_cursor")
+    gb = int(global_batch or 0)
+    sc = int(sd["global_sample_cursor"])
+    if gb <= 0 or sc % gb:
+        raise ValueError(f"global_sample_cursor={sc} is not a multiple of the global batch {gb}")
+    return sc // gb

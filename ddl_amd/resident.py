@@ -50,7 +50,7 @@ import torch
 from . import _native, ops
 from .ops import _dtypes
 from .parallel.order import LEDGER, loader_group
-from .permutation import EpochOrder
+from .permutation import EpochOrder, batch_cursor
 from .types import DDLEnv
 from .utils.logging import logger
 from .utils import streams
@@ -195,6 +195,8 @@ class PrefetchedIndexedLoader:
             "order_seed": self.seed,
             "epoch": self.epoch,
             "global_batch_cursor": self.cursor + (1 if self._pending else 0),
+            # the same position in samples of the epoch order (the epoch/sample-index format)
+            "global_sample_cursor": (self.cursor + (1 if self._pending else 0)) * self.order.global_batch,
             "batches_per_epoch": self.order.batches_per_epoch,
             "global_batch": self.order.global_batch,
             "n_samples": self.order.n_samples,
@@ -210,7 +212,7 @@ class PrefetchedIndexedLoader:
             if sd.get(key) is not None and sd[key] != mine:
                 raise ValueError(f"checkpoint {key}={sd[key]} does not match {mine}")
         self.epoch = int(sd["epoch"])
-        self.cursor = int(sd["global_batch_cursor"])
+        self.cursor = batch_cursor(sd, self.order.global_batch)
         if self.cursor >= self.order.batches_per_epoch:
             self.epoch, self.cursor = self.epoch + 1, 0
 

@@ -154,3 +154,15 @@ def test_load_state_dict_live_on_gpu():
         dl.load_state_dict(sd)
         tail = _take(dl, 10 ** 9)
     assert all(torch.equal(a, b) for a, b in zip(head + tail, full))
+
+
+def test_sample_index_cursor_in_indexed_checkpoints():
+    """Indexed checkpoints carry the epoch/sample-index position too; a state with only
+    ``global_sample_cursor`` resumes at the same global batch."""
+    from ddl_amd.permutation import batch_cursor
+
+    sd = {"global_batch_cursor": 5, "global_sample_cursor": 5 * 64}
+    assert batch_cursor(sd, 64) == 5
+    assert batch_cursor({"global_sample_cursor": 320}, 64) == 5
+    with pytest.raises(ValueError):
+        batch_cursor({"global_sample_cursor": 321}, 64)

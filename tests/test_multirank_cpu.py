@@ -60,7 +60,8 @@ def test_indexed_resume_at_different_world_size(shared_source):
     # run on 2 ranks, stop after epoch 0 batch 5 (global batch cursor = 5)
     res = run_ranks(_indexed_rank, 2, n, gb, 2, shared_source.name, None, (0, 5))
     sd = res[0][1]
-    assert sd["kind"] == "indexed" and sd["global_batch_cursor"] == 5
+    assert sd["kind"] == "indexed" and sd["global_batch_cursor"] == 5 and sd["global_sample_cursor"] == 5 * gb
+    sd = {k: v for k, v in sd.items() if k != "global_batch_cursor"}  # resume from the sample index alone
     # resume on 1 rank
     (out, _), = run_ranks(_indexed_rank, 1, n, gb, 2, shared_source.name, sd)
     from ddl_amd.permutation import EpochOrder
