@@ -72,10 +72,10 @@ def main(argv=None):
             else:
                 source = src
             n_epochs = (a.warmup + a.steps + a.idle_steps + a.warmup // 2) // (a.n_seqs // gb) + 2
-            dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(source, gb, a.seq_len, a.mode,
-                                                                  pack_order=a.pack_order if a.mode == "pack" else "in_order",
-                                                                  batches_per_window=a.batches_per_window,
-                                                                  host_threads=a.host_threads), a.batch, conn,
+            producer = TokenBatchProducer(source, gb, a.seq_len, a.mode,
+                                          pack_order=a.pack_order if a.mode == "pack" else "in_order",
+                                          batches_per_window=a.batches_per_window, host_threads=a.host_threads)
+            dl = ddl_amd.DistributedDataLoader(producer, a.batch, conn,
                                                n_epochs, mode="indexed", env=env, collate="tokens", auto_mark=True,
                                                n_slots=a.slots, token_rows=a.token_rows,
                                                native_dispatch=False if a.dispatch == "python" else a.dispatch)
@@ -154,7 +154,10 @@ def main(argv=None):
                     "row_density_est": round(a.batch * mean_len / (rows / a.steps) / a.seq_len, 3),
                     "n_gpus": env.world_size,
                     "steps": a.steps, "ms_per_step": round(1000 * dt / a.steps, 3), "batch_seqs": a.batch,
-                    "producers": a.producers, "host_threads": a.host_threads, "slots": a.slots, "batches_per_window": dl.batches_per_window[0], "dispatch": a.dispatch, "dispatch_mode": (st.get("native_dispatch") or {}).get("mode"), "token_rows": a.token_rows, "mean_len": round(mean_len, 1),
+                    "producers": a.producers, "host_threads": a.host_threads, "slots": a.slots,
+                    "batches_per_window": dl.batches_per_window[0], "dispatch": a.dispatch,
+                    "dispatch_mode": (st.get("native_dispatch") or {}).get("mode"), "token_rows": a.token_rows,
+                    "mean_len": round(mean_len, 1),
                     "consumer_wait_s": round(st["consumer_wait_s"], 3),
                     "stager_wait_producer_s": round(st.get("stager_wait_producer_s", 0.0), 3),
                     # per producer: rounds, mean fill and mean slot-wait per round (us) -- where the feed goes
