@@ -19,6 +19,7 @@ __all__ = [
     "FeistelPermutation",
     "EpochOrder",
     "IndexedProducer",
+    "DataLoader",
     "ops",
 ]
 
@@ -36,4 +37,8 @@ def __getattr__(name):
         from .models.producers import IndexedProducer
 
         return IndexedProducer
+    if name == "DataLoader":
+        from .frontend import DataLoader
+
+        return DataLoader
     raise AttributeError(name)

@@ -121,12 +121,13 @@ class IndexedProducer(ProducerFunctionSkeleton):
     """Producer of the world-size-invariant global order (one window = one local batch)."""
 
     def __init__(self, source, global_batch: int, seed: int | None = None, drop_last: bool = True,
-                 host_threads: int = 4):
+                 host_threads: int = 4, shuffle: bool = True):
         super().__init__()
         self.source = source
         self.global_batch = int(global_batch)
         self.seed = seed  # None: use the loader's seed
         self.drop_last = drop_last
+        self.shuffle = bool(shuffle)  # False: dataset order (evaluation)
         self.host_threads = host_threads
         self.world_size = 1
         self.order: EpochOrder | None = None
@@ -136,13 +137,13 @@ class IndexedProducer(ProducerFunctionSkeleton):
         self.world_size = int(kwargs.get("world_size", 1))
         if self.seed is None:
             self.seed = int(kwargs.get("seed", 0))
-        self.order = EpochOrder(self.source.n, self.global_batch, int(self.seed), self.drop_last)
+        self.order = EpochOrder(self.source.n, self.global_batch, int(self.seed), self.drop_last, self.shuffle)
         lb = self.order.local_batch(self.world_size)
         nv = int(math.prod(self.source.sample_shape)) if self.source.sample_shape else 1
         return DataProducerOnInitReturn(lb, nv, (lb, *self.source.sample_shape), (nv,), self.source.dtype,
                                         extra={"batches_per_epoch": self.order.batches_per_epoch,
                                                "global_batch": self.global_batch, "n_samples": self.source.n,
-                                               "order_seed": int(self.seed),
+                                               "order_seed": int(self.seed), "order_shuffle": self.shuffle,
                                                # MapDatasetSource: the loader rebuilds the sample structure
                                                "fields": getattr(self.source, "fields", None),
                                                "fields_kind": getattr(self.source, "kind", None)})

@@ -130,6 +130,22 @@ def _native_runtime():
         return None
 
 
+class IdentityOrder:
+    """The unshuffled order with the ``FeistelPermutation`` call surface (``EpochOrder(shuffle=False)``)."""
+
+    def __init__(self, n: int):
+        self.n = int(n)
+
+    def __call__(self, pos) -> np.ndarray:
+        pos = np.asarray(pos, dtype=np.int64)
+        if pos.size and (pos.min() < 0 or pos.max() >= self.n):
+            raise IndexError(f"positions out of range [0, {self.n})")
+        return pos
+
+    def full(self) -> np.ndarray:
+        return np.arange(self.n, dtype=np.int64)
+
+
 @dataclasses.dataclass
 class EpochOrder:
     """Global sample order for DP training, invariant to the world size."""
@@ -138,6 +154,7 @@ class EpochOrder:
     global_batch: int
     seed: int = 0
     drop_last: bool = True
+    shuffle: bool = True  # False: positions in dataset order (evaluation), same batching and checkpoints
 
     def __post_init__(self) -> None:
         if self.global_batch <= 0 or self.n_samples <= 0:
@@ -156,14 +173,20 @@ class EpochOrder:
             raise ValueError(f"global batch {self.global_batch} not divisible by world size {world_size}")
         return self.global_batch // world_size
 
-    def perm(self, epoch: int) -> FeistelPermutation:
+    def perm(self, epoch: int) -> FeistelPermutation | IdentityOrder:
+        if not self.shuffle:
+            return IdentityOrder(self.n_samples)
         return FeistelPermutation(self.n_samples, self.seed, epoch)
 
     def positions(self, g: int, rank: int, world_size: int) -> np.ndarray:
+        """Positions of rank ``rank``'s slice of global batch ``g``. With ``drop_last=False`` the last,
+        partial global batch is completed by wrapping around to the start of the epoch's order
+        (``DistributedSampler``-style padding): every batch has ``global_batch`` samples, and the
+        first ``batches_per_epoch * global_batch - n_samples`` samples of the epoch appear twice."""
         lb = self.local_batch(world_size)
         start = g * self.global_batch + rank * lb
         pos = np.arange(start, start + lb, dtype=np.int64)
-        return pos[pos < self.n_samples]
+        return pos % self.n_samples
 
     def indices(self, epoch: int, g: int, rank: int = 0, world_size: int = 1) -> np.ndarray:
         """Sample indices of rank ``rank``'s share of global batch ``g`` in ``epoch``."""

@@ -278,6 +278,8 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
         self.row_elems = int(math.prod(self.sample_shape)) if self.sample_shape else 1
         self.row_bytes = self.row_elems * _dtypes.itemsize(self.src_dtype)
         self.N = n
+        if not drop_last:  # the device-side order covers whole global batches only
+            raise ValueError(f"{type(self).__name__} needs drop_last=True")
         self.order = EpochOrder(n, global_batch, seed, drop_last)
         self.GB = int(global_batch)
         self.LB = self.order.local_batch(self.W)

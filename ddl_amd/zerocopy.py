@@ -59,6 +59,8 @@ class ZeroCopyLoader(PrefetchedIndexedLoader):
         self.W, self.rank = self.env.world_size, self.env.rank
         self.sample_shape, self.src_dtype = _source_geometry(source)
         addr, n = _source_address(source)
+        if not drop_last:  # the device-side order covers whole global batches only
+            raise ValueError(f"{type(self).__name__} needs drop_last=True")
         self.order = EpochOrder(n, global_batch, seed, drop_last)
         self.GB, self.LB = int(global_batch), self.order.local_batch(self.W)
         self.out_dtype = _dtypes.to_torch_dtype(out_dtype) if out_dtype is not None else self.src_dtype

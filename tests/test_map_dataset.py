@@ -123,3 +123,42 @@ def test_map_dataset_loader_gpu(native):
                 _check(b, _expected(ds, order.indices(e, g)))
         st = dl.stats()
     assert (st.get("native_dispatch") is not None) == native
+
+
+def test_dataloader_front_end_cpu(monkeypatch):
+    """``ddl_amd.DataLoader(dataset, batch_size, shuffle=...)``: torch DataLoader surface over the
+    indexed loader -- epochs via repeated iter(), len, shuffle=False order, state_dict round trip."""
+    monkeypatch.setenv("DDL_DEVICE", "cpu")
+    ds, bs = TupleDataset(40), 8
+    order = EpochOrder(len(ds), bs, 5)
+    with ddl_amd.DataLoader(ds, batch_size=bs, shuffle=True, num_workers=2, seed=5) as dl:
+        assert len(dl) == order.batches_per_epoch
+        for e in range(2):
+            got = [b[1].tolist() for b in dl]
+            assert got == [[7 * int(i) for i in order.indices(e, g)] for g in range(order.batches_per_epoch)]
+        it = iter(dl)
+        next(it)
+        next(it)
+        sd = dl.state_dict()
+        assert sd["epoch"] == 2 and sd["global_batch_cursor"] == 2
+    with ddl_amd.DataLoader(ds, batch_size=bs, shuffle=True, num_workers=2, seed=5, resume_state=sd) as dl:
+        rest = [b[1].tolist() for b in dl]
+        assert rest == [[7 * int(i) for i in order.indices(2, g)] for g in range(2, order.batches_per_epoch)]
+    with ddl_amd.DataLoader(ds, batch_size=bs, shuffle=False, drop_last=True, num_workers=1) as dl:
+        labels = [x for b in dl for x in b[1].tolist()]
+        assert labels == [7 * i for i in range(len(ds))]
+    # drop_last=False: the last batch is completed from the start of the epoch (DistributedSampler-style)
+    with ddl_amd.DataLoader(TupleDataset(43), batch_size=bs, shuffle=False, drop_last=False, num_workers=2) as dl:
+        labels = [x for b in dl for x in b[1].tolist()]
+        assert labels == [7 * (i % 43) for i in range(48)]
+
+
+@pytest.mark.gpu
+def test_dataloader_front_end_gpu():
+    ds, bs = TupleDataset(64), 16
+    order = EpochOrder(len(ds), bs, 5)
+    with ddl_amd.DataLoader(ds, batch_size=bs, shuffle=True, num_workers=2, seed=5) as dl:
+        for e in range(2):
+            for g, b in enumerate(dl):
+                assert b[0].is_cuda and b[0].shape == (bs, 3, 5, 7)
+                _check(b, _expected(ds, order.indices(e, g)))

@@ -98,7 +98,11 @@ def test_epoch_order_exactly_once():
     order2 = EpochOrder(1000, 64, seed=1, drop_last=False)
     assert order2.batches_per_epoch == 16
     idx = np.concatenate([order2.indices(0, g) for g in range(16)])
-    assert np.array_equal(np.sort(idx), np.arange(1000))
+    # the last global batch wraps around: every sample once, the epoch's first 24 twice, full batches
+    assert len(idx) == 16 * 64 and np.array_equal(np.unique(idx), np.arange(1000))
+    assert np.array_equal(idx[1000:], idx[:24])
+    parts = [order2.indices(0, 15, r, 4) for r in range(4)]
+    assert np.array_equal(np.concatenate(parts), idx[15 * 64:])
 
 
 def test_epoch_order_validation():
