@@ -4,6 +4,7 @@
     python examples/torch_dataset.py
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 examples/torch_dataset.py
 
+``ddl_amd.DataLoader`` is the torch-DataLoader-shaped front end of the pieces below.
 ``MapDatasetSource`` packs each sample (a tensor, or a flat tuple / dict of tensors, arrays and
 numbers) into a byte row. ``IndexedProducer`` workers call ``dataset[i]`` for their share of every
 global batch, in the world-size-invariant ``EpochOrder``. The loader hands back batches shaped like
@@ -16,7 +17,6 @@ import argparse
 import torch
 
 import ddl_amd
-from ddl_amd.models import IndexedProducer, MapDatasetSource
 
 
 class Squares(torch.utils.data.Dataset):
@@ -36,20 +36,20 @@ class Squares(torch.utils.data.Dataset):
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--n-samples", type=int, default=2048)
-    ap.add_argument("--global-batch", type=int, default=64)
+    ap.add_argument("--batch-size", type=int, default=32, help="per rank")
     ap.add_argument("--epochs", type=int, default=2)
     a = ap.parse_args()
 
-    with ddl_amd.start(n_producers=2) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(IndexedProducer(MapDatasetSource(Squares(a.n_samples)), a.global_batch),
-                                           a.global_batch // env.world_size, conn, a.epochs, mode="indexed", env=env,
-                                           auto_mark=True)
+    # ddl_amd.DataLoader = start() + IndexedProducer(MapDatasetSource(dataset)) + DistributedDataLoader
+    # (mode="indexed", auto_mark=True); built before the first CUDA call of the process
+    with ddl_amd.DataLoader(Squares(a.n_samples), batch_size=a.batch_size, shuffle=True, num_workers=2) as dl:
+        rank = dl.env.rank
         for epoch in range(a.epochs):
             seen = 0
             for img, label, weight in dl:
                 assert torch.equal(img[:, 0, 0, 0].long(), label % 256)  # the sample structure survives
                 seen += label.numel()
-            if env.rank == 0:
+            if rank == 0:
                 print(f"epoch {epoch}: {seen} samples on rank 0 as (image {tuple(img.shape)} {img.dtype}, "
                       f"label {label.dtype}, weight {weight.dtype}) on {img.device}", flush=True)
 

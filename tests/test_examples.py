@@ -121,7 +121,7 @@ def test_bench_plumbing_config1_two_ranks():
 @pytest.mark.parametrize("script,args", [("resident_images.py", ["--n-samples", "512", "--epochs", "2"]),
                                          ("tokens_packed.py", ["--n-seqs", "256", "--epochs", "2"]),
                                          ("tokens_packed.py", ["--n-seqs", "256", "--epochs", "1", "--mode", "pad"]),
-                                         ("torch_dataset.py", ["--n-samples", "256", "--epochs", "2"])])
+                                         ("torch_dataset.py", ["--n-samples", "256", "--epochs", "2", "--batch-size", "16"])])
 @pytest.mark.parametrize("ranks", [1, 2])
 def test_usage_examples(script, args, ranks):
     """The usage examples run end to end on CPU, alone and as two torchrun ranks (gloo)."""
