@@ -244,6 +244,7 @@ def _landed(dl) -> tuple[int, int]:
     st = getattr(dl, "_stager", None)
     if st is None:  # CPU rehearsal: the host path has no H2D; every delivered window counts
         return dl.window, 0
+    st.settle()  # called right after a device sync: count every copy that has completed, no retire lag
     return st.windows_landed, st.bytes_landed
 
 

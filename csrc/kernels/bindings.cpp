@@ -243,6 +243,7 @@ PYBIND11_MODULE(_ddl_hip, m) {
       .def_property_readonly("bytes_h2d", &ddl::NativeStager::bytes_h2d)
       .def_property_readonly("windows_staged", &ddl::NativeStager::windows_staged)
       .def_property_readonly("windows_landed", &ddl::NativeStager::windows_landed)
+      .def("settle", &ddl::NativeStager::settle, py::arg("timeout_ms") = 1000, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("bytes_landed", &ddl::NativeStager::bytes_landed)
       .def_property_readonly("wait_producer_s", &ddl::NativeStager::wait_producer_s)
       .def_property_readonly("wait_log", &ddl::NativeStager::wait_log,

@@ -88,6 +88,19 @@ void NativeStager::retire_loop() {
   }
 }
 
+void NativeStager::settle(int64_t timeout_ms) {
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+  std::unique_lock<std::mutex> lk(mu_);
+  while (!retire_q_.empty() && error_code_ == 0 && !stop_) {
+    const int64_t front = retire_q_.front().window;
+    if (hipEventQuery(retire_ev_[retire_q_.front().ev]) != hipSuccess) return;  // still in flight: not landed
+    if (!retire_cv_.wait_until(lk, deadline, [&] {
+          return stop_ || error_code_ != 0 || retire_q_.empty() || retire_q_.front().window != front;
+        }))
+      return;  // timed out
+  }
+}
+
 void NativeStager::fail(int code, int32_t producer, const std::string& msg) {
   std::lock_guard<std::mutex> lk(mu_);
   if (error_code_ == 0) {

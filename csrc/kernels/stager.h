@@ -90,6 +90,10 @@ class NativeStager {
   // Windows / bytes whose H2D copy has RETIRED (counted by the host callback that
   // runs after the DMA): what has actually landed in HBM, as opposed to enqueued.
   uint64_t windows_landed() const { return windows_landed_.load(); }
+  // Wait (bounded) until the retire thread has counted every copy whose retire event has completed:
+  // after a device synchronize, windows_landed() then counts exactly the windows in HBM (the retire
+  // thread's host-side lag -- up to one window with two copy streams in flight -- is gone).
+  void settle(int64_t timeout_ms);
   uint64_t bytes_landed() const { return bytes_landed_.load(); }
   double wait_producer_s() const { return wait_producer_ns_.load() * 1e-9; }
   // per staged window (first 4096): ns spent in each step of the stager loop -- waiting for the ring

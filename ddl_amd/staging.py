@@ -268,6 +268,10 @@ class WindowStager:
         """Windows whose H2D copy has been enqueued."""
         return int(self._native.windows_staged)
 
+    def settle(self, timeout_s: float = 1.0) -> None:
+        """After a device synchronize: wait until every completed copy has been counted as landed."""
+        self._native.settle(int(timeout_s * 1000))
+
     @property
     def windows_landed(self) -> int:
         """Windows whose H2D copy has retired (the data is in HBM)."""
