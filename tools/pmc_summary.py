@@ -10,8 +10,8 @@ name it reports the mean counter value per dispatch, the resources from the disp
 Derived fields where the counters are present:
 
 * ``hbm_GBps``: (FETCH_SIZE + WRITE_SIZE) KB per dispatch over the mean duration;
-* ``waves_per_dispatch`` and ``busy_fraction`` (SQ_BUSY_CYCLES / GRBM_GUI_ACTIVE over the
-  SE count is not normalised here: it is reported as measured);
+* ``waves_per_dispatch`` (SQ_WAVES) and ``occupancy_waves_per_simd``: the waves per SIMD the
+  kernel's VGPR/AGPR and LDS allocation allow on gfx950;
 * ``valu_per_vmem``: SQ_INSTS_VALU / SQ_INSTS_VMEM_RD (arithmetic intensity in instructions).
 """
 
@@ -33,6 +33,23 @@ def _short(name: str) -> str:
         if name.startswith(prefix):
             name = name[len(prefix):]
     return name[:90]
+
+
+def theoretical_occupancy(e: dict) -> int | None:
+    """Waves per SIMD the kernel's resources allow on gfx950 (MI355X_MICROARCH "Register files"):
+    min(8, 512 // VGPR+AGPR allocation in granules of 8), and the LDS limit (160 KiB per CU shared
+    by the resident workgroups, 4 SIMDs per CU)."""
+    regs = e.get("vgpr", 0) + e.get("agpr", 0)
+    if not regs or not e.get("workgroup"):
+        return None
+    alloc = -(-int(regs) // 8) * 8
+    waves = min(8, 512 // alloc)
+    lds = int(e.get("lds_bytes", 0))
+    if lds > 0:
+        wgs_per_cu = 163840 // lds
+        waves_per_wg = -(-int(e["workgroup"]) // 64)
+        waves = min(waves, max(1, wgs_per_cu * waves_per_wg // 4))
+    return waves
 
 
 def load(dirs: list[str]) -> dict:
@@ -70,6 +87,9 @@ def load(dirs: list[str]) -> dict:
             e["hbm_GBps"] = round((e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024 / (e["mean_us"] * 1e-6) / 1e9, 1)
         if "SQ_WAVES" in e:
             e["waves_per_dispatch"] = e["SQ_WAVES"]
+        occ = theoretical_occupancy(e)
+        if occ is not None:
+            e["occupancy_waves_per_simd"] = occ
         if e.get("SQ_INSTS_VMEM_RD"):
             e["valu_per_vmem"] = round(e.get("SQ_INSTS_VALU", 0) / e["SQ_INSTS_VMEM_RD"], 2)
         out[k] = e
@@ -85,7 +105,8 @@ def main() -> int:
         json.dump(summary, f, indent=1)
     for k, e in sorted(summary.items()):
         print(json.dumps({"kernel": k, **{x: e[x] for x in ("mean_us", "hbm_GBps", "vgpr", "lds_bytes",
-                                                               "waves_per_dispatch", "valu_per_vmem") if x in e}}))
+                                                               "waves_per_dispatch", "occupancy_waves_per_simd",
+                                                               "valu_per_vmem") if x in e}}))
     return 0
 
 
