@@ -5,6 +5,7 @@ ddl/connection.py:88-187); tested across real processes (SURVEY §4.4 level 1).
 """
 
 import multiprocessing as mp
+import multiprocessing.connection
 import os
 import threading
 import time
@@ -133,7 +134,9 @@ def test_dead_peer_detected_even_as_zombie(arena):
     ctx = mp.get_context("spawn")
     p = ctx.Process(target=_exit_child, args=(3,))
     p.start()
-    time.sleep(0.5)  # child is a zombie now (not reaped yet)
+    # The sentinel becomes readable when the child exits, without reaping it: the child is
+    # a zombie from here on (a spawn child can take seconds to start on a loaded host).
+    assert mp.connection.wait([p.sentinel], timeout=60)
     t0 = time.monotonic()
     rc = arena.wait_state(0, 0, rt.READY, 10_000, p.pid, -1)
     assert rc == rt.WaitResult.PEER_DEAD
