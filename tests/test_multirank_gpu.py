@@ -1,0 +1,105 @@
+"""Several DP ranks on the GPU box's one card: the multi-process device data path on hardware.
+
+RCCL refuses two ranks on one GPU ("Duplicate GPU detected", ``profiles/r1_rccl_probe``), so
+these runs build the DP group on gloo (``DDL_BACKEND=gloo``; gloo's all-to-all and all-reduce
+take device tensors and bounce them through host memory). Everything else is the production
+path of each rank: its own producer processes and pinned arena, H2D staging on the copy
+streams, the window exchange on the post-copy stream, the gfx950 gather/permute kernels and a
+DDP train step -- with two or four of them sharing the card. The reference's exchange this
+replaces is ``/root/reference/ddl/shuffle.py:92-108``; the CPU versions of these checks are in
+``test_multirank_cpu.py`` and ``test_examples.py``.
+"""
+
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from tests.mp_harness import free_port, run_ranks
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GPU_GLOO = {"DDL_DEVICE": "", "DDL_BACKEND": "gloo"}  # "" = not forced to the CPU
+
+
+def _exchange_rank_gpu(rank, world, method, fraction):
+    import ddl_amd
+    from ddl_amd import Marker
+    from tests.helpers import IdProducer
+
+    eps = []
+    with ddl_amd.start(n_producers=2) as (env, conn):
+        assert env.device.startswith("cuda"), env.device
+        dl = ddl_amd.DistributedDataLoader(IdProducer(64, 6), 16, conn, 3, fraction, method, env=env,
+                                           copy_batches=True, seed=1, device=torch.device(env.device))
+        assert dl._exchange_fn is not None
+        for _ in range(3):
+            rows = []
+            for a, b in dl:
+                assert a.is_cuda and b.is_cuda
+                rows.append(torch.cat([a, b], 1).cpu())
+                dl.mark(Marker.END_OF_BATCH)
+            dl.mark(Marker.END_OF_EPOCH)
+            eps.append(torch.cat(rows).numpy())
+        n_ex = dl._exchange_fn.n_exchange
+        dl.close()
+    return eps, n_ex
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("world", [2, 4])
+def test_exchange_conserves_rows_on_device(world):
+    """The all-to-all window exchange between ranks whose windows live in HBM: every (rank,
+    producer, row) of every round is delivered exactly once over all ranks, and each rank holds
+    exactly the foreign rows the exchange plan says."""
+    res = run_ranks(_exchange_rank_gpu, world, "alltoall", 0.5, timeout=200, env=GPU_GLOO)
+    n_ex = res[0][1]
+    assert n_ex > 0
+    for e in range(3):
+        all_rows = np.concatenate([r[0][e] for r in res])
+        keys = {tuple(x) for x in all_rows[:, :3].tolist()}
+        assert len(keys) == len(all_rows) == world * 64  # an epoch is one 64-row window per rank
+        for r in range(world):
+            mine = res[r][0][e]
+            assert (mine[:, 0] != r).sum() == n_ex - n_ex // world  # the chunk for self stays
+
+
+def _run_bench(n, launch, extra=()):
+    args = [os.path.join(REPO, "bench.py"), "--gpus", str(n), "--steps", "24", "--warmup", "6",
+            "--idle-steps", "6", *extra]
+    env = dict(os.environ, PYTHONPATH=REPO, **GPU_GLOO)
+    if launch == "torchrun":
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+               "--master-addr", "127.0.0.1", "--master-port", str(free_port()), *args]
+    else:
+        cmd = [sys.executable, *args]
+        for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+            env.pop(k, None)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=200, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("n,launch", [(2, "torchrun"), (2, "self")])
+def test_bench_multirank_device_path(n, launch):
+    """bench.py at N ranks on the card: the driver's torchrun line and the self-launch both give one
+    JSON line with n_gpus = N; every rank moved its windows H2D inside the timed region, ran the
+    window exchange, and issued loader exchanges and DDP all-reduces in one cross-rank order."""
+    out = _run_bench(n, launch)
+    assert out["n_gpus"] == n and out["config"]["parallelism"] == f"dp{n}" and out["value"] > 0
+    assert out["config"]["exchange_fraction"] == 0.5 and out["phase2_error"] is None
+    order = out["collective_order"]
+    assert order["same_order"] is True and order["by_kind"]["ddp.allreduce"] > 0
+    assert order["by_kind"]["loader.exchange"] > 0
+    assert len(out["per_rank"]) == n
+    for r in out["per_rank"]:
+        assert r["h2d_bytes_timed"] > 0 and r["exchange_calls"] > 0 and r["rccl_bytes"] > 0
+    assert out["indexed"] and "error" not in out["indexed"] and out["indexed"]["value"] > 0
