@@ -523,6 +523,32 @@ void parallel_copy(uint8_t* dst, const uint8_t* src, uint64_t bytes, int n_threa
   });
 }
 
+void copy_spans(const uintptr_t* dst, const uintptr_t* src, const uint64_t* sizes, uint64_t n, int n_threads) {
+  if (n == 0) return;
+  // task boundaries: consecutive spans until ~1 MiB
+  std::vector<uint64_t> starts{0};
+  uint64_t acc = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    acc += sizes[i];
+    if (acc >= (1ull << 20) && i + 1 < n) {
+      starts.push_back(i + 1);
+      acc = 0;
+    }
+  }
+  starts.push_back(n);
+  const int tasks = static_cast<int>(starts.size() - 1);
+  auto body = [&](int t) {
+    for (uint64_t i = starts[t]; i < starts[t + 1]; ++i)
+      std::memcpy(reinterpret_cast<void*>(dst[i]), reinterpret_cast<const void*>(src[i]), sizes[i]);
+  };
+  if (tasks == 1 || n_threads <= 1) {
+    for (int t = 0; t < tasks; ++t) body(t);
+    return;
+  }
+  std::lock_guard<std::mutex> lk(g_pool_call_mu);
+  Pool::get().run(tasks, n_threads, body);
+}
+
 void pack_columns(uint8_t* dst, const std::vector<const uint8_t*>& srcs, const std::vector<uint64_t>& widths,
                   uint64_t elem_bytes, uint64_t n, int n_threads) {
   // Window fill of the reference harness (tests/run_ddl.py:156-159): k

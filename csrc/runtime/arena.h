@@ -161,6 +161,10 @@ void gather_rows(uint8_t* dst, const uint8_t* src, uint64_t row_bytes, const int
                  uint64_t n, uint64_t src_rows, int n_threads);
 // Parallel memcpy (large contiguous copies: window replication).
 void parallel_copy(uint8_t* dst, const uint8_t* src, uint64_t bytes, int n_threads);
+// Many independent copies dst[i] <- src[i] (sizes[i] bytes) on the worker pool, split into
+// ~1 MiB tasks of consecutive spans: the packing step of map-style dataset producers, where
+// Python collects one span per sample field and the bytes move without the GIL.
+void copy_spans(const uintptr_t* dst, const uintptr_t* src, const uint64_t* sizes, uint64_t n, int n_threads);
 // Ragged (variable-length) gather: sequence idx[i] = src[src_offsets[idx[i]] :
 // src_offsets[idx[i]+1]) (elements of elem_bytes) is appended to dst;
 // dst_offsets[0..n] receives the running offsets. Throws if the result exceeds

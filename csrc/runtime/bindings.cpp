@@ -173,6 +173,20 @@ PYBIND11_MODULE(_ddl_runtime, m) {
       py::arg("n_threads") = 4,
       "dst[i*row_bytes:(i+1)*row_bytes] = src[idx[i]*row_bytes:...] on a host worker pool");
   m.def(
+      "copy_spans",
+      [](py::array_t<uint64_t, py::array::c_style> dst, py::array_t<uint64_t, py::array::c_style> src,
+         py::array_t<uint64_t, py::array::c_style> sizes, int n_threads) {
+        const py::ssize_t n = sizes.size();
+        if (dst.size() != n || src.size() != n) throw std::invalid_argument("copy_spans: length mismatch");
+        const auto* d = reinterpret_cast<const uintptr_t*>(dst.data());
+        const auto* s = reinterpret_cast<const uintptr_t*>(src.data());
+        const uint64_t* z = sizes.data();
+        py::gil_scoped_release nogil;
+        ddl::copy_spans(d, s, z, static_cast<uint64_t>(n), n_threads);
+      },
+      py::arg("dst"), py::arg("src"), py::arg("sizes"), py::arg("n_threads") = 4,
+      "memcpy(dst[i], src[i], sizes[i]) for every i on the host worker pool, without the GIL");
+  m.def(
       "feistel",
       [](std::vector<uint64_t> keys, uint32_t half_bits, uint64_t n, py::array_t<int64_t, py::array::c_style> pos) {
         if (keys.size() != ddl::kHostFeistelRounds) throw std::invalid_argument("feistel: need 6 round keys");

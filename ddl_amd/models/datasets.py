@@ -335,7 +335,6 @@ class MapDatasetSource:
         self.row_bytes = max(self.ALIGN, off)
         self.sample_shape = (self.row_bytes,)
         self.dtype = torch.uint8
-        self._pool = None
 
     # sample structure ---------------------------------------------------------------------------
     @staticmethod
@@ -379,40 +378,51 @@ class MapDatasetSource:
         return kind, fields
 
     # producer side --------------------------------------------------------------------------------
-    def __getstate__(self):
-        st = dict(self.__dict__)
-        st["_pool"] = None
-        return st
-
-    def _write(self, rows: np.ndarray, j: int, i: int) -> None:
+    def _spans(self, i: int, dst_row: int, spans: tuple[list, list, list, list]) -> None:
+        """Call ``ds[i]``, check it against sample 0, and append one (dst, src, bytes) copy span per field;
+        the source buffers are kept alive in ``spans[0]`` until the copies have run."""
+        keep, dsts, srcs, sizes = spans
         kind, items = self._items(self.dataset[i])
         if len(items) != len(self.fields):
             raise ValueError(f"MapDatasetSource: sample {i} has {len(items)} fields, sample 0 has {len(self.fields)}")
         for (key, v), (key0, shape, dt, off, nbytes) in zip(items, self.fields):
-            s, d, raw = self._leaf(v)
+            if isinstance(v, torch.Tensor):
+                t = v.detach()
+                if t.device.type != "cpu" or not t.is_contiguous():
+                    t = t.cpu().contiguous()
+                s, d, ptr, buf = tuple(t.shape), str(t.dtype).replace("torch.", ""), t.data_ptr(), t
+            else:
+                s, d, buf = self._leaf(v)
+                ptr = buf.ctypes.data
             if key != key0 or s != shape or d != dt:
                 raise ValueError(f"MapDatasetSource: sample {i} field {key!r} is {d}{list(s)}, "
                                  f"sample 0 has {dt}{list(shape)}")
-            rows[j, off:off + nbytes] = raw
+            keep.append(buf)
+            dsts.append(dst_row + off)
+            srcs.append(ptr)
+            sizes.append(nbytes)
 
     def gather(self, indices: np.ndarray, dst_address: int, n_threads: int = 4) -> None:
-        import ctypes
+        """Rows for ``indices`` into the pinned slot at ``dst_address``. ``ds[i]`` runs in this thread
+        (Python threads only contended for the GIL: 53 -> 68-79 us per 150 KB sample at 2-4 threads),
+        then every field's bytes move in one native ``copy_spans`` call on the runtime's ``n_threads``
+        worker pool without the GIL. Copying each field from Python instead (a torch / numpy copy per
+        field) cost 85 us per sample on the build host."""
+        from .. import _native
 
         idx = np.asarray(indices, dtype=np.int64)
         if len(idx) == 0:
             return
-        rows = np.ctypeslib.as_array((ctypes.c_uint8 * (len(idx) * self.row_bytes)).from_address(dst_address))
-        rows = rows.reshape(len(idx), self.row_bytes)
-        if n_threads <= 1 or len(idx) < 2 * n_threads:
-            for j, i in enumerate(idx):
-                self._write(rows, j, int(i))
-            return
-        if self._pool is None:
-            from concurrent.futures import ThreadPoolExecutor
-
-            self._pool = ThreadPoolExecutor(max_workers=n_threads, thread_name_prefix="ddl-dataset")
-        chunks = np.array_split(np.arange(len(idx)), n_threads)
-        list(self._pool.map(lambda js: [self._write(rows, int(j), int(idx[j])) for j in js], chunks))
+        ids = idx.tolist()
+        rb = self.row_bytes
+        parts = [([], [], [], [])]
+        for j, i in enumerate(ids):
+            self._spans(i, dst_address + j * rb, parts[0])
+        dsts = np.fromiter((d for p in parts for d in p[1]), dtype=np.uint64)
+        srcs = np.fromiter((x for p in parts for x in p[2]), dtype=np.uint64)
+        sizes = np.fromiter((z for p in parts for z in p[3]), dtype=np.uint64)
+        _native.runtime().copy_spans(dsts, srcs, sizes, max(1, n_threads))
+        del parts  # the source buffers may go now
 
 
 def _field_dtype(name: str) -> torch.dtype:

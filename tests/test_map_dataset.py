@@ -58,6 +58,32 @@ def test_layout_and_unpack_roundtrip():
     _check(unpack_fields(torch.from_numpy(rows), src.fields, src.kind), _expected(ds, [3, 1, 4, 1]))
 
 
+class ViewDataset(torch.utils.data.Dataset):
+    """Fields that are views: a row of a shared table (storage offset), a transposed (non-contiguous)
+    tensor and a strided numpy slice -- the native span copy must see their real bytes."""
+
+    def __init__(self, n):
+        self.n = n
+        self.table = torch.arange(n * 3 * 8 * 8, dtype=torch.int16).view(n, 3, 8, 8)
+        self.np_table = np.arange(n * 12, dtype=np.float32).reshape(n, 12)
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        return self.table[i], self.table[i].transpose(1, 2), self.np_table[i, ::2], i
+
+
+@pytest.mark.parametrize("n_threads", [1, 4])
+def test_views_and_threaded_span_copy(n_threads):
+    ds = ViewDataset(300)
+    src = MapDatasetSource(ds)
+    idx = np.random.default_rng(0).permutation(300)[:200]
+    rows = np.zeros((len(idx), src.row_bytes), dtype=np.uint8)
+    src.gather(idx, rows.ctypes.data, n_threads=n_threads)
+    _check(unpack_fields(torch.from_numpy(rows), src.fields, src.kind), _expected(ds, idx))
+
+
 def test_inconsistent_sample_is_rejected():
     class Bad(TupleDataset):
         def __getitem__(self, i):
