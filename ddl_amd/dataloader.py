@@ -139,6 +139,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
         pad_id: int = 0,
         native_dispatch: bool | str = True,
         token_rows: str = "exact",
+        verify_order: bool | None = None,
     ):
         if mode not in MODES:
             raise ValueError(f"unknown mode {mode!r}; one of {MODES}")
@@ -213,6 +214,8 @@ class DistributedDataLoader(DistributedDataloaderABC):
         self._stager = None
         self._batch_stream = None
         self._lookahead: dict = {}
+        self._verify = None  # verify_order's EpochOrder (_setup_verify)
+        self.verified_windows = 0
         self._win_done: dict = {}  # window -> event after its last batch kernel (Python dispatch path)
         self._host_window: int | None = None  # host path: window currently held
         self._cur = None                      # device path: StagedWindow of the current window
@@ -275,6 +278,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
             self.windows_per_epoch = P
         else:
             self.windows_per_epoch = 1
+        self._setup_verify(verify_order, md, env.rank if env else instance_idx, env.world_size if env else n_instances)
         self.sample_shape = self.shapes[0][1:]
         self.window_dtype = self.dtypes[0]
         # MapDatasetSource rows: batches come back in the dataset's sample structure (typed views)
@@ -498,6 +502,8 @@ class DistributedDataLoader(DistributedDataloaderABC):
         slot, prod, tags = eng.get(w, local, bpw, nxt, handle, self._timeout_ms)
         if slot < 0:
             self._engine_raise(slot, prod, f"batch {local} of window {w}")
+        if local == 0 and self._verify is not None:
+            self._verify_window(w, tags)
         if self._eng_window != w:
             self._eng_window = w
             self.metrics.windows += 1
@@ -559,6 +565,50 @@ class DistributedDataLoader(DistributedDataloaderABC):
                                           self.sample_shape, self.window_dtype, self.seed,
                                           device=self.device, shuffle=self.shuffle)
 
+    # ----------------------------------------------------------------- verification
+    def _setup_verify(self, verify_order: bool | None, md, rank, world) -> None:
+        """``verify_order`` (default ``$DDL_VERIFY_ORDER=1``): check every window of the indexed order
+        against the epoch order before its batches are used. ``IndexedProducer`` publishes (epoch,
+        global batch, digest of the sample ids) in the slot tags of each window; the consumer recomputes
+        them from its own cursor and ``EpochOrder``, so a producer/consumer cursor disagreement, a stale
+        or reused slot, or a wrong resume position raises ``DataIntegrityError`` instead of silently
+        training on the wrong samples (race detection). Costs one host-side Feistel
+        evaluation of the local batch and a hash per window."""
+        import os
+
+        self._verify = None
+        self.verified_windows = 0
+        want = verify_order if verify_order is not None else os.environ.get("DDL_VERIFY_ORDER") == "1"
+        if not want:
+            return
+        ex = md[0].extra if md else {}
+        ok = (self.mode == "indexed" and self.collate is None and "order_seed" in ex
+              and "windows_per_epoch" not in ex)  # one global batch per window (IndexedProducer)
+        if not ok:
+            if verify_order:
+                raise ValueError("verify_order needs mode='indexed' windows from IndexedProducer")
+            return
+        from .permutation import EpochOrder
+
+        self._verify = EpochOrder(int(ex["n_samples"]), int(ex["global_batch"]), int(ex["order_seed"]),
+                                  bool(ex.get("order_drop_last", True)), bool(ex.get("order_shuffle", True)))
+        self._verify_rank = (int(rank or 0), int(world or 1))
+
+    def _verify_window(self, w: int, tags) -> None:
+        from .exceptions import DataIntegrityError
+        from .permutation import ids_digest
+
+        epoch, g = divmod(int(w), self.windows_per_epoch)
+        ids = self._verify.indices(epoch, g, *self._verify_rank)
+        want = (epoch, g, ids_digest(ids))
+        got = tuple(int(x) for x in tuple(tags)[:3])
+        if got != want:
+            raise DataIntegrityError(
+                f"window {w}: the epoch order expects (epoch {epoch}, global batch {g}, ids digest {want[2]:#x}); "
+                f"the producer published (epoch {got[0] if got else None}, global batch "
+                f"{got[1] if len(got) > 1 else None}, ids digest {got[2] if len(got) > 2 else 0:#x})")
+        self.verified_windows += 1
+
     # ----------------------------------------------------------------- access
     def _window(self):
         """Make the current window available (device: staged; host: acquired)."""
@@ -577,6 +627,8 @@ class DistributedDataLoader(DistributedDataloaderABC):
                     self._cur = self._stager.get(self.window)
                 self.metrics.consumer_wait_s += time.perf_counter() - t0
                 self.metrics.windows += 1
+                if self._verify is not None:
+                    self._verify_window(self.window, self._cur.tags)
             return self._cur
         if self._host_window != self.window:
             p, s = self._schedule(self.window)
@@ -590,6 +642,8 @@ class DistributedDataLoader(DistributedDataloaderABC):
             self._host_window = self.window
             self._host_seq = int(info["seq"])
             self._host_tags = tuple(info["tag"])
+            if self._verify is not None:
+                self._verify_window(self.window, self._host_tags)
             if self.collate == "tokens":  # per-sub-batch sizes live at the head of the window
                 _, t = self.arys[p][s]
                 nb = int(self.metadata_from_producer[p].extra.get("meta_bytes", 0))
@@ -1135,6 +1189,8 @@ class DistributedDataLoader(DistributedDataloaderABC):
             d.update(self._stager.stats())
         if self.connection is not None:
             d["producers"] = self.connection.producer_stats()
+        if getattr(self, "_verify", None) is not None:
+            d["verified_windows"] = self.verified_windows
         return d
 
     def __del__(self):  # pragma: no cover - best effort

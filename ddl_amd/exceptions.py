@@ -49,6 +49,11 @@ class PeerDeathError(DDLError):
         super().__init__(message)
 
 
+class DataIntegrityError(DDLError):
+    """A delivered window is not the one the epoch order says comes next (``verify_order``): a
+    producer/consumer cursor disagreement, a stale or reused slot, or a bad resume."""
+
+
 class ShutdownError(DDLError):
     """The loader was shut down while an operation was waiting."""
 

@@ -26,7 +26,7 @@ from .. import ops
 from ..datapusher import DataProducerOnInitReturn
 from ..datasetwrapper import ProducerFunctionSkeleton
 from ..ops import _dtypes
-from ..permutation import EpochOrder
+from ..permutation import EpochOrder, ids_digest
 from .datasets import DummyDataset, synthetic_images
 
 
@@ -144,6 +144,7 @@ class IndexedProducer(ProducerFunctionSkeleton):
                                         extra={"batches_per_epoch": self.order.batches_per_epoch,
                                                "global_batch": self.global_batch, "n_samples": self.source.n,
                                                "order_seed": int(self.seed), "order_shuffle": self.shuffle,
+                                               "order_drop_last": self.drop_last,
                                                # MapDatasetSource: the loader rebuilds the sample structure
                                                "fields": getattr(self.source, "fields", None),
                                                "fields_kind": getattr(self.source, "kind", None)})
@@ -151,14 +152,21 @@ class IndexedProducer(ProducerFunctionSkeleton):
     def post_init(self, *args, **kwargs):
         super().post_init(*args, **kwargs)
 
-    def batch_indices(self, rnd: int) -> np.ndarray:
+    def batch_position(self, rnd: int) -> tuple[int, int]:
+        """(epoch, global batch) this producer delivers in round ``rnd``."""
         assert self.order is not None
         g_total = rnd * (self.n_producers or 1) + (self.producer_index or 0)
-        epoch, g = divmod(g_total, self.order.batches_per_epoch)
+        return divmod(g_total, self.order.batches_per_epoch)
+
+    def batch_indices(self, rnd: int) -> np.ndarray:
+        epoch, g = self.batch_position(rnd)
         return self.order.indices(epoch, g, self.rank_global or 0, self.world_size)
 
     def execute_function(self, *args, **kwargs):
         rnd = int(kwargs.get("round", 0))
         t: torch.Tensor = kwargs.get("my_tensor", self.my_tensor)
-        idx = self.batch_indices(rnd)
+        epoch, g = self.batch_position(rnd)
+        idx = self.order.indices(epoch, g, self.rank_global or 0, self.world_size)
         self.source.gather(idx, t.data_ptr(), self.host_threads)
+        # slot tags: which batch this window is, and a digest of its sample ids (verify_order)
+        return {"tags": [epoch, g, ids_digest(idx)]}

@@ -193,6 +193,15 @@ class EpochOrder:
         return self.perm(epoch)(self.positions(g, rank, world_size))
 
 
+def ids_digest(indices) -> int:
+    """64-bit digest (signed, to fit a slot tag) of an ordered list of sample indices: producers of the
+    indexed order publish it with every window; ``verify_order`` recomputes it on the consumer."""
+    import hashlib
+
+    raw = np.ascontiguousarray(np.asarray(indices, dtype=np.int64)).tobytes()
+    return int.from_bytes(hashlib.blake2b(raw, digest_size=8).digest(), "little", signed=True)
+
+
 def batch_cursor(sd: dict, global_batch) -> int:
     """The global-batch cursor of an indexed checkpoint: ``global_batch_cursor``, or derived from
     ``global_sample_cursor`` (epoch/sample-index checkpoints) when only that is given."""
