@@ -55,6 +55,8 @@ def main(argv=None) -> int:
     ap.add_argument("--n-samples", type=int, default=65536)
     ap.add_argument("--steps", type=int, default=150)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--host-threads", type=int, default=2,
+                    help="ddl: copy threads per producer for the packed-row span copies")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
 
@@ -62,7 +64,8 @@ def main(argv=None) -> int:
     if a.impl == "ddl":
         import ddl_amd
 
-        loader = ddl_amd.DataLoader(ds, batch_size=a.batch, shuffle=True, num_workers=a.workers, seed=0)
+        loader = ddl_amd.DataLoader(ds, batch_size=a.batch, shuffle=True, num_workers=a.workers, seed=0,
+                                    host_threads=a.host_threads)
         dev = torch.device(loader.env.device)
     else:
         loader = torch.utils.data.DataLoader(ds, batch_size=a.batch, shuffle=True, num_workers=a.workers,
@@ -101,7 +104,7 @@ def main(argv=None) -> int:
     assert label.shape == (a.batch,) and label.device == dev
     out = {"metric": "samples/s, map-style Dataset -> device batches (uint8 3x224x224 + label)",
            "impl": "ddl_amd.DataLoader" if a.impl == "ddl" else "torch.utils.data.DataLoader(pin_memory=True)",
-           "workers": a.workers, "batch": a.batch, "steps": a.steps, "warmup": a.warmup,
+           "workers": a.workers, "host_threads": a.host_threads if a.impl == "ddl" else None, "batch": a.batch, "steps": a.steps, "warmup": a.warmup,
            "samples_per_s": round(a.batch * a.steps / dt, 1), "ms_per_batch": round(1000 * dt / a.steps, 3),
            "h2d_gbps": round(a.batch * a.steps * 3 * 224 * 224 / dt / 1e9, 2), "device": str(dev)}
     line = json.dumps(out)
