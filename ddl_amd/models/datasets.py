@@ -397,6 +397,8 @@ class MapDatasetSource:
             if key != key0 or s != shape or d != dt:
                 raise ValueError(f"MapDatasetSource: sample {i} field {key!r} is {d}{list(s)}, "
                                  f"sample 0 has {dt}{list(shape)}")
+            if nbytes == 0:  # empty field: nothing to copy (its data pointer may be null)
+                continue
             keep.append(buf)
             dsts.append(dst_row + off)
             srcs.append(ptr)
