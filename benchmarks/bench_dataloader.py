@@ -5,7 +5,8 @@ Both loaders get the same ``Dataset`` object: ImageNet-shape uint8 images [3, 22
 label. ``__getitem__`` returns a view of a small pre-built image table, so the dataset costs almost
 nothing, and the numbers measure the loaders. The consumer is the same for both: the batch lands on the
 GPU, is made contiguous there if it is a strided view, and a checksum kernel reads every image byte. The timed region is K batches after W warmup
-batches, closed by a device synchronize.
+batches, closed by a device synchronize. Then (``--idle-steps``)
+the GPU idle % behind bench.py's PatchMLP train step fed by the same loader.
 
 * ``torch``: ``DataLoader(num_workers=P, pin_memory=True, persistent_workers=True, shuffle=True)``,
   then ``.to(device, non_blocking=True)``. Workers use the spawn start method; collate runs in the
@@ -57,6 +58,8 @@ def main(argv=None) -> int:
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--host-threads", type=int, default=2,
                     help="ddl: copy threads per producer for the packed-row span copies")
+    ap.add_argument("--idle-steps", type=int, default=100,
+                    help="then GPU idle %% behind the bench.py PatchMLP bf16 train step fed by this loader (0: skip)")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
 
@@ -107,6 +110,30 @@ def main(argv=None) -> int:
            "workers": a.workers, "host_threads": a.host_threads if a.impl == "ddl" else None, "batch": a.batch, "steps": a.steps, "warmup": a.warmup,
            "samples_per_s": round(a.batch * a.steps / dt, 1), "ms_per_batch": round(1000 * dt / a.steps, 3),
            "h2d_gbps": round(a.batch * a.steps * 3 * 224 * 224 / dt / 1e9, 2), "device": str(dev)}
+    if a.idle_steps and dev.type == "cuda":
+        from ddl_amd.models.trainstep import TrainStep
+        from ddl_amd.utils.tracing import ComputeIdleMeter
+
+        step = TrainStep(dev, dim=384, depth=4)
+
+        def prep(x):  # uint8 -> bf16 in [0, 1] on the device (the model's input)
+            return x.to(torch.bfloat16).mul_(1.0 / 255)
+
+        for _ in range(5):
+            step(prep(next(it)[0]))
+        meter = ComputeIdleMeter()
+        torch.cuda.synchronize(dev)
+        t2 = time.perf_counter()
+        for _ in range(a.idle_steps):
+            img, _ = next(it)
+            meter.step_begin()
+            step(prep(img))
+            meter.step_end()
+        torch.cuda.synchronize(dev)
+        res = meter.result()
+        out["gpu_idle_pct"] = round(res["gpu_idle_pct"], 2)
+        out["train_step"] = {"model": "PatchMLP dim=384 depth=4 fwd+bwd+SGD bf16 (bench.py phase 2)",
+                             "samples_per_s": round(a.batch * a.idle_steps / (time.perf_counter() - t2), 1)}
     line = json.dumps(out)
     print(line, flush=True)
     if a.json_out:
