@@ -10,6 +10,9 @@
   name. Producers gather samples out of it with the native multi-threaded
   gather (``_ddl_runtime.gather_rows``).
 * ``NpyMemmapSource``: an ``.npy`` file mapped read-only (page cache shared).
+* ``MapDatasetSource``: any map-style ``torch.utils.data.Dataset`` (the ``ddl_amd.DataLoader``
+  drop-in); producers call ``ds[i]`` and pack each sample's fields into one byte row with a single
+  native ``copy_spans`` call per batch (GIL released).
 """
 
 from __future__ import annotations
