@@ -53,7 +53,8 @@ def _cpu_view(source, n: int, shape, dtype) -> torch.Tensor:
 class ZeroCopyLoader(PrefetchedIndexedLoader):
     def __init__(self, source, global_batch: int, env: DDLEnv | None = None, *, seed: int = 0,
                  drop_last: bool = True, out_dtype: Any = None, normalize: dict | None = None, depth: int = 2,
-                 max_blocks: int = 64, device: str | torch.device | None = None, n_epochs: int | None = None,
+                 max_blocks: int | None = None, device: str | torch.device | None = None,
+                 n_epochs: int | None = None,
                  resume_state: dict | None = None):
         self.env = env or DDLEnv()
         self.W, self.rank = self.env.world_size, self.env.rank
@@ -65,6 +66,13 @@ class ZeroCopyLoader(PrefetchedIndexedLoader):
         self.GB, self.LB = int(global_batch), self.order.local_batch(self.W)
         self.out_dtype = _dtypes.to_torch_dtype(out_dtype) if out_dtype is not None else self.src_dtype
         self.normalize = normalize
+        if max_blocks is None:
+            # measured grid caps (profiles/r1_zerocopy, profiles/r2_misc): a same-width copy is PCIe-bound
+            # and peaks at 32 workgroups (bf16: 188k vs 182k samples/s at 64); a widening uint8 -> bf16
+            # gather writes twice the bytes it reads and keeps improving up to the full grid
+            src_bytes = torch.empty((), dtype=self.src_dtype).element_size()
+            out_bytes = torch.empty((), dtype=self.out_dtype).element_size()
+            max_blocks = 32 if out_bytes <= src_bytes else 0
         self.max_blocks = int(max_blocks)
         if device is None:
             device = self.env.device or ("cuda" if torch.cuda.is_available() else "cpu")
