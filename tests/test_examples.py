@@ -134,3 +134,18 @@ def test_usage_examples(script, args, ranks):
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=dict(_env(), DDL_DEVICE="cpu"))
     assert r.returncode == 0, r.stderr[-3000:]
     assert "epoch 0:" in r.stdout
+
+
+@pytest.mark.timeout(200)
+@pytest.mark.parametrize("impl", ["ddl", "torch"])
+def test_bench_dataloader_cpu(impl):
+    """benchmarks/bench_dataloader.py (the drop-in comparison) runs on CPU and prints one JSON line."""
+    import json
+
+    cmd = [sys.executable, os.path.join(REPO, "benchmarks", "bench_dataloader.py"), "--impl", impl,
+           "--workers", "2", "--batch", "32", "--n-samples", "1024", "--steps", "4", "--warmup", "1",
+           "--idle-steps", "0"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=180, env=dict(_env(), DDL_DEVICE="cpu"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert out["samples_per_s"] > 0 and out["batch"] == 32 and out["workers"] == 2
