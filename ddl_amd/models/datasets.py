@@ -338,6 +338,7 @@ class MapDatasetSource:
         self.row_bytes = max(self.ALIGN, off)
         self.sample_shape = (self.row_bytes,)
         self.dtype = torch.uint8
+        self._torch_dtypes = None
 
     # sample structure ---------------------------------------------------------------------------
     @staticmethod
@@ -388,18 +389,25 @@ class MapDatasetSource:
         kind, items = self._items(self.dataset[i])
         if len(items) != len(self.fields):
             raise ValueError(f"MapDatasetSource: sample {i} has {len(items)} fields, sample 0 has {len(self.fields)}")
-        for (key, v), (key0, shape, dt, off, nbytes) in zip(items, self.fields):
-            if isinstance(v, torch.Tensor):
-                t = v.detach()
-                if t.device.type != "cpu" or not t.is_contiguous():
-                    t = t.cpu().contiguous()
-                s, d, ptr, buf = tuple(t.shape), str(t.dtype).replace("torch.", ""), t.data_ptr(), t
+        tdts = self._torch_dtypes
+        if tdts is None:  # per-field torch dtypes (None: not a torch dtype name), for the fast tensor check
+            tdts = self._torch_dtypes = [getattr(torch, dt, None) for _, _, dt, _, _ in self.fields]
+        for (key, v), (key0, shape, dt, off, nbytes), tdt in zip(items, self.fields, tdts):
+            if type(v) is torch.Tensor and v.dtype is tdt and key == key0 and v.shape == shape \
+                    and v.device.type == "cpu" and v.is_contiguous():
+                buf, ptr = v, v.data_ptr()  # the common case: a contiguous CPU tensor, checked without strings
             else:
-                s, d, buf = self._leaf(v)
-                ptr = buf.ctypes.data
-            if key != key0 or s != shape or d != dt:
-                raise ValueError(f"MapDatasetSource: sample {i} field {key!r} is {d}{list(s)}, "
-                                 f"sample 0 has {dt}{list(shape)}")
+                if isinstance(v, torch.Tensor):
+                    t = v.detach()
+                    if t.device.type != "cpu" or not t.is_contiguous():
+                        t = t.cpu().contiguous()
+                    s_, d, ptr, buf = tuple(t.shape), str(t.dtype).replace("torch.", ""), t.data_ptr(), t
+                else:
+                    s_, d, buf = self._leaf(v)
+                    ptr = buf.ctypes.data
+                if key != key0 or s_ != shape or d != dt:
+                    raise ValueError(f"MapDatasetSource: sample {i} field {key!r} is {d}{list(s_)}, "
+                                     f"sample 0 has {dt}{list(shape)}")
             if nbytes == 0:  # empty field: nothing to copy (its data pointer may be null)
                 continue
             keep.append(buf)
