@@ -65,6 +65,11 @@ def parse(argv=None):
     ap.add_argument("--slots", type=int, default=1, help="windows per producer")
     ap.add_argument("--depth", type=int, default=2, help="HBM prefetch depth (windows)")
     ap.add_argument("--source-dtype", default="bfloat16", choices=["bfloat16", "uint8", "float32"])
+    ap.add_argument("--refill", default="stamp", choices=["stamp", "full"],
+                    help="producer work per round: stamp = one element per sample; full = rewrite every byte of "
+                         "the window (a row permutation of the pristine window, as the reference's producers "
+                         "shuffle theirs every round) with --producer-threads native host threads each")
+    ap.add_argument("--producer-threads", type=int, default=4)
     ap.add_argument("--shuffle", default="device", choices=["device", "none"])
     ap.add_argument("--exchange", type=float, default=None,
                     help="global-shuffle fraction per window over RCCL (default 0.5 when N>1, as the reference "
@@ -284,7 +289,8 @@ def main(argv=None) -> int:
 
     with ddl_amd.start(n_producers=args.producers) as (env, conn):
         dev = torch.device(env.device)
-        producer = ImageWindowProducer(args.window, shape, args.source_dtype, seed=args.seed, refill="stamp")
+        producer = ImageWindowProducer(args.window, shape, args.source_dtype, seed=args.seed, refill=args.refill,
+                                       host_threads=args.producer_threads)
         norm = None
         if args.source_dtype == "uint8":
             norm = {"mean": [0.485, 0.456, 0.406], "std": [0.229, 0.224, 0.225], "layout": "chw"}
@@ -321,6 +327,8 @@ def main(argv=None) -> int:
         w_land0, b_land0 = _landed(dl)
         w_cur0 = dl.window
         bytes_enq0 = dl._stager.bytes_h2d if dl._stager is not None else 0
+        prod0 = conn.producer_stats()
+        wait_prod0 = dl.stats().get("stager_wait_producer_s", 0.0)
         t0 = time.perf_counter()
         host_log = os.environ.get("DDL_HOST_LOG")
         ticks = []
@@ -334,6 +342,7 @@ def main(argv=None) -> int:
         t1 = time.perf_counter()
         w_land1, b_land1 = _landed(dl)
         bytes_enq1 = dl._stager.bytes_h2d if dl._stager is not None else 0
+        prod1 = conn.producer_stats()
         barrier()
         elapsed = t1 - t0
         landed_samples = (w_land1 - w_land0) * args.window
@@ -355,6 +364,22 @@ def main(argv=None) -> int:
         if os.environ.get("DDL_STAGER_LOG") and dl._stager is not None:  # per-window producer waits (debug)
             mine["stager_step_log_us"] = [[e[0]] + [round(x / 1e3, 1) for x in e[1:6]]
                                           for e in dl._stager._native.wait_log if max(e[1:6]) > 500_000]
+        # producer side of the timed region: rounds filled, fill rate while filling, busy fraction
+        win_bytes = args.window * sample_bytes
+        rounds = [b["rounds"] - a["rounds"] for a, b in zip(prod0, prod1)]
+        fill_s = [(b["fill_ns_total"] - a["fill_ns_total"]) * 1e-9 for a, b in zip(prod0, prod1)]
+        mine["producers"] = {
+            "refill": args.refill,
+            "rounds_timed": sum(rounds),
+            "fill_gbps_per_producer": [round(r * win_bytes / s / 1e9, 2) if s > 0 else None
+                                       for r, s in zip(rounds, fill_s)],
+            "fill_busy_pct": [round(100.0 * s / elapsed, 1) for s in fill_s],
+            "filled_gbps_total": round(sum(rounds) * win_bytes / elapsed / 1e9, 2),
+        }
+        mine["stager_wait_producer_s_timed"] = round(stats.get("stager_wait_producer_s", 0.0) - wait_prod0, 4)
+        nd = stats.get("native_dispatch")
+        mine["dispatch"] = {"mode": nd.get("mode"), "host_us_per_batch": nd.get("host_us_per_batch"),
+                            "compute_waits": nd.get("compute_waits")} if nd else {"mode": "python"}
         mine["stager_wait_producer_s"] = round(stats.get("stager_wait_producer_s", 0.0), 4)
         mine["exchange_issue_wait_s"] = stats.get("exchange_issue_wait_s", 0.0)
         mine["consumer_wait_s"] = round(stats["consumer_wait_s"], 4)
@@ -409,7 +434,7 @@ def main(argv=None) -> int:
                 "scaling": "weak",
                 "vs_baseline": round(value / (REF_SAMPLES_PER_S_PER_GPU * env.world_size), 3),
                 "dtype": "bf16",
-                "data": f"synthetic (random {args.source_dtype} images, refreshed every producer round)",
+                "data": f"synthetic (random {args.source_dtype} images, refreshed every producer round: {args.refill})",
                 "config": {
                     "model": "ddl_amd loader: ImageNet-shape 3x224x224 bf16, pinned H2D prefetch stream",
                     "global_batch": args.batch * env.world_size,
@@ -422,6 +447,8 @@ def main(argv=None) -> int:
                     "exchange_fraction": args.exchange,
                     "exchange_method": args.exchange_method if args.exchange > 0 else None,
                     "source_dtype": args.source_dtype,
+                    "producer_refill": args.refill,
+                    "dispatch": per_rank[0].get("dispatch", {}).get("mode"),
                 },
                 "delivered_samples_per_s": round(delivered, 1),
                 "landed_samples_per_s": round(landed, 1),

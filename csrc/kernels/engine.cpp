@@ -1,6 +1,7 @@
 // See engine.h.
 #include "engine.h"
 
+#include <algorithm>
 #include <chrono>
 
 #include "launch.h"
@@ -83,6 +84,7 @@ BatchEngine::~BatchEngine() {
   for (auto e : batch_events_) hipEventDestroy(e);
   for (auto& v : free_events_)
     for (auto e : v) hipEventDestroy(e);
+  for (auto e : join_events_) hipEventDestroy(e);
   hipEventDestroy(ww_ev_);
 }
 
@@ -124,6 +126,10 @@ int BatchEngine::enqueue(int64_t w, int64_t local, const StagedInfo& info, Pendi
   const int64_t slot = free_slots_.front();
   free_slots_.pop_front();
   if (launch(w, local, 1, info, slot, st) != 0) return -1;
+  if (on_caller) {  // every stream that read the window: its free event must follow all of them
+    auto& v = read_streams_[w];
+    if (std::find(v.begin(), v.end(), st) == v.end()) v.push_back(st);
+  }
   const uint64_t t2 = clock_ns();
   if (on_caller) {  // stream order is the dependency: no event
     *out = Pending{w, local, slot, -1};
@@ -362,6 +368,17 @@ int BatchEngine::release(int64_t w) {
   if (de != done_event_.end()) {
     ev = de->second;  // right after w's last batch kernel, not behind the next window's lookahead
   } else {
+    auto rs = read_streams_.find(w);
+    if (rs != read_streams_.end()) {
+      // inline batches of w were launched on several streams: `st` (the last one) waits for the others,
+      // so the free event recorded on it follows every read of the window
+      for (hipStream_t o : rs->second) {
+        if (o == st) continue;
+        hipEvent_t xe = join_event();
+        if (xe == nullptr || hipEventRecord(xe, o) != hipSuccess || hipStreamWaitEvent(st, xe, 0) != hipSuccess)
+          return -1;
+      }
+    }
     if ((ready_waited_ != w || ready_stream_ != st) && hipStreamWaitEvent(st, ready_[b], 0) != hipSuccess)
       return -1;
     ev = free_events_[b][free_next_[b]];
@@ -372,11 +389,27 @@ int BatchEngine::release(int64_t w) {
   stager_->release(w, ev);
   windows_.erase(it);
   keys_.erase(w);
+  read_streams_.erase(read_streams_.begin(), read_streams_.upper_bound(w));
   while (!pending_.empty() && pending_.front().w <= w) pending_.pop_front();
   return 0;
 }
 
+hipEvent_t BatchEngine::join_event() {
+  // a small ring: an event is re-recorded only kJoinEvents joins later, long after its wait was enqueued
+  // (hipStreamWaitEvent captures the event's state at enqueue time)
+  if (join_events_.size() < kJoinEvents) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    join_events_.push_back(e);
+    return e;
+  }
+  hipEvent_t e = join_events_[join_next_];
+  join_next_ = (join_next_ + 1) % kJoinEvents;
+  return e;
+}
+
 void BatchEngine::reset() {
+  read_streams_.clear();
   done_event_.clear();
   ww_w_ = -1;
   ww_slot0_ = -1;

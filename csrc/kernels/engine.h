@@ -172,6 +172,12 @@ class BatchEngine {
   hipEvent_t ww_ev_ = nullptr;         // orders a later batch of that window on another stream
   hipStream_t last_compute_ = nullptr;  // inline mode: where the window's reads were enqueued (0 = null stream)
   bool have_compute_ = false;
+  // inline mode: every stream a window's batches were launched on (release() joins them before the free event)
+  std::map<int64_t, std::vector<hipStream_t>> read_streams_;
+  static constexpr size_t kJoinEvents = 8;
+  std::vector<hipEvent_t> join_events_;
+  size_t join_next_ = 0;
+  hipEvent_t join_event();
 };
 
 // Host derivation of the Feistel round keys of (seed, key) -- ddl_amd/permutation.py round_keys --

@@ -312,9 +312,11 @@ class DistributedDataLoader(DistributedDataloaderABC):
     # ------------------------------------------------------ native dispatch
     def _engine_recipe(self) -> dict | None:
         """The batch recipe when the native engine can build batches exactly like ``_batch_from_window``:
-        a fused gather (one output) or a contiguous column split, no exchange / collate / augment."""
-        if (not self.native_dispatch or self._exchange_fn is not None or self.augment is not None
-                or self._batch_stream is None):
+        a fused gather (one output), a contiguous column split or a token pad/pack; no HWC collate or
+        augment. The global-shuffle exchange is compatible: it rewrites the staged window in place on the
+        post-copy stream before the window's ready event, which is what the engine's launches wait on
+        (``_ensure_posted`` issues it before the engine touches the window)."""
+        if not self.native_dispatch or self.augment is not None or self._batch_stream is None:
             return None
         if self.collate == "tokens":
             return self._token_recipe()
@@ -499,6 +501,12 @@ class DistributedDataLoader(DistributedDataloaderABC):
         cur, handle = hit
         w = self.window
         nxt = self.window_in_epoch + 1 < self.windows_per_epoch or self.epoch + 1 < self.n_epochs
+        if self._exchange_fn is not None:
+            posted = self._stager._posted
+            if w not in posted or (w + 1) not in posted:
+                self._ensure_posted(w)
+            # the engine's cross-window lookahead reads w + 1: only once its exchange is issued
+            nxt = nxt and (w + 1) in posted
         slot, prod, tags = eng.get(w, local, bpw, nxt, handle, self._timeout_ms)
         if slot < 0:
             self._engine_raise(slot, prod, f"batch {local} of window {w}")
@@ -610,9 +618,21 @@ class DistributedDataLoader(DistributedDataloaderABC):
         self.verified_windows += 1
 
     # ----------------------------------------------------------------- access
+    def _ensure_posted(self, w: int) -> None:
+        """Issue the exchange collectives of windows ``w`` and ``w + 1`` (in order; no-ops when already
+        issued). Called when the cursor enters window ``w`` -- a fixed point of the batch schedule, so
+        every rank issues the same collectives in the same order (parallel/order.py) -- one window
+        ahead, so window ``w + 1``'s exchange overlaps the consumption of ``w`` and the lookahead can
+        build ``w + 1``'s first batch before the consumer gets there."""
+        st = self._stager
+        st.post(w)
+        st.post(w + 1)
+
     def _window(self):
         """Make the current window available (device: staged; host: acquired)."""
         if self._engine is not None:
+            if self._exchange_fn is not None:
+                self._ensure_posted(self.window)
             if self._eng_window != self.window:
                 rc, prod = self._engine.acquire(self.window, self._timeout_ms)
                 if rc != 0:
@@ -623,6 +643,8 @@ class DistributedDataLoader(DistributedDataloaderABC):
         if self._stager is not None:
             if self._cur is None or self._cur.index != self.window:
                 t0 = time.perf_counter()
+                if self._exchange_fn is not None:
+                    self._ensure_posted(self.window)
                 with trace_range("ddl.consumer.wait_window"):
                     self._cur = self._stager.get(self.window)
                 self.metrics.consumer_wait_s += time.perf_counter() - t0
@@ -893,8 +915,8 @@ class DistributedDataLoader(DistributedDataloaderABC):
         st = self._stager
         if st is None or st.post_copy is None or self._finalized:
             return
-        st.post(self.window)
-        if self._batch_stream is not None and (self.window, 0) not in self._lookahead:
+        self._ensure_posted(self.window)
+        if self._engine is None and self._batch_stream is not None and (self.window, 0) not in self._lookahead:
             sw = st.peek(self.window)
             if sw is not None:
                 p, s = self._schedule(self.window)
@@ -1127,7 +1149,8 @@ class DistributedDataLoader(DistributedDataloaderABC):
                 self.connection.remove_finalizer(old.close)
                 self._stager = WindowStager(self.connection, self.n_slots, self.total_windows, self.prefetch_depth,
                                             self.device, old.max_window_bytes, post_copy=self._exchange_fn,
-                                            timeout_s=self.timeout_s, first_window=self.window)
+                                            timeout_s=self.timeout_s, first_window=self.window,
+                                            meta_bytes=old.meta_bytes)
                 self.connection.add_finalizer(self._stager.close)
                 self.metrics.bytes_h2d += old.bytes_h2d
                 del old

@@ -36,6 +36,12 @@ class ShapeMismatchError(DoesNotMatchError):
     """Producer metadata disagree (shape, splits, dtype, batches per window)."""
 
 
+class CommunicatorMismatchError(DoesNotMatchError):
+    """A loader collective was about to be issued on a process group other than the DP group
+    (``env.process_group``): it would run on another communicator / stream than DDP's and could
+    deadlock against it across ranks (``parallel/order.py``)."""
+
+
 class DDLTimeoutError(DDLError, TimeoutError):
     """A bounded wait expired (producer never published / consumer never released)."""
 

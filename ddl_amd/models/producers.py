@@ -79,16 +79,29 @@ class PointwiseProducer(ProducerFunctionSkeleton):
 
 
 class ImageWindowProducer(ProducerFunctionSkeleton):
+    """Synthetic image windows. ``refill`` -- what a producer round does to its slot:
+
+    * ``"stamp"``: writes the round into one element per sample (cheap, distinct windows);
+    * ``"full"``: rewrites EVERY byte, as the reference's producers do (``rng.shuffle`` of the whole
+      window every round, reference tests/run_ddl.py:163-167): the window is the pristine round-0
+      content permuted by the RNG of (seed, rank, producer, round), gathered row by row with the native
+      host pool (``host_threads`` threads) -- a function of the round, so resume stays exact;
+    * ``"regenerate"``: draws fresh random images (slow: torch RNG on one thread);
+    * ``"none"``: leaves the slot as it is.
+    """
+
     def __init__(self, n_samples: int, shape=(3, 224, 224), dtype: Any = "bfloat16", seed: int = 0,
-                 refill: str = "stamp"):
+                 refill: str = "stamp", host_threads: int = 4):
         super().__init__()
-        if refill not in ("stamp", "none", "regenerate"):
-            raise ValueError("refill must be 'stamp', 'none' or 'regenerate'")
+        if refill not in ("stamp", "none", "regenerate", "full"):
+            raise ValueError("refill must be 'stamp', 'full', 'none' or 'regenerate'")
         self.n_samples = int(n_samples)
         self.shape = tuple(shape)
         self.dtype = dtype
         self.seed = seed
         self.refill = refill
+        self.host_threads = int(host_threads)
+        self._base: torch.Tensor | None = None
 
     def on_init(self, *args, **kwargs):
         super().on_init(*args, **kwargs)
@@ -106,6 +119,8 @@ class ImageWindowProducer(ProducerFunctionSkeleton):
     def post_init(self, *args, **kwargs):
         super().post_init(*args, **kwargs)
         self._fill(self.my_tensor, 0)
+        if self.refill == "full":
+            self._base = self.my_tensor.clone()
 
     def execute_function(self, *args, **kwargs):
         rnd = int(kwargs.get("round", 0))
@@ -113,6 +128,14 @@ class ImageWindowProducer(ProducerFunctionSkeleton):
         if self.refill == "stamp":
             flat = t.view(self.n_samples, -1)
             flat[:, 0] = float(rnd % 251) if t.dtype != torch.uint8 else rnd % 251
+        elif self.refill == "full":
+            from .. import _native
+
+            rng = np.random.default_rng([self.seed, self.rank_global or 0, self.producer_index or 0, rnd])
+            base = self._base
+            _native.runtime().gather_rows(t.data_ptr(), base.data_ptr(), base[0].numel() * base.element_size(),
+                                          rng.permutation(self.n_samples).astype(np.int64), self.n_samples,
+                                          self.host_threads)
         elif self.refill == "regenerate":
             self._fill(t, rnd)
 

@@ -341,6 +341,16 @@ def _cached_views(buf: torch.Tensor, layout: TokenWindowLayout, sub: int = 0) ->
     return v
 
 
+def drop_cached_views(base_ptrs) -> int:
+    """Forget the cached views of buffers starting at ``base_ptrs`` (a staging ring being dropped: a
+    live seek or close), so the cache does not keep the old ring's HBM alive. Returns entries dropped."""
+    ptrs = set(int(p) for p in base_ptrs)
+    dead = [k for k in _VIEW_CACHE if k[0] in ptrs]
+    for k in dead:
+        del _VIEW_CACHE[k]
+    return len(dead)
+
+
 def collate_token_window(buf: torch.Tensor, layout: TokenWindowLayout, mode: str, meta, pad_id: int = 0,
                          sub: int = 0, fixed_rows: bool = False):
     """Expand sub-batch ``sub`` of one (device or host) token window into model inputs; ``meta`` is the

@@ -20,14 +20,22 @@ The invariant used here removes that hazard by construction:
    DDP. ProcessGroupNCCL runs every collective of a group (and batched P2P)
    on one ncclComm and one internal stream per device, so their device-side
    order is their issue order.
-2. **One issuing thread in program order.** Every loader collective is issued
-   by the consumer thread at a fixed point of the batch schedule (window
-   ``w+1``'s exchange when window ``w`` is handed back at its last
-   ``END_OF_BATCH``, ``dataloader._begin_window`` / ``staging.post``), never by
-   the native stager thread, whose progress depends on producer timing. DDP's
-   bucket all-reduces are launched while the same thread is blocked in
-   ``backward()``, in bucket order. So the issue order is a function of the
-   step/window schedule only, and it is identical on every rank.
+2. **One issue order, a function of the schedule only.** Every loader
+   collective is issued by the consumer thread at a fixed point of the batch
+   schedule (window ``w+1``'s exchange when the cursor enters window ``w``,
+   ``dataloader._ensure_posted`` / ``staging.post``), never by the native
+   stager thread, whose progress depends on producer timing. DDP's bucket
+   all-reduces are issued from autograd's device thread (the ledger reports
+   ``issuing_threads: 2``), but only while the consumer thread is blocked in
+   ``backward()``, in bucket order, so the two threads never issue
+   concurrently: the issue order is a function of the step/window schedule
+   and identical on every rank.
+3. **Enforced, not assumed.** Every loader collective and point-to-point
+   batch goes through :func:`issue` / :func:`check_group`, which raise
+   :class:`~ddl_amd.exceptions.CommunicatorMismatchError` if the group is not
+   ``env.process_group`` itself; the ledger records the group of every entry
+   (DDP's hook included) and :func:`check_same_order` reports how many
+   distinct groups were used (1 when the invariant holds).
 
 :data:`LEDGER` records the issue sequence (kind, key) when enabled, and
 :func:`check_same_order` compares a digest of it across ranks; the tests and
@@ -48,6 +56,7 @@ class CollectiveLedger:
         self.enabled = os.environ.get("DDL_TRACE_COLLECTIVES", "0") == "1"
         self.entries: list[tuple[str, object]] = []
         self.threads: set[int] = set()
+        self.groups: set[str] = set()
 
     def enable(self, on: bool = True) -> None:
         self.enabled = on
@@ -55,11 +64,14 @@ class CollectiveLedger:
     def clear(self) -> None:
         self.entries.clear()
         self.threads.clear()
+        self.groups.clear()
 
-    def record(self, kind: str, key: object = None) -> None:
+    def record(self, kind: str, key: object = None, group=None) -> None:
         if self.enabled:
             self.entries.append((kind, key))
             self.threads.add(threading.get_ident())
+            if group is not None:
+                self.groups.add(group_id(group))
 
     def digest(self) -> str:
         h = hashlib.sha1()
@@ -77,17 +89,42 @@ class CollectiveLedger:
 LEDGER = CollectiveLedger()
 
 
+def group_id(group) -> str:
+    """A stable name of a process group (its c10d name; the object id if it has none)."""
+    name = getattr(group, "group_name", None)
+    return str(name) if name else f"obj:{id(group):x}"
+
+
 def loader_group(env):
     """The process group the loader issues its collectives on: the DP group itself (see module doc)."""
     return env.process_group
 
 
+def check_group(env, group, what: str) -> None:
+    """Raise unless ``group`` is the DP group ``env.process_group`` itself (the same object: the same
+    ncclComm and stream as the trainer's DDP all-reduce)."""
+    if group is None or group is not env.process_group:
+        from ..exceptions import CommunicatorMismatchError
+
+        raise CommunicatorMismatchError(
+            (what, group_id(group) if group is not None else None,
+             group_id(env.process_group) if env.process_group is not None else None),
+            f"{what}: loader collectives must be issued on the DP process group (env.process_group), so that "
+            f"they share one communicator and device order with DDP (parallel/order.py); got another group")
+
+
+def issue(env, group, kind: str, key: object = None) -> None:
+    """Gate of every loader collective: check the group, then record (kind, key, group) in the ledger."""
+    check_group(env, group, kind)
+    LEDGER.record(kind, key, group)
+
+
 def ddp_ledger_hook(process_group):
-    """DDP comm hook: the default bucket all-reduce, recorded in :data:`LEDGER` at issue."""
+    """DDP comm hook: the default bucket all-reduce, recorded in :data:`LEDGER` at issue (with its group)."""
     from torch.distributed.algorithms.ddp_comm_hooks import default_hooks
 
     def hook(state, bucket):
-        LEDGER.record("ddp.allreduce", bucket.index())
+        LEDGER.record("ddp.allreduce", bucket.index(), process_group)
         return default_hooks.allreduce_hook(process_group, bucket)
 
     return hook
@@ -96,14 +133,15 @@ def ddp_ledger_hook(process_group):
 def check_same_order(control_group) -> dict:
     """All-gather the ledger digest over the (gloo) control group.
 
-    Returns ``{"same_order", "n_collectives", "by_kind", "issuing_threads"}``;
-    ``same_order`` is True when every rank issued the same sequence.
+    Returns ``{"same_order", "n_collectives", "by_kind", "issuing_threads", "groups"}``;
+    ``same_order`` is True when every rank issued the same sequence, ``groups`` is the number of
+    distinct process groups the recorded collectives were issued on (1: one communicator).
     """
     import torch.distributed as dist
 
     mine = (LEDGER.digest(), len(LEDGER.entries))
     out = {"same_order": True, "n_collectives": mine[1], "by_kind": LEDGER.counts(),
-           "issuing_threads": len(LEDGER.threads)}
+           "issuing_threads": len(LEDGER.threads), "groups": len(LEDGER.groups)}
     if control_group is None or not dist.is_initialized():
         return out
     allv: list = [None] * dist.get_world_size(control_group)

@@ -39,7 +39,7 @@ from ..ops import _dtypes
 from ..permutation import FeistelPermutation
 from ..types import DDLEnv
 from ..utils.logging import logger
-from .order import LEDGER, loader_group
+from .order import check_group, issue, loader_group
 
 _EXCHANGE_SALT = 0x5EED_C0DE
 
@@ -83,6 +83,7 @@ class GlobalShuffler:
         # the DP group itself: one communicator (and one RCCL stream) for loader and trainer
         # collectives, so their device order is the consumer thread's issue order (parallel/order.py)
         self.group = group if group is not None else loader_group(env)
+        check_group(env, self.group, f"{type(self).__name__}")
         if env.control_group is not None:
             # every rank must trade the same number of rows: agree on the smallest window
             t = torch.tensor([n_rows], dtype=torch.int64)
@@ -110,7 +111,7 @@ class GlobalShuffler:
 
         if self.n_exchange == 0:
             return
-        LEDGER.record("loader.exchange", window)
+        issue(self.env, self.group, "loader.exchange", window)
         t0 = time.perf_counter()
         ev = None
         if self.device.type == "cuda":

@@ -49,7 +49,7 @@ import torch
 
 from . import _native, ops
 from .ops import _dtypes
-from .parallel.order import LEDGER, loader_group
+from .parallel.order import check_group, issue, loader_group
 from .permutation import EpochOrder, batch_cursor
 from .types import DDLEnv
 from .utils.logging import logger
@@ -366,6 +366,7 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
         shard = torch.empty((rows,) + self.sample_shape, dtype=self.src_dtype, device=self.device)
         # first op on the group must be collective (communicator bring-up on every rank)
         probe = torch.zeros(1, device=self.device)
+        issue(self.env, self.group, "resident.bringup")
         dist.all_reduce(probe, group=self.group)
         rows_per_chunk = max(1, chunk_bytes // self.row_bytes)
         bounds = [(q * self.S, min(self.N, (q + 1) * self.S)) for q in range(self.W)]
@@ -415,6 +416,7 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
                                 ops_.append(dist.P2POp(dist.isend, piece, q, group=self.group))
                         self.bytes_exchanged += sum(p.tensor.numel() * p.tensor.element_size() for p in ops_)
                         if ops_:  # point-to-point (pairwise), not a collective: no ledger entry
+                            check_group(self.env, self.group, "resident.scatter_p2p")
                             for req in dist.batch_isend_irecv(ops_):
                                 req.wait()  # the send stream (not the host) waits for the sends
                         if gpu:
@@ -424,6 +426,7 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
                     if o0 < o1:
                         ops_.append(dist.P2POp(dist.irecv, shard[o0 - self.lo:o1 - self.lo], src_rank,
                                                group=self.group))
+                        check_group(self.env, self.group, "resident.scatter_p2p")
                         for req in dist.batch_isend_irecv(ops_):
                             req.wait()
         if gpu:
@@ -470,7 +473,7 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
                 send = ops.gather_rows(self.shard, index=send_idx) if n_send else \
                     torch.empty((0,) + self.sample_shape, dtype=self.src_dtype, device=self.device)
                 recv = torch.empty((self.LB,) + self.sample_shape, dtype=self.src_dtype, device=self.device)
-                LEDGER.record("resident.all_to_all", t)
+                issue(self.env, self.group, "resident.all_to_all", t)
                 dist.all_to_all_single(recv.view(self.LB, -1), send.view(send.shape[0], -1), recv_counts,
                                        send_counts, group=self.group)
                 self.bytes_exchanged += (n_send - send_counts[self.rank]) * self.row_bytes

@@ -33,6 +33,7 @@ from __future__ import annotations
 
 import dataclasses
 import os
+import sys
 import time
 from typing import Callable
 
@@ -128,11 +129,10 @@ class WindowStager:
         n_cs = int(os.environ.get("DDL_COPY_STREAMS", "2"))
         self.copy_stream2 = torch.cuda.Stream(device=self.device) if n_cs >= 2 else None
         self.stream = torch.cuda.Stream(device=self.device) if post_copy is not None else self.copy_stream
-        # The consumer posts window w+1's exchange when it hands window w back (the fixed,
-        # rank-identical issue point of the collective, parallel/order.py), and the first batch of
-        # w+1 is gathered right behind it: one ring buffer holds that posted window, so give it its
-        # own and keep `depth` windows of DMA in flight behind it.
-        n_buf = depth + 1 if post_copy is not None and depth >= 2 else depth
+        # The consumer posts window w+1's exchange when it enters window w (the fixed, rank-identical
+        # issue point of the collective, parallel/order.py), so two windows are held at once (w being
+        # consumed, w+1 exchanged ahead): one extra ring buffer, and `depth` windows of DMA behind them.
+        n_buf = depth + 1 if post_copy is not None else depth
         self.max_window_bytes = int(max_window_bytes)
         self.buffers = [torch.empty(max_window_bytes, dtype=torch.uint8, device=self.device) for _ in range(n_buf)]
         self.ready_events = [torch.cuda.Event() for _ in range(n_buf)]
@@ -255,8 +255,12 @@ class WindowStager:
         if self.copy_stream2 is not None:
             self.copy_stream2.synchronize()
         self.stream.synchronize()
-        # drop the ring (a live seek builds a new stager; batches handed out keep their own refs)
+        # drop the ring (a live seek builds a new stager; batches handed out keep their own refs) and any
+        # token-collate views cached over it (models/tokens.py), which would otherwise keep it allocated
         self._staged.clear()
+        tok = sys.modules.get("ddl_amd.models.tokens")
+        if tok is not None:
+            tok.drop_cached_views(b.data_ptr() for b in self.buffers)
         self.buffers = []
 
     @property

@@ -89,7 +89,7 @@ def test_bench_eight_ranks(method, launch):
     assert out["n_gpus"] == 8 and out["config"]["parallelism"] == "dp8" and out["config"]["global_batch"] == 128
     assert out["config"]["exchange_fraction"] == 0.5 and out["value"] > 0
     order = out["collective_order"]
-    assert order["same_order"] is True
+    assert order["same_order"] is True and order["groups"] == 1
     assert order["by_kind"]["loader.exchange"] >= 4 and order["by_kind"]["ddp.allreduce"] >= 4
     assert len(out["per_rank"]) == 8 and all(r_["exchange_calls"] >= 3 for r_ in out["per_rank"])
 

@@ -94,3 +94,63 @@ def test_partial_epochs_with_exchange_keep_windows_intact(rccl_env):
         assert dl._exchange_fn.calls >= 12
     finally:
         conn.finalize()
+
+
+def _exchange_run(env, dispatch, epochs=4, restore_at=None):
+    """Rows of every batch of an exchange-on loader; with ``restore_at`` a live load_state_dict is done
+    after that many batches (3 more are consumed first and then replayed)."""
+    import ddl_amd
+    from ddl_amd import Marker
+    from ddl_amd.parallel import launcher
+    from tests.helpers import IdProducer
+
+    conn = launcher.spawn_producers(ddl_amd.parallel.read_env(3), mode="thread")
+    out, sd, n = [], None, 0
+    try:
+        dl = ddl_amd.DistributedDataLoader(IdProducer(64, 8), 16, conn, epochs, 0.5, "alltoall", env=env,
+                                           shuffle="device", copy_batches=True, seed=2, native_dispatch=dispatch)
+        mode = dl.stats().get("native_dispatch", {}).get("mode") if dispatch else "python"
+        while dl.epoch < epochs:
+            for i in range(dl.epoch_batch, len(dl)):
+                out.append(torch.cat([t.reshape(t.shape[0], -1) for t in dl[i]], 1).cpu())
+                dl.mark(Marker.END_OF_BATCH)
+                n += 1
+                if restore_at is not None and n == restore_at:
+                    sd = dl.state_dict()
+                if sd is not None and n == restore_at + 3:
+                    dl.load_state_dict(sd)
+                    del out[restore_at:]
+                    sd, restore_at = None, None
+                    break
+            else:
+                dl.mark(Marker.END_OF_EPOCH)
+        calls = dl._exchange_fn.calls
+    finally:
+        conn.finalize()
+    return out, mode, calls
+
+
+@pytest.mark.parametrize("dispatch", ["inline", "lookahead", "auto"])
+def test_exchange_runs_on_the_native_engine(rccl_env, dispatch):
+    """With the exchange on, batches come from the native engine (not the Python fallback) and are
+    bit-identical to the Python dispatch path: the engine waits on the post-exchange ready event."""
+    ref, mode_ref, calls_ref = _exchange_run(rccl_env, False)
+    got, mode, calls = _exchange_run(rccl_env, dispatch)
+    assert mode_ref == "python" and mode in ("inline", "lookahead", "window")
+    if dispatch != "auto":
+        assert mode == dispatch
+    assert calls == calls_ref == 4 and len(got) == len(ref) == 16
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dispatch", ["auto", False])
+def test_exchange_loader_live_load_state_dict(rccl_env, dispatch):
+    """Live restore on an exchange-on loader: collectives restart at the checkpointed window and the
+    delivered batches equal the uninterrupted run."""
+    ref, _, _ = _exchange_run(rccl_env, dispatch)
+    for at in (2, 5):
+        got, _, _ = _exchange_run(rccl_env, dispatch, restore_at=at)
+        assert len(got) == len(ref)
+        for a, b in zip(got, ref):
+            assert torch.equal(a, b)

@@ -97,9 +97,13 @@ def test_bench_multirank_device_path(n, launch):
     assert out["n_gpus"] == n and out["config"]["parallelism"] == f"dp{n}" and out["value"] > 0
     assert out["config"]["exchange_fraction"] == 0.5 and out["phase2_error"] is None
     order = out["collective_order"]
-    assert order["same_order"] is True and order["by_kind"]["ddp.allreduce"] > 0
+    assert order["same_order"] is True and order["groups"] == 1 and order["by_kind"]["ddp.allreduce"] > 0
     assert order["by_kind"]["loader.exchange"] > 0
     assert len(out["per_rank"]) == n
     for r in out["per_rank"]:
         assert r["h2d_bytes_timed"] > 0 and r["exchange_calls"] > 0 and r["rccl_bytes"] > 0
+        # the exchange-on N > 1 point runs the same native batch engine as N = 1 (not the Python path)
+        assert r["dispatch"]["mode"] in ("inline", "lookahead", "window"), r["dispatch"]
+        assert r["dispatch"]["host_us_per_batch"]["get"] > 0
+    assert out["config"]["dispatch"] == out["per_rank"][0]["dispatch"]["mode"]
     assert out["indexed"] and "error" not in out["indexed"] and out["indexed"]["value"] > 0
