@@ -174,7 +174,7 @@ def indexed_phase(args, env, dev, barrier, sync) -> dict:
     import torch.distributed as dist
 
     from ddl_amd import ops
-    from ddl_amd.models.datasets import SharedArraySource
+    from ddl_amd.models.datasets import numa_local_source
     from ddl_amd.models.trainstep import TrainStep
     from ddl_amd.utils.tracing import ComputeIdleMeter, trace_range
     from ddl_amd.zerocopy import ZeroCopyLoader
@@ -182,13 +182,15 @@ def indexed_phase(args, env, dev, barrier, sync) -> dict:
     shape = (3, 224, 224)
     n = max(args.index_samples, args.batch * env.world_size)
     name = f"ddl_amd_bench_idx_{os.environ.get('MASTER_PORT', os.getpid())}"
-    creator = env.local_rank == 0
-    src = SharedArraySource(name, n, shape, torch.bfloat16, create=creator)
+
+    def fill(t):  # every page written (resident on the replica's node); sample i's first element is i
+        t.view(torch.uint8).fill_(0x3C)
+        t.view(n, -1)[:, 0] = torch.arange(n, dtype=torch.float32).to(torch.bfloat16)
+
+    # one replica per NUMA node of the node's GPUs: no GPU gathers across the socket link
+    src, node, _ = numa_local_source(name, n, shape, torch.bfloat16, env, fill=fill)
     try:
-        if creator:  # cheap distinct content: every sample's first element is its id
-            src.tensor().view(n, -1)[:, 0] = torch.arange(n, dtype=torch.float32).to(torch.bfloat16)
-        if env.world_size > 1:
-            dist.barrier(group=env.control_group)
+        pages = src.page_nodes(64)
         dl = ZeroCopyLoader(src, args.batch * env.world_size, env, seed=args.seed, out_dtype=torch.bfloat16,
                             device=dev)
 
@@ -213,9 +215,13 @@ def indexed_phase(args, env, dev, barrier, sync) -> dict:
             t = torch.tensor([el], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=env.control_group)
             el = float(t.item())
-        out = {"order": "indexed (EpochOrder, world-size-invariant), zero-copy gather from node-shared pinned bf16",
+        out = {"order": "indexed (EpochOrder, world-size-invariant), zero-copy gather from a NUMA-local pinned "
+                        "bf16 replica of the node-shared source",
                "value": round(args.batch * args.steps * env.world_size / el, 1), "ms_per_step":
-               round(1000 * el / args.steps, 4), "source_samples": n}
+               round(1000 * el / args.steps, 4), "source_samples": n,
+               "numa": {"gpu_node": node, "source_pages_on_gpu_node_pct":
+                        round(100.0 * sum(1 for p in pages if p == node) / max(1, len(pages)), 1)
+                        if node is not None else None}}
         idle_steps = args.steps if args.idle_steps < 0 else args.idle_steps
         if idle_steps and dev.type == "cuda":
             step = TrainStep(dev, dim=args.model_dim, depth=args.model_depth,
@@ -434,7 +440,8 @@ def main(argv=None) -> int:
                 "scaling": "weak",
                 "vs_baseline": round(value / (REF_SAMPLES_PER_S_PER_GPU * env.world_size), 3),
                 "dtype": "bf16",
-                "data": f"synthetic (random {args.source_dtype} images, refreshed every producer round: {args.refill})",
+                "data": f"synthetic (random {args.source_dtype} images, refreshed every producer round: "
+                        f"{args.refill})",
                 "config": {
                     "model": "ddl_amd loader: ImageNet-shape 3x224x224 bf16, pinned H2D prefetch stream",
                     "global_batch": args.batch * env.world_size,

@@ -167,6 +167,48 @@ def main():
     x = torch.randn(1_000_000, 9, device=dev)
     t = bench(lambda: ops.column_stats(x), reps=20)
     report("column_stats 1Mx9", t, x.numel() * 4)
+    del win_bf16, win_u8, win_hwc, raw, pw, x
+    out_of_cache(dev)
+
+
+def rotating(fns, reps=48):
+    """Time a list of calls issued round-robin (each touches its own buffers), per call."""
+    i = [0]
+
+    def one():
+        fns[i[0] % len(fns)]()
+        i[0] += 1
+
+    return bench(one, reps=reps)
+
+
+def out_of_cache(dev) -> None:
+    """The gather / cast / scatter kernels on working sets far beyond the 256 MB MALL: 1024-row batches
+    from an 8192-image window (2.5 GB bf16 / 1.2 GB uint8), 4 output buffers used round-robin, so every
+    call reads and writes memory the previous calls did not touch (>= 1.2 GB in flight per rotation).
+    These are the numbers to hold against the 1 GiB D2D roofline (``pct_of_d2d``)."""
+    B, C, H, W, n = 1024, 3, 224, 224, 8192
+    img = C * H * W
+    p = FeistelPermutation(n, 1, 2)
+    win = torch.empty(n, C, H, W, dtype=torch.bfloat16, device=dev).normal_()
+    outs = [torch.empty(B, C, H, W, dtype=torch.bfloat16, device=dev) for _ in range(4)]
+    fns = [lambda o=o, k=k: ops.gather_rows(win, perm=p, base=k * B, n_rows=B, out=o) for k, o in enumerate(outs)]
+    report("OOC permute_gather bf16->bf16 1024 rows (rotating)", rotating(fns), 2 * B * img * 2, rows=B)
+    idxs = [torch.from_numpy(p(np.arange(k * B, (k + 1) * B))).to(dev) for k in range(4)]
+    fns = [lambda o=o, ix=ix: ops.scatter_rows(win.view(n, -1), o.view(B, -1), ix) for o, ix in zip(outs, idxs)]
+    report("OOC scatter_rows bf16 1024 rows (rotating)", rotating(fns), 2 * B * img * 2, rows=B)
+    del win
+    win8 = torch.randint(0, 256, (n, C, H, W), dtype=torch.uint8, device=dev)
+    mean, std = [0.485, 0.456, 0.406], [0.229, 0.224, 0.225]
+    sc = [1 / (255 * s_) for s_ in std]
+    bi = [-m / s_ for m, s_ in zip(mean, std)]
+    fns = [lambda o=o, k=k: ops.gather_rows(win8, perm=p, base=k * B, n_rows=B, out=o, scale=sc, bias=bi,
+                                            plane=H * W) for k, o in enumerate(outs)]
+    report("OOC permute_gather u8->bf16 normalise 1024 rows (rotating)", rotating(fns), B * img * 3, rows=B)
+    del win8
+    f32s = [torch.empty(B, img, device=dev).normal_() for _ in range(2)]
+    fns = [lambda f=f, o=o: ops.gather_rows(f, out=o.view(B, img)) for f, o in zip(f32s * 2, outs)]
+    report("OOC cast f32->bf16 1024 rows (rotating)", rotating(fns), B * img * 6, rows=B)
 
 
 if __name__ == "__main__":

@@ -344,6 +344,8 @@ PYBIND11_MODULE(_ddl_hip, m) {
       .def_property("inline", &ddl::BatchEngine::is_inline, &ddl::BatchEngine::set_inline)
       .def("set_window_mode", &ddl::BatchEngine::set_window_mode, py::arg("on"), py::arg("slot_stride"))
       .def_property_readonly("window_mode", &ddl::BatchEngine::window_mode)
+      .def_property("early_release", &ddl::BatchEngine::early_release, &ddl::BatchEngine::set_early_release)
+      .def("set_batches_per_window", &ddl::BatchEngine::set_batches_per_window, py::arg("bpw"))
       .def_property_readonly("wait_s", &ddl::BatchEngine::wait_s)
       .def_property_readonly("batches", &ddl::BatchEngine::batches)
       .def_property_readonly("lookahead_hits", &ddl::BatchEngine::lookahead_hits)

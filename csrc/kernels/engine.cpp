@@ -132,6 +132,8 @@ int BatchEngine::enqueue(int64_t w, int64_t local, const StagedInfo& info, Pendi
   }
   const uint64_t t2 = clock_ns();
   if (on_caller) {  // stream order is the dependency: no event
+    if (last_of_window && early_ && hand_back(w, info, st) != 0) return -1;
+    record_ns_ += clock_ns() - t2;
     *out = Pending{w, local, slot, -1};
     return 0;
   }
@@ -145,11 +147,42 @@ int BatchEngine::enqueue(int64_t w, int64_t local, const StagedInfo& info, Pendi
     hipEvent_t fe = free_events_[b][free_next_[b]];
     free_next_[b] = (free_next_[b] + 1) % kFreeEvents;
     if (hipEventRecord(fe, bs_) != hipSuccess) return -1;
-    done_event_[w] = fe;
+    if (early_) {
+      stager_->release(w, fe);
+      handed_back_.insert(w);
+    } else {
+      done_event_[w] = fe;
+    }
   }
   record_ns_ += clock_ns() - t2;
   *out = Pending{w, local, slot, ev};
   return 0;
+}
+
+int BatchEngine::hand_back(int64_t w, const StagedInfo& info, hipStream_t st) {
+  // every read of the window's ring buffer is enqueued (on `st`, or joined into it): give the buffer
+  // back to the stager now, behind a free event, instead of at the consumer's release() one step later
+  auto rs = read_streams_.find(w);
+  if (rs != read_streams_.end()) {
+    for (hipStream_t o : rs->second) {
+      if (o == st) continue;
+      hipEvent_t xe = join_event();
+      if (xe == nullptr || hipEventRecord(xe, o) != hipSuccess || hipStreamWaitEvent(st, xe, 0) != hipSuccess)
+        return -1;
+    }
+  }
+  const int b = info.buffer;
+  hipEvent_t fe = free_events_[b][free_next_[b]];
+  free_next_[b] = (free_next_[b] + 1) % kFreeEvents;
+  if (hipEventRecord(fe, st) != hipSuccess) return -1;
+  stager_->release(w, fe);
+  handed_back_.insert(w);
+  return 0;
+}
+
+int64_t BatchEngine::bpw_of(const StagedInfo& info) const {
+  const size_t p = static_cast<size_t>(info.producer);
+  return p < bpw_.size() ? bpw_[p] : -1;
 }
 
 int BatchEngine::enqueue_window(int64_t w, int64_t bpw, const StagedInfo& info, hipStream_t st) {
@@ -171,7 +204,12 @@ int BatchEngine::enqueue_window(int64_t w, int64_t bpw, const StagedInfo& info, 
   hipEvent_t fe = free_events_[b][free_next_[b]];
   free_next_[b] = (free_next_[b] + 1) % kFreeEvents;
   if (hipEventRecord(fe, st) != hipSuccess) return -1;
-  done_event_[w] = fe;
+  if (early_) {
+    stager_->release(w, fe);
+    handed_back_.insert(w);
+  } else {
+    done_event_[w] = fe;
+  }
   record_ns_ += clock_ns() - t2;
   ww_w_ = w;
   ww_slot0_ = s0;
@@ -305,7 +343,7 @@ int64_t BatchEngine::get(int64_t w, int64_t local, int64_t bpw, bool next_ok, hi
   if (inline_) {
     last_compute_ = compute;
     have_compute_ = true;
-    rc = enqueue(w, local, windows_.at(w), &cur, true, compute);
+    rc = enqueue(w, local, windows_.at(w), &cur, true, compute, local + 1 == bpw);
     if (rc != 0) return rc;
     ++batches_;
     get_ns_ += clock_ns() - g0;
@@ -349,8 +387,8 @@ int64_t BatchEngine::get(int64_t w, int64_t local, int64_t bpw, bool next_ok, hi
       int32_t fp = -1;
       if (acquire(w + 1, 0, &fp) == 0) ni = acquired(w + 1);
     }
-    // (w + 1, 0) is the last batch of w + 1 only if it has one batch: its bpw is unknown here, so no done event
-    if (ni != nullptr && enqueue(w + 1, 0, *ni, &nxt) == 0) pending_.push_back(nxt);
+    // (w + 1, 0) is the last batch of w + 1 if that window holds one batch (bpw per producer, set_batches_per_window)
+    if (ni != nullptr && enqueue(w + 1, 0, *ni, &nxt, false, nullptr, bpw_of(*ni) == 1) == 0) pending_.push_back(nxt);
   }
   get_ns_ += clock_ns() - g0;
   return cur.slot;
@@ -359,6 +397,14 @@ int64_t BatchEngine::get(int64_t w, int64_t local, int64_t bpw, bool next_ok, hi
 int BatchEngine::release(int64_t w) {
   auto it = windows_.find(w);
   if (it == windows_.end()) return 0;
+  if (handed_back_.erase(w) != 0) {  // its buffer went back to the stager at its last batch launch
+    windows_.erase(it);
+    keys_.erase(w);
+    read_streams_.erase(read_streams_.begin(), read_streams_.upper_bound(w));
+    done_event_.erase(w);
+    while (!pending_.empty() && pending_.front().w <= w) pending_.pop_front();
+    return 0;
+  }
   const int b = it->second.buffer;
   // the stream that read the window (inline: the caller's), behind its copy (a window no batch was
   // built from still has its copy in flight): the free event goes there
@@ -410,6 +456,7 @@ hipEvent_t BatchEngine::join_event() {
 
 void BatchEngine::reset() {
   read_streams_.clear();
+  handed_back_.clear();
   done_event_.clear();
   ww_w_ = -1;
   ww_slot0_ = -1;

@@ -34,6 +34,7 @@
 #include <cstdint>
 #include <deque>
 #include <map>
+#include <set>
 #include <vector>
 
 #include "common.h"
@@ -107,6 +108,15 @@ class BatchEngine {
     slot_stride_ = slot_stride;
   }
   bool window_mode() const { return whole_; }
+  // Early hand-back (default on): a window's ring buffer goes back to the stager as soon as the launch
+  // of its LAST batch is enqueued (behind a free event on that launch's stream), not at release() --
+  // one consumer step earlier, so the next window's copy is already enqueued when the lookahead looks
+  // for it. release() then only drops the window's bookkeeping.
+  void set_early_release(bool on) { early_ = on; }
+  bool early_release() const { return early_; }
+  // Batches per window of each producer's windows (lets the lookahead know that (w + 1, 0) is the last
+  // batch of a one-batch window).
+  void set_batches_per_window(std::vector<int64_t> bpw) { bpw_ = std::move(bpw); }
 
   double wait_s() const { return wait_ns_ * 1e-9; }
   // host ns spent in get() in total, and inside HIP calls: kernel launches, event records, stream waits
@@ -178,6 +188,11 @@ class BatchEngine {
   std::vector<hipEvent_t> join_events_;
   size_t join_next_ = 0;
   hipEvent_t join_event();
+  int hand_back(int64_t w, const StagedInfo& info, hipStream_t st);
+  int64_t bpw_of(const StagedInfo& info) const;
+  bool early_ = true;
+  std::vector<int64_t> bpw_;
+  std::set<int64_t> handed_back_;  // windows whose buffer went back to the stager before release()
 };
 
 // Host derivation of the Feistel round keys of (seed, key) -- ddl_amd/permutation.py round_keys --

@@ -12,6 +12,7 @@
 #include "feistel.h"
 #include <algorithm>
 #include "fileio.h"
+#include "numa.h"
 
 namespace py = pybind11;
 using ddl::Arena;
@@ -294,6 +295,25 @@ PYBIND11_MODULE(_ddl_runtime, m) {
                            bytes, n_threads);
       },
       py::arg("dst"), py::arg("src"), py::arg("bytes"), py::arg("n_threads") = 4);
+  m.def(
+      "bind_memory_to_node",
+      [](uintptr_t addr, uint64_t len, int node, bool strict) {
+        return ddl::bind_memory_to_node(reinterpret_cast<void*>(addr), len, node, strict);
+      },
+      py::arg("addr"), py::arg("len"), py::arg("node"), py::arg("strict") = false,
+      "mbind [addr, addr+len) to a NUMA node (preferred, or bound when strict; faulted pages migrate); 0 or -errno");
+  m.def(
+      "memory_nodes",
+      [](uintptr_t addr, uint64_t len, uint64_t max_pages) {
+        std::vector<int> st;
+        {
+          py::gil_scoped_release nogil;
+          st = ddl::memory_nodes(reinterpret_cast<const void*>(addr), len, max_pages);
+        }
+        return st;
+      },
+      py::arg("addr"), py::arg("len"), py::arg("max_pages") = 64,
+      "NUMA node of pages sampled over [addr, addr+len) (move_pages query; -errno per page on failure)");
   m.def(
       "pack_columns",
       [](uintptr_t dst, std::vector<uintptr_t> srcs, std::vector<uint64_t> widths, uint64_t elem_bytes, uint64_t n,

@@ -78,8 +78,8 @@ def hip_target() -> str:
 
 
 def build_runtime(force: bool = False, extra_flags: list[str] | None = None) -> str:
-    srcs = [os.path.join(CSRC, "runtime", f) for f in ("arena.cpp", "fileio.cpp", "bindings.cpp")]
-    deps = srcs + [os.path.join(CSRC, "runtime", h) for h in ("arena.h", "feistel.h", "fileio.h")]
+    srcs = [os.path.join(CSRC, "runtime", f) for f in ("arena.cpp", "fileio.cpp", "numa.cpp", "bindings.cpp")]
+    deps = srcs + [os.path.join(CSRC, "runtime", h) for h in ("arena.h", "feistel.h", "fileio.h", "numa.h")]
     out = runtime_target()
     if not force and not _newer(out, deps):
         return out

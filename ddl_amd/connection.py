@@ -117,6 +117,7 @@ class Connection:
         self.pipes = [_Pipe(c, p, f"producer {i}") for i, (c, p) in enumerate(zip(pipes, procs))]
         self.processes = list(procs)
         self.arena = None
+        self.cpu_layout: dict | None = None  # consumer / producer CPU split (utils/numa.partition_after_spawn)
         self._finalizers: list = []
         self.window_shapes: list[tuple[int, ...]] = []
         self.window_dtypes: list[torch.dtype] = []

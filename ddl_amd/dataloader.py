@@ -33,6 +33,7 @@ where one window is one global batch).
 from __future__ import annotations
 
 import math
+import os
 import time
 from abc import ABC, abstractmethod
 from typing import Any, Iterator
@@ -431,6 +432,10 @@ class DistributedDataLoader(DistributedDataloaderABC):
             self._eng_block = max(self._eng_block, bpw_max)  # a window's slots come from one block
             self._engine.set_window_mode(True, self._eng_slot_bytes)
         self._engine.inline = mode in ("inline", "window")
+        self._engine.set_batches_per_window([int(b) for b in self.batches_per_window])
+        # hand a window's ring buffer back to the stager at its last batch launch (DDL_EARLY_RELEASE=0: at
+        # the consumer's release, one step later -- the round-2 behaviour, for A/B runs)
+        self._engine.early_release = os.environ.get("DDL_EARLY_RELEASE", "1") != "0"
         self._eng_mode = mode
         self._eng_slots: collections.deque = collections.deque()  # (slot id, outputs, block)
         self._eng_next_id = 0
@@ -853,6 +858,8 @@ class DistributedDataLoader(DistributedDataloaderABC):
                 from .exceptions import DDLError
 
                 raise DDLError(f"native batch engine: releasing window {self.window} failed")
+            if self._exchange_fn is not None:
+                self._stager.forget(self.window)  # the Python face's record of the posted window
             if self._eng_window == self.window:
                 self._eng_window = None
             return
@@ -1203,7 +1210,10 @@ class DistributedDataLoader(DistributedDataloaderABC):
                 g, la, rec, sw = self._engine.timing_ns
                 n = max(1, int(self._engine.batches))
                 nd["compute_waits"] = int(self._engine.compute_waits)
-                nd["host_us_per_batch"] = {"get": round(g / n / 1e3, 2), "kernel_launch": round(la / n / 1e3, 2),
+                wait_ns = self._engine.wait_s * 1e9
+                nd["host_us_per_batch"] = {"get": round(g / n / 1e3, 2),
+                                           "get_excl_staging_wait": round(max(0.0, g - wait_ns) / n / 1e3, 2),
+                                           "kernel_launch": round(la / n / 1e3, 2),
                                            "event_record": round(rec / n / 1e3, 2),
                                            "stream_wait": round(sw / n / 1e3, 2)}
             nd["mode"] = getattr(self, "_eng_mode", None)

@@ -17,7 +17,11 @@ What it wires together, each piece usable on its own:
   per-batch dispatch; batches come back as typed views in the sample's structure.
 
 ``batch_size`` is the per-rank batch, as with ``DistributedSampler`` under DDP: the global batch is
-``batch_size * world_size``, and rank r gets slice r of every global batch. Like torch's DataLoader
+``batch_size * world_size``, and rank r gets slice r of every global batch. ``drop_last`` defaults to
+False as in torch: no sample of the epoch is dropped. Every batch is full (static shapes): the last,
+partial global batch is completed from the start of the epoch's order, which is what
+``DistributedSampler(drop_last=False)`` does under DDP (torch's single-process DataLoader instead
+yields a shorter last batch). ``drop_last=True`` drops the partial batch. Like torch's DataLoader
 with worker processes, construct it before the first CUDA call of the process: the workers are
 spawned processes (on a box whose policy forbids spawning after GPU initialisation, that ordering
 is required).
@@ -32,7 +36,7 @@ from typing import Any, Iterator
 
 
 class DataLoader:
-    def __init__(self, dataset, batch_size: int = 1, shuffle: bool = False, drop_last: bool = True,
+    def __init__(self, dataset, batch_size: int = 1, shuffle: bool = False, drop_last: bool = False,
                  num_workers: int = 3, seed: int = 0, epochs: int | None = None, device: str | None = None,
                  resume_state: dict | None = None, host_threads: int = 2, **loader_kw: Any):
         from .dataloader import DistributedDataLoader

@@ -9,6 +9,7 @@ from .datasets import (
     SharedArraySource,
     SyntheticTokens,
     synthetic_images,
+    numa_local_source,
     unpack_fields,
 )
 from .producers import ImageWindowProducer, IndexedProducer, PointwiseProducer
@@ -22,6 +23,7 @@ __all__ = [
     "SharedArraySource",
     "SyntheticTokens",
     "synthetic_images",
+    "numa_local_source",
     "unpack_fields",
     "ImageWindowProducer",
     "IndexedProducer",

@@ -166,6 +166,19 @@ class SharedArraySource:
         _native.runtime().gather_rows(dst_address, self.address, self.row_bytes,
                                       np.ascontiguousarray(indices, dtype=np.int64), self.n, n_threads)
 
+    def bind_to_node(self, node: int, strict: bool = False) -> int:
+        """Place the segment's pages on NUMA ``node`` (mbind of the shared object: pages already
+        faulted in migrate, later faults by ANY process allocate there). 0 or -errno."""
+        from .. import _native
+
+        return int(_native.runtime().bind_memory_to_node(self.address, self.n * self.row_bytes, int(node), strict))
+
+    def page_nodes(self, max_pages: int = 64) -> list[int]:
+        """NUMA node of pages sampled evenly over the segment (for reports / tests)."""
+        from .. import _native
+
+        return list(_native.runtime().memory_nodes(self.address, self.n * self.row_bytes, max_pages))
+
     def close(self, unlink: bool | None = None) -> None:
         if self._shm is None:
             return
@@ -180,6 +193,44 @@ class SharedArraySource:
             except FileNotFoundError:
                 pass
         self._shm = None
+
+
+def numa_local_source(base_name: str, n: int, sample_shape, dtype, env, fill=None):
+    """One replica of a node-shared array per NUMA node that hosts a GPU of this node's ranks.
+
+    The reference keeps each GPU group's data in node-local shared memory (its MPI shared windows,
+    reference ddl/ddl_env.py:58-73, ddl/connection.py:88-139). A single node-wide segment read
+    by every GPU (the zero-copy gather, ``zerocopy.py``) would make the GPUs of the other socket
+    read across the inter-socket link. Here the ranks whose GPUs sit on the same NUMA node share
+    one replica ``{base_name}_numa{node}``: its lowest local rank creates it, binds it to the node
+    (``bind_to_node``, before any page is touched) and fills it with ``fill(tensor)``; the others
+    attach after a barrier on ``env.control_group``. Returns ``(source, node, created)``; the
+    caller closes the source (the creator unlinks) after every rank of the node is done with it.
+    Collective: every rank of the job calls it (the barrier is on the control group).
+    """
+    import torch.distributed as dist
+
+    from ..utils.numa import gpu_numa_node
+
+    lw = max(1, int(getattr(env, "local_world_size", 1) or 1))
+    lr = int(getattr(env, "local_rank", 0) or 0)
+    nodes = [gpu_numa_node(i) for i in range(lw)]
+    node = nodes[lr] if lr < len(nodes) else None
+    tag = "any" if node is None else str(node)
+    creator = nodes.index(node) == lr
+    src = SharedArraySource(f"{base_name}_numa{tag}", n, sample_shape, dtype, create=creator)
+    try:
+        if creator:
+            if node is not None:
+                src.bind_to_node(node)
+            if fill is not None:
+                fill(src.tensor())
+        if getattr(env, "world_size", 1) > 1 and dist.is_initialized():
+            dist.barrier(group=env.control_group)
+    except BaseException:
+        src.close()
+        raise
+    return src, node, creator
 
 
 class NpyMemmapSource:

@@ -227,6 +227,11 @@ class WindowStager:
             raise PeerDeathError(f"{what}: producer {producer} reported a failure", producer, pid)
         raise PeerDeathError(f"{what}: producer {producer} (pid {pid}) died", producer, pid)
 
+    def forget(self, w: int) -> None:
+        """Drop the Python-side record of window ``w`` (the native batch engine handed its buffer back)."""
+        self._staged.pop(w, None)
+        self._posted.discard(w)
+
     def release(self, w: int, stream: torch.cuda.Stream | None = None, event: torch.cuda.Event | None = None) -> None:
         """Consumer is done with window ``w`` as of ``stream``'s position (default: the current
         stream): every kernel that reads the window must be on that stream, before this call.

@@ -98,17 +98,70 @@ def node_cpus(node: int) -> set[int]:
     return cpus
 
 
-def bind_to_gpu_numa(local_index: int) -> int | None:
-    """Restrict this process's CPU affinity to its GPU's NUMA node; return the node (or None)."""
-    if os.environ.get("DDL_NUMA_BIND", "1") == "0":
-        return None
+def rank_cpu_slice(local_index: int, local_world: int, allowed: set[int] | None = None) -> tuple[int | None, set[int]]:
+    """(node, CPUs) of this local rank: its GPU's NUMA node's allowed CPUs, split into equal contiguous
+    slices among the local ranks whose GPUs sit on that node (in local-rank order), so the ranks of one
+    socket do not compete for the same cores. Falls back to the whole node (one rank on it, or fewer
+    CPUs than ranks) and to the allowed set when the GPU's node is unknown."""
+    allowed = set(os.sched_getaffinity(0)) if allowed is None else set(allowed)
     node = gpu_numa_node(local_index)
     if node is None:
+        return None, allowed
+    cpus = sorted(node_cpus(node) & allowed)
+    if not cpus:
+        return node, allowed
+    peers = [i for i in range(max(1, local_world)) if i == local_index or gpu_numa_node(i) == node]
+    k, i = len(peers), peers.index(local_index)
+    if k <= 1 or len(cpus) < k:
+        return node, set(cpus)
+    per = len(cpus) // k
+    return node, set(cpus[i * per:(i + 1) * per])
+
+
+def split_consumer_producers(cpus: set[int], n_producers: int, consumer_cpus: int = 4) -> tuple[set[int], set[int]]:
+    """Split a rank's CPUs between its consumer (main thread, native stager / retire threads, RCCL and
+    gloo helpers) and its producer processes (user hooks, native gather pools): the consumer keeps the
+    first ``consumer_cpus``, the producers share the rest. Only when there are enough CPUs for both
+    (at least ``consumer_cpus + 2 * n_producers``); otherwise both get all of them."""
+    c = sorted(cpus)
+    if n_producers < 1 or len(c) < consumer_cpus + 2 * n_producers:
+        return set(c), set(c)
+    return set(c[:consumer_cpus]), set(c[consumer_cpus:])
+
+
+def bind_to_gpu_numa(local_index: int, local_world: int = 1) -> int | None:
+    """Restrict this process's CPU affinity to its share of its GPU's NUMA node (``rank_cpu_slice``);
+    return the node (or None). ``DDL_NUMA_BIND=0`` disables it, ``DDL_CPU_PARTITION=0`` keeps the whole
+    node instead of a per-rank slice."""
+    if os.environ.get("DDL_NUMA_BIND", "1") == "0":
         return None
     allowed = os.sched_getaffinity(0)
-    cpus = node_cpus(node) & allowed
+    if os.environ.get("DDL_CPU_PARTITION", "1") == "0":
+        local_world = 1
+    node, cpus = rank_cpu_slice(local_index, local_world, allowed)
+    if node is None:
+        return None
     if not cpus or cpus == allowed:
         return node
     os.sched_setaffinity(0, cpus)
     logger.debug("bound to NUMA node %d (%d CPUs) for GPU %d", node, len(cpus), local_index)
     return node
+
+
+def partition_after_spawn(producer_pids: list[int], n_producers: int) -> dict | None:
+    """After the producers are spawned (they inherited this rank's CPU slice): the producers get the
+    slice minus the consumer's first CPUs, the consumer keeps those (``split_consumer_producers``).
+    Returns the layout, or None when not partitioned. ``DDL_CPU_PARTITION=0`` disables it."""
+    if os.environ.get("DDL_CPU_PARTITION", "1") == "0" or not producer_pids:
+        return None
+    mine = os.sched_getaffinity(0)
+    cons, prod = split_consumer_producers(mine, n_producers, int(os.environ.get("DDL_CONSUMER_CPUS", "4")))
+    if cons == prod:
+        return None
+    for pid in producer_pids:
+        try:
+            os.sched_setaffinity(pid, prod)
+        except OSError:
+            return None
+    os.sched_setaffinity(0, cons)
+    return {"consumer_cpus": sorted(cons), "producer_cpus": sorted(prod)}

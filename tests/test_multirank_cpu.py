@@ -279,7 +279,8 @@ def token_corpus():
     src.close()
 
 
-@pytest.mark.parametrize("world", [1, 2])
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
 def test_token_windows_world_size_invariant(token_corpus, world):
     """k-batch token windows keep the indexed order: global batch g = concat of rank slices, at any W."""
     from ddl_amd.permutation import EpochOrder
@@ -292,15 +293,20 @@ def test_token_windows_world_size_invariant(token_corpus, world):
         assert merged == [int(x) for x in order.indices(0, g)]
 
 
-def test_token_windows_resume_mid_window_at_other_world_size(token_corpus):
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("save_world,resume_world", [(2, 1), (4, 8), (8, 2)])
+def test_token_windows_resume_mid_window_at_other_world_size(token_corpus, save_world, resume_world):
+    """Checkpoint a k-batch token loader mid-window (global batch 6 = window 1, sub-batch 2) at one world
+    size and resume at another: the resumed ranks' slices merge into exactly the remaining global batches."""
     from ddl_amd.permutation import EpochOrder
 
     src, gb, k = token_corpus, 8, 4
-    res = run_ranks(_token_rank, 2, src.tokens.name[:-4], src.n, src.max_len, gb, k, None, 6,
+    res = run_ranks(_token_rank, save_world, src.tokens.name[:-4], src.n, src.max_len, gb, k, None, 6,
                     env={"DDL_DEVICE": "cpu"})
     sd = res[0][1]
-    assert sd["global_batch_cursor"] == 6 and sd["batches_per_window"] == k
-    (out, _), = run_ranks(_token_rank, 1, src.tokens.name[:-4], src.n, src.max_len, gb, k, sd,
-                          env={"DDL_DEVICE": "cpu"})
+    assert all(r[1]["global_batch_cursor"] == 6 for r in res) and sd["batches_per_window"] == k
+    out = run_ranks(_token_rank, resume_world, src.tokens.name[:-4], src.n, src.max_len, gb, k, sd,
+                    env={"DDL_DEVICE": "cpu"})
     order = EpochOrder(src.n, gb, 5)
-    assert out == [[int(x) for x in order.indices(0, g)] for g in range(6, order.batches_per_epoch)]
+    merged = [sum((r[0][i] for r in out), []) for i in range(len(out[0][0]))]
+    assert merged == [[int(x) for x in order.indices(0, g)] for g in range(6, order.batches_per_epoch)]

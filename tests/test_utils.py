@@ -167,6 +167,25 @@ def test_numa_helpers_do_not_fail():
     assert numa.bind_to_gpu_numa(0) in (None, 0, 1, 2, 3, 4, 5, 6, 7)
 
 
+def test_cpu_slices_partition_a_node(monkeypatch):
+    """4 GPUs on node 0 with 32 CPUs: each local rank gets a disjoint 8-CPU slice; the consumer keeps 4 of
+    its slice and its producers share the other 4 only when there is room for both."""
+    from ddl_amd.utils import numa
+
+    monkeypatch.setattr(numa, "gpu_numa_node", lambda i: 0 if i < 4 else 1)
+    monkeypatch.setattr(numa, "node_cpus", lambda n: set(range(32)) if n == 0 else set(range(32, 64)))
+    allowed = set(range(64))
+    slices = [numa.rank_cpu_slice(i, 8, allowed) for i in range(8)]
+    assert [n for n, _ in slices] == [0, 0, 0, 0, 1, 1, 1, 1]
+    for i, (_, c) in enumerate(slices):
+        assert len(c) == 8 and c == set(range(8 * i, 8 * i + 8))
+    cons, prod = numa.split_consumer_producers(slices[1][1], 2)
+    assert cons == {8, 9, 10, 11} and prod == {12, 13, 14, 15}
+    cons, prod = numa.split_consumer_producers(slices[1][1], 3)  # 4 + 2*3 > 8: no split
+    assert cons == prod == slices[1][1]
+    assert numa.rank_cpu_slice(0, 1, allowed) == (0, set(range(32)))  # alone on the node: all of it
+
+
 def test_normalize_columns_cpu_reference():
     import numpy as np
     import torch
