@@ -362,6 +362,9 @@ def main(argv=None) -> int:
             "h2d_enqueued_bytes_timed": bytes_enq1 - bytes_enq0,
             "windows_prestaged_at_t0": max(0, w_land0 - w_cur0),
             "numa_node": gpu_numa_node(env.local_rank) if dev.type == "cuda" else None,
+            "cpus": ({"consumer": len(conn.cpu_layout["consumer_cpus"]),
+                      "producers": len(conn.cpu_layout["producer_cpus"])} if conn.cpu_layout
+                     else {"shared": len(os.sched_getaffinity(0))}),
         }
         stats = dl.stats()
         if host_log:  # per-iteration host time of the timed loop (debug): the slow iterations

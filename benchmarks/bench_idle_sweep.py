@@ -155,6 +155,7 @@ def main(argv=None) -> int:
                 for _ in range(a.warmup):
                     step(next(it))
                 meter = ComputeIdleMeter()
+                nd0 = dl.stats().get("native_dispatch") or {}
                 torch.cuda.synchronize()
                 t2 = time.perf_counter()
                 with trace_range(f"sweep.p{i:02d}"):
@@ -175,6 +176,11 @@ def main(argv=None) -> int:
                       "achieved_per_s": round(B * a.steps / (t3 - t2), 1),
                       "gpu_idle_pct": round(res["gpu_idle_pct"], 3), "predicted_idle_pct": round(pred, 3),
                       "error_pp": round(res["gpu_idle_pct"] - pred, 3)}
+                nd1 = dl.stats().get("native_dispatch") or {}
+                if nd1:  # per point: batches built ahead (lookahead hits), batches the compute stream waited for
+                    pt["dispatch"] = {"mode": nd1.get("mode"),
+                                      **{k: nd1.get(k, 0) - nd0.get(k, 0)
+                                         for k in ("batches", "lookahead_hits", "compute_waits")}}
                 points.append(pt)
                 print(json.dumps(pt), flush=True)
             stats = dl.stats()

@@ -74,9 +74,9 @@ def start(n_producers: int | None = None, init_dist: bool = True, backend: str |
     from ..utils.numa import bind_to_gpu_numa, partition_after_spawn
 
     # before spawning: the producers inherit the rank's CPU slice of its GPU's NUMA node
-    bind_to_gpu_numa(env.local_rank, env.local_world_size)
+    node = bind_to_gpu_numa(env.local_rank, env.local_world_size)
     conn = spawn_producers(env, timeout_s, env_overrides) if env.n_producers > 0 else None
-    if conn is not None:
+    if conn is not None and node is not None:  # a GPU host: split the slice between consumer and producers
         pids = [p for p in conn.producer_pids if p and p != os.getpid()]  # thread-mode producers: none
         conn.cpu_layout = partition_after_spawn(pids, len(pids)) if len(pids) == env.n_producers else None
     created_pg = False

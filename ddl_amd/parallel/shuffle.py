@@ -122,14 +122,20 @@ class GlobalShuffler:
             ev[1].record()
             self._timing.append(ev)
             if len(self._timing) > 64:
-                self._resolve()
+                self._resolve(block=False)
         self.host_s += time.perf_counter() - t0
 
-    def _resolve(self) -> None:
-        for a, b in self._timing:
-            b.synchronize()
+    def _resolve(self, block: bool = True) -> None:
+        """Fold finished exchanges' device time into the total. ``block=False`` (the hot path) only takes
+        the ones that already retired, oldest first: never a host wait on an exchange still in flight."""
+        while self._timing:
+            a, b = self._timing[0]
+            if block:
+                b.synchronize()
+            elif not b.query():
+                break
             self._device_ms += a.elapsed_time(b)
-        self._timing.clear()
+            self._timing.pop(0)
 
     def stats(self) -> dict:
         """Exchange counters: calls, bytes sent to peers, host issue time, device time (ms)."""
