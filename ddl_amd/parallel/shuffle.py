@@ -96,6 +96,23 @@ class GlobalShuffler:
         self.host_s = 0.0
         self._timing: list = []  # (start, end) device events of the exchanges, resolved by stats()
         self._device_ms = 0.0
+        if self.device.type == "cuda" and self.world > 1 and self.n_exchange > 0:
+            self.warm_up()
+
+    def warm_up(self) -> None:
+        """Run this method's transfer pattern once on scratch buffers of the exchange's size, at
+        construction (every rank builds its loader at the same point of the program): RCCL sets up its
+        peer connections and buffers on the first transfer to each peer, which would otherwise land on
+        the first windows of the run."""
+        issue(self.env, self.group, "loader.exchange_warmup")
+        n = self.n_exchange * self.row_elems * _dtypes.itemsize(self.dtype)
+        send = torch.zeros(n, dtype=torch.uint8, device=self.device)
+        recv = torch.empty_like(send)
+        self._transfer(send, recv, 0)
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def _transfer(self, send: torch.Tensor, recv: torch.Tensor, window: int) -> None:  # pragma: no cover
+        raise NotImplementedError
 
     def _n_exchange(self) -> int:
         return int(self.n_rows * self.fraction)
@@ -143,8 +160,25 @@ class GlobalShuffler:
         return {"exchange_calls": self.calls, "rccl_bytes": self.bytes_sent,
                 "exchange_ms": round(self._device_ms, 3), "exchange_host_s": round(self.host_s, 4)}
 
-    def global_shuffle(self, win_bytes: torch.Tensor, window: int) -> None:  # pragma: no cover - abstract
-        raise NotImplementedError
+    def global_shuffle(self, win_bytes: torch.Tensor, window: int) -> None:
+        """Trade this window's ``n_exchange`` rows selected by ``rows_perm(window)``: gather them into a
+        contiguous send buffer, run the method's ``_transfer`` on the DP group, scatter the received rows
+        back into the same positions (all on the current stream: the stager's post-copy stream)."""
+        n_ex = self.n_exchange
+        if n_ex == 0:
+            return
+        rows = self._rows(win_bytes)
+        px = self.rows_perm(window)
+        send = ops.gather_rows(rows, perm=px, base=0, n_rows=n_ex)
+        recv = torch.empty_like(send)
+        self._transfer(send.view(-1).view(torch.uint8), recv.view(-1).view(torch.uint8), window)
+        idx = ops.feistel_indices(px, 0, n_ex, device=rows.device)
+        ops.scatter_rows(rows, recv, idx)
+        self.calls += 1
+        self.bytes_sent += self._peer_bytes(send.numel() * send.element_size())
+
+    def _peer_bytes(self, n: int) -> int:
+        return n
 
 
 class AllToAllGlobalShuffler(GlobalShuffler):
@@ -154,21 +188,13 @@ class AllToAllGlobalShuffler(GlobalShuffler):
         n = int(self.n_rows * self.fraction)
         return n // self.world * self.world
 
-    def global_shuffle(self, win_bytes: torch.Tensor, window: int) -> None:
+    def _peer_bytes(self, n: int) -> int:
+        return n * (self.world - 1) // self.world  # the chunk for self stays
+
+    def _transfer(self, send: torch.Tensor, recv: torch.Tensor, window: int) -> None:
         import torch.distributed as dist
 
-        n_ex = self.n_exchange
-        if n_ex == 0:
-            return
-        rows = self._rows(win_bytes)
-        px = self.rows_perm(window)
-        send = ops.gather_rows(rows, perm=px, base=0, n_rows=n_ex)
-        recv = torch.empty_like(send)
-        dist.all_to_all_single(recv.view(-1).view(torch.uint8), send.view(-1).view(torch.uint8), group=self.group)
-        idx = ops.feistel_indices(px, 0, n_ex, device=rows.device)
-        ops.scatter_rows(rows, recv, idx)
-        self.calls += 1
-        self.bytes_sent += send.numel() * send.element_size() * (self.world - 1) // self.world
+        dist.all_to_all_single(recv, send, group=self.group)
 
 
 class SendRecvReplaceGlobalShuffler(GlobalShuffler):
@@ -187,32 +213,21 @@ class SendRecvReplaceGlobalShuffler(GlobalShuffler):
         window from (seed, window), identical on every rank, nothing communicated."""
         return self.partners(window)
 
-    def global_shuffle(self, win_bytes: torch.Tensor, window: int) -> None:
+    def _transfer(self, send: torch.Tensor, recv: torch.Tensor, window: int) -> None:
+        """First half of the rows to ``send_to`` / from ``recv_from``, second half the other way round
+        (reference ddl/shuffle.py:95-108), as one batch of point-to-point ops on the DP group."""
         import torch.distributed as dist
 
-        n_ex = self.n_exchange
-        if n_ex == 0:
-            return
-        rows = self._rows(win_bytes)
-        px = self.rows_perm(window)
-        send = ops.gather_rows(rows, perm=px, base=0, n_rows=n_ex)
-        recv = torch.empty_like(send)
-        half = n_ex // 2
+        half = send.numel() // 2
         send_to, recv_from = self.partners(window)
-        sb = send.view(n_ex, -1)
-        rb = recv.view(n_ex, -1)
         p2p = [
-            dist.P2POp(dist.isend, sb[:half].contiguous(), send_to, group=self.group),
-            dist.P2POp(dist.irecv, rb[:half], recv_from, group=self.group),
-            dist.P2POp(dist.isend, sb[half:].contiguous(), recv_from, group=self.group),
-            dist.P2POp(dist.irecv, rb[half:], send_to, group=self.group),
+            dist.P2POp(dist.isend, send[:half], send_to, group=self.group),
+            dist.P2POp(dist.irecv, recv[:half], recv_from, group=self.group),
+            dist.P2POp(dist.isend, send[half:], recv_from, group=self.group),
+            dist.P2POp(dist.irecv, recv[half:], send_to, group=self.group),
         ]
         for req in dist.batch_isend_irecv(p2p):
             req.wait()
-        idx = ops.feistel_indices(px, 0, n_ex, device=rows.device)
-        ops.scatter_rows(rows, recv, idx)
-        self.calls += 1
-        self.bytes_sent += send.numel() * send.element_size()
 
 
 _METHODS = {
