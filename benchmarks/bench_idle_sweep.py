@@ -52,6 +52,14 @@ def _parse(argv=None):
                          "per-batch host cost)")
     ap.add_argument("--window", type=int, default=256)
     ap.add_argument("--producers", type=int, default=None)
+    ap.add_argument("--depth", type=int, default=None, help="HBM prefetch depth (windows); default: the loader's")
+    ap.add_argument("--tokens-k", type=int, default=1,
+                    help="tokens: global batches per window (k-batch windows amortise the per-window host path)")
+    ap.add_argument("--floor", action="store_true",
+                    help="after each point, run the same step on one held batch (no loader) with the same meter: "
+                         "the idle the measurement itself shows without any loader work (floor_idle_pct)")
+    ap.add_argument("--dispatch", default="auto", help="native_dispatch of the image loader (auto / inline / "
+                                                         "lookahead / python)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
 
@@ -70,7 +78,9 @@ def _image_loader(a, env, conn, n_steps):
     n_epochs = math.ceil(n_steps / max(1, a.window // B)) + 2
     dl = ddl_amd.DistributedDataLoader(
         ImageWindowProducer(a.window, (3, 224, 224), a.source_dtype, refill="stamp"), B, conn, n_epochs,
-        env=env, device=torch.device(env.device), out_dtype=torch.bfloat16, shuffle="device", normalize=norm)
+        env=env, device=torch.device(env.device), out_dtype=torch.bfloat16, shuffle="device", normalize=norm,
+        native_dispatch=False if a.dispatch == "python" else a.dispatch,
+        **({"prefetch_depth": a.depth} if a.depth else {}))
 
     def gen():
         while True:
@@ -88,8 +98,10 @@ def _token_loader(a, env, conn, n_steps, src):
 
     B = a.batch or 2048
     n_epochs = n_steps // (src.n // B) + 2
-    dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(src, B, 4096, "pack", pack_order="ffd"), B, conn,
-                                       n_epochs, mode="indexed", env=env, collate="tokens", auto_mark=True)
+    dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(src, B, 4096, "pack", pack_order="ffd",
+                                                          batches_per_window=a.tokens_k), B, conn,
+                                       n_epochs, mode="indexed", env=env, collate="tokens", auto_mark=True,
+                                       **({"prefetch_depth": a.depth} if a.depth else {}))
 
     def gen():
         while True:
@@ -108,6 +120,7 @@ def main(argv=None) -> int:
     from ddl_amd.utils.tracing import ComputeIdleMeter, trace_range
 
     ratios = [float(x) for x in a.ratios.split(",") if x]
+    host_marks = os.environ.get("DDL_SWEEP_MARKERS", "0") == "1"
     n_steps = a.warmup + 2 * a.feed_steps + len(ratios) * (a.steps + a.warmup + 30)
     src = None
     if a.family == "tokens":
@@ -160,7 +173,11 @@ def main(argv=None) -> int:
                 t2 = time.perf_counter()
                 with trace_range(f"sweep.p{i:02d}"):
                     for _ in range(a.steps):
-                        batch = next(it)
+                        if host_marks:  # DDL_SWEEP_MARKERS=1: the host's mark + get per step, for trace_gaps
+                            with trace_range("sweep.get"):
+                                batch = next(it)
+                        else:
+                            batch = next(it)
                         meter.step_begin()
                         step(batch)
                         meter.step_end()
@@ -176,6 +193,17 @@ def main(argv=None) -> int:
                       "achieved_per_s": round(B * a.steps / (t3 - t2), 1),
                       "gpu_idle_pct": round(res["gpu_idle_pct"], 3), "predicted_idle_pct": round(pred, 3),
                       "error_pp": round(res["gpu_idle_pct"] - pred, 3)}
+                if a.floor:  # the same step on one held batch, no loader calls: the meter's own floor
+                    fm = ComputeIdleMeter()
+                    torch.cuda.synchronize()
+                    with trace_range(f"sweep.floor{i:02d}"):
+                        for _ in range(a.steps):
+                            fm.step_begin()
+                            step(batch)
+                            fm.step_end()
+                        torch.cuda.synchronize()
+                    pt["floor_idle_pct"] = round(fm.result()["gpu_idle_pct"], 3)
+                    pt["error_vs_floor_pp"] = round(res["gpu_idle_pct"] - max(pred, pt["floor_idle_pct"]), 3)
                 nd1 = dl.stats().get("native_dispatch") or {}
                 if nd1:  # per point: batches built ahead (lookahead hits), batches the compute stream waited for
                     pt["dispatch"] = {"mode": nd1.get("mode"),

@@ -52,6 +52,7 @@ from .utils import streams
 from .utils.tracing import LoaderMetrics, trace_range
 
 STATE_VERSION = 1
+_TRACE_ENGINE = os.environ.get("DDL_TRACE_ENGINE", "0") == "1"
 MODES = ("do_not_split_along_epoch", "split_along_epoch", "window", "indexed")
 
 
@@ -453,7 +454,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
         The K slots' views of an output come from ONE strided view + ``unbind`` (per-slot slicing cost
         ~9 us per batch of host time on the box: three tensor ops per output per slot)."""
         K = self._eng_block
-        with streams.on_stream(self._batch_stream):
+        with streams.on_stream(self._batch_stream), trace_range("ddl.engine.provide"):
             block = torch.empty(K * self._eng_slot_bytes, dtype=torch.uint8, device=self.device)
         base, sb, per_group, ptrs = block.data_ptr(), self._eng_slot_bytes, [], [[] for _ in range(K)]
         for sh, dt, off in self._eng_layout:
@@ -512,7 +513,11 @@ class DistributedDataLoader(DistributedDataloaderABC):
                 self._ensure_posted(w)
             # the engine's cross-window lookahead reads w + 1: only once its exchange is issued
             nxt = nxt and (w + 1) in posted
-        slot, prod, tags = eng.get(w, local, bpw, nxt, handle, self._timeout_ms)
+        if _TRACE_ENGINE:  # roctx range per native get (DDL_TRACE_ENGINE=1: host timeline under rocprofv3)
+            with trace_range("ddl.engine.get"):
+                slot, prod, tags = eng.get(w, local, bpw, nxt, handle, self._timeout_ms)
+        else:
+            slot, prod, tags = eng.get(w, local, bpw, nxt, handle, self._timeout_ms)
         if slot < 0:
             self._engine_raise(slot, prod, f"batch {local} of window {w}")
         if local == 0 and self._verify is not None:

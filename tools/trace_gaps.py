@@ -5,9 +5,10 @@
 compute stream (the stream that ran the most kernel time in the range: the train step's) sat idle
 between two of its kernels. Each gap longer than ``--min-us`` is put in one bucket:
 
-* ``batch_kernel``: a loader kernel on another stream (the batch gather / collate) ended inside the
-  gap, or within ``--slack-us`` after it -- the compute stream waited for the batch (cross-stream
-  event wait);
+* ``batch_kernel``: a loader kernel on another stream (the batch gather / collate) ran inside the
+  gap (or ended within ``--slack-us`` of it) -- the compute stream waited for the batch (cross-stream
+  event wait); ``batch_kernel_after_h2d_copy`` when an H2D copy also landed in the gap: the batch
+  kernel itself had waited for its window's copy;
 * ``h2d_copy``: an H2D copy ended inside the gap -- the batch's window was still in flight;
 * ``host``: neither -- nothing on the device was pending, the host had not enqueued the next
   kernel yet (launch latency, a blocking host call).
@@ -51,8 +52,8 @@ def main(argv=None) -> int:
         busy[(r["Agent_Id"], r["Queue_Id"])] += e - s
     compute_q = busy.most_common(1)[0][0]
     comp = sorted((_ts(r) + (r["Kernel_Name"],) for r in inside if (r["Agent_Id"], r["Queue_Id"]) == compute_q))
-    loader_ends = sorted(_ts(r)[1] for r in inside if (r["Agent_Id"], r["Queue_Id"]) != compute_q
-                         and any(k in r["Kernel_Name"] for k in LOADER_KERNELS))
+    loader = sorted(_ts(r) for r in inside if (r["Agent_Id"], r["Queue_Id"]) != compute_q
+                    and any(k in r["Kernel_Name"] for k in LOADER_KERNELS))
     copy_ends = sorted(_ts(r)[1] for r in copies if r["Direction"].endswith("HOST_TO_DEVICE")
                        and _ts(r)[1] > lo and _ts(r)[0] < hi)
 
@@ -69,9 +70,17 @@ def main(argv=None) -> int:
         g = s1 - e0
         if g < a.min_us * 1000:
             continue
-        if ends_in(loader_ends, e0, s1 + slack):
+        # a loader kernel running in the gap, or ending within the slack of its end (queues' clocks
+        # differ by a few us): the compute stream waited for the batch; if an H2D copy landed in the
+        # gap too, the batch kernel itself waited for its window's copy
+        j = bisect.bisect_left(loader, (e0 - slack, 0))
+        waited = any(a0 < s1 + slack and b0 > e0 for a0, b0 in loader[max(0, j - 4):j + 8])
+        copy_late = ends_in(copy_ends, e0, s1 + slack)
+        if waited and copy_late:
+            b = "batch_kernel_after_h2d_copy"
+        elif waited:
             b = "batch_kernel"
-        elif ends_in(copy_ends, e0, s1 + slack):
+        elif copy_late:
             b = "h2d_copy"
         else:
             b = "host"
