@@ -3,6 +3,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
+#include <string>
 
 #include "launch.h"
 
@@ -30,6 +32,21 @@ uint64_t clock_ns() {
 
 constexpr int kBatchEvents = 16;  // lookahead is 1 batch; a ring this deep never re-records an unwaited event
 constexpr int kFreeEvents = 4;
+
+// Flags of the engine's synchronisation events (batch-ready, free, join). They order work between
+// streams of ONE device; a recorded event's default system-scope release (L2 writeback + invalidate,
+// for host visibility) is more than that needs. DDL_EVENT_SCOPE: "system" (HIP default), "device"
+// (hipEventReleaseToDevice: device-scope release), "nofence" (hipEventDisableSystemFence).
+unsigned event_flags() {
+  static const unsigned flags = [] {
+    const char* v = std::getenv("DDL_EVENT_SCOPE");
+    const std::string s = v == nullptr ? "system" : v;
+    if (s == "device") return static_cast<unsigned>(hipEventDisableTiming | hipEventReleaseToDevice);
+    if (s == "nofence") return static_cast<unsigned>(hipEventDisableTiming | hipEventDisableSystemFence);
+    return static_cast<unsigned>(hipEventDisableTiming);
+  }();
+  return flags;
+}
 
 }  // namespace
 
@@ -66,15 +83,15 @@ BatchEngine::BatchEngine(NativeStager* stager, BatchRecipe recipe, int32_t n_pro
   if (hipSetDevice(device_) != hipSuccess) throw std::runtime_error("BatchEngine: hipSetDevice failed");
   batch_events_.resize(kBatchEvents);
   for (auto& e : batch_events_)
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+    if (hipEventCreateWithFlags(&e, event_flags()) != hipSuccess)
       throw std::runtime_error("BatchEngine: hipEventCreate failed");
   free_events_.assign(buffers_.size(), std::vector<hipEvent_t>(kFreeEvents, nullptr));
   for (auto& v : free_events_)
     for (auto& e : v)
-      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+      if (hipEventCreateWithFlags(&e, event_flags()) != hipSuccess)
         throw std::runtime_error("BatchEngine: hipEventCreate failed");
   free_next_.assign(buffers_.size(), 0);
-  if (hipEventCreateWithFlags(&ww_ev_, hipEventDisableTiming) != hipSuccess)
+  if (hipEventCreateWithFlags(&ww_ev_, event_flags()) != hipSuccess)
     throw std::runtime_error("BatchEngine: hipEventCreate failed");
 }
 
@@ -445,7 +462,7 @@ hipEvent_t BatchEngine::join_event() {
   // (hipStreamWaitEvent captures the event's state at enqueue time)
   if (join_events_.size() < kJoinEvents) {
     hipEvent_t e = nullptr;
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&e, event_flags()) != hipSuccess) return nullptr;
     join_events_.push_back(e);
     return e;
   }

@@ -353,3 +353,37 @@ def test_window_dispatch_batches_on_other_streams():
     assert len(out) == len(ref) > 0
     for a, b in zip(out, ref):
         assert torch.equal(a, b)
+
+
+def test_inline_dispatch_window_read_on_two_streams_is_not_overwritten():
+    """Inline mode: the batches of one window are launched on two streams; the window's FIRST batch goes
+    to a stream held back by a long GEMM chain, the later ones to the default stream. The window's ring
+    buffer goes back to the stager (depth 1: the next copy lands in the SAME buffer) only behind BOTH
+    streams' reads, so the delayed batch still sees its own window."""
+    make = lambda: (IdProducer(64, 8), 16)  # noqa: E731
+    kw = dict(shuffle="device", seed=3, contiguous=True, prefetch_depth=1)
+    ref, _ = _collect(False, make, epochs=3, **kw)
+    slow = torch.cuda.Stream()
+    a = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+    out = []
+    with ddl_amd.start(n_producers=3) as (env, conn):
+        prod, bs = make()
+        dl = ddl_amd.DistributedDataLoader(prod, bs, conn, 3, env=env, native_dispatch="inline", **kw)
+        for e in range(3):
+            held = []
+            for i in range(len(dl)):
+                if i == 0:  # the window's first batch, on a stream busy for tens of ms
+                    with torch.cuda.stream(slow):
+                        for _ in range(60):
+                            a = a @ a * 1e-3
+                        held.append(dl[i])
+                else:
+                    held.append(dl[i])
+                dl.mark(Marker.END_OF_BATCH)
+            dl.mark(Marker.END_OF_EPOCH)
+            torch.cuda.synchronize()
+            out += [torch.cat([t.reshape(t.shape[0], -1).float() for t in b], 1).cpu() for b in held]
+        assert dl.stats()["native_dispatch"]["mode"] == "inline"
+    assert len(out) == len(ref) > 0
+    for x, y in zip(out, ref):
+        assert torch.equal(x, y)

@@ -406,3 +406,20 @@ def test_fixed_token_rows_gpu_native_and_python():
                         assert a[x] == b[x], (native, x)
     finally:
         src.close()
+
+
+def test_view_cache_entries_of_a_dropped_ring_are_forgotten():
+    """The collate view cache holds views of staging buffers; closing a stager (live seek / close)
+    drops that ring's entries so the cache does not keep its memory alive."""
+    from ddl_amd.models import tokens as tk
+
+    lay = tk.TokenWindowLayout(batch=4, seq_len=16, max_len=20, k=2)
+    a = torch.zeros(lay.nbytes, dtype=torch.uint8)
+    b = torch.zeros(lay.nbytes, dtype=torch.uint8)
+    for sub in range(2):
+        tk._cached_views(a, lay, sub)
+        tk._cached_views(b, lay, sub)
+    assert tk.drop_cached_views([a.data_ptr()]) == 2
+    assert not any(k[0] == a.data_ptr() for k in tk._VIEW_CACHE)
+    assert sum(1 for k in tk._VIEW_CACHE if k[0] == b.data_ptr()) == 2
+    tk.drop_cached_views([b.data_ptr()])
