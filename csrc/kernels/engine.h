@@ -191,6 +191,7 @@ class BatchEngine {
   int hand_back(int64_t w, const StagedInfo& info, hipStream_t st);
   int64_t bpw_of(const StagedInfo& info) const;
   bool early_ = true;
+  bool host_wait_ = false;  // DDL_ENGINE_HOST_WAIT=1 (diagnostics): hipEventSynchronize instead of a stream wait
   std::vector<int64_t> bpw_;
   std::set<int64_t> handed_back_;  // windows whose buffer went back to the stager before release()
 };
