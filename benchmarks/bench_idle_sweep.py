@@ -53,6 +53,9 @@ def _parse(argv=None):
     ap.add_argument("--window", type=int, default=256)
     ap.add_argument("--producers", type=int, default=None)
     ap.add_argument("--depth", type=int, default=None, help="HBM prefetch depth (windows); default: the loader's")
+    ap.add_argument("--feed-keepalive", action="store_true",
+                    help="keep the GPU busy with low-priority GEMMs while the feed rate F is measured (a GPU idling "
+                         "between loader kernels runs the host-latency-bound token path slower than under a step)")
     ap.add_argument("--tokens-k", type=int, default=1,
                     help="tokens: global batches per window (k-batch windows amortise the per-window host path)")
     ap.add_argument("--floor", action="store_true",
@@ -149,11 +152,18 @@ def main(argv=None) -> int:
             for _ in range(a.warmup):
                 read(next(it))
             feeds = []
+            keep = None
+            if a.feed_keepalive:  # GEMMs on a low-priority stream keep the GPU busy (clocks up) during the feed
+                keep = (torch.cuda.Stream(dev, priority=0), torch.randn(2048, 2048, device=dev, dtype=torch.bfloat16))
             for rep in range(2):
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 with trace_range(f"sweep.feed{rep}"):
-                    for _ in range(a.feed_steps):
+                    for k in range(a.feed_steps):
+                        if keep is not None and k % 8 == 0:
+                            with torch.cuda.stream(keep[0]):
+                                for _ in range(8):
+                                    torch.mm(keep[1], keep[1])
                         read(next(it))
                     torch.cuda.synchronize()
                 feeds.append(B * a.feed_steps / (time.perf_counter() - t0))

@@ -259,3 +259,26 @@ def test_trace_idle_analyse_regions():
     assert r["loader_kernel_pct"] == 60.0
     assert r["copy_busy_pct"] == 50.0
     assert r["kernel_dispatches"] == 3
+
+
+def test_numa_local_source_and_memory_binding():
+    """Per-NUMA-node replica of a node-shared array: created by the node's first rank, bound to the node
+    with mbind, filled; pages report the node (move_pages)."""
+    import numpy as np
+    import torch
+
+    from ddl_amd.models import numa_local_source
+    from ddl_amd.types import DDLEnv
+
+    env = DDLEnv(rank=0, world_size=1, local_rank=0, local_world_size=1)
+    name = f"ddl_amd_numa_t{np.random.randint(1 << 30)}"
+    src, node, created = numa_local_source(name, 64, (16,), "float32", env,
+                                           fill=lambda t: t.copy_(torch.arange(64 * 16.0).view(64, 16)))
+    try:
+        assert created and src.name.startswith(name + "_numa")
+        assert torch.equal(src.tensor().view(-1), torch.arange(64 * 16.0))
+        assert src.bind_to_node(0) == 0  # node 0 exists on every Linux host
+        pages = src.page_nodes(8)
+        assert pages and all(p == 0 for p in pages)
+    finally:
+        src.close()

@@ -8,3 +8,4 @@ run 200 bd_hw env DDL_ENGINE_HOST_WAIT=1 python bench.py --gpus 1 --steps 20 --w
 run 200 bd_sw python bench.py --gpus 1 --steps 20 --warmup 5 --json-out gpurun_out/bd_sw.json
 run 200 bd_hw200 env DDL_ENGINE_HOST_WAIT=1 python bench.py --order window --json-out gpurun_out/bd_hw200.json
 run 200 bd_sw200 python bench.py --order window --json-out gpurun_out/bd_sw200.json
+run 300 tok_k8_keep python benchmarks/bench_idle_sweep.py --family tokens --tokens-k 8 --floor --feed-keepalive --json-out gpurun_out/tok_k8_keep.jsonl
