@@ -129,7 +129,10 @@ def main(argv=None) -> int:
     if a.family == "tokens":
         from ddl_amd.models.tokens import SharedTokenSource
 
+        from ddl_amd.utils.numa import gpu_numa_node
+
         src = SharedTokenSource.synthetic(f"ddl_amd_sweep_{os.getpid()}", 8192, 256, 4096, seed=1)
+        src.bind_to_node(gpu_numa_node(0))  # next to the producers (bound to the GPU's node)
     producers = a.producers or (3 if a.family == "images" else 4)
     points = []
     try:

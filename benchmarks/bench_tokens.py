@@ -55,7 +55,10 @@ def main(argv=None):
     name = f"ddl_amd_benchtok_{os.environ.get('MASTER_PORT', '0')}"
     src = None
     if int(os.environ.get("LOCAL_RANK", "0")) == 0:
+        from ddl_amd.utils.numa import gpu_numa_node
+
         src = SharedTokenSource.synthetic(name, a.n_seqs, a.min_len, a.seq_len, seed=1)
+        src.bind_to_node(gpu_numa_node(int(os.environ.get("LOCAL_RANK", "0"))))  # the producers' node
     gb = a.batch * world
     try:
         with ddl_amd.start(n_producers=a.producers) as (env, conn):

@@ -137,6 +137,14 @@ class SharedTokenSource:
         toks = rng.integers(0, vocab, size=int(offs[-1]), dtype=np.int32)
         return cls.create(name, toks, offs)
 
+    def bind_to_node(self, node: int | None) -> int:
+        """Place the corpus on NUMA ``node`` (pages migrate; see ``SharedArraySource.bind_to_node``): the
+        producers' ragged gathers are latency-bound reads of ~8 KB runs, which cost far more from the
+        other socket. ``None`` (node unknown) is a no-op. 0 or -errno."""
+        if node is None:
+            return 0
+        return self.tokens.bind_to_node(node) or self.offsets.bind_to_node(node)
+
     def close(self) -> None:
         self.tokens.close()
         self.offsets.close()
