@@ -29,8 +29,11 @@ barrier + synchronize; max time over ranks. ``value`` is the SMALLER of
   * delivered: samples handed to the consumer in the timed region / time, and
   * landed: samples whose H2D copy retired in the timed region / time
     (counted by the stager's post-DMA host callback),
-so windows staged in HBM before t0 cannot inflate a short run; both are in
-the JSON line, with the H2D bytes and GB/s of the timed region.
+so windows staged in HBM before t0 cannot inflate a short run -- and of
+  * enqueued: samples whose H2D copy was enqueued in the timed region (all of
+    them land before the closing synchronize), so a copy already in flight at
+    t0 is not counted either;
+all three are in the JSON line, with the H2D bytes and GB/s of the timed region.
 Phase 2 (``gpu_idle_pct``): a fixed-cost bf16 train step (PatchMLP fwd+bwd+SGD)
 consumes the batches; the compute stream's idle fraction is measured with HIP
 events (idle = 1 - busy/wall). ``benchmarks/bench_idle_sweep.py`` sweeps a
@@ -63,7 +66,10 @@ def parse(argv=None):
     ap.add_argument("--window", type=int, default=256, help="samples per producer window")
     ap.add_argument("--producers", type=int, default=3)
     ap.add_argument("--slots", type=int, default=1, help="windows per producer")
-    ap.add_argument("--depth", type=int, default=2, help="HBM prefetch depth (windows)")
+    ap.add_argument("--depth", type=int, default=4,
+                    help="HBM prefetch depth (windows; 4 x 77 MB of HBM): deep enough that the copy engine restarts "
+                         "without a gap after the barrier + synchronize that opens the timed region "
+                         "(profiles/r3_variance: 20-step spread 176.7-188.1k at depth 2-3, 187.5-188.1k at 4)")
     ap.add_argument("--source-dtype", default="bfloat16", choices=["bfloat16", "uint8", "float32"])
     ap.add_argument("--refill", default="stamp", choices=["stamp", "full"],
                     help="producer work per round: stamp = one element per sample; full = rewrite every byte of "
@@ -387,7 +393,8 @@ def main(argv=None) -> int:
         }
         mine["stager_wait_producer_s_timed"] = round(stats.get("stager_wait_producer_s", 0.0) - wait_prod0, 4)
         nd = stats.get("native_dispatch")
-        mine["dispatch"] = {"mode": nd.get("mode"), "host_us_per_batch": nd.get("host_us_per_batch"),
+        mine["dispatch"] = {"mode": nd.get("mode"), "handoff": nd.get("handoff"),
+                            "host_us_per_batch": nd.get("host_us_per_batch"),
                             "compute_waits": nd.get("compute_waits")} if nd else {"mode": "python"}
         mine["stager_wait_producer_s"] = round(stats.get("stager_wait_producer_s", 0.0), 4)
         mine["exchange_issue_wait_s"] = stats.get("exchange_issue_wait_s", 0.0)
@@ -402,7 +409,14 @@ def main(argv=None) -> int:
         elapsed = max(r["elapsed_s"] for r in per_rank)
         delivered = args.batch * args.steps * env.world_size / elapsed
         landed = sum(r["landed_per_s"] * r["elapsed_s"] for r in per_rank) / elapsed
-        value = min(delivered, landed) if landed > 0 else delivered
+        # copies ENQUEUED in the timed region all land before its closing synchronize; a copy already in
+        # flight at t0 (enqueued while the opening synchronize ran) lands inside the region but moved part
+        # of its bytes before t0: counting only the enqueued ones keeps it out
+        enqueued = sum(r["h2d_enqueued_bytes_timed"] for r in per_rank) / sample_bytes / elapsed
+        if dev.type == "cuda":
+            value = min(delivered, landed, enqueued)
+        else:  # CPU rehearsal: no H2D, the host path delivers straight from the windows
+            value = min(delivered, landed) if landed > 0 else delivered
 
         # ---------------- phase 2: GPU idle % behind a fixed-cost train step
         idle = {}
@@ -462,6 +476,7 @@ def main(argv=None) -> int:
                 },
                 "delivered_samples_per_s": round(delivered, 1),
                 "landed_samples_per_s": round(landed, 1),
+                "enqueued_samples_per_s": round(enqueued, 1) if dev.type == "cuda" else None,
                 "h2d_bytes_timed": sum(r["h2d_bytes_timed"] for r in per_rank),
                 "h2d_gbps_timed": round(sum(r["h2d_bytes_timed"] for r in per_rank) / elapsed / 1e9, 3),
                 "sample_bytes": sample_bytes,

@@ -56,7 +56,7 @@ def _parse(argv=None):
     ap.add_argument("--feed-keepalive", action="store_true",
                     help="keep the GPU busy with low-priority GEMMs while the feed rate F is measured (a GPU idling "
                          "between loader kernels runs the host-latency-bound token path slower than under a step)")
-    ap.add_argument("--tokens-k", type=int, default=1,
+    ap.add_argument("--tokens-k", type=int, default=8,
                     help="tokens: global batches per window (k-batch windows amortise the per-window host path)")
     ap.add_argument("--floor", action="store_true",
                     help="after each point, run the same step on one held batch (no loader) with the same meter: "
@@ -101,9 +101,10 @@ def _token_loader(a, env, conn, n_steps, src):
 
     B = a.batch or 2048
     n_epochs = n_steps // (src.n // B) + 2
-    dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(src, B, 4096, "pack", pack_order="ffd",
+    dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(src, B, 4096, "pack", pack_order="ffd", host_threads=4,
                                                           batches_per_window=a.tokens_k), B, conn,
                                        n_epochs, mode="indexed", env=env, collate="tokens", auto_mark=True,
+                                       n_slots=2,
                                        **({"prefetch_depth": a.depth} if a.depth else {}))
 
     def gen():
@@ -133,7 +134,9 @@ def main(argv=None) -> int:
 
         src = SharedTokenSource.synthetic(f"ddl_amd_sweep_{os.getpid()}", 8192, 256, 4096, seed=1)
         src.bind_to_node(gpu_numa_node(0))  # next to the producers (bound to the GPU's node)
-    producers = a.producers or (3 if a.family == "images" else 4)
+    # tokens: 6 producers x 4 gather threads x 2 slots -- the host-bound feed then has headroom, so it is
+    # consumer-bound and stable from run to run (profiles/r3_tokens)
+    producers = a.producers or (3 if a.family == "images" else 6)
     points = []
     try:
         with ddl_amd.start(n_producers=producers) as (env, conn):

@@ -25,12 +25,12 @@ def main(argv=None):
     ap.add_argument("--seq-len", type=int, default=4096)
     ap.add_argument("--min-len", type=int, default=256)
     ap.add_argument("--n-seqs", type=int, default=8192)
-    ap.add_argument("--producers", type=int, default=4)
-    ap.add_argument("--slots", type=int, default=1, help="windows per producer (a producer fills one while the "
+    ap.add_argument("--producers", type=int, default=6)
+    ap.add_argument("--slots", type=int, default=2, help="windows per producer (a producer fills one while the "
                                                           "previous is in flight)")
     ap.add_argument("--batches-per-window", type=int, default=8,
                     help="global batches per producer window (per-window costs amortised over k batches)")
-    ap.add_argument("--host-threads", type=int, default=2, help="gather threads per producer")
+    ap.add_argument("--host-threads", type=int, default=4, help="gather threads per producer")
     ap.add_argument("--token-rows", default="exact", choices=["exact", "fixed"],
                     help="pack mode: exact packed rows per batch, or the window layout's fixed max rows (padding)")
     ap.add_argument("--dispatch", default="auto", choices=["auto", "inline", "lookahead", "window", "python"])

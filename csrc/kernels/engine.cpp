@@ -93,8 +93,6 @@ BatchEngine::BatchEngine(NativeStager* stager, BatchRecipe recipe, int32_t n_pro
   free_next_.assign(buffers_.size(), 0);
   if (hipEventCreateWithFlags(&ww_ev_, event_flags()) != hipSuccess)
     throw std::runtime_error("BatchEngine: hipEventCreate failed");
-  const char* hw = std::getenv("DDL_ENGINE_HOST_WAIT");
-  host_wait_ = hw != nullptr && std::string(hw) == "1";
 }
 
 BatchEngine::~BatchEngine() {
@@ -388,7 +386,7 @@ int64_t BatchEngine::get(int64_t w, int64_t local, int64_t bpw, bool next_ok, hi
   // every later dispatch on the device); only a pending one costs the compute stream a barrier.
   const hipError_t q = hipEventQuery(batch_events_[cur.ev]);
   if (q == hipErrorNotReady) {
-    if (host_wait_) {  // diagnostic (DDL_ENGINE_HOST_WAIT=1): the HOST waits for the batch kernel instead
+    if (host_wait_) {  // host hand-off: the HOST waits for the batch kernel, the compute stream needs no barrier
       if (hipEventSynchronize(batch_events_[cur.ev]) != hipSuccess) return -1;
     } else if (hipStreamWaitEvent(compute, batch_events_[cur.ev], 0) != hipSuccess) {
       return -1;

@@ -117,6 +117,13 @@ class BatchEngine {
   // Batches per window of each producer's windows (lets the lookahead know that (w + 1, 0) is the last
   // batch of a one-batch window).
   void set_batches_per_window(std::vector<int64_t> bpw) { bpw_ = std::move(bpw); }
+  // Hand-off of a lookahead batch whose kernel is still pending at get(): false (default) makes the
+  // compute stream wait for its event on the device; true makes the HOST wait for it
+  // (hipEventSynchronize). A device-side cross-queue wait costs the compute stream ~25 us per step on
+  // MI355X when it follows an H2D-fed kernel (profiles/r3_handoff); when the host runs ahead of the GPU
+  // -- the usual case -- the host wait costs nothing.
+  void set_host_handoff(bool on) { host_wait_ = on; }
+  bool host_handoff() const { return host_wait_; }
 
   double wait_s() const { return wait_ns_ * 1e-9; }
   // host ns spent in get() in total, and inside HIP calls: kernel launches, event records, stream waits
@@ -191,7 +198,7 @@ class BatchEngine {
   int hand_back(int64_t w, const StagedInfo& info, hipStream_t st);
   int64_t bpw_of(const StagedInfo& info) const;
   bool early_ = true;
-  bool host_wait_ = false;  // DDL_ENGINE_HOST_WAIT=1 (diagnostics): hipEventSynchronize instead of a stream wait
+  bool host_wait_ = false;  // host hand-off of lookahead batches (set_host_handoff)
   std::vector<int64_t> bpw_;
   std::set<int64_t> handed_back_;  // windows whose buffer went back to the stager before release()
 };

@@ -437,6 +437,11 @@ class DistributedDataLoader(DistributedDataloaderABC):
         # hand a window's ring buffer back to the stager at its last batch launch (DDL_EARLY_RELEASE=0: at
         # the consumer's release, one step later -- the round-2 behaviour, for A/B runs)
         self._engine.early_release = os.environ.get("DDL_EARLY_RELEASE", "1") != "0"
+        # lookahead batches still pending at get(): the host waits for them (no device-side cross-queue
+        # barrier on the compute stream) unless the exchange is on -- its kernels wait on peer ranks, and
+        # the host must never block on another rank's progress; DDL_HANDOFF=device|host overrides
+        handoff = os.environ.get("DDL_HANDOFF", "auto")
+        self._engine.host_handoff = handoff == "host" or (handoff == "auto" and self._exchange_fn is None)
         self._eng_mode = mode
         self._eng_slots: collections.deque = collections.deque()  # (slot id, outputs, block)
         self._eng_next_id = 0
@@ -1222,6 +1227,8 @@ class DistributedDataLoader(DistributedDataloaderABC):
                                            "event_record": round(rec / n / 1e3, 2),
                                            "stream_wait": round(sw / n / 1e3, 2)}
             nd["mode"] = getattr(self, "_eng_mode", None)
+            if self._engine is not None:
+                nd["handoff"] = "host" if self._engine.host_handoff else "device"
             d["native_dispatch"] = nd
         if self._stager is not None:
             d.update(self._stager.stats())
