@@ -335,25 +335,29 @@ def main(argv=None) -> int:
         for _ in range(args.warmup):
             (x,) = next(it)
             acc.add(x)
+        prod0 = conn.producer_stats()  # diagnostics: read before the region opens
+        wait_prod0 = dl.stats().get("stager_wait_producer_s", 0.0)
+        host_log = os.environ.get("DDL_HOST_LOG")
+        ticks = []
         barrier()
+        # t0 FIRST, then the copy counters: a copy enqueued or landing between the two moves bytes inside
+        # the region but is not counted (conservative); reading them first would count it with no time
+        t0 = time.perf_counter()
         w_land0, b_land0 = _landed(dl)
         w_cur0 = dl.window
         bytes_enq0 = dl._stager.bytes_h2d if dl._stager is not None else 0
-        prod0 = conn.producer_stats()
-        wait_prod0 = dl.stats().get("stager_wait_producer_s", 0.0)
-        t0 = time.perf_counter()
-        host_log = os.environ.get("DDL_HOST_LOG")
-        ticks = []
         with trace_range("bench.phase1"):  # roctx: lets tools/trace_idle.py find the timed region
             for _ in range(args.steps):
                 (x,) = next(it)
                 acc.add(x)
                 if host_log:
                     ticks.append(time.perf_counter())
+            # enqueued-copy counter BEFORE the closing synchronize: copies the stager enqueues while it
+            # runs may complete inside the region, but only those enqueued before it are counted
+            bytes_enq1 = dl._stager.bytes_h2d if dl._stager is not None else 0
             sync()
         t1 = time.perf_counter()
         w_land1, b_land1 = _landed(dl)
-        bytes_enq1 = dl._stager.bytes_h2d if dl._stager is not None else 0
         prod1 = conn.producer_stats()
         barrier()
         elapsed = t1 - t0
