@@ -7,3 +7,7 @@ for i in 1 2 3 4 5; do
   run 120 y_drv_$i python bench.py --gpus 1 --steps 20 --warmup 5 --json-out gpurun_out/y_drv_$i.json
 done
 run 300 y_default python bench.py --json-out gpurun_out/y_default.json
+for d in 2 4 6; do
+  run 300 dh_bf16_d$d python benchmarks/bench_idle_sweep.py --floor --depth $d --ratios 0.5,0.75,0.9,1.25,2.0 --json-out gpurun_out/dh_bf16_d$d.jsonl
+done
+run 300 dh_u8_d4 python benchmarks/bench_idle_sweep.py --floor --depth 4 --source-dtype uint8 --ratios 0.5,0.75,0.9,1.25,2.0 --json-out gpurun_out/dh_u8_d4.jsonl
