@@ -29,11 +29,11 @@ barrier + synchronize; max time over ranks. ``value`` is the SMALLER of
   * delivered: samples handed to the consumer in the timed region / time, and
   * landed: samples whose H2D copy retired in the timed region / time
     (counted by the stager's post-DMA host callback),
-so windows staged in HBM before t0 cannot inflate a short run -- and of
-  * enqueued: samples whose H2D copy was enqueued in the timed region (all of
-    them land before the closing synchronize), so a copy already in flight at
-    t0 is not counted either;
-all three are in the JSON line, with the H2D bytes and GB/s of the timed region.
+so windows staged in HBM before t0 cannot inflate a short run. A landed window
+counts only if its copy was also ENQUEUED inside the region (the native
+stager timestamps every copy): a copy already in flight at t0 moved part of
+its bytes before the region and is not counted. Both rates are in the JSON
+line, with the H2D bytes and GB/s of the timed region.
 Phase 2 (``gpu_idle_pct``): a fixed-cost bf16 train step (PatchMLP fwd+bwd+SGD)
 consumes the batches; the compute stream's idle fraction is measured with HIP
 events (idle = 1 - busy/wall). ``benchmarks/bench_idle_sweep.py`` sweeps a
@@ -283,9 +283,11 @@ def main(argv=None) -> int:
     from ddl_amd import Marker, ops
     from ddl_amd.models.producers import ImageWindowProducer
     from ddl_amd.parallel.order import LEDGER, check_same_order
+    from ddl_amd import _native
     from ddl_amd.utils.numa import gpu_numa_node
     from ddl_amd.utils.tracing import trace_range
 
+    rt = _native.runtime()  # CLOCK_MONOTONIC now_ns(), the native stager's clock
     n_world = int(os.environ.get("WORLD_SIZE", "1"))
     LEDGER.enable(n_world > 1)  # record every collective at issue; digests compared across ranks at the end
     idle_steps = args.steps if args.idle_steps < 0 else args.idle_steps
@@ -340,9 +342,10 @@ def main(argv=None) -> int:
         host_log = os.environ.get("DDL_HOST_LOG")
         ticks = []
         barrier()
-        # t0 FIRST, then the copy counters: a copy enqueued or landing between the two moves bytes inside
-        # the region but is not counted (conservative); reading them first would count it with no time
+        # the region's H2D work: copies ENQUEUED inside it (native stager timestamps, CLOCK_MONOTONIC) that
+        # retired by its end -- a copy already in flight at t0 moved bytes before it and is not counted
         t0 = time.perf_counter()
+        t0_ns = rt.now_ns()
         w_land0, b_land0 = _landed(dl)
         w_cur0 = dl.window
         bytes_enq0 = dl._stager.bytes_h2d if dl._stager is not None else 0
@@ -352,23 +355,27 @@ def main(argv=None) -> int:
                 acc.add(x)
                 if host_log:
                     ticks.append(time.perf_counter())
-            # enqueued-copy counter BEFORE the closing synchronize: copies the stager enqueues while it
-            # runs may complete inside the region, but only those enqueued before it are counted
-            bytes_enq1 = dl._stager.bytes_h2d if dl._stager is not None else 0
             sync()
         t1 = time.perf_counter()
+        t1_ns = rt.now_ns()
         w_land1, b_land1 = _landed(dl)
+        bytes_enq1 = dl._stager.bytes_h2d if dl._stager is not None else 0
+        if dl._stager is not None:
+            n_in, b_in = dl._stager._native.copies_between(t0_ns, t1_ns)
+        else:  # CPU rehearsal: the host path has no H2D; every delivered window counts
+            n_in, b_in = w_land1 - w_land0, 0
         prod1 = conn.producer_stats()
         barrier()
         elapsed = t1 - t0
-        landed_samples = (w_land1 - w_land0) * args.window
+        landed_samples = n_in * args.window
         mine = {
             "rank": env.rank,
             "elapsed_s": elapsed,
             "delivered_per_s": args.batch * args.steps / elapsed,
             "landed_per_s": landed_samples / elapsed,
-            "h2d_bytes_timed": b_land1 - b_land0,
-            "h2d_gbps_timed": (b_land1 - b_land0) / elapsed / 1e9,
+            "h2d_bytes_timed": b_in,
+            "h2d_gbps_timed": b_in / elapsed / 1e9,
+            "h2d_bytes_landed_any_enqueue_time": b_land1 - b_land0,
             "h2d_enqueued_bytes_timed": bytes_enq1 - bytes_enq0,
             "windows_prestaged_at_t0": max(0, w_land0 - w_cur0),
             "numa_node": gpu_numa_node(env.local_rank) if dev.type == "cuda" else None,
@@ -413,14 +420,7 @@ def main(argv=None) -> int:
         elapsed = max(r["elapsed_s"] for r in per_rank)
         delivered = args.batch * args.steps * env.world_size / elapsed
         landed = sum(r["landed_per_s"] * r["elapsed_s"] for r in per_rank) / elapsed
-        # copies ENQUEUED in the timed region all land before its closing synchronize; a copy already in
-        # flight at t0 (enqueued while the opening synchronize ran) lands inside the region but moved part
-        # of its bytes before t0: counting only the enqueued ones keeps it out
-        enqueued = sum(r["h2d_enqueued_bytes_timed"] for r in per_rank) / sample_bytes / elapsed
-        if dev.type == "cuda":
-            value = min(delivered, landed, enqueued)
-        else:  # CPU rehearsal: no H2D, the host path delivers straight from the windows
-            value = min(delivered, landed) if landed > 0 else delivered
+        value = min(delivered, landed) if landed > 0 else delivered
 
         # ---------------- phase 2: GPU idle % behind a fixed-cost train step
         idle = {}
@@ -480,7 +480,6 @@ def main(argv=None) -> int:
                 },
                 "delivered_samples_per_s": round(delivered, 1),
                 "landed_samples_per_s": round(landed, 1),
-                "enqueued_samples_per_s": round(enqueued, 1) if dev.type == "cuda" else None,
                 "h2d_bytes_timed": sum(r["h2d_bytes_timed"] for r in per_rank),
                 "h2d_gbps_timed": round(sum(r["h2d_bytes_timed"] for r in per_rank) / elapsed / 1e9, 3),
                 "sample_bytes": sample_bytes,

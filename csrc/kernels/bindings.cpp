@@ -246,6 +246,8 @@ PYBIND11_MODULE(_ddl_hip, m) {
       .def("settle", &ddl::NativeStager::settle, py::arg("timeout_ms") = 1000, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("bytes_landed", &ddl::NativeStager::bytes_landed)
       .def_property_readonly("wait_producer_s", &ddl::NativeStager::wait_producer_s)
+      .def("copies_between", &ddl::NativeStager::copies_between, py::arg("t0_ns"), py::arg("t1_ns"),
+           "(windows, bytes) of H2D copies enqueued in [t0_ns, t1_ns] (CLOCK_MONOTONIC) that have retired")
       .def_property_readonly("wait_log", &ddl::NativeStager::wait_log,
                              "per staged window (first 4096): [window, ns ring wait, ns free-event wait enqueue, "
                              "ns producer wait, ns copy enqueue, ns retire slot + event records, t0 ns]");

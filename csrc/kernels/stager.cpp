@@ -184,6 +184,7 @@ void NativeStager::run() {
     if (info.used_bytes > buffer_bytes_)
       return fail(-1, static_cast<int32_t>(p),
                   "window of " + std::to_string(info.used_bytes) + " B exceeds the staging buffer");
+    const uint64_t enq_ns = now_ns();  // before the call: the copy cannot start earlier
     if (info.used_bytes > 0 &&
         hipMemcpyAsync(buffers_[b], arena_->slot_data(p, s), info.used_bytes, hipMemcpyHostToDevice, cs) !=
             hipSuccess)
@@ -213,6 +214,8 @@ void NativeStager::run() {
       std::lock_guard<std::mutex> lk(mu_);
       staged_[w] = info;
       if (wait_log_.size() < 4096) wait_log_.push_back({w, s1 - s0, s2 - s1, s3 - s2, s4 - s3, s5 - s4, s0});
+      copy_log_.push_back(CopyRec{w, enq_ns, info.used_bytes});
+      if (copy_log_.size() > kCopyLog) copy_log_.pop_front();
     }
     cv_.notify_all();
   }
@@ -265,6 +268,18 @@ void NativeStager::close() {
   if (thread_.joinable()) thread_.join();
   // the retire thread drains the queue (every enqueued copy's slot goes back to its producer)
   if (retire_thread_.joinable()) retire_thread_.join();
+}
+
+std::pair<uint64_t, uint64_t> NativeStager::copies_between(uint64_t t0_ns, uint64_t t1_ns) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  uint64_t n = 0, bytes = 0;
+  for (const CopyRec& c : copy_log_) {
+    if (c.enq_ns >= t0_ns && c.enq_ns <= t1_ns && c.window < retired_upto_) {
+      ++n;
+      bytes += c.bytes;
+    }
+  }
+  return {n, bytes};
 }
 
 std::string NativeStager::error() const {

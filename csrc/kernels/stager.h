@@ -35,6 +35,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <utility>
 #include <vector>
 
 #include "arena.h"
@@ -95,6 +96,11 @@ class NativeStager {
   // thread's host-side lag -- up to one window with two copy streams in flight -- is gone).
   void settle(int64_t timeout_ms);
   uint64_t bytes_landed() const { return bytes_landed_.load(); }
+  // (windows, bytes) of the H2D copies ENQUEUED in [t0_ns, t1_ns] (CLOCK_MONOTONIC, ddl::now_ns) that have
+  // retired: every byte of such a copy crossed PCIe after t0 (a copy cannot start before it is enqueued)
+  // and before its retirement was observed. A benchmark's timed region counts these, not copies that were
+  // already in flight when it opened.
+  std::pair<uint64_t, uint64_t> copies_between(uint64_t t0_ns, uint64_t t1_ns) const;
   double wait_producer_s() const { return wait_producer_ns_.load() * 1e-9; }
   // per staged window (first 4096): ns spent in each step of the stager loop -- waiting for the ring
   // (consumer release), enqueueing the free-event wait, waiting for the producer, enqueueing the copy,
@@ -151,6 +157,12 @@ class NativeStager {
   std::atomic<uint64_t> bytes_h2d_{0}, windows_staged_{0}, wait_producer_ns_{0};
   std::atomic<uint64_t> windows_landed_{0}, bytes_landed_{0};
   std::vector<std::vector<int64_t>> wait_log_;  // guarded by mu_
+  struct CopyRec {
+    int64_t window;
+    uint64_t enq_ns, bytes;
+  };
+  std::deque<CopyRec> copy_log_;  // the last kCopyLog copies (guarded by mu_)
+  static constexpr size_t kCopyLog = 1 << 16;
   std::thread thread_;
 };
 
