@@ -358,12 +358,12 @@ def main(argv=None) -> int:
             sync()
         t1 = time.perf_counter()
         t1_ns = rt.now_ns()
+        # complete right now (before settle(): a copy still in flight at t1 must not finish into the count)
+        cb = dl._stager._native.copies_between(t0_ns, t1_ns) if dl._stager is not None else None
         w_land1, b_land1 = _landed(dl)
         bytes_enq1 = dl._stager.bytes_h2d if dl._stager is not None else 0
-        if dl._stager is not None:
-            n_in, b_in = dl._stager._native.copies_between(t0_ns, t1_ns)
-        else:  # CPU rehearsal: the host path has no H2D; every delivered window counts
-            n_in, b_in = w_land1 - w_land0, 0
+        # CPU rehearsal: the host path has no H2D; every delivered window counts
+        n_in, b_in = cb if cb is not None else (w_land1 - w_land0, 0)
         prod1 = conn.producer_stats()
         barrier()
         elapsed = t1 - t0

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <chrono>
 #include <climits>
+#include <set>
 
 namespace ddl {
 namespace {
@@ -271,10 +272,15 @@ void NativeStager::close() {
 }
 
 std::pair<uint64_t, uint64_t> NativeStager::copies_between(uint64_t t0_ns, uint64_t t1_ns) const {
+  // complete NOW: retired by the retire thread, or its retire event already signalled (the retire thread
+  // lags the device by its wake-up); call right at the end of the region, before any settle()
   std::lock_guard<std::mutex> lk(mu_);
+  std::set<int64_t> done;
+  for (const Retire& r : retire_q_)
+    if (hipEventQuery(retire_ev_[r.ev]) == hipSuccess) done.insert(r.window);
   uint64_t n = 0, bytes = 0;
   for (const CopyRec& c : copy_log_) {
-    if (c.enq_ns >= t0_ns && c.enq_ns <= t1_ns && c.window < retired_upto_) {
+    if (c.enq_ns >= t0_ns && c.enq_ns <= t1_ns && (c.window < retired_upto_ || done.count(c.window) != 0)) {
       ++n;
       bytes += c.bytes;
     }

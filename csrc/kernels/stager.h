@@ -96,10 +96,10 @@ class NativeStager {
   // thread's host-side lag -- up to one window with two copy streams in flight -- is gone).
   void settle(int64_t timeout_ms);
   uint64_t bytes_landed() const { return bytes_landed_.load(); }
-  // (windows, bytes) of the H2D copies ENQUEUED in [t0_ns, t1_ns] (CLOCK_MONOTONIC, ddl::now_ns) that have
-  // retired: every byte of such a copy crossed PCIe after t0 (a copy cannot start before it is enqueued)
-  // and before its retirement was observed. A benchmark's timed region counts these, not copies that were
-  // already in flight when it opened.
+  // (windows, bytes) of the H2D copies ENQUEUED in [t0_ns, t1_ns] (CLOCK_MONOTONIC, ddl::now_ns) that are
+  // complete at the call: every byte of such a copy crossed PCIe after t0 (a copy cannot start before it
+  // is enqueued) and before the call. Called at the end of a benchmark's timed region, it counts the
+  // region's own copies -- not ones already in flight when it opened, nor ones still in flight at its end.
   std::pair<uint64_t, uint64_t> copies_between(uint64_t t0_ns, uint64_t t1_ns) const;
   double wait_producer_s() const { return wait_producer_ns_.load() * 1e-9; }
   // per staged window (first 4096): ns spent in each step of the stager loop -- waiting for the ring
