@@ -387,3 +387,28 @@ def test_inline_dispatch_window_read_on_two_streams_is_not_overwritten():
     assert len(out) == len(ref) > 0
     for x, y in zip(out, ref):
         assert torch.equal(x, y)
+
+
+def test_stager_counts_the_copies_of_a_time_window():
+    """copies_between(t0, t1): the H2D copies enqueued inside [t0, t1] and complete -- what bench.py counts
+    as the timed region's own H2D work. Over the whole run it is every copy; over an empty window, none."""
+    from ddl_amd import _native
+
+    rt = _native.runtime()
+    with ddl_amd.start(n_producers=3) as (env, conn):
+        t0 = rt.now_ns()
+        dl = ddl_amd.DistributedDataLoader(IdProducer(64, 8), 16, conn, 4, env=env, shuffle="device", seed=2,
+                                           copy_batches=True)
+        st = dl._stager
+        for e in range(4):  # every window of the run: nothing is left to stage afterwards
+            for i in range(len(dl)):
+                dl[i]
+                dl.mark(Marker.END_OF_BATCH)
+            if e < 3:
+                dl.mark(Marker.END_OF_EPOCH)
+        torch.cuda.synchronize()
+        t1 = rt.now_ns()
+        n, b = st._native.copies_between(t0, t1)
+        assert n == st.windows_staged == 4 and b == st.bytes_h2d == n * 64 * 8 * 4
+        assert st._native.copies_between(t1 + 1, t1 + 2) == (0, 0)
+        dl.close()
