@@ -61,6 +61,11 @@ def _parse(argv=None):
     ap.add_argument("--floor", action="store_true",
                     help="after each point, run the same step on one held batch (no loader) with the same meter: "
                          "the idle the measurement itself shows without any loader work (floor_idle_pct)")
+    ap.add_argument("--floor-traffic", action="store_true",
+                    help="images: also run the floor loop with the loader's device traffic and no loader hand-off: "
+                         "per step one window H2D copy (two copy streams) and a device copy of it on a side stream, "
+                         "paced by the step's begin event; nothing waits on the compute stream "
+                         "(floor_traffic_idle_pct)")
     ap.add_argument("--dispatch", default="auto", help="native_dispatch of the image loader (auto / inline / "
                                                          "lookahead / python)")
     ap.add_argument("--json-out", default=None)
@@ -93,6 +98,37 @@ def _image_loader(a, env, conn, n_steps):
             dl.mark(Marker.END_OF_EPOCH)
 
     return dl, gen(), B, "samples"
+
+
+class _Traffic:
+    """The loader's device traffic without the loader: per step, one window-sized H2D copy from pinned memory
+    into a 2-buffer HBM ring (alternating copy streams, as the stager) and a device copy of the landed buffer on
+    a side stream behind it (the batch gather's bytes). Each copy waits for the step's begin event, so the
+    traffic is spread over the steps as the loader's is; the compute stream itself never waits for it."""
+
+    def __init__(self, dev, nbytes: int):
+        import torch
+
+        self.torch = torch
+        self.pinned = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+        self.ring = [torch.empty(nbytes, dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.out = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        self.copy = [torch.cuda.Stream(dev) for _ in range(2)]
+        self.side = torch.cuda.Stream(dev)
+        self.j = 0
+
+    def step(self, begin_event) -> None:
+        torch = self.torch
+        j = self.j
+        self.j += 1
+        cs = self.copy[j % 2]
+        cs.wait_event(begin_event)
+        with torch.cuda.stream(cs):
+            self.ring[j % 2].copy_(self.pinned, non_blocking=True)
+        self.side.wait_stream(cs)
+        with torch.cuda.stream(self.side):
+            self.out.copy_(self.ring[j % 2])
+        cs.wait_stream(self.side)  # the ring buffer is re-filled only after its device copy
 
 
 def _token_loader(a, env, conn, n_steps, src):
@@ -177,6 +213,10 @@ def main(argv=None) -> int:
             print(json.dumps({"family": a.family, "feed_per_s": round(feed, 1), "feed_passes": [round(f, 1) for f in feeds],
                               "unit": unit}), flush=True)
 
+            traffic = None
+            if a.floor_traffic and a.family == "images":
+                traffic = _Traffic(dev, a.window * 3 * 224 * 224 * (2 if a.source_dtype == "bfloat16" else 1))
+
             # ---- sweep
             for i, r in enumerate(ratios):
                 step = CalibratedStep(dev, step_ms=1000.0 * B / (r * feed))
@@ -220,6 +260,17 @@ def main(argv=None) -> int:
                         torch.cuda.synchronize()
                     pt["floor_idle_pct"] = round(fm.result()["gpu_idle_pct"], 3)
                     pt["error_vs_floor_pp"] = round(res["gpu_idle_pct"] - max(pred, pt["floor_idle_pct"]), 3)
+                if traffic is not None:  # the same floor loop, with the loader's copies running beside it
+                    tm = ComputeIdleMeter()
+                    torch.cuda.synchronize()
+                    with trace_range(f"sweep.traffic{i:02d}"):
+                        for _ in range(a.steps):
+                            tm.step_begin()
+                            traffic.step(tm._cur)
+                            step(batch)
+                            tm.step_end()
+                        torch.cuda.synchronize()
+                    pt["floor_traffic_idle_pct"] = round(tm.result()["gpu_idle_pct"], 3)
                 nd1 = dl.stats().get("native_dispatch") or {}
                 if nd1:  # per point: batches built ahead (lookahead hits), batches the compute stream waited for
                     pt["dispatch"] = {"mode": nd1.get("mode"),
