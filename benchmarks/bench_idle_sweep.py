@@ -66,6 +66,10 @@ def _parse(argv=None):
                          "per step one window H2D copy (two copy streams) and a device copy of it on a side stream, "
                          "paced by the step's begin event; nothing waits on the compute stream "
                          "(floor_traffic_idle_pct)")
+    ap.add_argument("--prealloc-gb", type=float, default=0.0,
+                    help="grow the caching allocator's pool on the loader's batch stream by this many GB before the "
+                         "sweep, so output blocks come from cached memory instead of new hipMalloc segments while the "
+                         "host runs ahead of the GPU")
     ap.add_argument("--dispatch", default="auto", help="native_dispatch of the image loader (auto / inline / "
                                                          "lookahead / python)")
     ap.add_argument("--json-out", default=None)
@@ -217,6 +221,11 @@ def main(argv=None) -> int:
             if a.floor_traffic and a.family == "images":
                 traffic = _Traffic(dev, a.window * 3 * 224 * 224 * (2 if a.source_dtype == "bfloat16" else 1))
 
+            if a.prealloc_gb > 0 and getattr(dl, "_batch_stream", None) is not None:
+                with torch.cuda.stream(dl._batch_stream):
+                    blob = torch.empty(int(a.prealloc_gb * (1 << 30)), dtype=torch.uint8, device=dev)
+                del blob
+
             # ---- sweep
             for i, r in enumerate(ratios):
                 step = CalibratedStep(dev, step_ms=1000.0 * B / (r * feed))
@@ -225,6 +234,7 @@ def main(argv=None) -> int:
                     step(next(it))
                 meter = ComputeIdleMeter()
                 nd0 = dl.stats().get("native_dispatch") or {}
+                seg0 = torch.cuda.memory_stats(dev).get("segment.all.allocated", 0)
                 torch.cuda.synchronize()
                 t2 = time.perf_counter()
                 with trace_range(f"sweep.p{i:02d}"):
@@ -239,6 +249,7 @@ def main(argv=None) -> int:
                         meter.step_end()
                     torch.cuda.synchronize()
                 t3 = time.perf_counter()
+                seg1 = torch.cuda.memory_stats(dev).get("segment.all.allocated", 0)
                 res = meter.result()
                 busy_per_step = res["busy_ms"] / max(1, res["steps"])
                 cap = 1000.0 * B / busy_per_step  # measured step capacity C
@@ -248,7 +259,8 @@ def main(argv=None) -> int:
                       "step_capacity_per_s": round(cap, 1), "ratio_measured": round(cap / feed, 3),
                       "achieved_per_s": round(B * a.steps / (t3 - t2), 1),
                       "gpu_idle_pct": round(res["gpu_idle_pct"], 3), "predicted_idle_pct": round(pred, 3),
-                      "error_pp": round(res["gpu_idle_pct"] - pred, 3)}
+                      "error_pp": round(res["gpu_idle_pct"] - pred, 3),
+                      "allocator_segments_created": seg1 - seg0}
                 if a.floor:  # the same step on one held batch, no loader calls: the meter's own floor
                     fm = ComputeIdleMeter()
                     torch.cuda.synchronize()
@@ -270,8 +282,13 @@ def main(argv=None) -> int:
                             step(batch)
                             tm.step_end()
                         torch.cuda.synchronize()
-                    pt["floor_traffic_idle_pct"] = round(tm.result()["gpu_idle_pct"], 3)
-                nd1 = dl.stats().get("native_dispatch") or {}
+                    tr = tm.result()
+                    pt["floor_traffic_idle_pct"] = round(tr["gpu_idle_pct"], 3)
+                    pt["floor_traffic_busy_ms_per_step"] = round(tr["busy_ms"] / max(1, tr["steps"]), 4)
+                st1 = dl.stats()
+                nd1 = st1.get("native_dispatch") or {}
+                if "run_ahead" in st1:
+                    pt["run_ahead"] = st1["run_ahead"]
                 if nd1:  # per point: batches built ahead (lookahead hits), batches the compute stream waited for
                     pt["dispatch"] = {"mode": nd1.get("mode"),
                                       **{k: nd1.get(k, 0) - nd0.get(k, 0)

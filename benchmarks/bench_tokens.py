@@ -41,6 +41,9 @@ def main(argv=None):
                     help="phase 2: steps of a fixed-cost token train step, for GPU idle %% (0 disables)")
     ap.add_argument("--model-dim", type=int, default=256)
     ap.add_argument("--model-depth", type=int, default=2)
+    ap.add_argument("--token-dtype", default="int32", choices=["int32", "uint16"],
+                    help="token ids in the corpus and on the wire (uint16: vocab < 65536, 2 B per token over PCIe, "
+                         "widened to int32 input_ids by the pack kernel)")
     a = ap.parse_args(argv)
 
     import torch
@@ -57,7 +60,7 @@ def main(argv=None):
     if int(os.environ.get("LOCAL_RANK", "0")) == 0:
         from ddl_amd.utils.numa import gpu_numa_node
 
-        src = SharedTokenSource.synthetic(name, a.n_seqs, a.min_len, a.seq_len, seed=1)
+        src = SharedTokenSource.synthetic(name, a.n_seqs, a.min_len, a.seq_len, seed=1, token_dtype=a.token_dtype)
         src.bind_to_node(gpu_numa_node(int(os.environ.get("LOCAL_RANK", "0"))))  # the producers' node
     gb = a.batch * world
     try:
@@ -67,7 +70,7 @@ def main(argv=None):
             if src is None:
                 from ddl_amd.models.datasets import SharedArraySource
 
-                t = SharedArraySource(name + "_tok", 0, (1,), "int32")
+                t = SharedArraySource(name + "_tok", 0, (1,), "int32" if a.token_dtype == "int32" else "int16")
                 o = SharedArraySource(name + "_off", a.n_seqs + 1, (1,), "int64")
                 offs = o.tensor().view(-1).numpy()
                 t.n = int(offs[-1])
@@ -160,7 +163,8 @@ def main(argv=None):
                     "producers": a.producers, "host_threads": a.host_threads, "slots": a.slots,
                     "batches_per_window": dl.batches_per_window[0], "dispatch": a.dispatch,
                     "dispatch_mode": (st.get("native_dispatch") or {}).get("mode"), "token_rows": a.token_rows,
-                    "mean_len": round(mean_len, 1),
+                    "mean_len": round(mean_len, 1), "token_wire_dtype": a.token_dtype,
+                    "h2d_token_gbps": round(real_tokens * source.token_bytes / dt / 1e9, 2),
                     "consumer_wait_s": round(st["consumer_wait_s"], 3),
                     "stager_wait_producer_s": round(st.get("stager_wait_producer_s", 0.0), 3),
                     # per producer: rounds, mean fill and mean slot-wait per round (us) -- where the feed goes

@@ -164,6 +164,29 @@ def main():
     report("pad_tokens 64x4096", t, toks.numel() * 4 + 64 * 4096 * (4 + 1 + 8))
     t = bench(lambda: ops.pack_tokens(toks, offs, 4096), reps=20)
     report("pack_tokens 64 seqs (incl. host plan)", t, toks.numel() * (4 + 4 + 1 + 8 + 4))
+    # the plan on the device: plan kernel + pack kernel reading the row count from device memory (no host
+    # round trip; static shapes), output rows = pack_capacity
+    t = bench(lambda: ops.pack_tokens_device(toks, offs_d, 4096), reps=20)
+    report("pack_tokens 64 seqs (device plan, 2 launches)", t, toks.numel() * (4 + 4 + 1 + 8 + 4))
+    lens2 = rng.integers(1, 4097, size=2048)
+    offs2 = torch.from_numpy(np.concatenate([[0], np.cumsum(lens2)]).astype(np.int64)).to(dev)
+    toks2 = torch.from_numpy(rng.integers(0, 50000, size=int(lens2.sum())).astype(np.int32)).to(dev)
+    t = bench(lambda: ops.pack_tokens_device(toks2, offs2, 4096), reps=20)
+    report("pack_tokens 2048 seqs (device plan, 2 launches)", t, toks2.numel() * (4 + 4 + 1 + 8 + 4))
+    t = bench(lambda: ops.pack_tokens(toks2, offs2.cpu().numpy(), 4096), reps=10)
+    report("pack_tokens 2048 seqs (incl. host plan)", t, toks2.numel() * (4 + 4 + 1 + 8 + 4))
+    # the same two launches captured in a HIP graph: device time only (no Python / allocator on the host)
+    for name, (tk, of) in (("64", (toks, offs_d)), ("2048", (toks2, offs2))):
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            ops.pack_tokens_device(tk, of, 4096)
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            ops.pack_tokens_device(tk, of, 4096)
+        t = bench(g.replay, reps=20)
+        report(f"pack_tokens {name} seqs (device plan, graph replay)", t, tk.numel() * (4 + 4 + 1 + 8 + 4))
     x = torch.randn(1_000_000, 9, device=dev)
     t = bench(lambda: ops.column_stats(x), reps=20)
     report("column_stats 1Mx9", t, x.numel() * 4)

@@ -272,7 +272,8 @@ PYBIND11_MODULE(_ddl_hip, m) {
              r.widths = std::move(widths);
              r.aff = make_affine(scale, bias, plane);
              if (kind == 2) {
-               if (token.size() != 10) throw std::invalid_argument("BatchEngine: token recipe needs 10 values");
+               if (token.size() != 10 && token.size() != 11)
+                 throw std::invalid_argument("BatchEngine: token recipe needs 10 or 11 values");
                r.token_mode = static_cast<int32_t>(token[0]);
                r.pad_id = static_cast<int32_t>(token[1]);
                r.seq_len = token[2];
@@ -283,6 +284,9 @@ PYBIND11_MODULE(_ddl_hip, m) {
                r.off_tokens = token[7];
                r.header_stride = token[8];
                r.token_fill_rows = token[9];
+               r.token_bytes = token.size() > 10 ? token[10] : 4;
+               if (r.token_bytes != 4 && r.token_bytes != 2)
+                 throw std::invalid_argument("BatchEngine: tokens are 4 (int32) or 2 (uint16) bytes");
              }
              std::vector<void*> bufs;
              for (auto b : buffers) bufs.push_back(as_ptr<void>(b));
@@ -569,10 +573,12 @@ PYBIND11_MODULE(_ddl_hip, m) {
       [](uintptr_t tokens, uintptr_t offsets, uintptr_t row_start, uintptr_t row_end, uintptr_t seg_offsets,
          int64_t n_seg, uintptr_t out_tokens, uintptr_t attn_mask, uintptr_t position_ids, bool pos_is_i64,
          uintptr_t segment_ids, uintptr_t cu_seqlens_out, int64_t rows, int64_t seq_len, int pad_id, int mode,
-         uintptr_t stream, int64_t fill_rows) {
+         uintptr_t stream, int64_t fill_rows, uintptr_t dev_counts, bool tok16) {
         ddl::TokenSpec sp{};
+        sp.tok16 = tok16 ? 1 : 0;
         sp.fill_rows = fill_rows;
-        sp.tokens = as_ptr<const int32_t>(tokens);
+        sp.dev_counts = as_ptr<const int64_t>(dev_counts);
+        sp.tokens = as_ptr<const void>(tokens);
         sp.offsets = as_ptr<const int64_t>(offsets);
         sp.row_start = as_ptr<const int64_t>(row_start);
         sp.row_end = as_ptr<const int64_t>(row_end);
@@ -593,7 +599,29 @@ PYBIND11_MODULE(_ddl_hip, m) {
       py::arg("tokens"), py::arg("offsets"), py::arg("row_start"), py::arg("row_end"), py::arg("seg_offsets"),
       py::arg("n_seg"), py::arg("out_tokens"), py::arg("attn_mask"), py::arg("position_ids"), py::arg("pos_is_i64"),
       py::arg("segment_ids"), py::arg("cu_seqlens_out"), py::arg("rows"), py::arg("seq_len"), py::arg("pad_id"),
-      py::arg("mode"), py::arg("stream"), py::arg("fill_rows") = 0);
+      py::arg("mode"), py::arg("stream"), py::arg("fill_rows") = 0, py::arg("dev_counts") = 0,
+      py::arg("tok16") = false);
+  m.def("pack_plan_scratch_ints", &ddl::pack_plan_scratch_ints, py::arg("max_segs"), py::arg("max_rows"));
+  m.def(
+      "pack_plan_device",
+      [](uintptr_t offsets, int64_t n, int64_t seq_len, int64_t max_segs, int64_t max_rows, uintptr_t seg_offsets,
+         uintptr_t row_start, uintptr_t row_end, uintptr_t counts, uintptr_t scratch, uintptr_t stream) {
+        ddl::PackPlanSpec sp{};
+        sp.offsets = as_ptr<const int64_t>(offsets);
+        sp.n = n;
+        sp.seq_len = seq_len;
+        sp.max_segs = max_segs;
+        sp.max_rows = max_rows;
+        sp.seg_offsets = as_ptr<int64_t>(seg_offsets);
+        sp.row_start = as_ptr<int64_t>(row_start);
+        sp.row_end = as_ptr<int64_t>(row_end);
+        sp.counts = as_ptr<int64_t>(counts);
+        sp.scratch = as_ptr<int32_t>(scratch);
+        check_rc(ddl::pack_plan_device(sp, as_stream(stream)), "pack_plan_device");
+      },
+      py::arg("offsets"), py::arg("n"), py::arg("seq_len"), py::arg("max_segs"), py::arg("max_rows"),
+      py::arg("seg_offsets"), py::arg("row_start"), py::arg("row_end"), py::arg("counts"), py::arg("scratch"),
+      py::arg("stream"));
   m.def(
       "stream_copy",
       [](uintptr_t src, uintptr_t dst, int64_t bytes, int blocks, uintptr_t stream) {

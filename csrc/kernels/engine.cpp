@@ -240,7 +240,8 @@ TokenSpec BatchEngine::token_spec(const StagedInfo& info, int64_t sub, const std
   const int64_t* m = token_meta(info, sub);
   const uint8_t* win = static_cast<const uint8_t*>(src) + sub * r_.header_stride;
   TokenSpec sp{};
-  sp.tokens = reinterpret_cast<const int32_t*>(static_cast<const uint8_t*>(src) + r_.off_tokens) + m[4];
+  sp.tok16 = r_.token_bytes == 2 ? 1 : 0;
+  sp.tokens = static_cast<const uint8_t*>(src) + r_.off_tokens + m[4] * r_.token_bytes;
   sp.out_tokens = static_cast<int32_t*>(dst[0]);
   sp.attn_mask = static_cast<uint8_t*>(dst[1]);
   sp.position_ids = dst[2];

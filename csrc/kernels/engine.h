@@ -64,6 +64,7 @@ struct BatchRecipe {
   int64_t off_offsets = 0, off_row_start = 0, off_row_end = 0, off_seg_offsets = 0, off_tokens = 0;
   int64_t header_stride = 0;  // bytes between the header blocks of consecutive sub-batches of a window
   int64_t token_fill_rows = 0;  // pack: fixed-shape batches of this many rows (0: exactly the packed rows)
+  int64_t token_bytes = 4;      // 4: int32 tokens in the window, 2: uint16 (widened by the kernel)
 };
 
 class BatchEngine {

@@ -75,7 +75,7 @@ int random_resized_crop(void* dst, int32_t out_dt, const void* src, int32_t in_d
 // stream; seg_offsets (sorted sequence starts, n_seg+1 entries) drive the
 // per-token position id (reset at every sequence start) and segment id.
 struct TokenSpec {
-  const int32_t* tokens;
+  const void* tokens;          // int32 tokens, or uint16 when tok16 (narrow on the wire, widened here)
   const int64_t* offsets;      // pad mode: [B+1]
   const int64_t* row_start;    // pack mode: [R]
   const int64_t* row_end;      // pack mode: [R]
@@ -91,12 +91,36 @@ struct TokenSpec {
   int32_t pad_id;
   int32_t pos_is_i64;
   int32_t mode;  // 0 pad, 1 pack
-  int32_t pad;
+  int32_t tok16;  // 1: tokens are uint16 (vocabularies < 65536 cross PCIe at 2 B per token)
   // > rows: rows [rows, fill_rows) are written as padding (pad_id, mask 0, position 0, segment -1), so a
   // packed batch has a fixed shape [fill_rows, seq_len] (static shapes for graphs / compiled steps)
   int64_t fill_rows;
+  // pack mode, plan built on the device (pack_plan_device): {n_rows, n_seg} read by the kernel instead of
+  // `rows` / `n_seg`, so plan and pack are two launches with no host round trip (fill_rows = the plan's
+  // row capacity; n_rows < 0, an overflowed plan, writes every row as padding)
+  const int64_t* dev_counts;
 };
 int pad_pack_tokens(const TokenSpec& spec, hipStream_t st);
+
+// In-order greedy packing plan of B ragged sequences, computed on the device (one workgroup): the same
+// plan as the host's pack_plan (runtime/arena.cpp). Sequences longer than seq_len are split into seq_len
+// segments; row r = segments [P(r), P(r + 1)) where P(r + 1) = the furthest segment end within seq_len of
+// P(r)'s start. The row starts are the orbit of segment 0 under that jump, built by pointer doubling
+// (orbit[2^t + i] = jump^(2^t)(orbit[i])), log2(rows) rounds instead of a rows-long dependent chain.
+struct PackPlanSpec {
+  const int64_t* offsets;  // [n + 1] flat token offsets of the sequences
+  int64_t n;
+  int64_t seq_len;
+  int64_t max_segs;      // seg_offsets holds max_segs + 1 entries
+  int64_t max_rows;      // row_start / row_end hold max_rows entries
+  int64_t* seg_offsets;  // out: segment starts + the end
+  int64_t* row_start;    // out
+  int64_t* row_end;      // out
+  int64_t* counts;       // out: {n_rows, n_seg}; n_rows = -1 when a capacity was exceeded
+  int32_t* scratch;      // >= pack_plan_scratch_ints(max_segs, max_rows) ints (used when LDS is too small)
+};
+int64_t pack_plan_scratch_ints(int64_t max_segs, int64_t max_rows);
+int pack_plan_device(const PackPlanSpec& spec, hipStream_t st);
 // Several independent token batches (the sub-batches of one multi-batch window) in one launch per
 // kMaxTokenSubs of them: grid.y = sub-batch.
 constexpr int kMaxTokenSubs = 16;

@@ -3,6 +3,8 @@
 //
 // Pad mode: B ragged sequences -> [B, S] tokens padded with pad_id, a u8
 // attention mask and position ids, truncated to S.
+// Tokens arrive as int32, or as uint16 (tok16: vocabularies below 65536 ship 2 B per token over PCIe and
+// are widened to int32 here, in the same pass).
 // Pack mode: consecutive sequences are packed into rows of S tokens (plan
 // computed on the host: row r = flat token span [row_start, row_end)); the
 // position id restarts at every sequence boundary and a segment id marks
@@ -43,7 +45,8 @@ template <typename At>
 __device__ __forceinline__ void emit4(const TokenSpec& sp, int64_t row, int64_t p0, int64_t start, int64_t len,
                                       At seg_at) {
   const int64_t S = sp.seq_len;
-  const int32_t* src = sp.tokens + start;
+  const int32_t* src = static_cast<const int32_t*>(sp.tokens) + start;
+  const uint16_t* src16 = static_cast<const uint16_t*>(sp.tokens) + start;
   int32_t tok[4], pos[4], seg[4];
   uint8_t msk[4];
   int64_t s = -1;  // current sequence (pack mode): searched once, then advanced
@@ -51,7 +54,7 @@ __device__ __forceinline__ void emit4(const TokenSpec& sp, int64_t row, int64_t 
   for (int k = 0; k < 4; ++k) {
     const int64_t p = p0 + k;
     const bool valid = p < len;
-    tok[k] = valid ? src[p] : sp.pad_id;
+    tok[k] = valid ? (sp.tok16 ? static_cast<int32_t>(src16[p]) : src[p]) : sp.pad_id;
     msk[k] = valid ? 1 : 0;
     if (sp.mode == 0) {
       pos[k] = valid ? static_cast<int32_t>(p) : 0;
@@ -103,7 +106,12 @@ __device__ __forceinline__ void emit4(const TokenSpec& sp, int64_t row, int64_t 
 
 // One workgroup = (row, chunk) `bx` of batch `sp`. Blocks past the batch's rows (a multi-batch launch is
 // sized for its largest sub-batch) only do block 0's cu_seqlens copy; the exit is block-uniform.
-__device__ __forceinline__ void pad_pack_block(const TokenSpec& sp, uint32_t bx, int32_t chunks, int64_t* seg_lds) {
+__device__ __forceinline__ void pad_pack_block(const TokenSpec& spec, uint32_t bx, int32_t chunks, int64_t* seg_lds) {
+  TokenSpec sp = spec;
+  if (sp.dev_counts != nullptr) {  // plan built on the device: its row / segment counts (block-uniform loads)
+    sp.rows = sp.dev_counts[0] < 0 ? 0 : sp.dev_counts[0];
+    sp.n_seg = sp.dev_counts[0] < 0 ? 0 : sp.dev_counts[1];
+  }
   const uint32_t row = bx / static_cast<uint32_t>(chunks);
   const bool live = row < (sp.fill_rows > sp.rows ? sp.fill_rows : sp.rows);  // data row or padding row
   const int64_t p0 = static_cast<int64_t>(bx - row * static_cast<uint32_t>(chunks)) * kSpan +
@@ -148,7 +156,132 @@ __global__ void __launch_bounds__(kThreads) pad_pack_multi_kernel(TokenMulti m, 
   pad_pack_block(m.sub[blockIdx.y], blockIdx.x, chunks, seg_lds);
 }
 
+// ---- device packing plan (one workgroup) ----------------------------------------------------------------
+constexpr int kPlanThreads = 1024;
+constexpr int kPlanWaves = kPlanThreads / 64;
+constexpr int64_t kPlanLdsInts = 12288;  // 48 KB of LDS for the jump tables + the orbit, else global scratch
+
+__device__ __forceinline__ int64_t wave_incl_scan(int64_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t u = __shfl_up(v, d, 64);
+    if (lane >= d) v += u;
+  }
+  return v;
+}
+
+__global__ void __launch_bounds__(kPlanThreads) pack_plan_kernel(PackPlanSpec sp) {
+  __shared__ int64_t wave_tot[kPlanWaves];
+  __shared__ int64_t carry_s;
+  __shared__ int32_t lds[kPlanLdsInts];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int64_t S = sp.seq_len;
+  if (t == 0) carry_s = 0;
+  __syncthreads();
+  // 1. segments: c_i = ceil(len_i / S) per sequence, exclusive scan over the sequences in 1024-wide tiles
+  for (int64_t b = 0; b < sp.n; b += kPlanThreads) {
+    const int64_t i = b + t;
+    int64_t s0 = 0, len = 0;
+    if (i < sp.n) {
+      s0 = sp.offsets[i];
+      len = sp.offsets[i + 1] - s0;
+    }
+    const int64_t c = len > 0 ? (len + S - 1) / S : 0;
+    const int64_t incl = wave_incl_scan(c);
+    if (lane == 63) wave_tot[wv] = incl;
+    __syncthreads();
+    int64_t before = carry_s;
+    for (int k = 0; k < wv; ++k) before += wave_tot[k];
+    const int64_t first = before + incl - c;
+    for (int64_t j = 0; j < c; ++j)
+      if (first + j < sp.max_segs) sp.seg_offsets[first + j] = s0 + j * S;
+    __syncthreads();
+    if (t == kPlanThreads - 1) carry_s = before + incl;
+    __syncthreads();
+  }
+  const int64_t n_seg = carry_s;
+  if (n_seg > sp.max_segs) {  // block-uniform exit
+    if (t == 0) {
+      sp.counts[0] = -1;
+      sp.counts[1] = n_seg;
+    }
+    return;
+  }
+  if (t == 0) sp.seg_offsets[n_seg] = n_seg > 0 ? sp.offsets[sp.n] : 0;
+  __syncthreads();
+  // 2. jump tables (ping-pong) and the orbit: LDS when they fit, else the caller's scratch
+  const int64_t need = 2 * (n_seg + 1) + sp.max_rows + 1;
+  int32_t* base = need <= kPlanLdsInts ? lds : sp.scratch;
+  int32_t* J = base;
+  int32_t* J2 = base + (n_seg + 1);
+  int32_t* P = base + 2 * (n_seg + 1);
+  const int64_t cap = sp.max_rows + 1;  // orbit entries: the rows' starts + the terminal n_seg
+  for (int64_t k = t; k <= n_seg; k += kPlanThreads) {
+    int32_t m = static_cast<int32_t>(n_seg);
+    if (k < n_seg) {  // furthest segment end m within S tokens of segment k's start (every segment >= 1 token)
+      const int64_t lim = sp.seg_offsets[k] + S;
+      int64_t lo = k + 1, hi = n_seg - k > S ? k + S : n_seg;  // seg_offsets[lo] <= lim always
+      while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (sp.seg_offsets[mid] <= lim)
+          lo = mid;
+        else
+          hi = mid - 1;
+      }
+      m = static_cast<int32_t>(lo);
+    }
+    J[k] = m;
+  }
+  if (t == 0) P[0] = 0;
+  __syncthreads();
+  int64_t len = 1;
+  while (P[len - 1] < n_seg && len < cap) {  // P[0..len) known, J = jump^len: P[len + i] = J[P[i]]
+    const int64_t add = len < cap - len ? len : cap - len;
+    for (int64_t i = t; i < add; i += kPlanThreads) P[len + i] = J[P[i]];
+    for (int64_t k = t; k <= n_seg; k += kPlanThreads) J2[k] = J[J[k]];
+    __syncthreads();
+    int32_t* tmp = J;
+    J = J2;
+    J2 = tmp;
+    len += add;
+  }
+  if (P[len - 1] < n_seg) {  // more rows than max_rows (block-uniform)
+    if (t == 0) {
+      sp.counts[0] = -1;
+      sp.counts[1] = n_seg;
+    }
+    return;
+  }
+  // 3. rows: the orbit entries before the terminal one (P strictly increases until it reaches n_seg)
+  for (int64_t i = t; i < len; i += kPlanThreads) {
+    if (P[i] < n_seg) {
+      sp.row_start[i] = sp.seg_offsets[P[i]];
+      sp.row_end[i] = sp.seg_offsets[P[i + 1]];
+      if (P[i + 1] == n_seg) {
+        sp.counts[0] = i + 1;
+        sp.counts[1] = n_seg;
+      }
+    }
+  }
+  if (t == 0 && n_seg == 0) {
+    sp.counts[0] = 0;
+    sp.counts[1] = 0;
+  }
+}
+
 }  // namespace
+
+int64_t pack_plan_scratch_ints(int64_t max_segs, int64_t max_rows) { return 2 * (max_segs + 1) + max_rows + 1; }
+
+int pack_plan_device(const PackPlanSpec& spec, hipStream_t st) {
+  if (spec.seq_len <= 0 || spec.n < 0 || spec.max_segs < 0 || spec.max_rows < 0) return -2;
+  if (!spec.offsets || !spec.seg_offsets || !spec.row_start || !spec.row_end || !spec.counts || !spec.scratch)
+    return -2;
+  if (spec.max_segs >= (int64_t{1} << 31) - 1) return -4;  // int32 segment ids in the jump tables
+  hipLaunchKernelGGL(pack_plan_kernel, dim3(1), dim3(kPlanThreads), 0, st, spec);
+  return static_cast<int>(hipGetLastError());
+}
 
 int pad_pack_tokens(const TokenSpec& spec, hipStream_t st) {
   const int64_t rows = spec.fill_rows > spec.rows ? spec.fill_rows : spec.rows;

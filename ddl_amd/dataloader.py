@@ -32,6 +32,7 @@ where one window is one global batch).
 
 from __future__ import annotations
 
+import collections
 import math
 import os
 import time
@@ -142,6 +143,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
         native_dispatch: bool | str = True,
         token_rows: str = "exact",
         verify_order: bool | None = None,
+        max_ahead: int | None = None,
     ):
         if mode not in MODES:
             raise ValueError(f"unknown mode {mode!r}; one of {MODES}")
@@ -230,6 +232,21 @@ class DistributedDataLoader(DistributedDataloaderABC):
         self.native_dispatch = "auto" if native_dispatch is True else native_dispatch
         self._engine = None                   # native per-batch dispatch (csrc/kernels/engine.cpp)
         self._fields = None                   # MapDatasetSource rows: (fields, kind) to unpack batches into
+        # Run-ahead bound (GPU device path): a host that never synchronises with its step (no .item(), no
+        # host-side metric) would otherwise take batches as fast as the copies land, however far behind the
+        # GPU's compute is, keeping the link and both copy engines saturated and a growing number of
+        # batches alive in HBM. Every `_ahead_every` batches an event goes on the consumer's stream, and
+        # fetching batch i waits (on the host) for the event of batch i - max_ahead: the copies then follow
+        # the step's pace when the step is the bottleneck. 0 disables. (`$DDL_MAX_AHEAD`, default 16.)
+        ma = int(os.environ.get("DDL_MAX_AHEAD", "16")) if max_ahead is None else int(max_ahead)
+        if ma < 0:
+            raise ValueError("max_ahead must be >= 0")
+        self.max_ahead = ma
+        self._ahead_every = max(1, ma // 4)
+        # (batch count, event on the consumer's stream)
+        self._ahead_q = collections.deque() if self.device.type == "cuda" and ma > 0 else None
+        self._ahead_n = 0
+        self.ahead_waits = 0
 
         if connection is None or connection.n_producers == 0:
             # Reference behaviour for a single-rank run: nothing to iterate (ddl/mpi_dataloader.py:173-174).
@@ -377,7 +394,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
             outs += [((rows, S), torch.int32), ((lay.max_segments + 1,), torch.int32)]
         fill = lay.max_segments if (mode == "pack" and self.token_rows == "fixed") else 0
         token = [0 if mode == "pad" else 1, int(self.pad_id), S, reg["offsets"][0], reg["row_start"][0],
-                 reg["row_end"][0], reg["seg_offsets"][0], reg["tokens"][0], lay.header_stride, fill]
+                 reg["row_end"][0], reg["seg_offsets"][0], reg["tokens"][0], lay.header_stride, fill, lay.token_bytes]
         return dict(kind=2, in_dt=_dtypes.code(torch.int32), out_dt=_dtypes.code(torch.int32), shuffle=False,
                     batch=lay.batch, row_elems=1, seed=0, max_blocks=0, scale=[], bias=[], plane=0,
                     n_data=[int(x.nData) for x in self.metadata_from_producer], widths=[], token=token,
@@ -687,7 +704,25 @@ class DistributedDataLoader(DistributedDataloaderABC):
                 self._host_meta = tuple(t.reshape(-1).view(torch.uint8)[:nb].view(torch.int64).tolist())
         return None
 
+    def _pace(self) -> None:
+        """The run-ahead bound (``max_ahead``): one event per ``_ahead_every`` batches on the consumer's
+        current stream; wait on the host for the one ``max_ahead`` batches back."""
+        n = self._ahead_n
+        self._ahead_n = n + 1
+        q = self._ahead_q
+        while q and q[0][0] <= n - self.max_ahead:
+            ev = q.popleft()[1]
+            if not ev.query():
+                self.ahead_waits += 1
+                ev.synchronize()
+        if n % self._ahead_every == 0:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            q.append((n, ev))
+
     def __getitem__(self, idx: int):
+        if self._ahead_q is not None:
+            self._pace()
         eng = self._engine
         if eng is not None and 0 <= idx < self._len:  # native dispatch: the lean path
             bpw = self.batches_per_window[self.window % self._n_prod]
@@ -1236,6 +1271,8 @@ class DistributedDataLoader(DistributedDataloaderABC):
             d["producers"] = self.connection.producer_stats()
         if getattr(self, "_verify", None) is not None:
             d["verified_windows"] = self.verified_windows
+        if getattr(self, "_ahead_q", None) is not None:
+            d["run_ahead"] = {"max_ahead": self.max_ahead, "host_waits": self.ahead_waits}
         return d
 
     def __del__(self):  # pragma: no cover - best effort

@@ -1,6 +1,6 @@
 """Token-sequence family (BASELINE config 4: seq_len = 4096, on-device pad/pack).
 
-The producer ships the batch RAGGED -- flat int32 tokens + int64 offsets (+ the
+The producer ships the batch RAGGED -- flat tokens + int64 offsets (+ the
 pack plan) -- so PCIe carries only real tokens (a padded [B, 4096] batch of
 sequences averaging 2k tokens would double the bytes); the consumer expands it
 on the GPU with the ``pad_pack_tokens`` gfx950 kernel into
@@ -15,6 +15,11 @@ longer than ``seq_len`` is split into ``seq_len`` chunks, each its own segment
 with its own position ids, and empty sequences have no segment.
 ``max_seqlen`` is the longest segment (a Python int, from the producer).
 Every batch also carries ``n_tokens``: the real tokens shipped for it.
+
+Tokens are int32 in the corpus and on the wire, or uint16 when every id is below 65536
+(``SharedTokenSource.create(..., token_dtype="auto")``: GPT-2-sized vocabularies): half the bytes per
+token cross PCIe -- the token feed is link-bound, like the image feed -- and the pad/pack kernel widens
+them to int32 ``input_ids`` as it writes them, so the model sees the same batch.
 
 Sequence order is the world-size-invariant ``EpochOrder`` over sequences, so
 token batches share the indexed-mode checkpoint format.
@@ -39,7 +44,7 @@ META_FIELDS = 5  # per sub-batch: n_tokens, n_rows, n_seg, max_seg, token start 
 
 
 @functools.lru_cache(maxsize=64)
-def _regions(batch: int, max_segments: int, max_len: int, k: int) -> dict[str, tuple[int, int]]:
+def _regions(batch: int, max_segments: int, max_len: int, k: int, token_bytes: int = 4) -> dict[str, tuple[int, int]]:
     """name -> (byte offset, element count): the meta table, sub-batch 0's header arrays (sub-batch j's are
     ``header_stride`` bytes further), the shared tokens region; ``_header_stride`` and ``_total`` bytes."""
     out, off = {"meta": (0, META_FIELDS * k)}, -(-META_FIELDS * k * 8 // 16) * 16
@@ -51,7 +56,7 @@ def _regions(batch: int, max_segments: int, max_len: int, k: int) -> dict[str, t
     stride = -(-(off - hdr0) // 16) * 16
     off = hdr0 + k * stride
     out["tokens"] = (off, k * batch * max_len)
-    off += -(-k * batch * max_len * 4 // 16) * 16
+    off += -(-k * batch * max_len * token_bytes // 16) * 16
     out["_header_stride"] = (stride, 0)
     out["_total"] = (off, 0)
     return out
@@ -71,6 +76,7 @@ class TokenWindowLayout:
     seq_len: int    # S
     max_len: int    # longest sequence in the corpus
     k: int = 1      # batches per window
+    token_bytes: int = 4  # 4: int32 tokens, 2: uint16 (widened on the device)
 
     @property
     def max_segments(self) -> int:
@@ -78,7 +84,7 @@ class TokenWindowLayout:
 
     def regions(self) -> dict[str, tuple[int, int]]:
         """name -> (byte offset, element count). Computed once per layout (per-batch host path)."""
-        return _regions(self.batch, self.max_segments, self.max_len, self.k)
+        return _regions(self.batch, self.max_segments, self.max_len, self.k, self.token_bytes)
 
     @property
     def nbytes(self) -> int:
@@ -105,7 +111,8 @@ class TokenWindowLayout:
             if name.startswith("_"):
                 continue
             if name == "tokens":
-                v[name] = buf[off:off + count * 4].view(torch.int32)
+                tb = self.token_bytes
+                v[name] = buf[off:off + count * tb].view(torch.int32 if tb == 4 else torch.int16)
             elif name == "meta":
                 v[name] = buf[off:off + count * 8].view(torch.int64).view(self.k, META_FIELDS)
             else:
@@ -114,15 +121,28 @@ class TokenWindowLayout:
 
 
 class SharedTokenSource:
-    """A tokenised corpus in node-wide shm: flat int32 tokens + int64 sequence offsets."""
+    """A tokenised corpus in node-wide shm: flat tokens (int32, or uint16 ids stored as int16) + int64
+    sequence offsets."""
 
     def __init__(self, tokens: SharedArraySource, offsets: SharedArraySource, max_len: int):
         self.tokens, self.offsets, self.max_len = tokens, offsets, int(max_len)
         self.n = offsets.n - 1
+        self.token_bytes = 2 if tokens.dtype in (torch.int16, torch.uint16) else 4
 
     @classmethod
-    def create(cls, name: str, tokens: np.ndarray, offsets: np.ndarray) -> "SharedTokenSource":
-        tok = torch.from_numpy(np.ascontiguousarray(tokens, np.int32)).view(-1, 1)
+    def create(cls, name: str, tokens: np.ndarray, offsets: np.ndarray,
+               token_dtype: str = "int32") -> "SharedTokenSource":
+        """``token_dtype``: "int32", "uint16" (every id must be < 65536) or "auto" (uint16 when they are)."""
+        tokens = np.asarray(tokens)
+        if token_dtype not in ("int32", "uint16", "auto"):
+            raise ValueError("token_dtype must be 'int32', 'uint16' or 'auto'")
+        fits = tokens.size == 0 or (int(tokens.min()) >= 0 and int(tokens.max()) < 65536)
+        if token_dtype == "uint16" and not fits:
+            raise ValueError("token ids outside [0, 65536) cannot be stored as uint16")
+        if token_dtype == "uint16" or (token_dtype == "auto" and fits):
+            tok = torch.from_numpy(np.ascontiguousarray(tokens, np.uint16).view(np.int16)).view(-1, 1)
+        else:
+            tok = torch.from_numpy(np.ascontiguousarray(tokens, np.int32)).view(-1, 1)
         off = torch.from_numpy(np.ascontiguousarray(offsets, np.int64)).view(-1, 1)
         t = SharedArraySource.create(name + "_tok", tok)
         o = SharedArraySource.create(name + "_off", off)
@@ -130,12 +150,12 @@ class SharedTokenSource:
 
     @classmethod
     def synthetic(cls, name: str, n: int, min_len: int = 128, max_len: int = 4096, vocab: int = 50257,
-                  seed: int = 0) -> "SharedTokenSource":
+                  seed: int = 0, token_dtype: str = "int32") -> "SharedTokenSource":
         rng = np.random.default_rng(seed)
         lens = rng.integers(min_len, max_len + 1, size=n).astype(np.int64)
         offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
         toks = rng.integers(0, vocab, size=int(offs[-1]), dtype=np.int32)
-        return cls.create(name, toks, offs)
+        return cls.create(name, toks, offs, token_dtype)
 
     def bind_to_node(self, node: int | None) -> int:
         """Place the corpus on NUMA ``node`` (pages migrate; see ``SharedArraySource.bind_to_node``): the
@@ -267,7 +287,7 @@ class TokenBatchProducer(ProducerFunctionSkeleton):
         # k consecutive global batches per window (per-window costs -- producer round, H2D, stager and
         # window hand-off -- amortised over k batches); k divides the epoch so windows never straddle it
         k = max(d for d in range(1, min(self.batches_per_window, bpe) + 1) if bpe % d == 0)
-        self.layout = TokenWindowLayout(lb, self.seq_len, self.source.max_len, k)
+        self.layout = TokenWindowLayout(lb, self.seq_len, self.source.max_len, k, self.source.token_bytes)
         rb = self.layout.row_bytes
         return DataProducerOnInitReturn(k * lb, rb, (k * lb, rb), (rb,), "uint8", extra={
             "batches_per_epoch": bpe, "windows_per_epoch": bpe // k, "batches_per_window": k,
@@ -306,6 +326,7 @@ class TokenBatchProducer(ProducerFunctionSkeleton):
         rt = _native.runtime()
         base = (rnd * (self.n_producers or 1) + (self.producer_index or 0)) * k
         rank, world, bpe, S = self.rank_global or 0, self.world_size, self.order.batches_per_epoch, self.seq_len
+        tb = lay.token_bytes
         pack, ffd, cap = self.mode == "pack", self.pack_order == "ffd", lay.max_segments
         tok0 = 0
         for j in range(k):
@@ -318,8 +339,8 @@ class TokenBatchProducer(ProducerFunctionSkeleton):
                     idx = idx[order]
             o_ptr, rs_ptr, re_ptr, so_ptr, so_np = subs[j]
             # native ragged gather (thread pool, GIL released): sequences -> window, offsets alongside
-            n_tokens = int(rt.gather_ragged(tok_ptr + 4 * tok0, o_ptr, toks_ptr, offs_ptr, n_src,
-                                            np.ascontiguousarray(idx, np.int64), 4, tok_cap - tok0,
+            n_tokens = int(rt.gather_ragged(tok_ptr + tb * tok0, o_ptr, toks_ptr, offs_ptr, n_src,
+                                            np.ascontiguousarray(idx, np.int64), tb, tok_cap - tok0,
                                             self.host_threads))
             n_rows = n_seg = max_seg = 0
             if pack:  # packing plan written straight into the window (native)
@@ -329,7 +350,7 @@ class TokenBatchProducer(ProducerFunctionSkeleton):
             meta[j] = (n_tokens, n_rows, n_seg, max_seg, tok0)
             tok0 += n_tokens
         tok_off = lay.regions()["tokens"][0]
-        return {"tags": [tok0, k, 0, 0], "used_bytes": tok_off + 4 * tok0}
+        return {"tags": [tok0, k, 0, 0], "used_bytes": tok_off + tb * tok0}
 
 
 _VIEW_CACHE: dict = {}
@@ -414,13 +435,15 @@ def collate_token_window(buf: torch.Tensor, layout: TokenWindowLayout, mode: str
             row_end=v["row_end"].data_ptr(), seg_offsets=v["seg_offsets"].data_ptr(), n_seg=n_seg,
             out_tokens=ids.data_ptr(), attn_mask=mask.data_ptr(), position_ids=pos.data_ptr(), pos_is_i64=True,
             segment_ids=seg.data_ptr(), cu_seqlens_out=cu.data_ptr(), rows=n_rows, seq_len=s, pad_id=pad_id, mode=1,
-            stream=_stream_handle(None), fill_rows=fill)
+            stream=_stream_handle(None), fill_rows=fill, tok16=layout.token_bytes == 2)
     return {"input_ids": ids, "attention_mask": mask, "position_ids": pos, "segment_ids": seg, "cu_seqlens": cu,
             "max_seqlen": max_seqlen, "n_tokens": n_tokens, **extra}
 
 
 def expected_tokens(source: SharedTokenSource, idx) -> list[np.ndarray]:
     toks = source.tokens.tensor().view(-1).numpy()
+    if source.token_bytes == 2:  # uint16 ids stored as int16
+        toks = toks.view(np.uint16).astype(np.int32)
     offs = source.offsets.tensor().view(-1).numpy()
     return [toks[offs[i]:offs[i + 1]] for i in idx]
 

@@ -478,11 +478,26 @@ def pack_columns(groups: Sequence[torch.Tensor], index: torch.Tensor | None = No
 
 
 # --------------------------------------------------------------------- tokens
+_TOK16 = (torch.int16, torch.uint16)
+
+
+def widen_tokens(tokens: torch.Tensor) -> torch.Tensor:
+    """int32 view of a token tensor: int32 as is; 2-byte tokens (uint16 ids on the wire, int16-typed views of
+    them) zero-extended."""
+    if tokens.dtype == torch.int32:
+        return tokens
+    if tokens.dtype == torch.int16:
+        return tokens.to(torch.int32) & 0xFFFF
+    if tokens.dtype == torch.uint16:
+        return tokens.view(torch.int16).to(torch.int32) & 0xFFFF
+    raise TypeError(f"tokens must be int32 or 16-bit, got {tokens.dtype}")
+
+
 def ref_pad_tokens(tokens: torch.Tensor, offsets: torch.Tensor, seq_len: int, pad_id: int = 0,
                    position_dtype=torch.int64):
     offs = offsets.to("cpu", torch.int64).tolist()
     b = len(offs) - 1
-    t = tokens.to("cpu", torch.int32)
+    t = widen_tokens(tokens.cpu())
     out = torch.full((b, seq_len), pad_id, dtype=torch.int32)
     mask = torch.zeros((b, seq_len), dtype=torch.uint8)
     pos = torch.zeros((b, seq_len), dtype=position_dtype)
@@ -497,9 +512,10 @@ def ref_pad_tokens(tokens: torch.Tensor, offsets: torch.Tensor, seq_len: int, pa
 
 def pad_tokens(tokens: torch.Tensor, offsets: torch.Tensor, seq_len: int, pad_id: int = 0,
                position_dtype=torch.int64, stream=None):
-    """Ragged int32 token stream + [B+1] int64 offsets -> (tokens [B,S], mask u8 [B,S], position ids [B,S])."""
-    if tokens.dtype != torch.int32 or offsets.dtype != torch.int64:
-        raise TypeError("tokens must be int32 and offsets int64")
+    """Ragged token stream (int32, or 16-bit ids widened by the kernel) + [B+1] int64 offsets ->
+    (tokens [B,S] i32, mask u8 [B,S], position ids [B,S])."""
+    if (tokens.dtype != torch.int32 and tokens.dtype not in _TOK16) or offsets.dtype != torch.int64:
+        raise TypeError("tokens must be int32 / 16-bit and offsets int64")
     if not tokens.is_cuda:
         return ref_pad_tokens(tokens, offsets, seq_len, pad_id, position_dtype)
     b = offsets.numel() - 1
@@ -511,7 +527,7 @@ def pad_tokens(tokens: torch.Tensor, offsets: torch.Tensor, seq_len: int, pad_id
         tokens=tokens.data_ptr(), offsets=offsets.data_ptr(), row_start=0, row_end=0, seg_offsets=0, n_seg=0,
         out_tokens=out.data_ptr(), attn_mask=mask.data_ptr(), position_ids=pos.data_ptr(),
         pos_is_i64=position_dtype == torch.int64, segment_ids=0, cu_seqlens_out=0, rows=b, seq_len=seq_len,
-        pad_id=pad_id, mode=0, stream=_stream_handle(stream))
+        pad_id=pad_id, mode=0, stream=_stream_handle(stream), tok16=tokens.dtype in _TOK16)
     return out, mask, pos
 
 
@@ -578,7 +594,7 @@ def ref_pack_plan(seq_offsets: np.ndarray, seq_len: int, max_rows: int | None = 
 def ref_pack_tokens(tokens, row_start, row_end, seg_offsets, seq_len, pad_id=0, position_dtype=torch.int64,
                     fill_rows: int = 0):
     """CPU reference of pack mode; ``fill_rows`` > packed rows: padding rows up to that fixed row count."""
-    t = tokens.to("cpu", torch.int32)
+    t = widen_tokens(tokens.cpu())
     rs, re_, so = (np.asarray(a) for a in (row_start, row_end, seg_offsets))
     r = max(len(rs), int(fill_rows))
     out = torch.full((r, seq_len), pad_id, dtype=torch.int32)
@@ -596,13 +612,104 @@ def ref_pack_tokens(tokens, row_start, row_end, seg_offsets, seq_len, pad_id=0, 
     return out, mask, pos, seg
 
 
+def pack_capacity(n_seq: int, n_tokens: int, seq_len: int) -> tuple[int, int]:
+    """(max segments, max rows) that in-order packing of ``n_seq`` sequences holding at most ``n_tokens``
+    tokens can produce: each sequence splits into ceil(len / S) segments (<= n_seq + n_tokens // S in total),
+    and two consecutive rows together hold more than S tokens (else the greedy pass would have merged them),
+    so rows <= 2 * ceil(n_tokens / S) + 1."""
+    S = int(seq_len)
+    max_segs = int(n_seq) + int(n_tokens) // S
+    max_rows = min(max_segs, 2 * (-(-int(n_tokens) // S)) + 1)
+    return max_segs, max(max_rows, 0)
+
+
+def pack_tokens_device(tokens: torch.Tensor, offsets: torch.Tensor, seq_len: int, pad_id: int = 0,
+                       position_dtype=torch.int64, max_rows: int | None = None, stream=None) -> dict:
+    """Pack with the plan built ON THE DEVICE: two launches (``pack_plan_device``, then the pack kernel
+    reading the plan's row count from device memory), no host round trip, static output shapes.
+
+    ``offsets`` is the [B+1] int64 offsets tensor on the tokens' device. Outputs have ``max_rows`` rows
+    (default: ``pack_capacity`` of the token buffer, an upper bound the plan cannot exceed); rows past the
+    plan's are padding (pad_id, mask 0, position 0, segment -1). Returns a dict: ``input_ids``,
+    ``attention_mask``, ``position_ids``, ``segment_ids``, ``cu_seqlens`` (int32, capacity max_segs + 1; only
+    the first n_seg + 1 entries are written), ``counts`` (device int64 [n_rows, n_seg]; n_rows = -1 if max_rows
+    was too small, every row then padding). Reference of the plan: ``pack_plan`` (host, runtime/arena.cpp).
+    Graph-capturable: nothing in it synchronises with the host.
+    """
+    if (tokens.dtype != torch.int32 and tokens.dtype not in _TOK16) or offsets.dtype != torch.int64:
+        raise TypeError("tokens must be int32 / 16-bit and offsets int64")
+    n = offsets.numel() - 1
+    if n < 0:
+        raise ValueError("offsets needs at least one entry")
+    S = int(seq_len)
+    max_segs, cap_rows = pack_capacity(n, tokens.numel(), S)
+    R = cap_rows if max_rows is None else int(max_rows)
+    dev = tokens.device
+    if not tokens.is_cuda:  # host reference: the same outputs from the host plan
+        rs, re_, so = ref_pack_plan(offsets.cpu().numpy(), S)
+        ok = len(rs) <= R
+        out, mask, pos, seg = ref_pack_tokens(tokens, rs[:R] if ok else rs[:0], re_[:R] if ok else re_[:0], so, S,
+                                              pad_id, position_dtype, fill_rows=R)
+        cu = torch.zeros(max_segs + 1, dtype=torch.int32)
+        cu[:len(so)] = torch.from_numpy(so.astype(np.int32))
+        counts = torch.tensor([len(rs) if ok else -1, len(so) - 1], dtype=torch.int64)
+        return {"input_ids": out[:R], "attention_mask": mask[:R], "position_ids": pos[:R], "segment_ids": seg[:R],
+                "cu_seqlens": cu, "counts": counts}
+    if not offsets.is_cuda or offsets.device != dev:
+        raise ValueError("offsets must be on the tokens' device (use pack_tokens for host offsets)")
+    h = _native.hip()
+    offsets = offsets.contiguous()
+    # one allocation for the plan, its scratch and the five outputs (16-byte aligned regions)
+    pb = 8 if position_dtype == torch.int64 else 4
+    sizes = [8 * (max_segs + 1), 8 * max(R, 1), 8 * max(R, 1), 16, 4 * h.pack_plan_scratch_ints(max_segs, R),
+             4 * R * S, R * S, pb * R * S, 4 * R * S, 4 * (max_segs + 1)]
+    offs_b = [0]
+    for n_b in sizes:
+        offs_b.append(offs_b[-1] + -(-n_b // 16) * 16)
+    whole = torch.empty(offs_b[-1], dtype=torch.uint8, device=dev)
+    reg = [whole[a:a + n_b] for a, n_b in zip(offs_b, sizes)]
+    so, rs, re_, counts = (r.view(torch.int64) for r in reg[:4])
+    scratch = reg[4].view(torch.int32)
+    out = reg[5].view(torch.int32).view(R, S)
+    mask = reg[6].view(R, S)
+    pos = reg[7].view(position_dtype).view(R, S)
+    seg = reg[8].view(torch.int32).view(R, S)
+    cu = reg[9].view(torch.int32)
+    sh = _stream_handle(stream)
+    h.pack_plan_device(offsets=offsets.data_ptr(), n=n, seq_len=S, max_segs=max_segs, max_rows=R,
+                       seg_offsets=so.data_ptr(), row_start=rs.data_ptr(), row_end=re_.data_ptr(),
+                       counts=counts.data_ptr(), scratch=scratch.data_ptr(), stream=sh)
+    if R > 0:
+        h.pad_pack_tokens(
+            tokens=tokens.data_ptr(), offsets=0, row_start=rs.data_ptr(), row_end=re_.data_ptr(),
+            seg_offsets=so.data_ptr(), n_seg=0, out_tokens=out.data_ptr(), attn_mask=mask.data_ptr(),
+            position_ids=pos.data_ptr(), pos_is_i64=position_dtype == torch.int64, segment_ids=seg.data_ptr(),
+            cu_seqlens_out=cu.data_ptr(), rows=0, seq_len=S, pad_id=pad_id, mode=1, stream=sh, fill_rows=R,
+            dev_counts=counts.data_ptr(), tok16=tokens.dtype in _TOK16)
+    else:  # no rows to launch over: the (empty) plan's cu_seqlens is the single 0
+        cu[:1].zero_()
+    return {"input_ids": out, "attention_mask": mask, "position_ids": pos, "segment_ids": seg, "cu_seqlens": cu,
+            "counts": counts}
+
+
 def pack_tokens(tokens: torch.Tensor, seq_offsets, seq_len: int, pad_id: int = 0, position_dtype=torch.int64,
                 stream=None):
     """Pack a ragged token stream into rows of ``seq_len`` (varlen-attention layout).
 
     Returns (tokens [R,S] i32, mask [R,S] u8, position_ids [R,S], segment_ids [R,S] i32 (-1 = pad),
     cu_seqlens [n_seg+1] i32 over the unpadded stream ``tokens[mask.bool()]``).
+
+    Offsets already on the tokens' GPU: the plan is built on the device (``pack_tokens_device``) and the
+    one host synchronisation is the read of the row count that sizes the result. Host offsets: the host
+    plan (native ``pack_plan``), uploaded with the launch.
     """
+    if tokens.is_cuda and torch.is_tensor(seq_offsets) and seq_offsets.device == tokens.device:
+        r = pack_tokens_device(tokens, seq_offsets.to(torch.int64), seq_len, pad_id, position_dtype, stream=stream)
+        n_rows, n_seg = (int(v) for v in r["counts"].cpu())
+        if n_rows < 0:  # cannot happen within pack_capacity; kept loud
+            raise RuntimeError(f"device pack plan overflowed ({n_seg} segments)")
+        return (r["input_ids"][:n_rows], r["attention_mask"][:n_rows], r["position_ids"][:n_rows],
+                r["segment_ids"][:n_rows], r["cu_seqlens"][:n_seg + 1])
     rs, re_, so = pack_plan(np.asarray(seq_offsets.cpu() if torch.is_tensor(seq_offsets) else seq_offsets),
                             seq_len)
     cu = torch.from_numpy(so.astype(np.int32))
@@ -619,7 +726,8 @@ def pack_tokens(tokens: torch.Tensor, seq_offsets, seq_len: int, pad_id: int = 0
         tokens=tokens.data_ptr(), offsets=0, row_start=rs_d.data_ptr(), row_end=re_d.data_ptr(),
         seg_offsets=so_d.data_ptr(), n_seg=len(so) - 1, out_tokens=out.data_ptr(), attn_mask=mask.data_ptr(),
         position_ids=pos.data_ptr(), pos_is_i64=position_dtype == torch.int64, segment_ids=seg.data_ptr(),
-        cu_seqlens_out=0, rows=r, seq_len=seq_len, pad_id=pad_id, mode=1, stream=_stream_handle(stream))
+        cu_seqlens_out=0, rows=r, seq_len=seq_len, pad_id=pad_id, mode=1, stream=_stream_handle(stream),
+        tok16=tokens.dtype in _TOK16)
     return out, mask, pos, seg, so_d.to(torch.int32)
 
 

@@ -208,6 +208,81 @@ def test_pack_tokens_many_short_sequences():
     assert torch.equal(out[4].cpu(), torch.from_numpy(so.astype(np.int32)))
 
 
+def _device_pack_case(seed, n, lo, hi, seq_len, empty_frac=0.0):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(lo, hi, size=n)
+    lens[rng.random(n) < empty_frac] = 0
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    toks = torch.from_numpy(rng.integers(0, 50000, size=max(int(offs[-1]), 1)).astype(np.int32))
+    return offs, toks
+
+
+@pytest.mark.parametrize("case", [
+    (0, 40, 1, 6000, 4096, 0.0),      # long sequences split into seq_len segments
+    (1, 64, 1, 300, 4096, 0.2),       # the kernel-bench shape, empty sequences among them
+    (2, 2048, 1, 3000, 4096, 0.0),    # a loader-sized batch (jump tables in LDS)
+    (3, 5000, 0, 9, 64, 0.1),         # many short sequences: jump tables in global scratch
+    (4, 7, 0, 1, 16, 0.0),            # every sequence empty
+    (5, 1, 8192, 8193, 4096, 0.0),    # one sequence of exactly 2 * seq_len
+])
+def test_pack_plan_on_device_matches_host_plan(case):
+    """The device plan (pointer doubling over the greedy jump) == the host's sequential plan, and the pack that
+    reads its row count from device memory == the reference pack padded to the plan's capacity."""
+    seed, n, lo, hi, S, empty = case
+    offs, toks = _device_pack_case(seed, n, lo, hi, S, empty)
+    rs, re_, so = ops.ref_pack_plan(offs, S)
+    r = ops.pack_tokens_device(toks.to(_dev()), torch.from_numpy(offs).to(_dev()), S, pad_id=5)
+    n_rows, n_seg = (int(v) for v in r["counts"].cpu())
+    assert (n_rows, n_seg) == (len(rs), len(so) - 1)
+    R = r["input_ids"].shape[0]
+    assert R >= n_rows
+    ref = ops.ref_pack_tokens(toks, rs, re_, so, S, pad_id=5, fill_rows=R)
+    for k, b in zip(("input_ids", "attention_mask", "position_ids", "segment_ids"), ref):
+        assert torch.equal(r[k].cpu(), b), k
+    assert torch.equal(r["cu_seqlens"][:n_seg + 1].cpu(), torch.from_numpy(so.astype(np.int32)))
+
+
+def test_pack_plan_on_device_overflow_is_flagged_and_padded():
+    offs, toks = _device_pack_case(7, 50, 100, 200, 256)
+    rs, _, _ = ops.ref_pack_plan(offs, 256)
+    r = ops.pack_tokens_device(toks.to(_dev()), torch.from_numpy(offs).to(_dev()), 256, max_rows=len(rs) - 1)
+    assert int(r["counts"][0]) == -1
+    assert int(r["attention_mask"].sum()) == 0 and bool((r["segment_ids"] == -1).all())
+
+
+def test_pack_tokens_with_device_offsets_uses_the_device_plan():
+    offs, toks = _device_pack_case(8, 300, 1, 5000, 4096)
+    ref = ops.pack_tokens(toks.to(_dev()), offs, 4096)  # host plan
+    out = ops.pack_tokens(toks.to(_dev()), torch.from_numpy(offs).to(_dev()), 4096)
+    for a, b in zip(out, ref):
+        assert a.shape == b.shape and torch.equal(a.cpu(), b.cpu())
+
+
+def test_pack_plan_on_device_is_graph_capturable():
+    """No host synchronisation inside: the plan + pack capture into a HIP graph and replay on new offsets."""
+    offs, toks = _device_pack_case(9, 128, 1, 900, 1024)
+    dt, do = toks.to(_dev()), torch.from_numpy(offs).to(_dev())
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.pack_tokens_device(dt, do, 1024)  # warm-up allocations outside the capture
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        r = ops.pack_tokens_device(dt, do, 1024)
+    offs2, toks2 = _device_pack_case(10, 128, 1, 900, 1024)
+    n2 = min(len(toks2), len(toks))
+    offs2 = np.minimum(offs2, n2)
+    dt[:n2].copy_(toks2[:n2].to(_dev()))
+    do.copy_(torch.from_numpy(offs2).to(_dev()))
+    g.replay()
+    torch.cuda.synchronize()
+    rs, re_, so = ops.ref_pack_plan(offs2, 1024)
+    assert int(r["counts"][0]) == len(rs)
+    ref = ops.ref_pack_tokens(dt.cpu(), rs, re_, so, 1024, fill_rows=r["input_ids"].shape[0])
+    assert torch.equal(r["input_ids"].cpu(), ref[0]) and torch.equal(r["position_ids"].cpu(), ref[2])
+
+
 @pytest.mark.parametrize("nbytes", [4, 1000, 4096 * 77 + 12, 256 * 3 * 224 * 224 * 2])
 def test_checksum(nbytes):
     x = torch.randint(0, 256, (nbytes,), dtype=torch.uint8)

@@ -17,6 +17,17 @@ def corpus():
     src.close()
 
 
+@pytest.fixture(params=["int32", "uint16"])
+def wire_corpus(request):
+    """The corpus with int32 tokens, and with uint16 tokens (2 B per token on the wire, widened on the
+    device); vocab 65536 so the top ids (sign bit of an int16) are exercised."""
+    src = SharedTokenSource.synthetic(f"ddl_amd_tok_{np.random.randint(1 << 30)}", 200, 5, 300, seed=3,
+                                      vocab=65536, token_dtype=request.param)
+    assert src.token_bytes == (2 if request.param == "uint16" else 4)
+    yield src
+    src.close()
+
+
 def _check_pad(batch, source, idx, seq_len):
     ids, mask, pos = batch["input_ids"].cpu(), batch["attention_mask"].cpu(), batch["position_ids"].cpu()
     for r, seq in enumerate(expected_tokens(source, idx)):
@@ -28,14 +39,14 @@ def _check_pad(batch, source, idx, seq_len):
 
 @pytest.mark.parametrize("k", [1, 5])
 @pytest.mark.parametrize("mode", ["pad", "pack"])
-def test_token_batches_cpu(corpus, mode, k, monkeypatch):
+def test_token_batches_cpu(wire_corpus, mode, k, monkeypatch):
     """k=5 asks for 5 batches per window: 12 batches per epoch -> 4 (the largest divisor <= 5)."""
     monkeypatch.setenv("DDL_DEVICE", "cpu")  # host collate path, even on a GPU box
     seq_len, gb = 256, 16
-    order = EpochOrder(corpus.n, gb, 4)
+    order = EpochOrder(wire_corpus.n, gb, 4)
     with ddl_amd.start(n_producers=2) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(corpus, gb, seq_len, mode, batches_per_window=k), gb,
-                                           conn, 2, mode="indexed", env=env, auto_mark=True, collate="tokens", seed=4)
+        prod = TokenBatchProducer(wire_corpus, gb, seq_len, mode, batches_per_window=k)
+        dl = ddl_amd.DistributedDataLoader(prod, gb, conn, 2, mode="indexed", env=env, auto_mark=True, collate="tokens", seed=4)
         assert dl.batches_per_window == [1 if k == 1 else 4] * 2
         assert len(dl) == order.batches_per_epoch
         for e in range(2):
@@ -43,11 +54,11 @@ def test_token_batches_cpu(corpus, mode, k, monkeypatch):
                 idx = order.indices(e, g)
                 if mode == "pad":
                     assert batch["input_ids"].shape == (gb, seq_len)
-                    _check_pad(batch, corpus, idx, seq_len)
+                    _check_pad(batch, wire_corpus, idx, seq_len)
                 else:
                     m = batch["attention_mask"].bool()
                     flat = batch["input_ids"][m]
-                    ref = np.concatenate(expected_tokens(corpus, idx))
+                    ref = np.concatenate(expected_tokens(wire_corpus, idx))
                     assert np.array_equal(flat.numpy(), ref)  # every token exactly once, in order
                     assert batch["input_ids"].shape[1] == seq_len
                     cu = batch["cu_seqlens"]
@@ -57,25 +68,24 @@ def test_token_batches_cpu(corpus, mode, k, monkeypatch):
 @pytest.mark.gpu
 @pytest.mark.parametrize("k", [1, 4])
 @pytest.mark.parametrize("mode", ["pad", "pack"])
-def test_token_batches_gpu(corpus, mode, k):
+def test_token_batches_gpu(wire_corpus, mode, k):
     seq_len, gb = 256, 16
-    order = EpochOrder(corpus.n, gb, 4)
+    order = EpochOrder(wire_corpus.n, gb, 4)
     with ddl_amd.start(n_producers=2) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(corpus, gb, seq_len, mode, batches_per_window=k), gb,
-                                           conn, 1,
-                                           mode="indexed", env=env, auto_mark=True, collate="tokens", seed=4)
+        prod = TokenBatchProducer(wire_corpus, gb, seq_len, mode, batches_per_window=k)
+        dl = ddl_amd.DistributedDataLoader(prod, gb, conn, 1, mode="indexed", env=env, auto_mark=True, collate="tokens", seed=4)
         held = None
         for g, batch in enumerate(dl):
             assert batch["input_ids"].is_cuda
             idx = order.indices(0, g)
             if mode == "pad":
-                _check_pad(batch, corpus, idx, seq_len)
+                _check_pad(batch, wire_corpus, idx, seq_len)
             else:
                 m = batch["attention_mask"].bool().cpu()
                 flat = batch["input_ids"].cpu()[m]
-                assert np.array_equal(flat.numpy(), np.concatenate(expected_tokens(corpus, idx)))
+                assert np.array_equal(flat.numpy(), np.concatenate(expected_tokens(wire_corpus, idx)))
                 if held is None:
-                    lens = [len(x) for x in expected_tokens(corpus, idx)]
+                    lens = [len(x) for x in expected_tokens(wire_corpus, idx)]
                     held = (batch["cu_seqlens"], ops.pack_plan(np.concatenate([[0], np.cumsum(lens)]), seq_len)[2])
         if held is not None:  # cu_seqlens is owned: still intact after the staging buffers were reused
             assert held[0].dtype == torch.int32
@@ -94,6 +104,80 @@ def test_native_pack_plan_matches_reference(seq_len):
         ref = ops.ref_pack_plan(offs, seq_len)
         for a, b in zip(got, ref):
             assert np.array_equal(a, b), (n, a, b)
+
+
+def _doubling_plan(offs, S):
+    """numpy mirror of the device planner (tokens.hip pack_plan_kernel): segments by a scan, the greedy jump
+    by a search over segment starts, the rows as the orbit of segment 0 by pointer doubling."""
+    lens = np.diff(offs)
+    c = np.where(lens > 0, -(-lens // S), 0)
+    first = np.concatenate([[0], np.cumsum(c)])[:-1]
+    n_seg = int(c.sum())
+    so = np.empty(n_seg + 1, np.int64)
+    for i in np.nonzero(c)[0]:
+        so[first[i]:first[i] + c[i]] = offs[i] + S * np.arange(c[i])
+    so[n_seg] = offs[-1] if n_seg else 0
+    J = np.append(np.searchsorted(so, so[:n_seg] + S, side="right") - 1, n_seg)
+    P = np.array([0])
+    while P[-1] < n_seg:  # P[len + i] = jump^len(P[i]); jump^len -> jump^(2 len)
+        P = np.concatenate([P, J[P]])
+        J = J[J]
+    P = P[: np.argmax(P == n_seg) + 1]
+    return so[P[:-1]], so[P[1:]], so
+
+
+@pytest.mark.parametrize("seq_len", [4096, 100, 7, 1])
+def test_pointer_doubling_plan_equals_the_sequential_plan(seq_len):
+    """The device planner's algorithm (checked here in numpy; the kernel itself in test_kernels_gpu.py)."""
+    rng = np.random.default_rng(11 + seq_len)
+    for n in (0, 1, 2, 5, 64, 333):
+        for hi in (2, seq_len + 1, 3 * seq_len):
+            lens = rng.integers(0, hi, size=n)
+            offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+            got = _doubling_plan(offs, seq_len)
+            ref = ops.ref_pack_plan(offs, seq_len)
+            for a, b in zip(got, ref):
+                assert np.array_equal(a, b), (n, hi, a, b)
+            n_segs, n_rows = ops.pack_capacity(n, int(offs[-1]), seq_len)
+            assert len(ref[0]) <= n_rows and len(ref[2]) - 1 <= n_segs
+
+
+def test_sixteen_bit_tokens_widen_in_the_host_references():
+    ids = np.array([0, 1, 32767, 32768, 65535, 7], np.uint16)
+    t16 = torch.from_numpy(ids.view(np.int16))
+    offs = torch.tensor([0, 2, 6], dtype=torch.int64)
+    out, mask, _ = ops.ref_pad_tokens(t16, offs, 5)
+    assert out[1, :4].tolist() == [32767, 32768, 65535, 7]
+    rs, re_, so = ops.ref_pack_plan(offs.numpy(), 8)
+    packed = ops.ref_pack_tokens(t16, rs, re_, so, 8)[0]
+    assert packed[0, :6].tolist() == ids.astype(np.int64).tolist()
+
+
+def test_token_source_dtype_choice():
+    ok = SharedTokenSource.create(f"ddl_amd_tokdt_{np.random.randint(1 << 30)}", np.array([1, 65535]),
+                                  np.array([0, 2]), "auto")
+    wide = SharedTokenSource.create(f"ddl_amd_tokdt_{np.random.randint(1 << 30)}", np.array([1, 70000]),
+                                    np.array([0, 2]), "auto")
+    try:
+        assert ok.token_bytes == 2 and wide.token_bytes == 4
+        assert [x.tolist() for x in expected_tokens(ok, [0])] == [[1, 65535]]
+        with pytest.raises(ValueError):
+            SharedTokenSource.create("ddl_amd_never", np.array([70000]), np.array([0, 1]), "uint16")
+    finally:
+        ok.close()
+        wide.close()
+
+
+def test_pack_tokens_device_host_reference_shapes():
+    """CPU form of pack_tokens_device: fixed capacity rows, counts, padding rows after the plan's."""
+    offs = np.array([0, 10, 10, 60, 61, 100], np.int64)
+    toks = torch.arange(100, dtype=torch.int32)
+    r = ops.pack_tokens_device(toks, torch.from_numpy(offs), 16, pad_id=9)
+    rs, re_, so = ops.ref_pack_plan(offs, 16)
+    assert r["counts"].tolist() == [len(rs), len(so) - 1]
+    assert r["input_ids"].shape == (ops.pack_capacity(5, 100, 16)[1], 16)
+    assert torch.equal(r["input_ids"][r["attention_mask"].bool()], toks)
+    assert bool((r["input_ids"][len(rs):] == 9).all()) and bool((r["segment_ids"][len(rs):] == -1).all())
 
 
 def test_native_gather_ragged():
