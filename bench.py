@@ -27,13 +27,15 @@ sample crosses PCIe in every step (each window is re-copied H2D each visit;
 no caching). W warmup steps, then EXACTLY K timed steps bracketed by
 barrier + synchronize; max time over ranks. ``value`` is the SMALLER of
   * delivered: samples handed to the consumer in the timed region / time, and
-  * landed: samples whose H2D copy retired in the timed region / time
-    (counted by the stager's post-DMA host callback),
-so windows staged in HBM before t0 cannot inflate a short run. A landed window
-counts only if its copy was also ENQUEUED inside the region (the native
-stager timestamps every copy): a copy already in flight at t0 moved part of
-its bytes before the region and is not counted. Both rates are in the JSON
-line, with the H2D bytes and GB/s of the timed region.
+  * landed: samples whose bytes crossed PCIe inside the timed region / time,
+    on the GPU clock: the native stager times every window copy on the device
+    (an event when its stream reaches the copy, its retire event), HIP timing
+    events bracket the region on the idle compute stream, and each copy counts
+    with the share of its [start, end] inside the region (pro rata, so the
+    ~1.4 ms window granularity no longer quantises a 27 ms region),
+so windows staged in HBM before t0 cannot inflate a short run. Both rates are
+in the JSON line, with the H2D bytes and GB/s of the timed region and the
+older whole-window count (copies enqueued AND retired inside the region).
 Phase 2 (``gpu_idle_pct``): a fixed-cost bf16 train step (PatchMLP fwd+bwd+SGD)
 consumes the batches; the compute stream's idle fraction is measured with HIP
 events (idle = 1 - busy/wall). ``benchmarks/bench_idle_sweep.py`` sweeps a
@@ -342,9 +344,16 @@ def main(argv=None) -> int:
         host_log = os.environ.get("DDL_HOST_LOG")
         ticks = []
         barrier()
-        # the region's H2D work: copies ENQUEUED inside it (native stager timestamps, CLOCK_MONOTONIC) that
-        # retired by its end -- a copy already in flight at t0 moved bytes before it and is not counted
+        # the region's H2D work, on the GPU clock: events bracket the region on the (idle) compute stream, and
+        # every window copy is timed on the device, so exactly the bytes that crossed PCIe inside the region
+        # count (pro rata for the copies in flight at either end); the older whole-window counts (copies
+        # ENQUEUED inside the region, native CLOCK_MONOTONIC timestamps) stay in the JSON as diagnostics
+        ev0 = ev1 = None
+        if dev.type == "cuda":
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
+        if ev0 is not None:
+            ev0.record()
         t0_ns = rt.now_ns()
         w_land0, b_land0 = _landed(dl)
         w_cur0 = dl.window
@@ -357,6 +366,8 @@ def main(argv=None) -> int:
                     ticks.append(time.perf_counter())
             sync()
         t1 = time.perf_counter()
+        if ev1 is not None:
+            ev1.record()
         t1_ns = rt.now_ns()
         # complete right now (before settle(): a copy still in flight at t1 must not finish into the count)
         cb = dl._stager._native.copies_between(t0_ns, t1_ns) if dl._stager is not None else None
@@ -364,17 +375,27 @@ def main(argv=None) -> int:
         bytes_enq1 = dl._stager.bytes_h2d if dl._stager is not None else 0
         # CPU rehearsal: the host path has no H2D; every delivered window counts
         n_in, b_in = cb if cb is not None else (w_land1 - w_land0, 0)
+        pro = dl._stager.bytes_in_interval(ev0, ev1) if dl._stager is not None and ev0 is not None else None
+        if pro is not None and pro["ok"]:
+            # the device interval is the region as the GPU saw it; its length next to the host's is a check
+            n_in_prorata, b_in_prorata = pro["windows"], pro["bytes"]
+        else:
+            n_in_prorata, b_in_prorata = float(n_in), float(b_in)
         prod1 = conn.producer_stats()
         barrier()
         elapsed = t1 - t0
-        landed_samples = n_in * args.window
+        landed_samples = n_in_prorata * args.window
         mine = {
             "rank": env.rank,
             "elapsed_s": elapsed,
             "delivered_per_s": args.batch * args.steps / elapsed,
             "landed_per_s": landed_samples / elapsed,
-            "h2d_bytes_timed": b_in,
-            "h2d_gbps_timed": b_in / elapsed / 1e9,
+            "h2d_bytes_timed": int(b_in_prorata),
+            "h2d_gbps_timed": b_in_prorata / elapsed / 1e9,
+            "h2d_accounting": "device-timed pro rata" if pro is not None and pro["ok"] else "whole windows",
+            "device_region_ms": round(pro["t1_ms"] - pro["t0_ms"], 4) if pro is not None and pro["ok"] else None,
+            "h2d_copies_overlapping_region": pro["copies"] if pro is not None else None,
+            "h2d_bytes_whole_windows_enqueued_and_retired_in_region": b_in,
             "h2d_bytes_landed_any_enqueue_time": b_land1 - b_land0,
             "h2d_enqueued_bytes_timed": bytes_enq1 - bytes_enq0,
             "windows_prestaged_at_t0": max(0, w_land0 - w_cur0),

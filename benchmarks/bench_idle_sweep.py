@@ -72,6 +72,14 @@ def _parse(argv=None):
                          "host runs ahead of the GPU")
     ap.add_argument("--dispatch", default="auto", help="native_dispatch of the image loader (auto / inline / "
                                                          "lookahead / python)")
+    ap.add_argument("--tune-passes", type=int, default=2,
+                    help="per point: re-size the calibrated step this many times from its busy time measured on the "
+                         "loader's batches (the isolated calibration runs at other clocks and without the loader's "
+                         "memory traffic, and landed 0.75 at a measured 0.91-0.94)")
+    ap.add_argument("--tune-steps", type=int, default=30)
+    ap.add_argument("--read", default="all", choices=["all", "ids"],
+                    help="tokens: the consumer reads every tensor of the batch (all) or only input_ids (ids, as "
+                         "bench_tokens.py's feed phase)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
 
@@ -165,7 +173,7 @@ def main(argv=None) -> int:
 
     ratios = [float(x) for x in a.ratios.split(",") if x]
     host_marks = os.environ.get("DDL_SWEEP_MARKERS", "0") == "1"
-    n_steps = a.warmup + 2 * a.feed_steps + len(ratios) * (a.steps + a.warmup + 30)
+    n_steps = a.warmup + 2 * a.feed_steps + len(ratios) * (a.steps + a.warmup + a.tune_passes * a.tune_steps + 30)
     src = None
     if a.family == "tokens":
         from ddl_amd.models.tokens import SharedTokenSource
@@ -187,8 +195,12 @@ def main(argv=None) -> int:
             dev = torch.device(env.device)
             acc = ops.ChecksumAccumulator(dev)
 
+            keys = ("input_ids",) if a.read == "ids" and a.family == "tokens" else None
+
             def read(batch):
-                for t in (batch.values() if isinstance(batch, dict) else batch):
+                if isinstance(batch, dict):
+                    batch = batch.values() if keys is None else [batch[k] for k in keys]
+                for t in batch:
                     if isinstance(t, torch.Tensor):
                         acc.add(t)
 
@@ -228,10 +240,20 @@ def main(argv=None) -> int:
 
             # ---- sweep
             for i, r in enumerate(ratios):
-                step = CalibratedStep(dev, step_ms=1000.0 * B / (r * feed))
+                step = CalibratedStep(dev, step_ms=1000.0 * B / (r * feed), read_keys=keys)
                 step.calibrate(next(it))
                 for _ in range(a.warmup):
                     step(next(it))
+                for _ in range(a.tune_passes):  # re-size the step from its busy time in this very loop
+                    tm = ComputeIdleMeter()
+                    for _ in range(a.tune_steps):
+                        batch = next(it)
+                        tm.step_begin()
+                        step(batch)
+                        tm.step_end()
+                    torch.cuda.synchronize()
+                    tr = tm.result()
+                    step.tune(tr["busy_ms"] / max(1, tr["steps"]))
                 meter = ComputeIdleMeter()
                 nd0 = dl.stats().get("native_dispatch") or {}
                 seg0 = torch.cuda.memory_stats(dev).get("segment.all.allocated", 0)
@@ -255,7 +277,8 @@ def main(argv=None) -> int:
                 cap = 1000.0 * B / busy_per_step  # measured step capacity C
                 pred = 100.0 * max(0.0, 1.0 - feed / cap)
                 pt = {"point": f"sweep.p{i:02d}", "ratio_target": r, "step_ms_target": round(step.step_ms, 4),
-                      "gemm_reps": step.reps, "gemm_rows": step.a.shape[0], "busy_ms_per_step": round(busy_per_step, 4),
+                      "gemm_reps": step.reps, "gemm_rows": step.a.shape[0], "gemm_tail_rows": step.tail_rows,
+                      "busy_ms_per_step": round(busy_per_step, 4),
                       "step_capacity_per_s": round(cap, 1), "ratio_measured": round(cap / feed, 3),
                       "achieved_per_s": round(B * a.steps / (t3 - t2), 1),
                       "gpu_idle_pct": round(res["gpu_idle_pct"], 3), "predicted_idle_pct": round(pred, 3),

@@ -192,7 +192,8 @@ PYBIND11_MODULE(_ddl_hip, m) {
       .def(py::init([](uintptr_t arena, int32_t n_producers, int32_t n_slots, int64_t first, int64_t total,
                        std::vector<uintptr_t> buffers, uint64_t buffer_bytes, uintptr_t copy_stream, int device,
                        std::vector<int32_t> peer_pids, int64_t timeout_ms, std::vector<uintptr_t> ready,
-                       std::vector<uintptr_t> copy_done, bool post_copy, int64_t meta_bytes, uintptr_t copy_stream2) {
+                       std::vector<uintptr_t> copy_done, bool post_copy, int64_t meta_bytes, uintptr_t copy_stream2,
+                       int copy_policy) {
              std::vector<void*> bufs;
              for (auto b : buffers) bufs.push_back(as_ptr<void>(b));
              std::vector<hipEvent_t> rd, cd;
@@ -201,12 +202,13 @@ PYBIND11_MODULE(_ddl_hip, m) {
              return std::make_unique<ddl::NativeStager>(
                  reinterpret_cast<const ddl::Arena*>(arena), n_producers, n_slots, first, total, std::move(bufs),
                  buffer_bytes, as_stream(copy_stream), device, std::move(peer_pids), timeout_ms, std::move(rd),
-                 std::move(cd), post_copy, meta_bytes, as_stream(copy_stream2));
+                 std::move(cd), post_copy, meta_bytes, as_stream(copy_stream2), copy_policy);
            }),
            py::arg("arena"), py::arg("n_producers"), py::arg("n_slots"), py::arg("first"), py::arg("total"),
            py::arg("buffers"), py::arg("buffer_bytes"), py::arg("copy_stream"), py::arg("device"),
            py::arg("peer_pids"), py::arg("timeout_ms"), py::arg("ready"), py::arg("copy_done"),
-           py::arg("post_copy"), py::arg("meta_bytes") = 0, py::arg("copy_stream2") = 0)
+           py::arg("post_copy"), py::arg("meta_bytes") = 0, py::arg("copy_stream2") = 0,
+           py::arg("copy_policy") = 1)
       .def(
           "wait",
           [](ddl::NativeStager& st, int64_t w, int64_t timeout_ms) {
@@ -246,8 +248,28 @@ PYBIND11_MODULE(_ddl_hip, m) {
       .def("settle", &ddl::NativeStager::settle, py::arg("timeout_ms") = 1000, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("bytes_landed", &ddl::NativeStager::bytes_landed)
       .def_property_readonly("wait_producer_s", &ddl::NativeStager::wait_producer_s)
+      .def_property_readonly("free_waits", &ddl::NativeStager::free_waits)
       .def("copies_between", &ddl::NativeStager::copies_between, py::arg("t0_ns"), py::arg("t1_ns"),
            "(windows, bytes) of H2D copies enqueued in [t0_ns, t1_ns] (CLOCK_MONOTONIC) that have retired")
+      .def(
+          "bytes_in_interval",
+          [](ddl::NativeStager& st, uintptr_t e0, uintptr_t e1, int64_t timeout_ms) {
+            ddl::InIntervalBytes r;
+            {
+              py::gil_scoped_release nogil;
+              r = st.bytes_in_interval(reinterpret_cast<hipEvent_t>(e0), reinterpret_cast<hipEvent_t>(e1), timeout_ms);
+            }
+            py::dict d;
+            d["ok"] = r.ok;
+            d["bytes"] = r.bytes;
+            d["windows"] = r.windows;
+            d["copies"] = r.copies;
+            d["t0_ms"] = r.t0_ms;
+            d["t1_ms"] = r.t1_ms;
+            return d;
+          },
+          py::arg("e0"), py::arg("e1"), py::arg("timeout_ms") = 2000,
+          "H2D bytes that crossed PCIe between two completed timing events (device clock, pro rata per copy)")
       .def_property_readonly("wait_log", &ddl::NativeStager::wait_log,
                              "per staged window (first 4096): [window, ns ring wait, ns free-event wait enqueue, "
                              "ns producer wait, ns copy enqueue, ns retire slot + event records, t0 ns]");

@@ -27,7 +27,7 @@ NativeStager::NativeStager(const Arena* arena, int32_t n_producers, int32_t n_sl
                            std::vector<void*> buffers, uint64_t buffer_bytes, hipStream_t copy_stream, int device,
                            std::vector<int32_t> peer_pids, int64_t timeout_ms, std::vector<hipEvent_t> ready,
                            std::vector<hipEvent_t> copy_done, bool post_copy, int64_t meta_bytes,
-                           hipStream_t copy_stream2)
+                           hipStream_t copy_stream2, int copy_policy)
     : arena_(arena),
       P_(n_producers),
       n_slots_(n_slots),
@@ -37,6 +37,7 @@ NativeStager::NativeStager(const Arena* arena, int32_t n_producers, int32_t n_sl
       buffer_bytes_(buffer_bytes),
       copy_stream_(copy_stream),
       copy_stream2_(copy_stream2),
+      copy_policy_(copy_policy),
       device_(device),
       peer_pids_(std::move(peer_pids)),
       timeout_ms_(timeout_ms),
@@ -52,10 +53,17 @@ NativeStager::NativeStager(const Arena* arena, int32_t n_producers, int32_t n_sl
       (post_copy_ && copy_done_.size() != buffers_.size()) || static_cast<int32_t>(peer_pids_.size()) != P_)
     throw std::invalid_argument("NativeStager: inconsistent arguments");
   if (hipSetDevice(device_) != hipSuccess) throw std::runtime_error("NativeStager: hipSetDevice failed");
+  // retire / start events carry device timestamps: every copy's [start, end] on the GPU clock, so a region's
+  // landed bytes can be counted pro rata (bytes_in_interval) instead of in whole windows
   retire_ev_.resize(kRetireEvents);
-  for (auto& e : retire_ev_)
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventBlockingSync) != hipSuccess)
-      throw std::runtime_error("NativeStager: hipEventCreate failed");
+  start_ev_.resize(kRetireEvents);
+  for (auto* ring : {&retire_ev_, &start_ev_})
+    for (auto& e : *ring)
+      if (hipEventCreateWithFlags(&e, hipEventBlockingSync) != hipSuccess)
+        throw std::runtime_error("NativeStager: hipEventCreate failed");
+  if (hipEventCreateWithFlags(&epoch_ev_, hipEventBlockingSync) != hipSuccess ||
+      hipEventRecord(epoch_ev_, copy_stream_) != hipSuccess || hipEventSynchronize(epoch_ev_) != hipSuccess)
+    throw std::runtime_error("NativeStager: epoch event failed");
   thread_ = std::thread([this] { run(); });
   retire_thread_ = std::thread([this] { retire_loop(); });
 }
@@ -63,6 +71,8 @@ NativeStager::NativeStager(const Arena* arena, int32_t n_producers, int32_t n_sl
 NativeStager::~NativeStager() {
   close();
   for (auto e : retire_ev_) hipEventDestroy(e);
+  for (auto e : start_ev_) hipEventDestroy(e);
+  if (epoch_ev_ != nullptr) hipEventDestroy(epoch_ev_);
 }
 
 void NativeStager::retire_loop() {
@@ -77,11 +87,18 @@ void NativeStager::retire_loop() {
     }
     if (hipEventSynchronize(retire_ev_[r.ev]) != hipSuccess) return fail(-1, static_cast<int32_t>(r.producer),
                                                                          "hipEventSynchronize(retire) failed");
+    float t_start = 0.f, t_end = 0.f;  // ms since the epoch event, GPU clock
+    const bool timed = hipEventElapsedTime(&t_start, epoch_ev_, start_ev_[r.ev]) == hipSuccess &&
+                       hipEventElapsedTime(&t_end, epoch_ev_, retire_ev_[r.ev]) == hipSuccess;
     bytes_landed_.fetch_add(r.bytes, std::memory_order_relaxed);
     windows_landed_.fetch_add(1, std::memory_order_release);
     arena_->set_state(r.producer, r.slot, kEmpty);  // slot back to its producer (release store + futex wake)
     {
       std::lock_guard<std::mutex> lk(mu_);
+      if (timed) {
+        done_log_.push_back(DoneRec{r.window, r.bytes, static_cast<double>(t_start), static_cast<double>(t_end)});
+        if (done_log_.size() > kCopyLog) done_log_.pop_front();
+      }
       retire_q_.pop_front();
       retired_upto_ = r.window + 1;
     }
@@ -113,6 +130,24 @@ void NativeStager::fail(int code, int32_t producer, const std::string& msg) {
   retire_cv_.notify_all();
 }
 
+bool NativeStager::copy_in_flight(int i, int64_t w) const {
+  const int64_t lw = last_copy_[i];
+  // a retire event is re-recorded only after its window retired, so a copy kRetireEvents windows back is done
+  if (lw < 0 || w - lw >= kRetireEvents) return false;
+  return hipEventQuery(retire_ev_[static_cast<size_t>((lw - first_) % kRetireEvents)]) == hipErrorNotReady;
+}
+
+int NativeStager::pick_copy_stream(int64_t w) const {
+  if (copy_stream2_ == nullptr) return 0;
+  if (copy_policy_ == 0) return static_cast<int>((w - first_) & 1);  // strict alternation
+  // adaptive: stream 0 whenever its engine is idle. When the consumer is slower than the link (copies spaced
+  // out) every copy runs on one stream and one SDMA engine, as with a single copy stream; back to back
+  // (loader-bound) the next copy goes to the idle second engine, so the link never waits for a copy to end.
+  if (!copy_in_flight(0, w)) return 0;
+  if (!copy_in_flight(1, w)) return 1;
+  return 1 - last_stream_;  // both busy: behind the older copy
+}
+
 void NativeStager::run() {
   if (hipSetDevice(device_) != hipSuccess) return fail(-1, -1, "hipSetDevice failed in the stager thread");
   auto ns = [] {
@@ -122,7 +157,6 @@ void NativeStager::run() {
   };
   for (int64_t w = first_; w < first_ + total_; ++w) {
     const int b = static_cast<int>((w - first_) % depth_);
-    hipStream_t cs = copy_stream2_ != nullptr && ((w - first_) & 1) ? copy_stream2_ : copy_stream_;
     hipEvent_t free_ev = nullptr;
     const int64_t s0 = ns();
     {
@@ -132,10 +166,7 @@ void NativeStager::run() {
       free_ev = free_events_[b];
     }
     const int64_t s1 = ns();
-    // the consumer's kernels reading this ring buffer (window w - depth) finish first
-    if (free_ev != nullptr && hipStreamWaitEvent(cs, free_ev, 0) != hipSuccess)
-      return fail(-1, -1, "hipStreamWaitEvent(free) failed");
-    const int64_t s2 = ns();
+    const int64_t s2 = s1;
     const uint32_t p = static_cast<uint32_t>(w % P_);
     const uint32_t s = static_cast<uint32_t>((w / P_) % n_slots_);
     // futex wait in short slices so close() never waits behind a long timeout
@@ -185,19 +216,33 @@ void NativeStager::run() {
     if (info.used_bytes > buffer_bytes_)
       return fail(-1, static_cast<int32_t>(p),
                   "window of " + std::to_string(info.used_bytes) + " B exceeds the staging buffer");
-    const uint64_t enq_ns = now_ns();  // before the call: the copy cannot start earlier
-    if (info.used_bytes > 0 &&
-        hipMemcpyAsync(buffers_[b], arena_->slot_data(p, s), info.used_bytes, hipMemcpyHostToDevice, cs) !=
-            hipSuccess)
-      return fail(-1, static_cast<int32_t>(p), "hipMemcpyAsync H2D failed");
-    const int64_t s4 = ns();
-    // retire event of w: a ring, so window w - kRetireEvents must have been retired before it is re-recorded
+    // stream choice as late as possible, when the engines' state is known (see pick_copy_stream)
+    const int si = pick_copy_stream(w);
+    hipStream_t cs = si == 0 ? copy_stream_ : copy_stream2_;
+    // the consumer's kernels reading this ring buffer (window w - depth) finish first; a free event that
+    // has already completed needs no device-side wait (no cross-stream dependency on the compute stream)
+    if (free_ev != nullptr && hipEventQuery(free_ev) != hipSuccess) {
+      if (hipStreamWaitEvent(cs, free_ev, 0) != hipSuccess) return fail(-1, -1, "hipStreamWaitEvent(free) failed");
+      free_waits_ += 1;
+    }
+    last_copy_[si] = w;
+    last_stream_ = si;
+    // start / retire events of w: a ring, so window w - kRetireEvents must have been retired before they are
+    // re-recorded (never waits with depth < kRetireEvents ring buffers)
     const int rev = static_cast<int>((w - first_) % kRetireEvents);
     {
       std::unique_lock<std::mutex> lk(mu_);
       retire_cv_.wait(lk, [&] { return stop_ || error_code_ != 0 || w - kRetireEvents < retired_upto_; });
       if (stop_ || error_code_ != 0) return;
     }
+    if (hipEventRecord(start_ev_[rev], cs) != hipSuccess)  // the stream reaches the copy: it can start
+      return fail(-1, static_cast<int32_t>(p), "hipEventRecord(start) failed");
+    const uint64_t enq_ns = now_ns();  // before the call: the copy cannot start earlier
+    if (info.used_bytes > 0 &&
+        hipMemcpyAsync(buffers_[b], arena_->slot_data(p, s), info.used_bytes, hipMemcpyHostToDevice, cs) !=
+            hipSuccess)
+      return fail(-1, static_cast<int32_t>(p), "hipMemcpyAsync H2D failed");
+    const int64_t s4 = ns();
     if (hipEventRecord(retire_ev_[rev], cs) != hipSuccess)
       return fail(-1, static_cast<int32_t>(p), "hipEventRecord(retire) failed");
     {
@@ -286,6 +331,37 @@ std::pair<uint64_t, uint64_t> NativeStager::copies_between(uint64_t t0_ns, uint6
     }
   }
   return {n, bytes};
+}
+
+InIntervalBytes NativeStager::bytes_in_interval(hipEvent_t e0, hipEvent_t e1, int64_t timeout_ms) {
+  InIntervalBytes out;
+  float T0 = 0.f, T1 = 0.f;
+  if (hipEventSynchronize(e0) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+      hipEventElapsedTime(&T0, epoch_ev_, e0) != hipSuccess || hipEventElapsedTime(&T1, epoch_ev_, e1) != hipSuccess)
+    return out;  // ok = false
+  out.t0_ms = T0;
+  out.t1_ms = T1;
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+  std::unique_lock<std::mutex> lk(mu_);
+  // every copy enqueued so far retires (and is timed) first: one still in flight at e1 may have moved part of
+  // its bytes inside the interval
+  const int64_t last = retire_q_.empty() ? INT64_MIN : retire_q_.back().window;
+  if (!retire_cv_.wait_until(lk, deadline, [&] {
+        return stop_ || error_code_ != 0 || retire_q_.empty() || retire_q_.front().window > last;
+      }))
+    return out;
+  for (const DoneRec& d : done_log_) {
+    const double a = std::max(d.t_start_ms, static_cast<double>(T0));
+    const double b = std::min(d.t_end_ms, static_cast<double>(T1));
+    if (b <= a) continue;
+    const double span = d.t_end_ms - d.t_start_ms;
+    const double frac = span > 0 ? (b - a) / span : 1.0;  // uniform rate over the copy's [start, end]
+    out.bytes += frac * static_cast<double>(d.bytes);
+    out.windows += frac;
+    out.copies += 1;
+  }
+  out.ok = true;
+  return out;
 }
 
 std::string NativeStager::error() const {

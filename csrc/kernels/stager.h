@@ -56,6 +56,14 @@ struct StagedInfo {
   std::vector<int64_t> meta;
 };
 
+// H2D bytes that crossed the link inside a device-time interval (NativeStager::bytes_in_interval)
+struct InIntervalBytes {
+  bool ok = false;
+  double bytes = 0.0, windows = 0.0;  // pro rata: each copy's share of [start, end] inside the interval
+  int64_t copies = 0;                 // copies overlapping the interval
+  double t0_ms = 0.0, t1_ms = 0.0;    // the interval on the stager's epoch clock
+};
+
 class NativeStager {
  public:
   // arena: the consumer's Arena (its mapping is the hipHostRegister'ed one).
@@ -67,7 +75,7 @@ class NativeStager {
                std::vector<void*> buffers, uint64_t buffer_bytes, hipStream_t copy_stream, int device,
                std::vector<int32_t> peer_pids, int64_t timeout_ms, std::vector<hipEvent_t> ready,
                std::vector<hipEvent_t> copy_done, bool post_copy, int64_t meta_bytes = 0,
-               hipStream_t copy_stream2 = nullptr);
+               hipStream_t copy_stream2 = nullptr, int copy_policy = 1);
   ~NativeStager();
 
   NativeStager(const NativeStager&) = delete;
@@ -101,7 +109,13 @@ class NativeStager {
   // is enqueued) and before the call. Called at the end of a benchmark's timed region, it counts the
   // region's own copies -- not ones already in flight when it opened, nor ones still in flight at its end.
   std::pair<uint64_t, uint64_t> copies_between(uint64_t t0_ns, uint64_t t1_ns) const;
+  // H2D bytes that crossed PCIe between two completed (timing) events, on the GPU clock: every copy is timed by
+  // a start event (its stream reaches it) and its retire event, and contributes the share of its bytes whose
+  // [start, end] lies inside [e0, e1] (uniform rate within a copy). Waits (bounded) for copies in flight.
+  InIntervalBytes bytes_in_interval(hipEvent_t e0, hipEvent_t e1, int64_t timeout_ms);
   double wait_producer_s() const { return wait_producer_ns_.load() * 1e-9; }
+  // free-event waits actually enqueued on a copy stream (the rest had completed and were skipped)
+  uint64_t free_waits() const { return free_waits_.load(); }
   // per staged window (first 4096): ns spent in each step of the stager loop -- waiting for the ring
   // (consumer release), enqueueing the free-event wait, waiting for the producer, enqueueing the copy,
   // waiting for a retire-event slot + recording the events
@@ -122,7 +136,14 @@ class NativeStager {
     int ev;
   };
   static constexpr int kRetireEvents = 16;
-  std::vector<hipEvent_t> retire_ev_;
+  std::vector<hipEvent_t> retire_ev_, start_ev_;
+  hipEvent_t epoch_ev_ = nullptr;  // recorded once at construction: the zero of every copy's device times
+  struct DoneRec {
+    int64_t window;
+    uint64_t bytes;
+    double t_start_ms, t_end_ms;
+  };
+  std::deque<DoneRec> done_log_;  // retired copies with device times, last kCopyLog (guarded by mu_)
   std::deque<Retire> retire_q_;  // guarded by mu_
   int64_t retired_upto_ = 0;     // windows < this are retired (guarded by mu_)
   std::condition_variable retire_cv_;
@@ -137,6 +158,13 @@ class NativeStager {
   // optional second copy stream: windows alternate between the two, so the next window's copy is
   // already running on another SDMA engine when one finishes (no per-copy gap on the link)
   hipStream_t copy_stream2_;
+  // 0: windows strictly alternate between the two copy streams; 1 (default): adaptive, the second stream
+  // only while the first one's copy is still in flight (pick_copy_stream)
+  const int copy_policy_;
+  int64_t last_copy_[2] = {-1, -1};  // last window copied on each stream (stager thread only)
+  int last_stream_ = 1;
+  bool copy_in_flight(int i, int64_t w) const;
+  int pick_copy_stream(int64_t w) const;
   const int device_;
   const std::vector<int32_t> peer_pids_;
   const int64_t timeout_ms_;
@@ -155,7 +183,7 @@ class NativeStager {
   int32_t error_producer_ = -1;
   std::string error_msg_;
   std::atomic<uint64_t> bytes_h2d_{0}, windows_staged_{0}, wait_producer_ns_{0};
-  std::atomic<uint64_t> windows_landed_{0}, bytes_landed_{0};
+  std::atomic<uint64_t> windows_landed_{0}, bytes_landed_{0}, free_waits_{0};
   std::vector<std::vector<int64_t>> wait_log_;  // guarded by mu_
   struct CopyRec {
     int64_t window;

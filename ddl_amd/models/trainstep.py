@@ -132,14 +132,18 @@ class CalibratedStep:
     (``benchmarks/bench_idle_sweep.py``), so GPU idle % is measured where the loader is the
     bottleneck, not only behind a model far slower than the feed. The batch is read by the
     streaming checksum kernel (every byte, one launch); the GEMM chain (``m x k @ k x k``,
-    hipBLASLt) is sized by timing it on this GPU: ``reps = round((step_ms - read_ms) / gemm_ms)``.
+    hipBLASLt) is sized by timing it on this GPU: ``reps = round((step_ms - read_ms) / gemm_ms)`` whole
+    GEMMs plus one GEMM over the first ``tail_rows`` rows (multiples of 256) for the remainder, so the
+    step time is tunable to ~1% instead of one GEMM's ~10%. ``tune`` re-sizes the chain from a busy time
+    measured in the real loop (clocks and memory traffic there differ from the isolated timing).
     """
 
     def __init__(self, device, step_ms: float, m: int | None = None, k: int = 4096, dtype=torch.bfloat16,
-                 min_reps: int = 8):
+                 min_reps: int = 8, read_keys: tuple | None = None):
         from .. import ops
 
         self.device = torch.device(device)
+        self.read_keys = read_keys  # dict batches: read only these entries (None: every tensor)
         self.step_ms = float(step_ms)
         g = torch.Generator(device="cpu").manual_seed(0)
         self.w = (torch.randn(k, k, generator=g) / k ** 0.5).to(self.device, dtype)
@@ -153,6 +157,7 @@ class CalibratedStep:
         self.acc = ops.ChecksumAccumulator(self.device)
         self.gemm_ms = self._time(lambda: torch.mm(self.a, self.w, out=self.out))
         self.reps = 0
+        self.tail_rows = 0
         self.read_ms = 0.0
 
     def _time(self, fn, reps: int = 20) -> float:
@@ -169,21 +174,41 @@ class CalibratedStep:
     def calibrate(self, batch) -> "CalibratedStep":
         """Time the batch read on a real batch and size the GEMM chain to fill the step."""
         self.read_ms = self._time(lambda: self._read(batch))
-        self.reps = max(0, round((self.step_ms - self.read_ms) / self.gemm_ms))
+        self._size(self.gemm_ms)
+        return self
+
+    def _size(self, gemm_ms: float) -> None:
+        m = self.a.shape[0]
+        work = max(0.0, self.step_ms - self.read_ms) / max(gemm_ms, 1e-6)  # in whole GEMMs
+        self.reps = int(work)
+        self.tail_rows = min(m, int(round((work - self.reps) * m / 256)) * 256)
+        if self.tail_rows == m:
+            self.reps, self.tail_rows = self.reps + 1, 0
+
+    def tune(self, busy_ms_per_step: float) -> "CalibratedStep":
+        """Re-size the GEMM chain from the busy time per step measured in the real loop."""
+        units = self.reps + self.tail_rows / self.a.shape[0]
+        if units > 0 and busy_ms_per_step > self.read_ms:
+            self.gemm_ms = (busy_ms_per_step - self.read_ms) / units
+            self._size(self.gemm_ms)
         return self
 
     def _read(self, batch) -> None:
-        tensors = batch.values() if isinstance(batch, dict) else (batch if isinstance(batch, (tuple, list))
-                                                                  else (batch,))
+        if isinstance(batch, dict):
+            tensors = batch.values() if self.read_keys is None else (batch[k] for k in self.read_keys)
+        else:
+            tensors = batch if isinstance(batch, (tuple, list)) else (batch,)
         for t in tensors:
             if isinstance(t, torch.Tensor) and t.is_cuda:
                 self.acc.add(t)
 
     @property
     def planned_ms(self) -> float:
-        return self.read_ms + self.reps * self.gemm_ms
+        return self.read_ms + (self.reps + self.tail_rows / self.a.shape[0]) * self.gemm_ms
 
     def __call__(self, batch) -> None:
         self._read(batch)
         for _ in range(self.reps):
             torch.mm(self.a, self.w, out=self.out)
+        if self.tail_rows:
+            torch.mm(self.a[:self.tail_rows], self.w, out=self.out[:self.tail_rows])

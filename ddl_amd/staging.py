@@ -123,10 +123,16 @@ class WindowStager:
         # exchange) on a second stream, so window w's exchange overlaps window
         # w+1's DMA instead of idling the copy engine.
         self.copy_stream = torch.cuda.Stream(device=self.device)
-        # windows alternate between two copy streams (two SDMA engines): the next copy is already
+        # two copy streams (two SDMA engines): when copies run back to back the next one is already
         # running when one finishes, so the ~25 us gap per copy on one engine is gone (+1.8%,
-        # profiles/r2_copy_streams); DDL_COPY_STREAMS=1 restores one stream
+        # profiles/r2_copy_streams). The second stream is used only while the first one's copy is in
+        # flight (DDL_COPY_POLICY=adaptive, the default); below the feed rate every copy then runs on one
+        # engine, which halves the step-boundary idle of alternating (profiles/r3_copy_policy).
+        # DDL_COPY_POLICY=alternate restores strict alternation, DDL_COPY_STREAMS=1 one stream.
         n_cs = int(os.environ.get("DDL_COPY_STREAMS", "2"))
+        policy = os.environ.get("DDL_COPY_POLICY", "adaptive")
+        if policy not in ("adaptive", "alternate"):
+            raise ValueError(f"DDL_COPY_POLICY must be adaptive or alternate, not {policy!r}")
         self.copy_stream2 = torch.cuda.Stream(device=self.device) if n_cs >= 2 else None
         self.stream = torch.cuda.Stream(device=self.device) if post_copy is not None else self.copy_stream
         # The consumer posts window w+1's exchange when it enters window w (the fixed, rank-identical
@@ -152,7 +158,9 @@ class WindowStager:
             peer_pids=list(connection.producer_pids), timeout_ms=int(timeout_s * 1000),
             ready=[e.cuda_event for e in self.ready_events], copy_done=[e.cuda_event for e in self._copy_done],
             post_copy=post_copy is not None, meta_bytes=int(meta_bytes),
-            copy_stream2=self.copy_stream2.cuda_stream if self.copy_stream2 is not None else 0)
+            copy_stream2=self.copy_stream2.cuda_stream if self.copy_stream2 is not None else 0,
+            copy_policy=1 if policy == "adaptive" else 0)
+        self.copy_policy = policy if self.copy_stream2 is not None else "one stream"
         self.meta_bytes = int(meta_bytes)
 
     # -------------------------------------------------------------- consumer
@@ -281,6 +289,13 @@ class WindowStager:
         """After a device synchronize: wait until every completed copy has been counted as landed."""
         self._native.settle(int(timeout_s * 1000))
 
+    def bytes_in_interval(self, e0: torch.cuda.Event, e1: torch.cuda.Event, timeout_s: float = 2.0) -> dict:
+        """H2D bytes that crossed PCIe between two recorded timing events (``enable_timing=True``), on the
+        GPU clock: each copy is timed on the device (start and retire events) and counts with the share of
+        its bytes whose [start, end] lies between the events. ``{"ok", "bytes", "windows", "copies",
+        "t0_ms", "t1_ms"}``; waits (bounded) for copies still in flight."""
+        return dict(self._native.bytes_in_interval(e0.cuda_event, e1.cuda_event, int(timeout_s * 1000)))
+
     @property
     def windows_landed(self) -> int:
         """Windows whose H2D copy has retired (the data is in HBM)."""
@@ -299,4 +314,5 @@ class WindowStager:
         return {"bytes_h2d": self.bytes_h2d, "windows_staged": self.windows_staged,
                 "windows_landed": self.windows_landed, "bytes_landed": self.bytes_landed,
                 "stager_wait_producer_s": float(self._native.wait_producer_s),
+                "copy_policy": self.copy_policy, "free_waits_enqueued": int(self._native.free_waits),
                 "exchange_issue_wait_s": round(self.post_wait_s, 6)}

@@ -412,3 +412,50 @@ def test_stager_counts_the_copies_of_a_time_window():
         assert n == st.windows_staged == 4 and b == st.bytes_h2d == n * 64 * 8 * 4
         assert st._native.copies_between(t1 + 1, t1 + 2) == (0, 0)
         dl.close()
+
+
+def test_stager_bytes_in_interval_is_pro_rata_and_additive():
+    """bytes_in_interval(e0, e1): the H2D bytes that crossed PCIe between two timing events, from the
+    device times of every copy (bench.py's landed count). An interval around the whole run holds every byte;
+    splitting it at an event in the middle splits the bytes exactly (pro rata per copy, nothing lost or
+    counted twice); an interval after the run holds none."""
+    from ddl_amd.models.producers import ImageWindowProducer
+
+    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    with ddl_amd.start(n_producers=2) as (env, conn):
+        e0 = ev()
+        e0.record()
+        dl = ddl_amd.DistributedDataLoader(ImageWindowProducer(64, (3, 64, 64), "bfloat16", refill="stamp"), 32,
+                                           conn, 6, env=env, device=torch.device("cuda"),
+                                           out_dtype=torch.bfloat16, shuffle="device", prefetch_depth=2)
+        st = dl._stager
+        n_batches = 0
+        em = None
+        for e in range(6):
+            for i in range(len(dl)):
+                dl[i]
+                dl.mark(Marker.END_OF_BATCH)
+                n_batches += 1
+                if n_batches == 5:
+                    em = ev()
+                    em.record()
+            if e < 5:
+                dl.mark(Marker.END_OF_EPOCH)
+        torch.cuda.synchronize()
+        e1 = ev()
+        e1.record()
+        e1.synchronize()
+        whole = st.bytes_in_interval(e0, e1)
+        first, second = st.bytes_in_interval(e0, em), st.bytes_in_interval(em, e1)
+        assert whole["ok"] and first["ok"] and second["ok"]
+        total = st.bytes_h2d
+        assert total == st.windows_staged * 64 * 3 * 64 * 64 * 2 > 0
+        assert abs(whole["bytes"] - total) <= 1e-6 * total and whole["copies"] == st.windows_staged
+        assert 0 < first["bytes"] < total and abs(first["bytes"] + second["bytes"] - total) <= 1e-6 * total
+        assert abs(first["windows"] + second["windows"] - st.windows_staged) < 1e-6
+        e2, e3 = ev(), ev()
+        e2.record()
+        e3.record()
+        after = st.bytes_in_interval(e2, e3)
+        assert after["ok"] and after["bytes"] == 0.0 and after["copies"] == 0
+        dl.close()
