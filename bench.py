@@ -395,6 +395,12 @@ def main(argv=None) -> int:
             "h2d_accounting": "device-timed pro rata" if pro is not None and pro["ok"] else "whole windows",
             "device_region_ms": round(pro["t1_ms"] - pro["t0_ms"], 4) if pro is not None and pro["ok"] else None,
             "h2d_copies_overlapping_region": pro["copies"] if pro is not None else None,
+            # device-timed link occupancy in the region: share of it with >= 1 / 2 window copies running
+            "h2d_link_busy_pct": (round(100.0 * pro["busy_ms"] / max(1e-9, pro["t1_ms"] - pro["t0_ms"]), 2)
+                                  if pro is not None and pro["ok"] else None),
+            "h2d_two_copies_pct": (round(100.0 * pro["overlap_ms"] / max(1e-9, pro["t1_ms"] - pro["t0_ms"]), 2)
+                                   if pro is not None and pro["ok"] else None),
+            "h2d_copies_per_stream": list(pro["copies_per_stream"]) if pro is not None and pro["ok"] else None,
             "h2d_bytes_whole_windows_enqueued_and_retired_in_region": b_in,
             "h2d_bytes_landed_any_enqueue_time": b_land1 - b_land0,
             "h2d_enqueued_bytes_timed": bytes_enq1 - bytes_enq0,

@@ -208,7 +208,7 @@ PYBIND11_MODULE(_ddl_hip, m) {
            py::arg("buffers"), py::arg("buffer_bytes"), py::arg("copy_stream"), py::arg("device"),
            py::arg("peer_pids"), py::arg("timeout_ms"), py::arg("ready"), py::arg("copy_done"),
            py::arg("post_copy"), py::arg("meta_bytes") = 0, py::arg("copy_stream2") = 0,
-           py::arg("copy_policy") = 1)
+           py::arg("copy_policy") = 2)
       .def(
           "wait",
           [](ddl::NativeStager& st, int64_t w, int64_t timeout_ms) {
@@ -266,6 +266,9 @@ PYBIND11_MODULE(_ddl_hip, m) {
             d["copies"] = r.copies;
             d["t0_ms"] = r.t0_ms;
             d["t1_ms"] = r.t1_ms;
+            d["busy_ms"] = r.busy_ms;
+            d["overlap_ms"] = r.overlap_ms;
+            d["copies_per_stream"] = py::make_tuple(r.copies_per_stream[0], r.copies_per_stream[1]);
             return d;
           },
           py::arg("e0"), py::arg("e1"), py::arg("timeout_ms") = 2000,

@@ -96,7 +96,8 @@ void NativeStager::retire_loop() {
     {
       std::lock_guard<std::mutex> lk(mu_);
       if (timed) {
-        done_log_.push_back(DoneRec{r.window, r.bytes, static_cast<double>(t_start), static_cast<double>(t_end)});
+        done_log_.push_back(
+            DoneRec{r.window, r.bytes, static_cast<double>(t_start), static_cast<double>(t_end), r.stream});
         if (done_log_.size() > kCopyLog) done_log_.pop_front();
       }
       retire_q_.pop_front();
@@ -137,12 +138,18 @@ bool NativeStager::copy_in_flight(int i, int64_t w) const {
   return hipEventQuery(retire_ev_[static_cast<size_t>((lw - first_) % kRetireEvents)]) == hipErrorNotReady;
 }
 
-int NativeStager::pick_copy_stream(int64_t w) const {
+int NativeStager::pick_copy_stream(int64_t w, bool ring_waited) const {
   if (copy_stream2_ == nullptr) return 0;
   if (copy_policy_ == 0) return static_cast<int>((w - first_) & 1);  // strict alternation
-  // adaptive: stream 0 whenever its engine is idle. When the consumer is slower than the link (copies spaced
-  // out) every copy runs on one stream and one SDMA engine, as with a single copy stream; back to back
-  // (loader-bound) the next copy goes to the idle second engine, so the link never waits for a copy to end.
+  if (copy_policy_ == 2) {
+    // auto: the stager had to wait for a ring buffer, so the consumer is slower than the link and the feed has
+    // slack: one stream (one SDMA engine), which shows a lower step-boundary idle below the crossover
+    // (profiles/r3_copy_policy). Otherwise (loader-bound) alternate, so two copies overlap and the link never
+    // waits for one to end (+2.5% feed).
+    return ring_waited ? 0 : 1 - last_stream_;
+  }
+  // adaptive (policy 1): stream 0 whenever its last copy has retired. Measured to serialise nearly every copy
+  // on stream 0 at the link rate as well (192 of 199 copies), so it loses the overlap; kept for A/B runs.
   if (!copy_in_flight(0, w)) return 0;
   if (!copy_in_flight(1, w)) return 1;
   return 1 - last_stream_;  // both busy: behind the older copy
@@ -217,7 +224,7 @@ void NativeStager::run() {
       return fail(-1, static_cast<int32_t>(p),
                   "window of " + std::to_string(info.used_bytes) + " B exceeds the staging buffer");
     // stream choice as late as possible, when the engines' state is known (see pick_copy_stream)
-    const int si = pick_copy_stream(w);
+    const int si = pick_copy_stream(w, s1 - s0 > kRingWaitNs);
     hipStream_t cs = si == 0 ? copy_stream_ : copy_stream2_;
     // the consumer's kernels reading this ring buffer (window w - depth) finish first; a free event that
     // has already completed needs no device-side wait (no cross-stream dependency on the compute stream)
@@ -247,7 +254,7 @@ void NativeStager::run() {
       return fail(-1, static_cast<int32_t>(p), "hipEventRecord(retire) failed");
     {
       std::lock_guard<std::mutex> lk(mu_);
-      retire_q_.push_back(Retire{w, p, s, info.used_bytes, rev});
+      retire_q_.push_back(Retire{w, p, s, info.used_bytes, rev, si});
     }
     retire_cv_.notify_all();
     if (hipEventRecord(post_copy_ ? copy_done_[b] : ready_[b], cs) != hipSuccess)
@@ -350,6 +357,7 @@ InIntervalBytes NativeStager::bytes_in_interval(hipEvent_t e0, hipEvent_t e1, in
         return stop_ || error_code_ != 0 || retire_q_.empty() || retire_q_.front().window > last;
       }))
     return out;
+  std::vector<std::pair<double, int>> edges;  // clipped [start, end] of every overlapping copy: +1 / -1
   for (const DoneRec& d : done_log_) {
     const double a = std::max(d.t_start_ms, static_cast<double>(T0));
     const double b = std::min(d.t_end_ms, static_cast<double>(T1));
@@ -359,6 +367,17 @@ InIntervalBytes NativeStager::bytes_in_interval(hipEvent_t e0, hipEvent_t e1, in
     out.bytes += frac * static_cast<double>(d.bytes);
     out.windows += frac;
     out.copies += 1;
+    out.copies_per_stream[d.stream & 1] += 1;
+    edges.emplace_back(a, +1);
+    edges.emplace_back(b, -1);
+  }
+  std::sort(edges.begin(), edges.end());
+  int live = 0;
+  for (size_t i = 0; i + 1 < edges.size(); ++i) {
+    live += edges[i].second;
+    const double dt = edges[i + 1].first - edges[i].first;
+    if (live >= 1) out.busy_ms += dt;
+    if (live >= 2) out.overlap_ms += dt;
   }
   out.ok = true;
   return out;

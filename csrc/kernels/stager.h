@@ -62,6 +62,9 @@ struct InIntervalBytes {
   double bytes = 0.0, windows = 0.0;  // pro rata: each copy's share of [start, end] inside the interval
   int64_t copies = 0;                 // copies overlapping the interval
   double t0_ms = 0.0, t1_ms = 0.0;    // the interval on the stager's epoch clock
+  // link occupancy inside the interval: time with >= 1 / >= 2 copies between their start and end
+  double busy_ms = 0.0, overlap_ms = 0.0;
+  int64_t copies_per_stream[2] = {0, 0};
 };
 
 class NativeStager {
@@ -75,7 +78,7 @@ class NativeStager {
                std::vector<void*> buffers, uint64_t buffer_bytes, hipStream_t copy_stream, int device,
                std::vector<int32_t> peer_pids, int64_t timeout_ms, std::vector<hipEvent_t> ready,
                std::vector<hipEvent_t> copy_done, bool post_copy, int64_t meta_bytes = 0,
-               hipStream_t copy_stream2 = nullptr, int copy_policy = 1);
+               hipStream_t copy_stream2 = nullptr, int copy_policy = 2);
   ~NativeStager();
 
   NativeStager(const NativeStager&) = delete;
@@ -134,6 +137,7 @@ class NativeStager {
     uint32_t producer, slot;
     uint64_t bytes;
     int ev;
+    int stream;  // 0 / 1: which copy stream
   };
   static constexpr int kRetireEvents = 16;
   std::vector<hipEvent_t> retire_ev_, start_ev_;
@@ -142,6 +146,7 @@ class NativeStager {
     int64_t window;
     uint64_t bytes;
     double t_start_ms, t_end_ms;
+    int stream;
   };
   std::deque<DoneRec> done_log_;  // retired copies with device times, last kCopyLog (guarded by mu_)
   std::deque<Retire> retire_q_;  // guarded by mu_
@@ -158,13 +163,15 @@ class NativeStager {
   // optional second copy stream: windows alternate between the two, so the next window's copy is
   // already running on another SDMA engine when one finishes (no per-copy gap on the link)
   hipStream_t copy_stream2_;
-  // 0: windows strictly alternate between the two copy streams; 1 (default): adaptive, the second stream
-  // only while the first one's copy is still in flight (pick_copy_stream)
+  // 0: windows strictly alternate between the two copy streams; 1: adaptive (second stream only while the
+  // first one's copy is in flight); 2 (default): auto, one stream while the stager waits on the consumer for
+  // ring buffers, alternation otherwise (pick_copy_stream)
   const int copy_policy_;
+  static constexpr int64_t kRingWaitNs = 50000;  // a ring wait longer than this: the consumer is the bottleneck
   int64_t last_copy_[2] = {-1, -1};  // last window copied on each stream (stager thread only)
   int last_stream_ = 1;
   bool copy_in_flight(int i, int64_t w) const;
-  int pick_copy_stream(int64_t w) const;
+  int pick_copy_stream(int64_t w, bool ring_waited) const;
   const int device_;
   const std::vector<int32_t> peer_pids_;
   const int64_t timeout_ms_;

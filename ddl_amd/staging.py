@@ -124,15 +124,17 @@ class WindowStager:
         # w+1's DMA instead of idling the copy engine.
         self.copy_stream = torch.cuda.Stream(device=self.device)
         # two copy streams (two SDMA engines): when copies run back to back the next one is already
-        # running when one finishes, so the ~25 us gap per copy on one engine is gone (+1.8%,
-        # profiles/r2_copy_streams). The second stream is used only while the first one's copy is in
-        # flight (DDL_COPY_POLICY=adaptive, the default); below the feed rate every copy then runs on one
-        # engine, which halves the step-boundary idle of alternating (profiles/r3_copy_policy).
-        # DDL_COPY_POLICY=alternate restores strict alternation, DDL_COPY_STREAMS=1 one stream.
+        # running when one finishes, so the ~25 us gap per copy on one engine is gone (+1.8-2.5%,
+        # profiles/r2_copy_streams, profiles/r3_copy_policy). DDL_COPY_POLICY=auto (default): alternate
+        # while the loader is the bottleneck, one stream while the stager waits on the consumer for ring
+        # buffers (below the crossover one engine shows a lower step-boundary idle); alternate: strict
+        # alternation; adaptive: second stream only while the first copy is in flight (A/B only: it
+        # serialises the copies). DDL_COPY_STREAMS=1: one stream.
         n_cs = int(os.environ.get("DDL_COPY_STREAMS", "2"))
-        policy = os.environ.get("DDL_COPY_POLICY", "adaptive")
-        if policy not in ("adaptive", "alternate"):
-            raise ValueError(f"DDL_COPY_POLICY must be adaptive or alternate, not {policy!r}")
+        policy = os.environ.get("DDL_COPY_POLICY", "auto")
+        codes = {"alternate": 0, "adaptive": 1, "auto": 2}
+        if policy not in codes:
+            raise ValueError(f"DDL_COPY_POLICY must be one of {sorted(codes)}, not {policy!r}")
         self.copy_stream2 = torch.cuda.Stream(device=self.device) if n_cs >= 2 else None
         self.stream = torch.cuda.Stream(device=self.device) if post_copy is not None else self.copy_stream
         # The consumer posts window w+1's exchange when it enters window w (the fixed, rank-identical
@@ -159,7 +161,7 @@ class WindowStager:
             ready=[e.cuda_event for e in self.ready_events], copy_done=[e.cuda_event for e in self._copy_done],
             post_copy=post_copy is not None, meta_bytes=int(meta_bytes),
             copy_stream2=self.copy_stream2.cuda_stream if self.copy_stream2 is not None else 0,
-            copy_policy=1 if policy == "adaptive" else 0)
+            copy_policy=codes[policy])
         self.copy_policy = policy if self.copy_stream2 is not None else "one stream"
         self.meta_bytes = int(meta_bytes)
 
