@@ -138,15 +138,16 @@ bool NativeStager::copy_in_flight(int i, int64_t w) const {
   return hipEventQuery(retire_ev_[static_cast<size_t>((lw - first_) % kRetireEvents)]) == hipErrorNotReady;
 }
 
-int NativeStager::pick_copy_stream(int64_t w, bool ring_waited) const {
+int NativeStager::pick_copy_stream(int64_t w) const {
   if (copy_stream2_ == nullptr) return 0;
   if (copy_policy_ == 0) return static_cast<int>((w - first_) & 1);  // strict alternation
   if (copy_policy_ == 2) {
-    // auto: the stager had to wait for a ring buffer, so the consumer is slower than the link and the feed has
-    // slack: one stream (one SDMA engine), which shows a lower step-boundary idle below the crossover
-    // (profiles/r3_copy_policy). Otherwise (loader-bound) alternate, so two copies overlap and the link never
-    // waits for one to end (+2.5% feed).
-    return ring_waited ? 0 : 1 - last_stream_;
+    // auto: the stager waited for a ring buffer on kRingWaitRun windows in a row, so the consumer is slower
+    // than the link and the feed has slack: one stream (one SDMA engine), which shows a lower step-boundary
+    // idle below the crossover (profiles/r3_copy_policy). Otherwise (loader-bound) alternate, so two copies
+    // overlap and the link never waits for one to end (+2.5% feed). The run length keeps an isolated wait --
+    // e.g. the one across a benchmark's opening synchronize -- from serialising the copies after it.
+    return ring_wait_run_ >= kRingWaitRun ? 0 : 1 - last_stream_;
   }
   // adaptive (policy 1): stream 0 whenever its last copy has retired. Measured to serialise nearly every copy
   // on stream 0 at the link rate as well (192 of 199 copies), so it loses the overlap; kept for A/B runs.
@@ -224,7 +225,8 @@ void NativeStager::run() {
       return fail(-1, static_cast<int32_t>(p),
                   "window of " + std::to_string(info.used_bytes) + " B exceeds the staging buffer");
     // stream choice as late as possible, when the engines' state is known (see pick_copy_stream)
-    const int si = pick_copy_stream(w, s1 - s0 > kRingWaitNs);
+    ring_wait_run_ = s1 - s0 > kRingWaitNs ? ring_wait_run_ + 1 : 0;
+    const int si = pick_copy_stream(w);
     hipStream_t cs = si == 0 ? copy_stream_ : copy_stream2_;
     // the consumer's kernels reading this ring buffer (window w - depth) finish first; a free event that
     // has already completed needs no device-side wait (no cross-stream dependency on the compute stream)

@@ -167,11 +167,13 @@ class NativeStager {
   // first one's copy is in flight); 2 (default): auto, one stream while the stager waits on the consumer for
   // ring buffers, alternation otherwise (pick_copy_stream)
   const int copy_policy_;
-  static constexpr int64_t kRingWaitNs = 50000;  // a ring wait longer than this: the consumer is the bottleneck
+  static constexpr int64_t kRingWaitNs = 50000;  // a ring wait longer than this: the consumer held the ring
+  static constexpr int kRingWaitRun = 3;          // ... on this many windows in a row: the consumer is the bottleneck
+  int ring_wait_run_ = 0;                         // consecutive windows that waited for the ring (stager thread)
   int64_t last_copy_[2] = {-1, -1};  // last window copied on each stream (stager thread only)
   int last_stream_ = 1;
   bool copy_in_flight(int i, int64_t w) const;
-  int pick_copy_stream(int64_t w, bool ring_waited) const;
+  int pick_copy_stream(int64_t w) const;
   const int device_;
   const std::vector<int32_t> peer_pids_;
   const int64_t timeout_ms_;
