@@ -6,6 +6,7 @@
 // .cuda_stream); dtype/shape validation lives in ddl_amd/ops/kernels.py.
 // Keeping torch headers out of this TU keeps one HIP runtime (torch/lib's,
 // linked by path) and no libtorch ABI coupling.
+#include <dlfcn.h>
 #include <errno.h>
 #include <hip/hip_runtime.h>
 #include <linux/futex.h>
@@ -141,6 +142,51 @@ PYBIND11_MODULE(_ddl_hip, m) {
     check(hipHostGetDevicePointer(&d, as_ptr<void>(addr), 0), "hipHostGetDevicePointer");
     return reinterpret_cast<uintptr_t>(d);
   });
+  m.def(
+      "dma_gather_rows",
+      [](uintptr_t dst, uintptr_t src, uint64_t row_bytes, uintptr_t idx_ptr, int64_t n, uintptr_t stream,
+         bool batched) {
+        // SDMA gather: row idx[i] of the (pinned, registered) host source -> row i of dst, as n copies in ONE
+        // hipMemcpyBatchAsync (batched) or n hipMemcpyAsync calls; runs of consecutive rows become one copy.
+        // Returns the host ns spent enqueueing.
+        const auto t0 = std::chrono::steady_clock::now();
+        const auto* idx = reinterpret_cast<const int64_t*>(idx_ptr);
+        std::vector<void*> dsts, srcs;
+        std::vector<size_t> sizes;
+        dsts.reserve(static_cast<size_t>(n));
+        srcs.reserve(static_cast<size_t>(n));
+        sizes.reserve(static_cast<size_t>(n));
+        auto* d = reinterpret_cast<char*>(dst);
+        const auto* sb = reinterpret_cast<const char*>(src);
+        for (int64_t i = 0; i < n;) {
+          int64_t j = i + 1;
+          while (j < n && idx[j] == idx[j - 1] + 1) ++j;
+          dsts.push_back(d + static_cast<uint64_t>(i) * row_bytes);
+          srcs.push_back(const_cast<char*>(sb) + static_cast<uint64_t>(idx[i]) * row_bytes);
+          sizes.push_back(static_cast<size_t>(j - i) * row_bytes);
+          i = j;
+        }
+        py::gil_scoped_release nogil;
+        // hipMemcpyBatchAsync is newer than the HIP runtime torch ships (ROCm 7.0): looked up at run time
+        using BatchFn = hipError_t (*)(void**, void**, size_t*, size_t, hipMemcpyAttributes*, size_t*, size_t,
+                                       size_t*, hipStream_t);
+        static const auto batch_fn = reinterpret_cast<BatchFn>(dlsym(RTLD_DEFAULT, "hipMemcpyBatchAsync"));
+        if (batched && batch_fn != nullptr) {
+          size_t fail = 0;
+          check(batch_fn(dsts.data(), srcs.data(), sizes.data(), dsts.size(), nullptr, nullptr, 0, &fail,
+                         as_stream(stream)),
+                "hipMemcpyBatchAsync");
+        } else {
+          for (size_t k = 0; k < dsts.size(); ++k)
+            check(hipMemcpyAsync(dsts[k], srcs[k], sizes[k], hipMemcpyHostToDevice, as_stream(stream)),
+                  "hipMemcpyAsync");
+        }
+        return static_cast<int64_t>(
+            std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
+      },
+      py::arg("dst"), py::arg("src"), py::arg("row_bytes"), py::arg("idx"), py::arg("n"), py::arg("stream"),
+      py::arg("batched") = true);
+  m.def("has_memcpy_batch", [] { return dlsym(RTLD_DEFAULT, "hipMemcpyBatchAsync") != nullptr; });
   m.def("pointer_is_host_registered", [](uintptr_t addr) {
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, as_ptr<void>(addr)) != hipSuccess) {
