@@ -41,9 +41,10 @@ def main(argv=None):
                     help="phase 2: steps of a fixed-cost token train step, for GPU idle %% (0 disables)")
     ap.add_argument("--model-dim", type=int, default=256)
     ap.add_argument("--model-depth", type=int, default=2)
-    ap.add_argument("--token-dtype", default="int32", choices=["int32", "uint16"],
-                    help="token ids in the corpus and on the wire (uint16: vocab < 65536, 2 B per token over PCIe, "
-                         "widened to int32 input_ids by the pack kernel)")
+    ap.add_argument("--token-dtype", default="auto", choices=["auto", "int32", "uint16"],
+                    help="token ids in the corpus and on the wire: auto = uint16 when every id is < 65536 (the "
+                         "synthetic GPT-2-sized vocabulary is), else int32; uint16 ships 2 B per token over PCIe "
+                         "and the pack kernel widens it to int32 input_ids (profiles/r3_tok16)")
     a = ap.parse_args(argv)
 
     import torch
@@ -62,6 +63,10 @@ def main(argv=None):
 
         src = SharedTokenSource.synthetic(name, a.n_seqs, a.min_len, a.seq_len, seed=1, token_dtype=a.token_dtype)
         src.bind_to_node(gpu_numa_node(int(os.environ.get("LOCAL_RANK", "0"))))  # the producers' node
+        from ddl_amd.models.datasets import SharedArraySource
+
+        tb_seg = SharedArraySource(name + "_tb", 1, (1,), "int64", create=True)  # the wire dtype, for the node's ranks
+        tb_seg.tensor().view(-1)[0] = src.token_bytes
     gb = a.batch * world
     try:
         with ddl_amd.start(n_producers=a.producers) as (env, conn):
@@ -70,7 +75,11 @@ def main(argv=None):
             if src is None:
                 from ddl_amd.models.datasets import SharedArraySource
 
-                t = SharedArraySource(name + "_tok", 0, (1,), "int32" if a.token_dtype == "int32" else "int16")
+                # local rank 0 created the corpus; its wire dtype travels in the offsets segment's neighbour
+                tb_view = SharedArraySource(name + "_tb", 1, (1,), "int64")  # held: its tensor maps the segment
+                tb = int(tb_view.tensor().view(-1)[0])
+                del tb_view
+                t = SharedArraySource(name + "_tok", 0, (1,), torch.int32 if tb == 4 else torch.int16)
                 o = SharedArraySource(name + "_off", a.n_seqs + 1, (1,), "int64")
                 offs = o.tensor().view(-1).numpy()
                 t.n = int(offs[-1])
@@ -88,6 +97,10 @@ def main(argv=None):
             dev = torch.device(env.device)
             acc = ops.ChecksumAccumulator(dev)  # one streaming launch per batch
 
+            def sync():  # the CPU rehearsal (DDL_DEVICE=cpu) has nothing to synchronise
+                if dev.type == "cuda":
+                    torch.cuda.synchronize(dev)
+
             def gen():
                 while True:
                     yield from dl
@@ -97,7 +110,7 @@ def main(argv=None):
             for _ in range(a.warmup):
                 b = next(it)
                 acc.add(b["input_ids"])
-            torch.cuda.synchronize()
+            sync()
             if env.world_size > 1:
                 dist.barrier(group=env.control_group)
             t0 = time.perf_counter()
@@ -107,7 +120,7 @@ def main(argv=None):
                 acc.add(b["input_ids"])
                 rows += b.get("n_rows", b["input_ids"].shape[0])
                 real += b["n_tokens"]  # counted from the delivered batches (producer tag), not estimated
-            torch.cuda.synchronize()
+            sync()
             dt = time.perf_counter() - t0
             st = dl.stats()
             if env.world_size > 1:
@@ -124,14 +137,14 @@ def main(argv=None):
                 for _ in range(max(1, a.warmup // 2)):
                     step(next(it))
                 meter = ComputeIdleMeter()
-                torch.cuda.synchronize()
+                sync()
                 t2 = time.perf_counter()
                 for _ in range(a.idle_steps):
                     b = next(it)
                     meter.step_begin()
                     step(b)
                     meter.step_end()
-                torch.cuda.synchronize()
+                sync()
                 t3 = time.perf_counter()
                 idle = meter.result()
                 idle["train_sequences_per_s"] = a.idle_steps * a.batch * env.world_size / (t3 - t2)
@@ -163,7 +176,8 @@ def main(argv=None):
                     "producers": a.producers, "host_threads": a.host_threads, "slots": a.slots,
                     "batches_per_window": dl.batches_per_window[0], "dispatch": a.dispatch,
                     "dispatch_mode": (st.get("native_dispatch") or {}).get("mode"), "token_rows": a.token_rows,
-                    "mean_len": round(mean_len, 1), "token_wire_dtype": a.token_dtype,
+                    "mean_len": round(mean_len, 1),
+                    "token_wire_dtype": "uint16" if source.token_bytes == 2 else "int32",
                     "h2d_token_gbps": round(real_tokens * source.token_bytes / dt / 1e9, 2),
                     "consumer_wait_s": round(st["consumer_wait_s"], 3),
                     "stager_wait_producer_s": round(st.get("stager_wait_producer_s", 0.0), 3),
@@ -180,6 +194,7 @@ def main(argv=None):
     finally:
         if src is not None:
             src.close()
+            tb_seg.close()
 
 
 if __name__ == "__main__":

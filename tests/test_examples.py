@@ -103,6 +103,26 @@ def test_bench_refuses_world_size_mismatch():
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
 
 
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("token_dtype", ["auto", "int32"])
+def test_bench_tokens_two_ranks(token_dtype):
+    """BASELINE config 4's bench at 2 ranks (CPU/gloo): local rank 0 creates the corpus (uint16 on the wire
+    with "auto": the synthetic vocabulary fits), the other rank attaches to it with the right id width, and
+    the token count is the delivered one."""
+    import json
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(REPO, "benchmarks", "bench_tokens.py"), "--steps", "5", "--warmup", "2", "--idle-steps", "0",
+           "--batch", "64", "--n-seqs", "1024", "--token-dtype", token_dtype]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=dict(_env(), DDL_DEVICE="cpu"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert out["n_gpus"] == 2 and out["value"] > 0
+    assert out["token_wire_dtype"] == ("uint16" if token_dtype == "auto" else "int32")
+    assert abs(out["value"] / out["value_est_from_mean_len"] - 1) < 0.2
+
+
 @pytest.mark.timeout(200)
 def test_bench_plumbing_config1_two_ranks():
     """BASELINE config 1 (1k x 3x32x32, world 2, CPU): exactly-once delivery every epoch, one JSON line."""

@@ -459,3 +459,49 @@ def test_stager_bytes_in_interval_is_pro_rata_and_additive():
         after = st.bytes_in_interval(e2, e3)
         assert after["ok"] and after["bytes"] == 0.0 and after["copies"] == 0
         dl.close()
+
+
+@pytest.mark.parametrize("policy,streams", [("auto", "2"), ("alternate", "2"), ("adaptive", "2"), ("auto", "1")])
+def test_copy_stream_policies_deliver_identical_batches(monkeypatch, policy, streams):
+    """The copy-stream policy only decides which SDMA stream each window copy runs on: every policy (and one
+    stream) delivers the same batches, bit for bit, including when the consumer is slow enough for `auto` to
+    switch to one stream (a sleep per batch makes the stager wait on the ring)."""
+    import time
+
+    from ddl_amd.models.producers import ImageWindowProducer
+
+    def run(pol, n_cs, slow):
+        monkeypatch.setenv("DDL_COPY_POLICY", pol)
+        monkeypatch.setenv("DDL_COPY_STREAMS", n_cs)
+        out = []
+        with ddl_amd.start(n_producers=2) as (env, conn):
+            dl = ddl_amd.DistributedDataLoader(ImageWindowProducer(32, (3, 16, 16), "bfloat16", seed=5), 8, conn, 6,
+                                               env=env, device=torch.device("cuda"), out_dtype=torch.bfloat16,
+                                               shuffle="device", seed=3, prefetch_depth=2)
+            assert dl.stats()["copy_policy"] == (pol if n_cs == "2" else "one stream")
+            for e in range(6):
+                for i in range(len(dl)):
+                    (x,) = dl[i]
+                    out.append(x.float().sum(dim=(1, 2, 3)).cpu())
+                    if slow:
+                        time.sleep(0.002)
+                    dl.mark(Marker.END_OF_BATCH)
+                if e < 5:
+                    dl.mark(Marker.END_OF_EPOCH)
+            dl.close()
+        return torch.stack(out)
+
+    ref = run("alternate", "2", False)
+    for slow in (False, True):
+        got = run(policy, streams, slow)
+        assert torch.equal(got, ref)
+
+
+def test_copy_policy_rejects_unknown(monkeypatch):
+    from ddl_amd.models.producers import ImageWindowProducer
+
+    monkeypatch.setenv("DDL_COPY_POLICY", "round_robin")
+    with ddl_amd.start(n_producers=1) as (env, conn):
+        with pytest.raises(ValueError, match="DDL_COPY_POLICY"):
+            ddl_amd.DistributedDataLoader(ImageWindowProducer(16, (3, 8, 8), "bfloat16"), 8, conn, 1, env=env,
+                                          device=torch.device("cuda"), out_dtype=torch.bfloat16)
