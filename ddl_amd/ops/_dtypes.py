@@ -19,6 +19,7 @@ _TORCH_TO_CODE = {
 _NAME_TO_TORCH = {
     "uint8": torch.uint8,
     "u8": torch.uint8,
+    "int16": torch.int16,
     "int32": torch.int32,
     "int64": torch.int64,
     "float16": torch.float16,
@@ -49,8 +50,8 @@ def to_torch_dtype(dt) -> torch.dtype:
         except KeyError:
             raise TypeError(f"unknown dtype name {dt!r}") from None
     npd = np.dtype(dt)
-    m = {np.dtype(np.uint8): torch.uint8, np.dtype(np.int32): torch.int32, np.dtype(np.int64): torch.int64,
-         np.dtype(np.float16): torch.float16, np.dtype(np.float32): torch.float32}
+    m = {np.dtype(np.uint8): torch.uint8, np.dtype(np.int16): torch.int16, np.dtype(np.int32): torch.int32,
+         np.dtype(np.int64): torch.int64, np.dtype(np.float16): torch.float16, np.dtype(np.float32): torch.float32}
     if npd in m:
         return m[npd]
     raise TypeError(f"unsupported dtype {dt!r}")
@@ -58,8 +59,8 @@ def to_torch_dtype(dt) -> torch.dtype:
 
 def numpy_view_dtype(dt: torch.dtype):
     """numpy dtype for a host view of ``dt`` (bf16 has none: returns None)."""
-    m = {torch.uint8: np.uint8, torch.int32: np.int32, torch.int64: np.int64, torch.float16: np.float16,
-         torch.float32: np.float32}
+    m = {torch.uint8: np.uint8, torch.int16: np.int16, torch.int32: np.int32, torch.int64: np.int64,
+         torch.float16: np.float16, torch.float32: np.float32}
     return m.get(dt)
 
 
