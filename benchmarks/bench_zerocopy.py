@@ -23,6 +23,7 @@ def main(argv=None):
     ap.add_argument("--n-samples", type=int, default=16384)
     ap.add_argument("--dtype", default="bfloat16", choices=["bfloat16", "uint8"])
     ap.add_argument("--blocks", default="16,32,64,128,0")
+    ap.add_argument("--prep-streams", default="1", help="comma list: gather streams per loader (1, 2)")
     ap.add_argument("--train-steps", type=int, default=100)
     a = ap.parse_args(argv)
 
@@ -56,9 +57,9 @@ def main(argv=None):
             dev = torch.device(env.device)
             norm = {"mean": [0.485, 0.456, 0.406], "std": [0.229, 0.224, 0.225]} if a.dtype == "uint8" else None
             best = None
-            for mb in [int(x) for x in a.blocks.split(",")]:
+            for mb, ps in [(int(x), int(y)) for y in a.prep_streams.split(",") for x in a.blocks.split(",")]:
                 dl = ZeroCopyLoader(src, a.batch * env.world_size, env, seed=1, out_dtype=torch.bfloat16,
-                                    normalize=norm, max_blocks=mb, depth=2)
+                                    normalize=norm, max_blocks=mb, depth=2, prep_streams=ps)
                 acc = ops.ChecksumAccumulator(dev)  # one streaming launch per batch
 
                 def gen():
@@ -75,7 +76,7 @@ def main(argv=None):
                 torch.cuda.synchronize()
                 el = time.perf_counter() - t0
                 rate = a.batch * a.steps * env.world_size / el
-                out["sweep"].append({"max_blocks": mb, "samples_per_s": round(rate, 1),
+                out["sweep"].append({"max_blocks": mb, "prep_streams": ps, "samples_per_s": round(rate, 1),
                                      "GBps_pcie": round(rate * src.row_bytes / env.world_size / 1e9, 2)})
                 if best is None or rate > best[1] * 1.02 or (mb and rate > 0.97 * best[1] and best[0] == 0):
                     best = (mb, rate)

@@ -55,7 +55,7 @@ class ZeroCopyLoader(PrefetchedIndexedLoader):
                  drop_last: bool = True, out_dtype: Any = None, normalize: dict | None = None, depth: int = 2,
                  max_blocks: int | None = None, device: str | torch.device | None = None,
                  n_epochs: int | None = None,
-                 resume_state: dict | None = None):
+                 resume_state: dict | None = None, prep_streams: int = 1):
         self.env = env or DDLEnv()
         self.W, self.rank = self.env.world_size, self.env.rank
         self.sample_shape, self.src_dtype = _source_geometry(source)
@@ -104,6 +104,10 @@ class ZeroCopyLoader(PrefetchedIndexedLoader):
                 dptr = hip.host_device_pointer(base) + (addr - base)
             self.rows = ops.HostRows(self.cpu, dptr)
             self.prep_stream = streams.batch_stream(self.device)
+            # prep_streams = 2: consecutive batches' gathers alternate between two streams, so the next one
+            # starts while the previous one's last workgroups drain (the link idles in a lone kernel's tail)
+            self._prep = [self.prep_stream] + [torch.cuda.Stream(self.device, priority=-1)
+                                               for _ in range(max(1, int(prep_streams)) - 1)]
         else:
             self.rows = self.cpu
 
@@ -114,19 +118,22 @@ class ZeroCopyLoader(PrefetchedIndexedLoader):
         if self.prep_stream is None:
             return ops.gather_rows(self.rows, perm=self.order.perm(e), base=base, n_rows=self.LB,
                                    out_dtype=self.out_dtype, **kw), None
-        with streams.on_stream(self.prep_stream):
+        st = self._prep[t % len(self._prep)]
+        with streams.on_stream(st):
             batch = ops.gather_rows(self.rows, perm=self.order.perm(e), base=base, n_rows=self.LB,
                                     out_dtype=self.out_dtype, max_blocks=self.max_blocks, **kw)
             ev = torch.cuda.Event()
-            ev.record(self.prep_stream)
+            ev.record(st)
         return batch, ev
 
     def stats(self) -> dict:
-        return {"batches": self.batches, "source_bytes": self.nbytes, "max_blocks": self.max_blocks}
+        return {"batches": self.batches, "source_bytes": self.nbytes, "max_blocks": self.max_blocks,
+                "prep_streams": len(self._prep) if self.prep_stream is not None else 0}
 
     def close(self) -> None:
         if self.prep_stream is not None:
-            self.prep_stream.synchronize()
+            for st in self._prep:
+                st.synchronize()
         self._queue.clear()
         if self._reg_base is not None:
             torch.cuda.synchronize(self.device)

@@ -31,14 +31,14 @@ def test_zerocopy_cpu_order_and_resume():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("max_blocks", [0, 4, 64])
+@pytest.mark.parametrize("max_blocks,prep_streams", [(0, 1), (4, 1), (64, 1), (16, 2)])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.uint8])
-def test_zerocopy_gpu_matches_reference(max_blocks, dtype):
+def test_zerocopy_gpu_matches_reference(max_blocks, prep_streams, dtype):
     n, shape = 512, (3, 32, 32)
     src = (torch.rand((n, *shape)) * 255).to(dtype)
     norm = {"mean": [0.5, 0.4, 0.3], "std": [0.2, 0.2, 0.2]} if dtype == torch.uint8 else None
     dl = ZeroCopyLoader(src, 64, seed=1, n_epochs=1, out_dtype=torch.bfloat16, normalize=norm, max_blocks=max_blocks,
-                        depth=3)
+                        depth=3, prep_streams=prep_streams)
     order = EpochOrder(n, 64, 1)
     got = torch.cat([b.float().cpu() for b in dl])
     idx = torch.from_numpy(order.perm(0).full()[: order.batches_per_epoch * 64])
