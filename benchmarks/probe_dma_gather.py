@@ -39,7 +39,7 @@ def main() -> int:
             host_ns = 0
             for k in range(20):
                 host_ns += hip.dma_gather_rows(out.data_ptr(), src.data_ptr(), row_bytes, idx[k].ctypes.data, rows,
-                                               s.cuda_stream, mode == "batched")
+                                               n, s.cuda_stream, mode == "batched")
             s.synchronize()
             dt = time.perf_counter() - t0
         res[f"dma_{mode}_GBps"] = round(20 * rows * row_bytes / dt / 1e9, 2)

@@ -144,13 +144,15 @@ PYBIND11_MODULE(_ddl_hip, m) {
   });
   m.def(
       "dma_gather_rows",
-      [](uintptr_t dst, uintptr_t src, uint64_t row_bytes, uintptr_t idx_ptr, int64_t n, uintptr_t stream,
-         bool batched) {
+      [](uintptr_t dst, uintptr_t src, uint64_t row_bytes, uintptr_t idx_ptr, int64_t n, int64_t src_rows,
+         uintptr_t stream, bool batched) {
         // SDMA gather: row idx[i] of the (pinned, registered) host source -> row i of dst, as n copies in ONE
         // hipMemcpyBatchAsync (batched) or n hipMemcpyAsync calls; runs of consecutive rows become one copy.
         // Returns the host ns spent enqueueing.
         const auto t0 = std::chrono::steady_clock::now();
         const auto* idx = reinterpret_cast<const int64_t*>(idx_ptr);
+        for (int64_t i = 0; i < n; ++i)  // an out-of-range row would DMA from unrelated host memory
+          if (idx[i] < 0 || idx[i] >= src_rows) throw std::out_of_range("dma_gather_rows: row index out of range");
         std::vector<void*> dsts, srcs;
         std::vector<size_t> sizes;
         dsts.reserve(static_cast<size_t>(n));
@@ -184,8 +186,8 @@ PYBIND11_MODULE(_ddl_hip, m) {
         return static_cast<int64_t>(
             std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
       },
-      py::arg("dst"), py::arg("src"), py::arg("row_bytes"), py::arg("idx"), py::arg("n"), py::arg("stream"),
-      py::arg("batched") = true);
+      py::arg("dst"), py::arg("src"), py::arg("row_bytes"), py::arg("idx"), py::arg("n"), py::arg("src_rows"),
+      py::arg("stream"), py::arg("batched") = true);
   m.def("has_memcpy_batch", [] { return dlsym(RTLD_DEFAULT, "hipMemcpyBatchAsync") != nullptr; });
   m.def("pointer_is_host_registered", [](uintptr_t addr) {
     hipPointerAttribute_t a;
