@@ -142,11 +142,12 @@ int NativeStager::pick_copy_stream(int64_t w) const {
   if (copy_stream2_ == nullptr) return 0;
   if (copy_policy_ == 0) return static_cast<int>((w - first_) & 1);  // strict alternation
   if (copy_policy_ == 2) {
-    // auto: the stager waited for a ring buffer on kRingWaitRun windows in a row, so the consumer is slower
-    // than the link and the feed has slack: one stream (one SDMA engine), which shows a lower step-boundary
-    // idle below the crossover (profiles/r3_copy_policy). Otherwise (loader-bound) alternate, so two copies
-    // overlap and the link never waits for one to end (+2.5% feed). The run length keeps an isolated wait --
-    // e.g. the one across a benchmark's opening synchronize -- from serialising the copies after it.
+    // auto: on kRingWaitRun windows in a row the stager waited for a ring buffer while the link went idle, so
+    // the consumer is slower than the link and the feed has slack: one stream (one SDMA engine), which shows a
+    // lower step-boundary idle below the crossover (profiles/r3_copy_policy). Otherwise (loader-bound)
+    // alternate, so two copies overlap and the link never waits for one to end (+2.5% feed). The run length
+    // keeps an isolated wait -- e.g. the one across a benchmark's opening synchronize -- from serialising the
+    // copies after it.
     return ring_wait_run_ >= kRingWaitRun ? 0 : 1 - last_stream_;
   }
   // adaptive (policy 1): stream 0 whenever its last copy has retired. Measured to serialise nearly every copy
@@ -225,7 +226,11 @@ void NativeStager::run() {
       return fail(-1, static_cast<int32_t>(p),
                   "window of " + std::to_string(info.used_bytes) + " B exceeds the staging buffer");
     // stream choice as late as possible, when the engines' state is known (see pick_copy_stream)
-    ring_wait_run_ = s1 - s0 > kRingWaitNs ? ring_wait_run_ + 1 : 0;
+    // the consumer is the bottleneck when the stager had to wait for a ring buffer AND the link went idle
+    // meanwhile (no copy still in flight): a ring wait with copies in flight is the loader-bound steady state
+    // of a stager that runs ahead of the ring (e.g. 2 slots per producer)
+    const bool link_idle = !copy_in_flight(0, w) && (copy_stream2_ == nullptr || !copy_in_flight(1, w));
+    ring_wait_run_ = s1 - s0 > kRingWaitNs && link_idle ? ring_wait_run_ + 1 : 0;
     const int si = pick_copy_stream(w);
     hipStream_t cs = si == 0 ? copy_stream_ : copy_stream2_;
     // the consumer's kernels reading this ring buffer (window w - depth) finish first; a free event that

@@ -168,8 +168,8 @@ class NativeStager {
   // ring buffers, alternation otherwise (pick_copy_stream)
   const int copy_policy_;
   static constexpr int64_t kRingWaitNs = 50000;  // a ring wait longer than this: the consumer held the ring
-  static constexpr int kRingWaitRun = 3;          // ... on this many windows in a row: the consumer is the bottleneck
-  int ring_wait_run_ = 0;                         // consecutive windows that waited for the ring (stager thread)
+  static constexpr int kRingWaitRun = 3;  // ... with the link idle, this many windows in a row: consumer-bound
+  int ring_wait_run_ = 0;                 // consecutive such windows (stager thread)
   int64_t last_copy_[2] = {-1, -1};  // last window copied on each stream (stager thread only)
   int last_stream_ = 1;
   bool copy_in_flight(int i, int64_t w) const;
