@@ -6,4 +6,4 @@ run 300 smoke python -c "import __graft_entry__ as g; g.smoke()"
 for i in 1 2 3; do
   run 120 f_drv_$i python bench.py --gpus 1 --steps 20 --warmup 5 --json-out gpurun_out/f_drv_$i.json
 done
-run 300 f_probe python benchmarks/probe_indexed_phase.py
+
