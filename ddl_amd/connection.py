@@ -332,6 +332,20 @@ class Connection:
                 logger.warning("hipHostUnregister failed: %s", e)
             self._registered = False
 
+    def kill(self) -> None:
+        """Job abort (``parallel/abort.py``): stop the producers NOW -- no joins, no device sync (the
+        GPU may be stuck behind a collective that will never complete). The arena file is already
+        unlinked, so nothing is left in /dev/shm."""
+        self._closed = True
+        if self.arena is not None:
+            self.arena.request_shutdown()
+        for proc in self.processes:
+            if proc is not None and hasattr(proc, "kill"):
+                try:
+                    proc.kill()
+                except Exception:  # pragma: no cover - already gone
+                    pass
+
     def producer_stats(self) -> list[dict]:
         if self.arena is None:
             return []

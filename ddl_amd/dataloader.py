@@ -54,6 +54,7 @@ from .utils.tracing import LoaderMetrics, trace_range
 
 STATE_VERSION = 1
 _TRACE_ENGINE = os.environ.get("DDL_TRACE_ENGINE", "0") == "1"
+_FAULT_RANK = bool(os.environ.get("DDL_FAULT_RANK"))  # test hook (utils/faults.py)
 MODES = ("do_not_split_along_epoch", "split_along_epoch", "window", "indexed")
 
 
@@ -964,6 +965,10 @@ class DistributedDataLoader(DistributedDataloaderABC):
     def _begin_window(self) -> None:
         """The cursor moved to a new window: issue its exchange collective now (consumer thread,
         fixed point of the schedule, parallel/order.py) and start gathering its first batch."""
+        if _FAULT_RANK:
+            from .utils.faults import maybe_fail_rank
+
+            maybe_fail_rank(self.env.rank if self.env else 0, self.window)
         st = self._stager
         if st is None or st.post_copy is None or self._finalized:
             return

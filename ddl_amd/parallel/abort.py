@@ -1,0 +1,179 @@
+"""Job-wide failure propagation: the ``MPI_Abort`` of a torch.distributed job.
+
+In the reference a fatal error ``Abort(1)``s every rank (``/root/reference/ddl/ddl_env.py:25-30``) and
+mpirun tears the whole job down when one rank dies. A torch.distributed job has neither: a rank that
+raises mid-epoch leaves its peers blocked inside the next exchange all-to-all or DDP all-reduce until
+the process-group timeout, and a rank that is SIGKILLed leaves them there too.
+
+``JobWatchdog`` closes that gap with one daemon thread per rank and a side channel that does not go
+through the (possibly blocked) collectives: a client of the job's rendezvous ``TCPStore``
+(``MASTER_ADDR:MASTER_PORT``, under a per-job prefix).
+
+* **Raise -> abort.** ``start()`` catches an exception escaping the user's code on any rank, publishes
+  ``abort = "rank r: <error>"`` in the store, prints the traceback and exits the process with status 1
+  (the failing rank never waits in the final barrier or in ``torch.cuda.synchronize`` behind a
+  collective its peers will never join).
+* **Abort -> exit.** Every other rank's watchdog sees the key within ``poll_s``, logs it, stops its
+  producer workers and exits with ``PEER_ABORT_EXIT`` (``os._exit``: the main thread may be blocked in
+  a collective that will never complete).
+* **Silent death.** Each rank bumps a heartbeat counter; rank r watches rank ``(r + 1) % W`` only (O(W)
+  store traffic). A counter that has not moved for ``peer_timeout_s`` (SIGKILL, OOM kill, a hang with
+  the GIL held) makes the watcher publish the abort for it. An unreachable store (its host rank died)
+  is an abort too.
+* **Clean exit.** ``stop()`` marks the rank done (watchers of a finished rank stop checking it) before
+  the final barrier, so a slow rank is never mistaken for a dead one once its neighbour finished.
+
+The process-group timeout itself is ``start(timeout_s=)`` (``parallel/env.init_distributed``); the
+watchdog makes the typical failure end the job in about ``poll_s`` instead of that timeout.
+"""
+
+from __future__ import annotations
+
+import os
+import sys
+import threading
+import time
+import traceback
+from datetime import timedelta
+from typing import Any, Callable
+
+from ..utils.logging import logger
+
+PEER_ABORT_EXIT = 75  # exit status of a rank torn down because ANOTHER rank failed
+DEFAULT_PEER_TIMEOUT_S = 60.0
+
+
+def _store_client(prefix: str, timeout_s: float):
+    """A private client of the rendezvous TCPStore (never shares a socket with the collectives'
+    bootstrap); the default group's store when the job was not rendezvoused over MASTER_ADDR/PORT."""
+    import torch.distributed as dist
+
+    try:
+        host = os.environ["MASTER_ADDR"]
+        port = int(os.environ["MASTER_PORT"])
+        store = dist.TCPStore(host, port, is_master=False, timeout=timedelta(seconds=timeout_s),
+                              wait_for_workers=False)
+    except Exception:
+        from torch.distributed.distributed_c10d import _get_default_store
+
+        store = _get_default_store()
+    return dist.PrefixStore(prefix, store)
+
+
+class JobWatchdog:
+    """One per rank; see the module docstring. ``on_abort`` runs (best effort) before the exit."""
+
+    def __init__(self, rank: int, world_size: int, *, peer_timeout_s: float = DEFAULT_PEER_TIMEOUT_S,
+                 poll_s: float = 0.25, on_abort: Callable[[], None] | None = None, store: Any = None,
+                 job_key: str | None = None, exit_fn: Callable[[int], None] | None = None):
+        self.rank, self.world = int(rank), int(world_size)
+        self.peer_timeout_s = float(peer_timeout_s)
+        self.poll_s = float(poll_s)
+        self.on_abort = on_abort
+        self._exit = exit_fn or os._exit
+        key = job_key or os.environ.get("TORCHELASTIC_RUN_ID") or os.environ.get("MASTER_PORT", "0")
+        self._store = store if store is not None else _store_client(f"ddl_amd/abort/{key}/", 30.0)
+        self._stop = threading.Event()
+        self._thread: threading.Thread | None = None
+        self.aborted: str | None = None  # the abort message this rank acted on (tests, exit_fn overrides)
+        self._beat = 0
+        self._done = False
+
+    # ------------------------------------------------------------------ store keys
+    def _hb(self, r: int) -> str:
+        return f"hb/{r}"
+
+    def start(self) -> "JobWatchdog":
+        self._store.set(self._hb(self.rank), "0")
+        self._thread = threading.Thread(target=self._run, name=f"ddl-watchdog-{self.rank}", daemon=True)
+        self._thread.start()
+        return self
+
+    def abort(self, reason: str) -> None:
+        """Publish a job-wide abort (the first reason wins: ``compare_set`` on an absent key)."""
+        msg = f"rank {self.rank}: {reason}"[:2000]
+        try:
+            self._store.compare_set("abort", "", msg)
+        except Exception as e:  # the store is gone: the peers' watchdogs will see that too
+            logger.error("could not publish the abort (%s); peers will detect the store loss", e)
+
+    def finishing(self) -> None:
+        """This rank's work is done: watchers of this rank stop watching it (a rank that finished
+        first is not 'dead'), but this rank keeps acting on aborts -- a peer can still fail while
+        this one waits in the final barrier."""
+        try:
+            self._store.set(self._hb(self.rank), "done")
+        except Exception:  # pragma: no cover - the thread reports a lost store
+            pass
+        self._done = True
+
+    def stop(self) -> None:
+        """After the final barrier: no more checks."""
+        if not self._done:
+            self.finishing()
+        self._stop.set()
+        if self._thread is not None:
+            self._thread.join(2 * self.poll_s + 1.0)
+
+    # ------------------------------------------------------------------ thread
+    def _fire(self, msg: str) -> None:
+        if self._stop.is_set():
+            return
+        self.aborted = msg
+        sys.stdout.flush()
+        print(f"ddl_amd: rank {self.rank}: job aborted ({msg}); exiting with {PEER_ABORT_EXIT}",
+              file=sys.stderr, flush=True)
+        if self.on_abort is not None:
+            try:
+                self.on_abort()
+            except Exception:  # pragma: no cover - best effort
+                pass
+        self._exit(PEER_ABORT_EXIT)
+
+    def _run(self) -> None:
+        target = (self.rank + 1) % self.world
+        watch = target != self.rank
+        last_val, last_change = None, time.monotonic()
+        while not self._stop.wait(self.poll_s):
+            try:
+                if not self._done:
+                    self._beat += 1
+                    self._store.set(self._hb(self.rank), str(self._beat))
+                if self._store.check(["abort"]):
+                    msg = self._store.get("abort").decode(errors="replace")
+                    if msg:
+                        return self._fire(msg)
+                if watch:
+                    v = self._store.get(self._hb(target)) if self._store.check([self._hb(target)]) else b""
+                    if v == b"done":
+                        watch = False
+                    elif v != last_val:
+                        last_val, last_change = v, time.monotonic()
+                    elif time.monotonic() - last_change > self.peer_timeout_s:
+                        msg = f"no heartbeat from rank {target} for {self.peer_timeout_s:.0f}s (dead or hung)"
+                        self.abort(msg)
+                        return self._fire(f"rank {self.rank}: {msg}")
+            except Exception as e:  # store unreachable: its host rank (or the agent) is gone
+                # ... or the job just ended cleanly and the store's host exited first: give stop() a
+                # moment to arrive after the final barrier before calling it a failure
+                if self._stop.wait(4 * self.poll_s + 1.0):
+                    return
+                return self._fire(f"rendezvous store unreachable ({type(e).__name__}: {e})")
+
+
+def abort_on_exception(watchdog: JobWatchdog | None, exc: BaseException, cleanup: Callable[[], None] | None = None,
+                       exit_fn: Callable[[int], None] | None = None) -> None:
+    """The failing rank's side: publish, report, clean up what is safe, exit(1) without waiting on peers."""
+    reason = f"{type(exc).__name__}: {exc}"
+    if watchdog is not None:
+        watchdog._stop.set()  # its own abort key must not make it exit with the peer status
+        watchdog.abort(reason)
+    traceback.print_exception(type(exc), exc, exc.__traceback__, file=sys.stderr)
+    print(f"ddl_amd: rank {getattr(watchdog, 'rank', '?')} failed ({reason}); aborting the job",
+          file=sys.stderr, flush=True)
+    if cleanup is not None:
+        try:
+            cleanup()
+        except Exception:  # pragma: no cover - best effort
+            pass
+    (exit_fn or os._exit)(1)

@@ -78,6 +78,7 @@ def init_distributed(env: DDLEnv, backend: str | None = None, timeout_s: float =
 
     ``backend`` defaults to ``$DDL_BACKEND``, else RCCL ("nccl") on a GPU and gloo on
     the CPU; at world size 1 no group is built unless a backend is named.
+    ``timeout_s`` is both groups' collective timeout (``start(timeout_s=)`` passes its own through).
     ``device="cpu"`` (or ``$DDL_DEVICE=cpu``) keeps the rank off the GPU even
     when one is visible (CPU rehearsals of multi-rank runs). Touches the GPU
     otherwise: call it only after producer workers have been spawned.
@@ -110,7 +111,8 @@ def init_distributed(env: DDLEnv, backend: str | None = None, timeout_s: float =
             kwargs["device_id"] = torch.device(env.device)
         dist.init_process_group(**kwargs)
     env.process_group = dist.group.WORLD
-    env.control_group = dist.new_group(backend="gloo") if backend != "gloo" else dist.group.WORLD
+    env.control_group = (dist.new_group(backend="gloo", timeout=timedelta(seconds=timeout_s)) if backend != "gloo"
+                         else dist.group.WORLD)
     check_node_locality(env)
     return env
 

@@ -24,6 +24,7 @@ from typing import Any, Callable, Iterator
 from ..connection import DEFAULT_TIMEOUT_S, Connection
 from ..types import DDLEnv
 from ..utils.logging import configure, logger
+from .abort import DEFAULT_PEER_TIMEOUT_S, JobWatchdog, abort_on_exception
 from .env import destroy_distributed, init_distributed, read_env
 
 
@@ -67,8 +68,17 @@ def spawn_producers(env: DDLEnv, timeout_s: float = DEFAULT_TIMEOUT_S, env_overr
 @contextlib.contextmanager
 def start(n_producers: int | None = None, init_dist: bool = True, backend: str | None = None,
           timeout_s: float = DEFAULT_TIMEOUT_S, env_overrides: dict | None = None,
-          device: str | None = None) -> Iterator[tuple[DDLEnv, Connection | None]]:
-    """Context-manager form of the launcher: ``with start() as (env, conn): ...``."""
+          device: str | None = None, abort_on_error: bool = True,
+          peer_timeout_s: float = DEFAULT_PEER_TIMEOUT_S) -> Iterator[tuple[DDLEnv, Connection | None]]:
+    """Context-manager form of the launcher: ``with start() as (env, conn): ...``.
+
+    ``timeout_s`` bounds every wait: the shm hand-offs with the producers AND the process groups'
+    collectives (``init_distributed``). With ``abort_on_error`` (default) and more than one rank, a
+    failure on any rank ends the whole job, as the reference's ``Abort(1)`` does
+    (``/root/reference/ddl/ddl_env.py:25-30``): the failing rank publishes the error and exits 1, its
+    peers exit ``PEER_ABORT_EXIT`` within a fraction of a second, and a rank that dies silently is
+    declared dead after ``peer_timeout_s`` without a heartbeat (``parallel/abort.py``).
+    """
     configure()
     env = read_env(n_producers)
     from ..utils.numa import bind_to_gpu_numa, partition_after_spawn
@@ -80,15 +90,25 @@ def start(n_producers: int | None = None, init_dist: bool = True, backend: str |
         pids = [p for p in conn.producer_pids if p and p != os.getpid()]  # thread-mode producers: none
         conn.cpu_layout = partition_after_spawn(pids, len(pids)) if len(pids) == env.n_producers else None
     created_pg = False
+    watchdog = None
     try:
         if init_dist:
             import torch.distributed as dist
 
             was = dist.is_available() and dist.is_initialized()
-            init_distributed(env, backend, device=device)
+            init_distributed(env, backend, timeout_s=timeout_s, device=device)
             created_pg = not was and env.world_size > 1
+            if abort_on_error and env.world_size > 1 and env.control_group is not None:
+                watchdog = JobWatchdog(env.rank, env.world_size, peer_timeout_s=peer_timeout_s,
+                                       on_abort=conn.kill if conn is not None else None).start()
         yield env, conn
+    except BaseException as e:
+        if watchdog is not None and not (isinstance(e, SystemExit) and e.code in (None, 0)):
+            abort_on_exception(watchdog, e, cleanup=conn.kill if conn is not None else None)
+        raise
     finally:
+        if watchdog is not None:
+            watchdog.finishing()
         if conn is not None:
             conn.finalize()
         if created_pg:
@@ -98,11 +118,16 @@ def start(n_producers: int | None = None, init_dist: bool = True, backend: str |
                 dist.barrier(group=env.control_group)
             except Exception as e:  # pragma: no cover
                 logger.warning("final barrier failed: %s", e)
+            if watchdog is not None:
+                watchdog.stop()
             destroy_distributed()
+        elif watchdog is not None:
+            watchdog.stop()
 
 
 def distributed_dataloader(func: Callable | None = None, *, n_producers: int | None = None, init_dist: bool = True,
-                           backend: str | None = None, timeout_s: float = DEFAULT_TIMEOUT_S):
+                           backend: str | None = None, timeout_s: float = DEFAULT_TIMEOUT_S,
+                           abort_on_error: bool = True):
     """Decorator: run ``func(*args, env, conn, **kwargs)`` as this rank's consumer with its producers.
 
     Usable bare (``@distributed_dataloader``) or with options
@@ -113,7 +138,7 @@ def distributed_dataloader(func: Callable | None = None, *, n_producers: int | N
     def deco(f: Callable) -> Callable:
         @functools.wraps(f)
         def wrapper(*args: Any, **kwargs: Any) -> Any:
-            with start(n_producers, init_dist, backend, timeout_s) as (env, conn):
+            with start(n_producers, init_dist, backend, timeout_s, abort_on_error=abort_on_error) as (env, conn):
                 return f(*args, env, conn, **kwargs)
 
         return wrapper

@@ -6,6 +6,10 @@
 * ``exit``  -- hard crash (``os._exit(17)``, no cleanup, no error report);
 * ``raise`` -- a Python exception (reported to the consumer, status FAILED);
 * ``hang``  -- sleep forever (exercises the consumer's bounded waits).
+
+``DDL_FAULT_RANK="<rank>:<window>[:<kind>]"`` makes DP rank ``<rank>``'s consumer fail when its
+cursor enters global window ``<window>`` (``raise``: a Python exception; ``exit``: ``os._exit(17)``,
+a silent death) -- the job-wide abort tests (``parallel/abort.py``).
 """
 
 from __future__ import annotations
@@ -35,3 +39,15 @@ def maybe_fail_producer(index: int, rnd: int) -> None:
         while True:
             time.sleep(3600)
     raise RuntimeError(f"injected fault in producer {index} at round {rnd}")
+
+
+def maybe_fail_rank(rank: int, window: int) -> None:
+    v = os.environ.get("DDL_FAULT_RANK")
+    if not v:
+        return
+    parts = v.split(":")
+    if int(parts[0]) != rank or int(parts[1]) != window:
+        return
+    if (parts[2] if len(parts) > 2 else "raise") == "exit":
+        os._exit(17)
+    raise RuntimeError(f"injected fault in rank {rank} at window {window}")

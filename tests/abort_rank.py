@@ -1,0 +1,39 @@
+"""One rank of the job-abort tests (``test_job_abort.py``): a loop of control-group all-reduces inside
+``ddl_amd.start``; ``--stop-rank`` SIGSTOPs itself mid-loop (a silent hang: sockets open, no heartbeat),
+``--raise-rank`` raises mid-loop."""
+
+import argparse
+import os
+import signal
+import time
+
+import torch
+import torch.distributed as dist
+
+import ddl_amd
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--stop-rank", type=int, default=-1)
+    ap.add_argument("--raise-rank", type=int, default=-1)
+    ap.add_argument("--iters", type=int, default=400)
+    ap.add_argument("--peer-timeout", type=float, default=3.0)
+    ap.add_argument("--timeout", type=float, default=600.0, help="start(timeout_s=): shm waits + process groups")
+    ap.add_argument("--no-abort", action="store_true", help="start(abort_on_error=False): no watchdog")
+    args = ap.parse_args()
+    with ddl_amd.start(n_producers=1, peer_timeout_s=args.peer_timeout, timeout_s=args.timeout,
+                       abort_on_error=not args.no_abort) as (env, conn):
+        t = torch.ones(1)
+        for i in range(args.iters):
+            if i == 10 and env.rank == args.stop_rank:
+                os.kill(os.getpid(), signal.SIGSTOP)
+            if i == 10 and env.rank == args.raise_rank:
+                raise RuntimeError("abort_rank: injected failure")
+            dist.all_reduce(t, group=env.control_group)
+            time.sleep(0.02)
+    print(f"rank {env.rank} done", flush=True)
+
+
+if __name__ == "__main__":
+    main()
