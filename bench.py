@@ -407,6 +407,7 @@ def main(argv=None) -> int:
             "windows_prestaged_at_t0": max(0, w_land0 - w_cur0),
             "numa_node": gpu_numa_node(env.local_rank) if dev.type == "cuda" else None,
             "cpus": ({"consumer": len(conn.cpu_layout["consumer_cpus"]),
+                      "consumer_reserved": len(conn.cpu_layout["consumer_reserved_cpus"]),
                       "producers": len(conn.cpu_layout["producer_cpus"])} if conn.cpu_layout
                      else {"shared": len(os.sched_getaffinity(0))}),
         }

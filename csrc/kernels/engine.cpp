@@ -358,7 +358,11 @@ int64_t BatchEngine::get(int64_t w, int64_t local, int64_t bpw, bool next_ok, hi
     get_ns_ += clock_ns() - g0;
     return ww_slot0_ + local;
   }
+  // a window is handed back to the stager at its last batch launch (early release): a batch of it that
+  // was not launched before then would read a buffer the stager may already be refilling
+  const bool gone = handed_back_.count(w) != 0;
   if (inline_) {
+    if (gone) return -3;
     last_compute_ = compute;
     have_compute_ = true;
     rc = enqueue(w, local, windows_.at(w), &cur, true, compute, local + 1 == bpw);
@@ -379,6 +383,7 @@ int64_t BatchEngine::get(int64_t w, int64_t local, int64_t bpw, bool next_ok, hi
     }
   }
   if (!have) {
+    if (gone) return -3;
     rc = enqueue(w, local, windows_.at(w), &cur, false, nullptr, local + 1 == bpw);
     if (rc != 0) return rc;
   }

@@ -64,6 +64,23 @@ NativeStager::NativeStager(const Arena* arena, int32_t n_producers, int32_t n_sl
   if (hipEventCreateWithFlags(&epoch_ev_, hipEventBlockingSync) != hipSuccess ||
       hipEventRecord(epoch_ev_, copy_stream_) != hipSuccess || hipEventSynchronize(epoch_ev_) != hipSuccess)
     throw std::runtime_error("NativeStager: epoch event failed");
+  if (hipStreamCreateWithFlags(&anchor_stream_, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&anchor_ev_[0], hipEventBlockingSync) != hipSuccess ||
+      hipEventCreateWithFlags(&anchor_ev_[1], hipEventBlockingSync) != hipSuccess ||
+      hipEventRecord(anchor_ev_[0], anchor_stream_) != hipSuccess || hipEventSynchronize(anchor_ev_[0]) != hipSuccess)
+    throw std::runtime_error("NativeStager: anchor event failed");
+  {
+    float a0 = 0.f;
+    if (hipEventElapsedTime(&a0, epoch_ev_, anchor_ev_[0]) != hipSuccess)
+      throw std::runtime_error("NativeStager: anchor event failed");
+    anchor_ms_[0] = anchor_ms_[1] = a0;
+    // until the first re-anchor both slots name the construction-time anchor
+    if (hipEventRecord(anchor_ev_[1], anchor_stream_) != hipSuccess || hipEventSynchronize(anchor_ev_[1]) != hipSuccess ||
+        hipEventElapsedTime(&a0, epoch_ev_, anchor_ev_[1]) != hipSuccess)
+      throw std::runtime_error("NativeStager: anchor event failed");
+    anchor_ms_[1] = a0;
+    anchor_cur_ = 1;
+  }
   thread_ = std::thread([this] { run(); });
   retire_thread_ = std::thread([this] { retire_loop(); });
 }
@@ -73,6 +90,36 @@ NativeStager::~NativeStager() {
   for (auto e : retire_ev_) hipEventDestroy(e);
   for (auto e : start_ev_) hipEventDestroy(e);
   if (epoch_ev_ != nullptr) hipEventDestroy(epoch_ev_);
+  for (auto e : anchor_ev_)
+    if (e != nullptr) hipEventDestroy(e);
+  if (anchor_stream_ != nullptr) hipStreamDestroy(anchor_stream_);
+}
+
+bool NativeStager::device_ms(hipEvent_t e, double* out) const {
+  // relative to the current anchor; an event older than it (a copy in flight across a re-anchor) is measured
+  // from the previous one, which precedes every copy still in flight by construction
+  float d = 0.f;
+  const int c = anchor_cur_;
+  if (hipEventElapsedTime(&d, anchor_ev_[c], e) == hipSuccess && d >= 0.f) {
+    *out = anchor_ms_[c] + d;
+    return true;
+  }
+  if (hipEventElapsedTime(&d, anchor_ev_[c ^ 1], e) != hipSuccess) return false;
+  *out = anchor_ms_[c ^ 1] + d;
+  return true;
+}
+
+void NativeStager::reanchor() {
+  // the idle anchor stream: the new event completes at once; its time since construction is the old
+  // anchor's plus a short (sub-second) float interval
+  std::lock_guard<std::mutex> lk(mu_);
+  const int nxt = anchor_cur_ ^ 1;
+  float d = 0.f;
+  if (hipEventRecord(anchor_ev_[nxt], anchor_stream_) != hipSuccess || hipEventSynchronize(anchor_ev_[nxt]) != hipSuccess ||
+      hipEventElapsedTime(&d, anchor_ev_[anchor_cur_], anchor_ev_[nxt]) != hipSuccess)
+    return;  // keep the current anchor (times stay correct, only coarser)
+  anchor_ms_[nxt] = anchor_ms_[anchor_cur_] + d;
+  anchor_cur_ = nxt;
 }
 
 void NativeStager::retire_loop() {
@@ -87,17 +134,18 @@ void NativeStager::retire_loop() {
     }
     if (hipEventSynchronize(retire_ev_[r.ev]) != hipSuccess) return fail(-1, static_cast<int32_t>(r.producer),
                                                                          "hipEventSynchronize(retire) failed");
-    float t_start = 0.f, t_end = 0.f;  // ms since the epoch event, GPU clock
-    const bool timed = hipEventElapsedTime(&t_start, epoch_ev_, start_ev_[r.ev]) == hipSuccess &&
-                       hipEventElapsedTime(&t_end, epoch_ev_, retire_ev_[r.ev]) == hipSuccess;
     bytes_landed_.fetch_add(r.bytes, std::memory_order_relaxed);
     windows_landed_.fetch_add(1, std::memory_order_release);
     arena_->set_state(r.producer, r.slot, kEmpty);  // slot back to its producer (release store + futex wake)
+    if (++retires_since_anchor_ >= kAnchorEvery) {
+      retires_since_anchor_ = 0;
+      reanchor();
+    }
     {
       std::lock_guard<std::mutex> lk(mu_);
-      if (timed) {
-        done_log_.push_back(
-            DoneRec{r.window, r.bytes, static_cast<double>(t_start), static_cast<double>(t_end), r.stream});
+      double t_start = 0.0, t_end = 0.0;  // ms since construction, GPU clock
+      if (device_ms(start_ev_[r.ev], &t_start) && device_ms(retire_ev_[r.ev], &t_end)) {
+        done_log_.push_back(DoneRec{r.window, r.bytes, t_start, t_end, r.stream});
         if (done_log_.size() > kCopyLog) done_log_.pop_front();
       }
       retire_q_.pop_front();
@@ -349,14 +397,13 @@ std::pair<uint64_t, uint64_t> NativeStager::copies_between(uint64_t t0_ns, uint6
 
 InIntervalBytes NativeStager::bytes_in_interval(hipEvent_t e0, hipEvent_t e1, int64_t timeout_ms) {
   InIntervalBytes out;
-  float T0 = 0.f, T1 = 0.f;
-  if (hipEventSynchronize(e0) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
-      hipEventElapsedTime(&T0, epoch_ev_, e0) != hipSuccess || hipEventElapsedTime(&T1, epoch_ev_, e1) != hipSuccess)
-    return out;  // ok = false
-  out.t0_ms = T0;
-  out.t1_ms = T1;
+  double T0 = 0.0, T1 = 0.0;
+  if (hipEventSynchronize(e0) != hipSuccess || hipEventSynchronize(e1) != hipSuccess) return out;  // ok = false
   const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
   std::unique_lock<std::mutex> lk(mu_);
+  if (!device_ms(e0, &T0) || !device_ms(e1, &T1)) return out;
+  out.t0_ms = T0;
+  out.t1_ms = T1;
   // every copy enqueued so far retires (and is timed) first: one still in flight at e1 may have moved part of
   // its bytes inside the interval
   const int64_t last = retire_q_.empty() ? INT64_MIN : retire_q_.back().window;
@@ -366,8 +413,8 @@ InIntervalBytes NativeStager::bytes_in_interval(hipEvent_t e0, hipEvent_t e1, in
     return out;
   std::vector<std::pair<double, int>> edges;  // clipped [start, end] of every overlapping copy: +1 / -1
   for (const DoneRec& d : done_log_) {
-    const double a = std::max(d.t_start_ms, static_cast<double>(T0));
-    const double b = std::min(d.t_end_ms, static_cast<double>(T1));
+    const double a = std::max(d.t_start_ms, T0);
+    const double b = std::min(d.t_end_ms, T1);
     if (b <= a) continue;
     const double span = d.t_end_ms - d.t_start_ms;
     const double frac = span > 0 ? (b - a) / span : 1.0;  // uniform rate over the copy's [start, end]

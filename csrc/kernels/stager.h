@@ -142,6 +142,18 @@ class NativeStager {
   static constexpr int kRetireEvents = 16;
   std::vector<hipEvent_t> retire_ev_, start_ev_;
   hipEvent_t epoch_ev_ = nullptr;  // recorded once at construction: the zero of every copy's device times
+  // Device times are float ms from hipEventElapsedTime: measured from the construction event they would lose
+  // resolution as a run goes on (~0.25 ms after an hour). So they are measured from a recent ANCHOR event,
+  // re-recorded every kAnchorEvery retires on an idle stream, whose own time since construction is kept in
+  // double precision (anchor_ms_); the previous anchor covers copies that started before the current one.
+  static constexpr int64_t kAnchorEvery = 4096;  // ~6 s of 1.4 ms windows: float ms stay at sub-us resolution
+  hipStream_t anchor_stream_ = nullptr;
+  hipEvent_t anchor_ev_[2] = {nullptr, nullptr};
+  double anchor_ms_[2] = {0.0, 0.0};  // guarded by mu_ (with anchor_cur_)
+  int anchor_cur_ = 0;
+  int64_t retires_since_anchor_ = 0;  // retire thread only
+  bool device_ms(hipEvent_t e, double* out) const;  // ms since construction; call with mu_ held
+  void reanchor();                                  // retire thread
   struct DoneRec {
     int64_t window;
     uint64_t bytes;
@@ -199,7 +211,7 @@ class NativeStager {
     uint64_t enq_ns, bytes;
   };
   std::deque<CopyRec> copy_log_;  // the last kCopyLog copies (guarded by mu_)
-  static constexpr size_t kCopyLog = 1 << 16;
+  static constexpr size_t kCopyLog = 1 << 12;
   std::thread thread_;
 };
 

@@ -238,7 +238,8 @@ class DistributedDataLoader(DistributedDataloaderABC):
         # GPU's compute is, keeping the link and both copy engines saturated and a growing number of
         # batches alive in HBM. Every `_ahead_every` batches an event goes on the consumer's stream, and
         # fetching batch i waits (on the host) for the event of batch i - max_ahead: the copies then follow
-        # the step's pace when the step is the bottleneck. 0 disables. (`$DDL_MAX_AHEAD`, default 16.)
+        # the step's pace when the step is the bottleneck. 0 disables. (`$DDL_MAX_AHEAD`, default 16; off
+        # with the global-shuffle exchange, see _setup_exchange.)
         ma = int(os.environ.get("DDL_MAX_AHEAD", "16")) if max_ahead is None else int(max_ahead)
         if ma < 0:
             raise ValueError("max_ahead must be >= 0")
@@ -465,6 +466,8 @@ class DistributedDataLoader(DistributedDataloaderABC):
         self._eng_next_id = 0
         self._eng_rec = (None, None)  # (block, stream) of the last record_stream
         self._eng_window = None
+        self._eng_given: dict = {}  # local batch -> (outputs, block, tags) of the current window (re-fetch)
+        self._eng_spare: dict = {}  # whole-window mode: slot id -> (outputs, block) built but not yet fetched
         self._eng_streams: dict = {}  # torch stream id -> (Stream, raw hipStream_t)
         self._eng_budget = 0
         # the first blocks are allocated up front, outside any timed loop: >= 24 slots, so that in steady
@@ -508,6 +511,10 @@ class DistributedDataLoader(DistributedDataloaderABC):
                 raise PeerDeathError(f"{what}: producer {producer} (pid {pid}) "
                                      + ("reported a failure" if rc == 4 else "died"), producer, pid)
             raise DDLError(f"{what}: {self._stager._native.error()}")
+        if code == -3:
+            raise DDLError(f"{what}: requested out of order after the window's last batch -- a window goes back "
+                           "to the prefetcher when its last batch is launched; within a window, fetch batches "
+                           "in order (a batch already fetched can be fetched again)")
         raise DDLError(f"{what}: native batch engine error {code}")
 
     def _engine_batch(self, local: int, bpw: int):
@@ -529,6 +536,14 @@ class DistributedDataLoader(DistributedDataloaderABC):
             hit = self._eng_streams[sid] = (st, st.cuda_stream)
         cur, handle = hit
         w = self.window
+        if self._eng_window == w:
+            again = self._eng_given.get(local)
+            if again is not None:  # fetched before in this window: the same outputs (slots are used once)
+                out, block, tags = again
+                if self._eng_rec[0] is not block or self._eng_rec[1] is not cur:
+                    block.record_stream(cur)
+                    self._eng_rec = (block, cur)
+                return self._engine_outputs(out, tags)
         nxt = self.window_in_epoch + 1 < self.windows_per_epoch or self.epoch + 1 < self.n_epochs
         if self._exchange_fn is not None:
             posted = self._stager._posted
@@ -547,14 +562,26 @@ class DistributedDataLoader(DistributedDataloaderABC):
             self._verify_window(w, tags)
         if self._eng_window != w:
             self._eng_window = w
+            self._eng_given.clear()
+            self._eng_spare.clear()
             self.metrics.windows += 1
-        q = self._eng_slots
-        while q[0][0] != slot:  # slots the engine skipped (dropped lookahead)
-            q.popleft()
-        _, out, block = q.popleft()
+        spare = self._eng_spare.pop(slot, None) if self._eng_spare else None
+        if spare is not None:  # whole-window mode: a batch of this window fetched after a later one
+            out, block = spare
+        else:
+            q = self._eng_slots
+            while q[0][0] != slot:  # slots the engine skipped (dropped lookahead; whole-window: fetched later)
+                sid, o, b = q.popleft()
+                if self._eng_whole:
+                    self._eng_spare[sid] = (o, b)
+            _, out, block = q.popleft()
+        self._eng_given[local] = (out, block, tags)
         if self._eng_rec[0] is not block or self._eng_rec[1] is not cur:
             block.record_stream(cur)  # the compute stream uses this block from now on
             self._eng_rec = (block, cur)
+        return self._engine_outputs(out, tags)
+
+    def _engine_outputs(self, out, tags):
         if self._eng_tokens is None:
             return out
         n_tokens, n_rows, n_seg, max_seg = tags
@@ -605,6 +632,11 @@ class DistributedDataLoader(DistributedDataloaderABC):
         self._exchange_fn = make_exchange(self.env, self.exchange_method, self.fraction_exchange, n_min,
                                           self.sample_shape, self.window_dtype, self.seed,
                                           device=self.device, shuffle=self.shuffle)
+        # no host-side run-ahead wait with the exchange on: the event it would wait for sits on the
+        # compute stream behind collectives that wait on peer ranks, and the host must never block on
+        # another rank's progress (the same rule as the device hand-off below). The exchange itself
+        # bounds the run-ahead: window w + 2 is not exchanged before every rank has posted it.
+        self._ahead_q = None
 
     # ----------------------------------------------------------------- verification
     def _setup_verify(self, verify_order: bool | None, md, rank, world) -> None:
@@ -671,6 +703,8 @@ class DistributedDataLoader(DistributedDataloaderABC):
                 if rc != 0:
                     self._engine_raise(-(10 + rc), prod, f"staging window {self.window}")
                 self._eng_window = self.window
+                self._eng_given.clear()
+                self._eng_spare.clear()
                 self.metrics.windows += 1
             return None
         if self._stager is not None:
@@ -908,6 +942,8 @@ class DistributedDataLoader(DistributedDataloaderABC):
                 self._stager.forget(self.window)  # the Python face's record of the posted window
             if self._eng_window == self.window:
                 self._eng_window = None
+                self._eng_given.clear()
+                self._eng_spare.clear()
             return
         if self._stager is not None:
             stream = None
@@ -1076,6 +1112,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
                 "global_batch": extra.get("global_batch"),
                 "n_samples": extra.get("n_samples"),
                 "order_seed": extra.get("order_seed"),
+                "drop_last": extra.get("order_drop_last"),
             })
             return base
         base.update({
@@ -1161,6 +1198,12 @@ class DistributedDataLoader(DistributedDataloaderABC):
         if chk is None or not self.metadata_from_producer:
             return
         ex = self.metadata_from_producer[0].extra
+        dl_ck, dl_now = chk.get("drop_last"), ex.get("order_drop_last")
+        if dl_ck is not None and dl_now is not None and bool(dl_ck) != bool(dl_now):
+            raise ShapeMismatchError(("drop_last", dl_ck, dl_now),
+                                     f"checkpoint was saved with drop_last={bool(dl_ck)}, this loader has "
+                                     f"drop_last={bool(dl_now)} (the epoch has a different number of batches; "
+                                     "note ddl_amd.DataLoader's default is drop_last=False since round 3)")
         for key in ("global_batch", "n_samples", "order_seed"):
             if chk.get(key) is not None and ex.get(key) is not None and chk[key] != ex[key]:
                 raise ShapeMismatchError((key, chk[key], ex[key]),

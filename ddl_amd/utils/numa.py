@@ -149,9 +149,12 @@ def bind_to_gpu_numa(local_index: int, local_world: int = 1) -> int | None:
 
 
 def partition_after_spawn(producer_pids: list[int], n_producers: int) -> dict | None:
-    """After the producers are spawned (they inherited this rank's CPU slice): the producers get the
-    slice minus the consumer's first CPUs, the consumer keeps those (``split_consumer_producers``).
-    Returns the layout, or None when not partitioned. ``DDL_CPU_PARTITION=0`` disables it."""
+    """After the producers are spawned (they inherited this rank's CPU slice): move the producers off the
+    first CPUs of the slice (``split_consumer_producers``), which stay free for the consumer's loader
+    threads (native stager / retire, RCCL proxy, gloo). The consumer process itself keeps the WHOLE
+    slice: it is the user's training process, and narrowing it would also confine the user's main thread,
+    torch's intra-op pool and any workers it spawns later. Returns the layout, or None when not
+    partitioned. ``DDL_CPU_PARTITION=0`` disables it."""
     if os.environ.get("DDL_CPU_PARTITION", "1") == "0" or not producer_pids:
         return None
     mine = os.sched_getaffinity(0)
@@ -163,5 +166,6 @@ def partition_after_spawn(producer_pids: list[int], n_producers: int) -> dict | 
             os.sched_setaffinity(pid, prod)
         except OSError:
             return None
-    os.sched_setaffinity(0, cons)
-    return {"consumer_cpus": sorted(cons), "producer_cpus": sorted(prod)}
+    logger.info("CPU layout: consumer process keeps %d CPUs (%d kept free of producers), %d producers on %d CPUs",
+                len(mine), len(cons), len(producer_pids), len(prod))
+    return {"consumer_cpus": sorted(mine), "consumer_reserved_cpus": sorted(cons), "producer_cpus": sorted(prod)}

@@ -505,3 +505,39 @@ def test_copy_policy_rejects_unknown(monkeypatch):
         with pytest.raises(ValueError, match="DDL_COPY_POLICY"):
             ddl_amd.DistributedDataLoader(ImageWindowProducer(16, (3, 8, 8), "bfloat16"), 8, conn, 1, env=env,
                                           device=torch.device("cuda"), out_dtype=torch.bfloat16)
+
+
+@pytest.mark.parametrize("mode", ["inline", "lookahead", "window"])
+def test_native_dispatch_refetch_after_last_batch(mode):
+    """Early hand-back (a window's ring buffer goes back to the stager when its LAST batch is launched)
+    must not let a later fetch read a buffer that is being refilled: re-fetching a batch already fetched
+    in the window returns the same batch (checksum unchanged, even after the next windows were staged
+    over the buffer), and fetching a never-fetched batch after the last one raises DDLError in the
+    per-batch modes (the whole-window mode built every batch at the first get)."""
+    from ddl_amd import ops
+    from ddl_amd.exceptions import DDLError
+    from ddl_amd.models.producers import ImageWindowProducer
+
+    with ddl_amd.start(n_producers=2) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(ImageWindowProducer(32, (3, 16, 16), "bfloat16", seed=3), 8, conn, 4,
+                                           env=env, shuffle="device", seed=2, native_dispatch=mode,
+                                           prefetch_depth=2)
+        assert len(dl) == 4
+        first = [ops.checksum(dl[i][0]).item() for i in range(4)]  # batch 3 is the last: window handed back
+        torch.cuda.synchronize()
+        import time
+
+        time.sleep(0.5)  # the stager is free to refill the buffer with a later window now
+        again = ops.checksum(dl[2][0]).item()
+        assert again == first[2]
+        for i in range(4):
+            dl.mark(Marker.END_OF_BATCH)
+        dl.mark(Marker.END_OF_EPOCH)
+        # epoch 1: skip batch 1, fetch the last one, then the skipped one
+        dl[0], dl[3]
+        if mode == "window":
+            dl[1]  # built with the window at its first get
+        else:
+            with pytest.raises(DDLError, match="out of order"):
+                dl[1]
+        dl.close()

@@ -6,6 +6,7 @@ import pytest
 import torch
 
 import ddl_amd
+from ddl_amd.exceptions import ShapeMismatchError
 from ddl_amd.models import IndexedProducer, MapDatasetSource, unpack_fields
 from ddl_amd.permutation import EpochOrder
 from tests.mp_harness import run_ranks
@@ -177,6 +178,14 @@ def test_dataloader_front_end_cpu(monkeypatch):
     with ddl_amd.DataLoader(TupleDataset(43), batch_size=bs, shuffle=False, drop_last=False, num_workers=2) as dl:
         labels = [x for b in dl for x in b[1].tolist()]
         assert labels == [7 * (i % 43) for i in range(48)]
+        it = iter(dl)
+        next(it)
+        sd43 = dl.state_dict()
+    assert sd43["drop_last"] is False
+    # a checkpoint taken with one drop_last does not resume under the other: the error names the cause
+    with pytest.raises(ShapeMismatchError, match="drop_last"):
+        ddl_amd.DataLoader(TupleDataset(43), batch_size=bs, shuffle=False, drop_last=True, num_workers=1,
+                           resume_state=sd43)
 
 
 @pytest.mark.gpu

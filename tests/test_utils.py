@@ -1,6 +1,7 @@
 """Cross-cutting layer: hook dispatch, lazy logging, typed errors, env parsing, NUMA."""
 
 import logging
+import os
 
 import pytest
 
@@ -282,3 +283,27 @@ def test_numa_local_source_and_memory_binding():
         assert pages and all(p == 0 for p in pages)
     finally:
         src.close()
+
+
+def test_partition_after_spawn_leaves_the_consumer_process_alone():
+    """The consumer is the user's training process: the CPU split moves only the producers (ADVICE r3:
+    confining the whole process to 4 CPUs also confined torch's intra-op pool and the user's threads)."""
+    import subprocess
+    import sys
+
+    from ddl_amd.utils import numa
+
+    mine = os.sched_getaffinity(0)
+    if len(mine) < 6:
+        pytest.skip("needs >= 6 CPUs")
+    child = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(30)"])
+    try:
+        layout = numa.partition_after_spawn([child.pid], 1)
+        assert layout is not None
+        assert os.sched_getaffinity(0) == mine
+        assert set(layout["consumer_cpus"]) == mine
+        assert os.sched_getaffinity(child.pid) == set(layout["producer_cpus"])
+        assert not set(layout["consumer_reserved_cpus"]) & set(layout["producer_cpus"])
+    finally:
+        child.kill()
+        child.wait()
