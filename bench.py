@@ -38,8 +38,10 @@ in the JSON line, with the H2D bytes and GB/s of the timed region and the
 older whole-window count (copies enqueued AND retired inside the region).
 Phase 2 (``gpu_idle_pct``): a fixed-cost bf16 train step (PatchMLP fwd+bwd+SGD)
 consumes the batches; the compute stream's idle fraction is measured with HIP
-events (idle = 1 - busy/wall). ``benchmarks/bench_idle_sweep.py`` sweeps a
-calibrated step across the feed rate.
+events (idle = 1 - busy/wall). That step is ~4x slower than the feed, so phase 3
+(``gpu_idle_pct_r090``, ``pressure``) repeats the measurement behind a calibrated
+step whose capacity is 0.9x the phase-1 feed: the loader as the near-bottleneck.
+``benchmarks/bench_idle_sweep.py`` sweeps that step across the whole ratio range.
 
 vs_baseline = value / (28,500 samples/s x N): BASELINE.md's reference
 ceiling for this shape (P=3 host producers, f32, no H2D) scaled linearly.
@@ -84,6 +86,9 @@ def parse(argv=None):
                          "harness's fraction_exchange; 0 disables)")
     ap.add_argument("--exchange-method", default="alltoall")
     ap.add_argument("--idle-steps", type=int, default=-1, help="phase-2 steps (default: = --steps; 0 disables)")
+    ap.add_argument("--pressure-ratio", type=float, default=0.9,
+                    help="phase 3: GPU idle %% behind a calibrated step whose capacity is this multiple of the "
+                         "phase-1 feed (the loader as the near-bottleneck); 0 disables")
     ap.add_argument("--model-dim", type=int, default=384)
     ap.add_argument("--model-depth", type=int, default=4)
     ap.add_argument("--seed", type=int, default=0)
@@ -169,6 +174,62 @@ def phase2(args, env, dev, it, idle_steps: int, barrier, sync) -> dict:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=env.control_group)
         idle["gpu_idle_pct"] = float(t.item())
     return idle
+
+
+def pressure_phase(args, env, dev, it, feed_per_rank: float, barrier, sync) -> dict:
+    """GPU idle % with the LOADER as the near-bottleneck: a calibrated step (reads the whole batch, then a
+    bf16 GEMM chain, ``CalibratedStep``) sized so its capacity is ``--pressure-ratio`` x this rank's phase-1
+    feed, re-sized twice from its busy time measured in this very loop, then timed. Behind the PatchMLP
+    step of phase 2 (~4x slower than the feed) any loader shows ~0 idle; here a loader that does not
+    overlap its copies and kernels with the step shows up directly (``benchmarks/bench_idle_sweep.py``
+    sweeps the whole ratio range)."""
+    import torch
+    import torch.distributed as dist
+
+    from ddl_amd.models.trainstep import CalibratedStep
+    from ddl_amd.utils.tracing import ComputeIdleMeter, trace_range
+
+    r, B = args.pressure_ratio, args.batch
+    step = CalibratedStep(dev, step_ms=1000.0 * B / (r * feed_per_rank))
+    step.calibrate(next(it)[0])
+    for _ in range(max(2, args.warmup // 2)):
+        step(next(it)[0])
+    for _ in range(2):  # re-size from the busy time on the loader's batches (clocks, memory traffic)
+        tm = ComputeIdleMeter()
+        for _ in range(20):
+            (x,) = next(it)
+            tm.step_begin()
+            step(x)
+            tm.step_end()
+        sync()
+        tr = tm.result()
+        step.tune(tr["busy_ms"] / max(1, tr["steps"]))
+    n = max(args.steps, 100)
+    meter = ComputeIdleMeter()
+    barrier()
+    t0 = time.perf_counter()
+    with trace_range("bench.pressure"):
+        for _ in range(n):
+            (x,) = next(it)
+            meter.step_begin()
+            step(x)
+            meter.step_end()
+        sync()
+    el = time.perf_counter() - t0
+    res = meter.result()
+    busy = res["busy_ms"] / max(1, res["steps"])
+    cap = 1000.0 * B / busy
+    out = {"ratio_target": r, "ratio_measured": round(cap / feed_per_rank, 3), "steps": n,
+           "step_ms": round(busy, 4), "gpu_idle_pct": res["gpu_idle_pct"],
+           "predicted_idle_pct": round(100.0 * max(0.0, 1.0 - feed_per_rank / cap), 3),
+           "achieved_samples_per_s": B * n * env.world_size / el}
+    if env.world_size > 1:
+        t = torch.tensor([out["gpu_idle_pct"]], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=env.control_group)
+        out["gpu_idle_pct"] = float(t.item())
+    out["gpu_idle_pct"] = round(out["gpu_idle_pct"], 3)
+    out["achieved_samples_per_s"] = round(out["achieved_samples_per_s"], 1)
+    return out
 
 
 def indexed_phase(args, env, dev, barrier, sync) -> dict:
@@ -296,6 +357,8 @@ def main(argv=None) -> int:
     if args.exchange is None:
         args.exchange = 0.5 if n_world > 1 else 0.0
     total_steps = args.warmup + args.steps + (args.warmup // 2 + idle_steps if idle_steps else 0)
+    if args.pressure_ratio > 0:
+        total_steps += 1 + max(2, args.warmup // 2) + 40 + max(args.steps, 100)
     bpw = args.window // args.batch
     if bpw < 1:
         raise SystemExit("--window must hold at least one --batch")
@@ -461,6 +524,16 @@ def main(argv=None) -> int:
 
             traceback.print_exc()
             phase2_error, idle = repr(e)[:300], {}
+        # ---------------- phase 3: GPU idle % with the loader as the near-bottleneck
+        pressure = None
+        if args.pressure_ratio > 0 and dev.type == "cuda":
+            try:
+                pressure = pressure_phase(args, env, dev, it, value / env.world_size, barrier, sync)
+            except Exception as e:  # the headline is still reported
+                import traceback
+
+                traceback.print_exc()
+                pressure = {"error": repr(e)[:300]}
         dl.close()
         order = check_same_order(env.control_group) if env.world_size > 1 else None
         indexed = None
@@ -520,6 +593,9 @@ def main(argv=None) -> int:
                     "samples_per_s": round(idle["train_samples_per_s"], 1),
                     "busy_ms": round(idle["busy_ms"], 3), "wall_ms": round(idle["wall_ms"], 3)},
                 "phase2_error": phase2_error,
+                # the loader as the near-bottleneck: a calibrated step at --pressure-ratio x the feed
+                f"gpu_idle_pct_r{round(100 * args.pressure_ratio):03d}": (pressure or {}).get("gpu_idle_pct"),
+                "pressure": pressure,
                 "collective_order": order,
                 "indexed": indexed,
                 "per_rank": per_rank,

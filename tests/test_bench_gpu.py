@@ -1,0 +1,31 @@
+"""bench.py on one MI355X: the driver's N=1 line produces the credited JSON with every phase's fields."""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.timeout(200)
+def test_bench_n1_reports_pressure_idle():
+    """Phase 3 puts the loader-pressure idle into the credited line: a calibrated step at 0.9x the feed,
+    its achieved ratio, and the idle % behind it next to the PatchMLP figure."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["PYTHONPATH"] = REPO
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "20", "--warmup", "5",
+                        "--order", "window"], capture_output=True, text=True, timeout=180, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert out["n_gpus"] == 1 and out["value"] > 0 and out["dtype"] == "bf16"
+    p = out["pressure"]
+    assert p and "error" not in p, p
+    assert out["gpu_idle_pct_r090"] == p["gpu_idle_pct"] is not None
+    assert 0.7 < p["ratio_measured"] < 1.1, p  # the step landed near the target ratio
+    assert 0.0 <= p["gpu_idle_pct"] < 20.0
+    assert out["gpu_idle_pct"] is not None  # the PatchMLP phase still runs

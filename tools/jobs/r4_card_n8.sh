@@ -5,7 +5,7 @@
 source tools/gpu_job.sh
 export DDL_BACKEND=gloo
 TR="python -m torch.distributed.run --nnodes=1 --master-addr 127.0.0.1"
-run 200 refetch_test python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_loader_gpu.py -k "refetch or native_dispatch_matches or held_batches"
+run 200 refetch_test python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_loader_gpu.py tests/test_bench_gpu.py -k "refetch or native_dispatch_matches or held_batches or pressure"
 run 400 n8_torchrun $TR --nproc-per-node 8 --master-port 29631 bench.py --gpus 8 --steps 20 --warmup 5 --json-out gpurun_out/n8_torchrun.json
 run 400 n8_self python bench.py --gpus 8 --steps 20 --warmup 5 --json-out gpurun_out/n8_self.json
 run 300 n4_torchrun $TR --nproc-per-node 4 --master-port 29632 bench.py --gpus 4 --steps 20 --warmup 5 --json-out gpurun_out/n4_torchrun.json
