@@ -102,6 +102,8 @@ def parse(argv=None):
     ap.add_argument("--dispatch", default="auto", choices=["auto", "inline", "lookahead", "python"],
                     help="per-batch dispatch: the native engine (auto / inline / lookahead) or the Python path")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--debug-log", action="store_true",
+                    help="slow host iterations of the timed loop and long per-window stager waits in the JSON line")
     return ap.parse_args(argv)
 
 
@@ -404,7 +406,7 @@ def main(argv=None) -> int:
             acc.add(x)
         prod0 = conn.producer_stats()  # diagnostics: read before the region opens
         wait_prod0 = dl.stats().get("stager_wait_producer_s", 0.0)
-        host_log = os.environ.get("DDL_HOST_LOG")
+        host_log = args.debug_log
         ticks = []
         barrier()
         # the region's H2D work, on the GPU clock: events bracket the region on the (idle) compute stream, and
@@ -478,7 +480,7 @@ def main(argv=None) -> int:
         if host_log:  # per-iteration host time of the timed loop (debug): the slow iterations
             dts = [b - a for a, b in zip([t0] + ticks[:-1], ticks)]
             mine["host_iter_ms_slow"] = [(i, round(1e3 * d, 2)) for i, d in enumerate(dts) if d > 0.002]
-        if os.environ.get("DDL_STAGER_LOG") and dl._stager is not None:  # per-window producer waits (debug)
+        if args.debug_log and dl._stager is not None:  # per-window producer waits (debug)
             mine["stager_step_log_us"] = [[e[0]] + [round(x / 1e3, 1) for x in e[1:6]]
                                           for e in dl._stager._native.wait_log if max(e[1:6]) > 500_000]
         # producer side of the timed region: rounds filled, fill rate while filling, busy fraction

@@ -81,6 +81,7 @@ def _parse(argv=None):
                     help="tokens: the consumer reads every tensor of the batch (all) or only input_ids (ids, as "
                          "bench_tokens.py's feed phase)")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--markers", action="store_true", help="roctx markers around each step's fetch (trace_gaps)")
     return ap.parse_args(argv)
 
 
@@ -172,7 +173,7 @@ def main(argv=None) -> int:
     from ddl_amd.utils.tracing import ComputeIdleMeter, trace_range
 
     ratios = [float(x) for x in a.ratios.split(",") if x]
-    host_marks = os.environ.get("DDL_SWEEP_MARKERS", "0") == "1"
+    host_marks = a.markers
     n_steps = a.warmup + 2 * a.feed_steps + len(ratios) * (a.steps + a.warmup + a.tune_passes * a.tune_steps + 30)
     src = None
     if a.family == "tokens":
@@ -261,7 +262,7 @@ def main(argv=None) -> int:
                 t2 = time.perf_counter()
                 with trace_range(f"sweep.p{i:02d}"):
                     for _ in range(a.steps):
-                        if host_marks:  # DDL_SWEEP_MARKERS=1: the host's mark + get per step, for trace_gaps
+                        if host_marks:  # --markers: the host's mark + get per step, for trace_gaps
                             with trace_range("sweep.get"):
                                 batch = next(it)
                         else:

@@ -33,20 +33,10 @@ uint64_t clock_ns() {
 constexpr int kBatchEvents = 16;  // lookahead is 1 batch; a ring this deep never re-records an unwaited event
 constexpr int kFreeEvents = 4;
 
-// Flags of the engine's synchronisation events (batch-ready, free, join). They order work between
-// streams of ONE device; a recorded event's default system-scope release (L2 writeback + invalidate,
-// for host visibility) is more than that needs. DDL_EVENT_SCOPE: "system" (HIP default), "device"
-// (hipEventReleaseToDevice: device-scope release), "nofence" (hipEventDisableSystemFence).
-unsigned event_flags() {
-  static const unsigned flags = [] {
-    const char* v = std::getenv("DDL_EVENT_SCOPE");
-    const std::string s = v == nullptr ? "system" : v;
-    if (s == "device") return static_cast<unsigned>(hipEventDisableTiming | hipEventReleaseToDevice);
-    if (s == "nofence") return static_cast<unsigned>(hipEventDisableTiming | hipEventDisableSystemFence);
-    return static_cast<unsigned>(hipEventDisableTiming);
-  }();
-  return flags;
-}
+// Flags of the engine's synchronisation events (batch-ready, free, join): no timing. Device-scope release
+// (hipEventReleaseToDevice) and no system fence were A/B'd against the default and showed no measured effect
+// (profiles/r3_idle_residual), so the default system-scope release stays.
+unsigned event_flags() { return static_cast<unsigned>(hipEventDisableTiming); }
 
 }  // namespace
 

@@ -189,20 +189,13 @@ bool NativeStager::copy_in_flight(int i, int64_t w) const {
 int NativeStager::pick_copy_stream(int64_t w) const {
   if (copy_stream2_ == nullptr) return 0;
   if (copy_policy_ == 0) return static_cast<int>((w - first_) & 1);  // strict alternation
-  if (copy_policy_ == 2) {
-    // auto: on kRingWaitRun windows in a row the stager waited for a ring buffer while the link went idle, so
-    // the consumer is slower than the link and the feed has slack: one stream (one SDMA engine), which shows a
-    // lower step-boundary idle below the crossover (profiles/r3_copy_policy). Otherwise (loader-bound)
-    // alternate, so two copies overlap and the link never waits for one to end (+2.5% feed). The run length
-    // keeps an isolated wait -- e.g. the one across a benchmark's opening synchronize -- from serialising the
-    // copies after it.
-    return ring_wait_run_ >= kRingWaitRun ? 0 : 1 - last_stream_;
-  }
-  // adaptive (policy 1): stream 0 whenever its last copy has retired. Measured to serialise nearly every copy
-  // on stream 0 at the link rate as well (192 of 199 copies), so it loses the overlap; kept for A/B runs.
-  if (!copy_in_flight(0, w)) return 0;
-  if (!copy_in_flight(1, w)) return 1;
-  return 1 - last_stream_;  // both busy: behind the older copy
+  // auto: on kRingWaitRun windows in a row the stager waited for a ring buffer while the link went idle, so
+  // the consumer is slower than the link and the feed has slack: one stream (one SDMA engine), which shows a
+  // lower step-boundary idle below the crossover (profiles/r3_copy_policy). Otherwise (loader-bound)
+  // alternate, so two copies overlap and the link never waits for one to end (+2.5% feed). The run length
+  // keeps an isolated wait -- e.g. the one across a benchmark's opening synchronize -- from serialising the
+  // copies after it.
+  return ring_wait_run_ >= kRingWaitRun ? 0 : 1 - last_stream_;
 }
 
 void NativeStager::run() {

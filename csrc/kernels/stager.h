@@ -175,16 +175,15 @@ class NativeStager {
   // optional second copy stream: windows alternate between the two, so the next window's copy is
   // already running on another SDMA engine when one finishes (no per-copy gap on the link)
   hipStream_t copy_stream2_;
-  // 0: windows strictly alternate between the two copy streams; 1: adaptive (second stream only while the
-  // first one's copy is in flight); 2 (default): auto, one stream while the stager waits on the consumer for
-  // ring buffers, alternation otherwise (pick_copy_stream)
+  // 0: windows strictly alternate between the two copy streams; 2 (default): auto, one stream while the
+  // stager waits on the consumer for ring buffers, alternation otherwise (pick_copy_stream)
   const int copy_policy_;
+  bool copy_in_flight(int i, int64_t w) const;
   static constexpr int64_t kRingWaitNs = 50000;  // a ring wait longer than this: the consumer held the ring
   static constexpr int kRingWaitRun = 3;  // ... with the link idle, this many windows in a row: consumer-bound
   int ring_wait_run_ = 0;                 // consecutive such windows (stager thread)
   int64_t last_copy_[2] = {-1, -1};  // last window copied on each stream (stager thread only)
   int last_stream_ = 1;
-  bool copy_in_flight(int i, int64_t w) const;
   int pick_copy_stream(int64_t w) const;
   const int device_;
   const std::vector<int32_t> peer_pids_;

@@ -29,7 +29,8 @@ REPO = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(REPO, "csrc")
 BUILD = os.path.join(REPO, "build", "native")
 EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
-ARCH = os.environ.get("DDL_AMD_ARCH", "gfx950")
+ARCH = "gfx950"  # MI355X (CDNA4) only
+VERBOSE = False  # echo the compiler output (``--verbose``)
 
 
 def _hipcc() -> str:
@@ -65,7 +66,7 @@ def _run(cmd: list[str]) -> None:
     if proc.returncode != 0:
         sys.stderr.write(proc.stdout)
         raise RuntimeError(f"native build failed ({proc.returncode}): {' '.join(cmd[:4])} ...")
-    if os.environ.get("DDL_AMD_BUILD_VERBOSE"):
+    if VERBOSE:
         sys.stderr.write(proc.stdout)
 
 
@@ -153,7 +154,10 @@ def main(argv: list[str] | None = None) -> None:
     ap.add_argument("--only", choices=["runtime", "hip"], default=None)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=8)
+    ap.add_argument("-v", "--verbose", action="store_true", help="echo the compiler output")
     a = ap.parse_args(argv)
+    global VERBOSE
+    VERBOSE = a.verbose
     if a.only in (None, "runtime"):
         print(build_runtime(force=a.force))
     if a.only in (None, "hip"):

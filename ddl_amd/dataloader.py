@@ -53,7 +53,7 @@ from .utils import streams
 from .utils.tracing import LoaderMetrics, trace_range
 
 STATE_VERSION = 1
-_TRACE_ENGINE = os.environ.get("DDL_TRACE_ENGINE", "0") == "1"
+_TRACE_ENGINE = os.environ.get("DDL_ROCTX", "1") == "2"  # roctx level 2: also a range per native get
 _FAULT_RANK = bool(os.environ.get("DDL_FAULT_RANK"))  # test hook (utils/faults.py)
 MODES = ("do_not_split_along_epoch", "split_along_epoch", "window", "indexed")
 
@@ -238,9 +238,9 @@ class DistributedDataLoader(DistributedDataloaderABC):
         # GPU's compute is, keeping the link and both copy engines saturated and a growing number of
         # batches alive in HBM. Every `_ahead_every` batches an event goes on the consumer's stream, and
         # fetching batch i waits (on the host) for the event of batch i - max_ahead: the copies then follow
-        # the step's pace when the step is the bottleneck. 0 disables. (`$DDL_MAX_AHEAD`, default 16; off
-        # with the global-shuffle exchange, see _setup_exchange.)
-        ma = int(os.environ.get("DDL_MAX_AHEAD", "16")) if max_ahead is None else int(max_ahead)
+        # the step's pace when the step is the bottleneck. 0 disables. (Default 16; off with the
+        # global-shuffle exchange, see _setup_exchange.)
+        ma = 16 if max_ahead is None else int(max_ahead)
         if ma < 0:
             raise ValueError("max_ahead must be >= 0")
         self.max_ahead = ma
@@ -453,14 +453,13 @@ class DistributedDataLoader(DistributedDataloaderABC):
             self._engine.set_window_mode(True, self._eng_slot_bytes)
         self._engine.inline = mode in ("inline", "window")
         self._engine.set_batches_per_window([int(b) for b in self.batches_per_window])
-        # hand a window's ring buffer back to the stager at its last batch launch (DDL_EARLY_RELEASE=0: at
-        # the consumer's release, one step later -- the round-2 behaviour, for A/B runs)
-        self._engine.early_release = os.environ.get("DDL_EARLY_RELEASE", "1") != "0"
+        # a window's ring buffer goes back to the stager at its last batch launch, one step before the
+        # consumer's release (profiles/r3_early_release); a later out-of-order fetch of that window raises
+        self._engine.early_release = True
         # lookahead batches still pending at get(): the host waits for them (no device-side cross-queue
-        # barrier on the compute stream) unless the exchange is on -- its kernels wait on peer ranks, and
-        # the host must never block on another rank's progress; DDL_HANDOFF=device|host overrides
-        handoff = os.environ.get("DDL_HANDOFF", "auto")
-        self._engine.host_handoff = handoff == "host" or (handoff == "auto" and self._exchange_fn is None)
+        # barrier on the compute stream, profiles/r3_handoff) unless the exchange is on -- its kernels wait
+        # on peer ranks, and the host must never block on another rank's progress
+        self._engine.host_handoff = self._exchange_fn is None
         self._eng_mode = mode
         self._eng_slots: collections.deque = collections.deque()  # (slot id, outputs, block)
         self._eng_next_id = 0
@@ -551,7 +550,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
                 self._ensure_posted(w)
             # the engine's cross-window lookahead reads w + 1: only once its exchange is issued
             nxt = nxt and (w + 1) in posted
-        if _TRACE_ENGINE:  # roctx range per native get (DDL_TRACE_ENGINE=1: host timeline under rocprofv3)
+        if _TRACE_ENGINE:  # roctx range per native get (DDL_ROCTX=2: host timeline under rocprofv3)
             with trace_range("ddl.engine.get"):
                 slot, prod, tags = eng.get(w, local, bpw, nxt, handle, self._timeout_ms)
         else:

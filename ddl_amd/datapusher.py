@@ -222,8 +222,8 @@ def producer_main(pipe, producer_index: int, consumer_pid: int, rank: int, world
         if env_overrides:
             os.environ.update(env_overrides)
         # Producers are host-only: make sure nothing in them can grab the GPU.
-        os.environ["HIP_VISIBLE_DEVICES"] = os.environ.get("DDL_PRODUCER_VISIBLE_DEVICES", "-1")
-        torch.set_num_threads(max(1, int(os.environ.get("DDL_PRODUCER_TORCH_THREADS", "1"))))
+        os.environ["HIP_VISIBLE_DEVICES"] = "-1"  # producers never touch a GPU
+        torch.set_num_threads(1)  # heavy host work runs on the native gather pools, not torch's
     set_role("producer", producer_index)
     from .utils.logging import configure
 

@@ -78,7 +78,7 @@ def warm_copy_engines(device: torch.device, n_engines: int = 4, nbytes: int = 51
     import time
 
     key = (device.type, device.index)
-    if key in _SDMA_WARM or device.type != "cuda" or os.environ.get("DDL_WARM_SDMA", "1") == "0":
+    if key in _SDMA_WARM or device.type != "cuda":
         return 0.0
     _SDMA_WARM.add(key)
     t0 = time.perf_counter()
@@ -94,6 +94,9 @@ def warm_copy_engines(device: torch.device, n_engines: int = 4, nbytes: int = 51
     return time.perf_counter() - t0
 
 
+COPY_POLICY = "auto"  # the stager's default copy-stream policy ("alternate": strict alternation; tests A/B it)
+
+
 class WindowStager:
     """Python face of the native stager (``_ddl_hip.NativeStager``).
 
@@ -103,7 +106,7 @@ class WindowStager:
 
     def __init__(self, connection, n_slots: int, total_windows: int, depth: int, device: torch.device,
                  max_window_bytes: int, post_copy: Callable | None = None, timeout_s: float = 600.0,
-                 first_window: int = 0, meta_bytes: int = 0):
+                 first_window: int = 0, meta_bytes: int = 0, copy_policy: str | None = None):
         if depth < 1:
             raise ValueError("prefetch depth must be >= 1")
         hip, rt = _native.hip(), _native.runtime()
@@ -125,16 +128,16 @@ class WindowStager:
         self.copy_stream = torch.cuda.Stream(device=self.device)
         # two copy streams (two SDMA engines): when copies run back to back the next one is already
         # running when one finishes, so the ~25 us gap per copy on one engine is gone (+1.8-2.5%,
-        # profiles/r2_copy_streams, profiles/r3_copy_policy). DDL_COPY_POLICY=auto (default): alternate
+        # profiles/r2_copy_streams, profiles/r3_copy_policy). copy_policy "auto" (default): alternate
         # while the loader is the bottleneck, one stream while the stager waits on the consumer for ring
-        # buffers (below the crossover one engine shows a lower step-boundary idle); alternate: strict
-        # alternation; adaptive: second stream only while the first copy is in flight (A/B only: it
-        # serialises the copies). DDL_COPY_STREAMS=1: one stream.
+        # buffers (below the crossover one engine shows a lower step-boundary idle); "alternate": strict
+        # alternation. DDL_COPY_STREAMS=1: one stream.
         n_cs = int(os.environ.get("DDL_COPY_STREAMS", "2"))
-        policy = os.environ.get("DDL_COPY_POLICY", "auto")
-        codes = {"alternate": 0, "adaptive": 1, "auto": 2}
-        if policy not in codes:
-            raise ValueError(f"DDL_COPY_POLICY must be one of {sorted(codes)}, not {policy!r}")
+        codes = {"alternate": 0, "auto": 2}
+        copy_policy = copy_policy or COPY_POLICY
+        if copy_policy not in codes:
+            raise ValueError(f"copy_policy must be one of {sorted(codes)}, not {copy_policy!r}")
+        policy = copy_policy
         self.copy_stream2 = torch.cuda.Stream(device=self.device) if n_cs >= 2 else None
         self.stream = torch.cuda.Stream(device=self.device) if post_copy is not None else self.copy_stream
         # The consumer posts window w+1's exchange when it enters window w (the fixed, rank-identical

@@ -158,7 +158,7 @@ def partition_after_spawn(producer_pids: list[int], n_producers: int) -> dict | 
     if os.environ.get("DDL_CPU_PARTITION", "1") == "0" or not producer_pids:
         return None
     mine = os.sched_getaffinity(0)
-    cons, prod = split_consumer_producers(mine, n_producers, int(os.environ.get("DDL_CONSUMER_CPUS", "4")))
+    cons, prod = split_consumer_producers(mine, n_producers)
     if cons == prod:
         return None
     for pid in producer_pids:

@@ -49,17 +49,13 @@ class on_stream:  # noqa: N801  (used like torch.cuda.stream)
 
 
 def batch_stream(device) -> torch.cuda.Stream:
-    """The stream the loader builds batches on, at HIGH priority unless ``DDL_BATCH_STREAM_PRIORITY=normal``.
+    """The stream the loader builds batches on, at HIGH priority.
 
     A batch kernel (gather / cast / collate, tens of microseconds) runs next to the training
     step's GEMMs, which occupy every CU. At normal priority the dispatcher only gets to its
     workgroups when the step's kernels drain, so the next step waits for it; a high-priority
     hardware queue has its workgroups dispatched as soon as any CU frees up.
     """
-    import os
-
-    if os.environ.get("DDL_BATCH_STREAM_PRIORITY", "high") == "normal":
-        return torch.cuda.Stream(device)
     try:
         _, hi = torch.cuda.Stream.priority_range()  # (least, greatest); greatest is the most negative
     except Exception:  # pragma: no cover - older torch

@@ -461,7 +461,7 @@ def test_stager_bytes_in_interval_is_pro_rata_and_additive():
         dl.close()
 
 
-@pytest.mark.parametrize("policy,streams", [("auto", "2"), ("alternate", "2"), ("adaptive", "2"), ("auto", "1")])
+@pytest.mark.parametrize("policy,streams", [("auto", "2"), ("alternate", "2"), ("auto", "1")])
 def test_copy_stream_policies_deliver_identical_batches(monkeypatch, policy, streams):
     """The copy-stream policy only decides which SDMA stream each window copy runs on: every policy (and one
     stream) delivers the same batches, bit for bit, including when the consumer is slow enough for `auto` to
@@ -471,7 +471,9 @@ def test_copy_stream_policies_deliver_identical_batches(monkeypatch, policy, str
     from ddl_amd.models.producers import ImageWindowProducer
 
     def run(pol, n_cs, slow):
-        monkeypatch.setenv("DDL_COPY_POLICY", pol)
+        from ddl_amd import staging
+
+        monkeypatch.setattr(staging, "COPY_POLICY", pol)
         monkeypatch.setenv("DDL_COPY_STREAMS", n_cs)
         out = []
         with ddl_amd.start(n_producers=2) as (env, conn):
@@ -500,9 +502,11 @@ def test_copy_stream_policies_deliver_identical_batches(monkeypatch, policy, str
 def test_copy_policy_rejects_unknown(monkeypatch):
     from ddl_amd.models.producers import ImageWindowProducer
 
-    monkeypatch.setenv("DDL_COPY_POLICY", "round_robin")
+    from ddl_amd import staging
+
+    monkeypatch.setattr(staging, "COPY_POLICY", "adaptive")  # removed in round 4 (it serialised the copies)
     with ddl_amd.start(n_producers=1) as (env, conn):
-        with pytest.raises(ValueError, match="DDL_COPY_POLICY"):
+        with pytest.raises(ValueError, match="copy_policy"):
             ddl_amd.DistributedDataLoader(ImageWindowProducer(16, (3, 8, 8), "bfloat16"), 8, conn, 1, env=env,
                                           device=torch.device("cuda"), out_dtype=torch.bfloat16)
 
