@@ -71,7 +71,8 @@ def parse(argv=None):
     ap.add_argument("--producers", type=int, default=3)
     ap.add_argument("--slots", type=int, default=1, help="windows per producer")
     ap.add_argument("--depth", type=int, default=4,
-                    help="HBM prefetch depth (windows; 4 x 77 MB of HBM): deep enough that the copy engine restarts "
+                    help="HBM prefetch depth (windows; 4 x 77 MB of HBM; the library default): deep enough that the "
+                         "copy engine restarts "
                          "without a gap after the barrier + synchronize that opens the timed region "
                          "(profiles/r3_variance: 20-step spread 176.7-188.1k at depth 2-3, 187.5-188.1k at 4)")
     ap.add_argument("--source-dtype", default="bfloat16", choices=["bfloat16", "uint8", "float32"])

@@ -127,7 +127,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
         shuffle: str = "none",
         seed: int = 0,
         n_slots: int = 1,
-        prefetch_depth: int = 2,
+        prefetch_depth: int = 4,
         mode: str = "window",
         normalize: dict | None = None,
         augment: dict | None = None,
