@@ -18,7 +18,7 @@
 // bilinear tap is an LDS read. The earlier form read each tap straight from
 // global memory: 48 one-byte VMEM instructions per lane for 4 uint8 pixels,
 // which PMC showed to be memory-instruction-issue bound (SQ_WAIT_INST_ANY
-// ~2.6x the active cycles, profiles/r1_augment/). Consecutive lanes write
+// ~2.6x the active cycles, archive/profiles/r1_augment/). Consecutive lanes write
 // consecutive output pixels of each channel plane (8 B / 16 B stores,
 // coalesced). A geometry whose band does not fit the LDS budget runs the same
 // kernel with the taps read from global memory.
@@ -188,7 +188,7 @@ __device__ __forceinline__ void resample_band(void* __restrict__ dst, int64_t im
 // coordinate and both source-row offsets are computed once instead of per
 // pixel, the horizontal offsets once per pixel instead of per tap and channel,
 // and every tap is one add + one LDS read (PMC of the generic form: ~1960 VALU
-// instructions per wave, issue-stalled 44% of its cycles, profiles/r1_augment_v2/).
+// instructions per wave, issue-stalled 44% of its cycles, archive/profiles/r1_augment_v2/).
 // Same float math in the same order as resample_band: bit-identical output.
 template <int OUT_BF16, typename Tin, int HWC, int NC>
 __device__ __forceinline__ void resample_band_rows(void* __restrict__ dst, int64_t img, const AugmentSpec& a,

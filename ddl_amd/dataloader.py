@@ -441,7 +441,7 @@ class DistributedDataLoader(DistributedDataloaderABC):
             # small batches are host-bound: inline (no batch events, ~3 us of C++ per batch), or one launch per
             # window when a window holds several small batches; a large batch kernel (25 us for 256 images) is
             # worth overlapping with the previous step on the batch stream (GPU idle behind a train step 0.17%
-            # lookahead vs 0.71% inline, profiles/r2_native_dispatch)
+            # lookahead vs 0.71% inline, archive/profiles/r2_native_dispatch)
             mode = "inline" if self._eng_slot_bytes < (16 << 20) else "lookahead"
             if mode == "inline" and whole_ok and self._eng_slot_bytes * bpw_max <= (256 << 20):
                 mode = "window"

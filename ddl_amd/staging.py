@@ -68,7 +68,7 @@ def warm_copy_engines(device: torch.device, n_engines: int = 4, nbytes: int = 51
     The HIP runtime spreads back-to-back async copies over the GPU's SDMA engines: each copy goes to
     the lowest-numbered engine that is idle at enqueue time. The FIRST copy an engine runs in a
     process costs the enqueueing thread 6.5-11 ms (engine bring-up, measured with AMD_LOG_LEVEL=4:
-    ``profiles/r2_sdma_warmup``). The stager enqueues copies while earlier ones are still in
+    ``archive/profiles/r2_sdma_warmup``). The stager enqueues copies while earlier ones are still in
     flight, so its 2nd and 3rd engines came up in the middle of a run -- a 6.5 ms stall of the
     stager thread each time, i.e. a hole of ~5 windows of H2D in a short benchmark.
     Here ``n_engines`` copies of ``nbytes`` are enqueued on separate streams back to back, each
