@@ -144,14 +144,31 @@ def build_hip(force: bool = False, jobs: int = 8) -> str:
     return out
 
 
+def build_benchmarks(force: bool = False) -> list[str]:
+    """Standalone gfx950 microbenchmarks (``benchmarks/*.hip`` -> ``benchmarks/bin/``): HIP executables that
+    need no torch, built next to the extensions so the GPU box runs them without compiling."""
+    out = []
+    bin_dir = os.path.join(REPO, "benchmarks", "bin")
+    os.makedirs(bin_dir, exist_ok=True)
+    for src in sorted(glob.glob(os.path.join(REPO, "benchmarks", "*.hip"))):
+        target = os.path.join(bin_dir, os.path.splitext(os.path.basename(src))[0])
+        deps = [src, *glob.glob(os.path.join(CSRC, "kernels", "*.h"))]
+        if force or _newer(target, deps):
+            _run([_hipcc(), "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-I", os.path.join(CSRC, "kernels"),
+                  src, "-o", target])
+        out.append(target)
+    return out
+
+
 def build_all(force: bool = False, jobs: int = 8) -> None:
     build_runtime(force=force)
     build_hip(force=force, jobs=jobs)
+    build_benchmarks(force=force)
 
 
 def main(argv: list[str] | None = None) -> None:
     ap = argparse.ArgumentParser(description=__doc__)
-    ap.add_argument("--only", choices=["runtime", "hip"], default=None)
+    ap.add_argument("--only", choices=["runtime", "hip", "benchmarks"], default=None)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=8)
     ap.add_argument("-v", "--verbose", action="store_true", help="echo the compiler output")
@@ -162,6 +179,8 @@ def main(argv: list[str] | None = None) -> None:
         print(build_runtime(force=a.force))
     if a.only in (None, "hip"):
         print(build_hip(force=a.force, jobs=a.jobs))
+    if a.only in (None, "benchmarks"):
+        print("\n".join(build_benchmarks(force=a.force)))
 
 
 if __name__ == "__main__":

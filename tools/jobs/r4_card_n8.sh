@@ -6,6 +6,8 @@ source tools/gpu_job.sh
 export DDL_BACKEND=gloo
 TR="python -m torch.distributed.run --nnodes=1 --master-addr 127.0.0.1"
 run 200 refetch_test python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_loader_gpu.py tests/test_bench_gpu.py -k "refetch or native_dispatch_matches or held_batches or pressure"
+run 200 socket_dram python benchmarks/probe_socket_dram.py --json-out gpurun_out/socket_dram.json
+run 200 hbm_ceilings benchmarks/bin/hbm_ceilings 4
 run 400 n8_torchrun $TR --nproc-per-node 8 --master-port 29631 bench.py --gpus 8 --steps 20 --warmup 5 --json-out gpurun_out/n8_torchrun.json
 run 400 n8_self python bench.py --gpus 8 --steps 20 --warmup 5 --json-out gpurun_out/n8_self.json
 run 300 n4_torchrun $TR --nproc-per-node 4 --master-port 29632 bench.py --gpus 4 --steps 20 --warmup 5 --json-out gpurun_out/n4_torchrun.json
@@ -13,4 +15,3 @@ run 300 tokens_n4 $TR --nproc-per-node 4 --master-port 29633 benchmarks/bench_to
 run 300 tokens_n8 $TR --nproc-per-node 8 --master-port 29634 benchmarks/bench_tokens.py --steps 40 --warmup 10 --idle-steps 10 --producers 3
 run 300 resident_n4 $TR --nproc-per-node 4 --master-port 29635 benchmarks/bench_resident.py --steps 40 --warmup 10 --depths 2
 run 300 resident_n8 $TR --nproc-per-node 8 --master-port 29636 benchmarks/bench_resident.py --steps 40 --warmup 10 --depths 2
-run 200 socket_dram python benchmarks/probe_socket_dram.py --json-out gpurun_out/socket_dram.json
