@@ -100,6 +100,8 @@ def parse(argv=None):
                          "next to the headline in the JSON line ('indexed')")
     ap.add_argument("--index-samples", type=int, default=4096,
                     help="indexed order: samples in the node-shared synthetic source")
+    ap.add_argument("--index-no-prefault", action="store_true",
+                    help="indexed order: skip the one-word-per-page touch of the mapped source (A/B)")
     ap.add_argument("--dispatch", default="auto", choices=["auto", "inline", "lookahead", "python"],
                     help="per-batch dispatch: the native engine (auto / inline / lookahead) or the Python path")
     ap.add_argument("--json-out", default=None)
@@ -264,7 +266,7 @@ def indexed_phase(args, env, dev, barrier, sync) -> dict:
     try:
         pages = src.page_nodes(64)
         dl = ZeroCopyLoader(src, args.batch * env.world_size, env, seed=args.seed, out_dtype=torch.bfloat16,
-                            device=dev)
+                            device=dev, prefault=not args.index_no_prefault)
 
         def gen():
             while True:
@@ -289,6 +291,7 @@ def indexed_phase(args, env, dev, barrier, sync) -> dict:
             el = float(t.item())
         out = {"order": "indexed (EpochOrder, world-size-invariant), zero-copy gather from a NUMA-local pinned "
                         "bf16 replica of the node-shared source",
+               "prefault_s": dl.stats().get("prefault_s"),
                "value": round(args.batch * args.steps * env.world_size / el, 1), "ms_per_step":
                round(1000 * el / args.steps, 4), "source_samples": n,
                "numa": {"gpu_node": node, "source_pages_on_gpu_node_pct":

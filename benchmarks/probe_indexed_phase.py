@@ -13,12 +13,13 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 
 
-def main() -> int:
+def main(argv=None) -> int:
     import ddl_amd
     from ddl_amd import Marker, ops
     from ddl_amd.models.producers import ImageWindowProducer
 
-    args = bench.parse(["--steps", "200", "--warmup", "20", "--idle-steps", "0"])
+    extra = list(sys.argv[1:] if argv is None else argv)  # e.g. --index-no-prefault
+    args = bench.parse(["--steps", "200", "--warmup", "20", "--idle-steps", "0", *extra])
     res = {}
     with ddl_amd.start(n_producers=args.producers) as (env, conn):
         dev = torch.device(env.device)

@@ -696,6 +696,14 @@ PYBIND11_MODULE(_ddl_hip, m) {
       py::arg("seg_offsets"), py::arg("row_start"), py::arg("row_end"), py::arg("counts"), py::arg("scratch"),
       py::arg("stream"));
   m.def(
+      "touch_pages",
+      [](uintptr_t ptr, int64_t bytes, int64_t page, uintptr_t sink, int blocks, uintptr_t stream) {
+        check_rc(ddl::touch_pages(as_ptr<const void>(ptr), bytes, page, as_ptr<uint32_t>(sink), blocks,
+                                  as_stream(stream)),
+                 "touch_pages");
+      },
+      py::arg("ptr"), py::arg("bytes"), py::arg("page"), py::arg("sink"), py::arg("blocks"), py::arg("stream"));
+  m.def(
       "stream_copy",
       [](uintptr_t src, uintptr_t dst, int64_t bytes, int blocks, uintptr_t stream) {
         check_rc(ddl::stream_copy(as_ptr<const void>(src), as_ptr<void>(dst), bytes, blocks,

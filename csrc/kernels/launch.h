@@ -154,6 +154,9 @@ int bucket_recv(const BucketSpec& sp, int64_t* inv, hipStream_t st);
 constexpr int64_t kChecksumMaxBlocks = 1024;
 // Streaming 16 B copy (bandwidth roofline probe); bytes and both pointers 16 B aligned.
 int stream_copy(const void* src, void* dst, int64_t bytes, int blocks, hipStream_t st);
+// One 4 B read per `page` bytes of [ptr, ptr + bytes) (e.g. a host-mapped source before zero-copy gathers);
+// sink >= blocks u32 (device memory).
+int touch_pages(const void* ptr, int64_t bytes, int64_t page, uint32_t* sink, int blocks, hipStream_t st);
 int checksum_words(const void* ptr, int64_t bytes, uint64_t* out, uint64_t* scratch, int64_t scratch_len,
                    hipStream_t st);
 // Streaming form: partials[b] += block b's share (grid = n_partials, fixed for the

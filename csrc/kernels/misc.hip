@@ -229,6 +229,37 @@ int stream_copy(const void* src, void* dst, int64_t bytes, int blocks, hipStream
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+namespace {
+// One 4-byte read per page of a (host-mapped) range: every page's GPU-side translation is exercised once, so a
+// zero-copy gather's first pass over the source does not pay for it (bench.py's indexed phase ran 162k samples/s
+// on its first pass in a process, 188k afterwards: archive/profiles/r3_s2_final2). The xor of the words goes to
+// sink[block] through a plain vector store, so the loads cannot be dropped.
+__global__ void __launch_bounds__(kThreads) touch_pages_kernel(const uint8_t* __restrict__ p, int64_t n_pages,
+                                                               int64_t page, uint32_t* __restrict__ sink) {
+  uint32_t acc = 0;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < n_pages; i += stride)
+    acc ^= *reinterpret_cast<const uint32_t*>(p + i * page);
+  __shared__ uint32_t red[kThreads];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = kThreads / 2; o > 0; o >>= 1) {
+    if (static_cast<int>(threadIdx.x) < o) red[threadIdx.x] ^= red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) sink[blockIdx.x] = red[0];
+}
+}  // namespace
+
+int touch_pages(const void* ptr, int64_t bytes, int64_t page, uint32_t* sink, int blocks, hipStream_t st) {
+  if (bytes <= 0) return 0;
+  if (page < 4 || page % 4 != 0 || reinterpret_cast<uintptr_t>(ptr) % 4 != 0 || blocks < 1) return -2;
+  const int64_t n_pages = (bytes - 4) / page + 1;  // every page start inside [ptr, ptr + bytes - 4]
+  hipLaunchKernelGGL(touch_pages_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(kThreads), 0, st,
+                     static_cast<const uint8_t*>(ptr), n_pages, page, sink);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int checksum_words(const void* ptr, int64_t bytes, uint64_t* out, uint64_t* scratch, int64_t scratch_len,
                    hipStream_t st) {
   if (bytes <= 0) return 0;

@@ -48,4 +48,23 @@ def test_zerocopy_gpu_matches_reference(max_blocks, prep_streams, dtype):
         s = torch.tensor(norm["std"]).view(1, 3, 1, 1)
         ref = (ref / 255 - m) / s
     torch.testing.assert_close(got, ref.to(torch.bfloat16).float(), rtol=1e-2, atol=2e-2)
+    assert dl.stats()["prefault_s"] > 0  # every page of the mapped source was touched once before batch 0
     dl.close()
+
+
+@pytest.mark.gpu
+def test_touch_pages_reads_every_page():
+    """touch_pages: one 4 B read per page; the per-block xor of the words lands in the sink (the loads are real)."""
+    from ddl_amd import _native
+
+    page, n_pages = 4096, 1000
+    host = torch.zeros(n_pages * page // 4, dtype=torch.int32).pin_memory()
+    host.view(n_pages, page // 4)[:, 0] = torch.arange(1, n_pages + 1, dtype=torch.int32)
+    hip = _native.hip()
+    sink = torch.zeros(1, dtype=torch.int32, device="cuda")
+    hip.touch_pages(hip.host_device_pointer(host.data_ptr()), host.numel() * 4, page, sink.data_ptr(), 1,
+                    torch.cuda.current_stream().cuda_stream)
+    want = 0
+    for i in range(1, n_pages + 1):
+        want ^= i
+    assert int(sink.item()) == want

@@ -15,3 +15,5 @@ run 300 tokens_n4 $TR --nproc-per-node 4 --master-port 29633 benchmarks/bench_to
 run 300 tokens_n8 $TR --nproc-per-node 8 --master-port 29634 benchmarks/bench_tokens.py --steps 40 --warmup 10 --idle-steps 10 --producers 3
 run 300 resident_n4 $TR --nproc-per-node 4 --master-port 29635 benchmarks/bench_resident.py --steps 40 --warmup 10 --depths 2
 run 300 resident_n8 $TR --nproc-per-node 8 --master-port 29636 benchmarks/bench_resident.py --steps 40 --warmup 10 --depths 2
+run 300 indexed_probe_prefault python benchmarks/probe_indexed_phase.py
+run 300 indexed_probe_noprefault python benchmarks/probe_indexed_phase.py --index-no-prefault
