@@ -42,18 +42,18 @@ from typing import Any, Iterator
 import torch
 
 from . import ops
+from .checkpoint import STATE_VERSION, CheckpointMixin  # noqa: F401  (STATE_VERSION: public name)
 from .connection import Connection
+from .engine_dispatch import _TRACE_ENGINE, NativeDispatchMixin  # noqa: F401
 from .datasetwrapper import ProducerFunctionSkeleton
 from .exceptions import ShapeMismatchError
 from .ops import _dtypes
-from .permutation import FeistelPermutation, batch_cursor
+from .permutation import FeistelPermutation
 from .types import DDLEnv, Marker, MetaData_Consumer_To_Producer, MetaData_Producer_To_Consumer
 from .utils.logging import for_all_methods, with_logging
 from .utils import streams
 from .utils.tracing import LoaderMetrics, trace_range
 
-STATE_VERSION = 1
-_TRACE_ENGINE = os.environ.get("DDL_ROCTX", "1") == "2"  # roctx level 2: also a range per native get
 _FAULT_RANK = bool(os.environ.get("DDL_FAULT_RANK"))  # test hook (utils/faults.py)
 MODES = ("do_not_split_along_epoch", "split_along_epoch", "window", "indexed")
 
@@ -110,7 +110,7 @@ class DistributedDataloaderABC(ABC):
                                         "_engine_provide", "_release_window", "_advance_window",
                                         "_advance_to_next_producer", "_begin_window", "_update_len",
                                         "_end_access_epoch", "_device_batch", "_enqueue_batch"])
-class DistributedDataLoader(DistributedDataloaderABC):
+class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDataloaderABC):
     def __init__(
         self,
         producer_function: ProducerFunctionSkeleton,
@@ -330,270 +330,6 @@ class DistributedDataLoader(DistributedDataloaderABC):
                 self._make_engine()
         self._update_len()
 
-    # ------------------------------------------------------ native dispatch
-    def _engine_recipe(self) -> dict | None:
-        """The batch recipe when the native engine can build batches exactly like ``_batch_from_window``:
-        a fused gather (one output), a contiguous column split or a token pad/pack; no HWC collate or
-        augment. The global-shuffle exchange is compatible: it rewrites the staged window in place on the
-        post-copy stream before the window's ready event, which is what the engine's launches wait on
-        (``_ensure_posted`` issues it before the engine touches the window)."""
-        if not self.native_dispatch or self.augment is not None or self._batch_stream is None:
-            return None
-        if self.collate == "tokens":
-            return self._token_recipe()
-        if self.collate is not None:
-            return None
-        norm = self.normalize
-        if norm is not None and norm.get("layout", "chw") == "hwc":
-            return None
-        wdt = self.window_dtype
-        out_dtype = self.out_dtype or (torch.float32 if norm is not None else wdt)
-        splits = list(self.splits[0])
-        rec = dict(in_dt=_dtypes.code(wdt), out_dt=_dtypes.code(out_dtype), shuffle=self.shuffle == "device",
-                   batch=self.batch_size, seed=self.seed & ((1 << 64) - 1), max_blocks=0, scale=[], bias=[],
-                   plane=0, n_data=[int(x.nData) for x in self.metadata_from_producer], widths=[])
-        if (self.contiguous or self.copy_batches) and len(splits) > 1 and len(self.sample_shape) == 1 \
-                and norm is None:
-            if out_dtype != wdt and out_dtype not in (torch.bfloat16, torch.float32):
-                return None
-            rec.update(kind=1, row_elems=int(self.sample_shape[0]), widths=[int(w) for w in splits],
-                       out_shapes=[(self.batch_size, int(w)) for w in splits], out_dtype=out_dtype)
-            return rec
-        if len(splits) != 1:
-            return None  # gather + split views: Python path
-        if self.shuffle != "device" and out_dtype == wdt and norm is None and not self.copy_batches:
-            return None  # zero-copy view of the window
-        if out_dtype != wdt and (out_dtype not in (torch.bfloat16, torch.float16, torch.float32)
-                                 or wdt not in (torch.uint8, torch.float32, torch.bfloat16, torch.float16)):
-            return None  # a conversion the gather kernel does not do: the Python path reports it
-        if norm is not None:
-            plane = int(math.prod(self.sample_shape[1:])) if len(self.sample_shape) > 1 else 1
-            c = self.sample_shape[0] if len(self.sample_shape) > 1 else len(norm.get("mean", [0]))
-            sc, bi = ops.norm_affine(c, norm.get("mean"), norm.get("std"), norm.get("scale"), norm.get("bias"),
-                                     ops.pixel_max(wdt))
-            if out_dtype in (torch.uint8, torch.int32, torch.int64):
-                return None
-            rec.update(scale=[float(x) for x in sc], bias=[float(x) for x in bi], plane=plane)
-        rec.update(kind=0, row_elems=int(math.prod(self.sample_shape)) if self.sample_shape else 1,
-                   out_shapes=[(self.batch_size,) + tuple(self.sample_shape)], out_dtype=out_dtype)
-        return rec
-
-    def _token_recipe(self) -> dict | None:
-        """Token windows (models/tokens.py): the pad/pack kernel straight from the staged window."""
-        from .models.tokens import TokenWindowLayout
-
-        ex = [m.extra for m in self.metadata_from_producer]
-        if any(e.get("token_layout") != ex[0].get("token_layout") or e.get("token_mode") != ex[0].get("token_mode")
-               for e in ex):
-            return None
-        lay = TokenWindowLayout(**ex[0]["token_layout"])
-        mode = ex[0]["token_mode"]
-        reg = lay.regions()
-        S = lay.seq_len
-        rows = lay.batch if mode == "pad" else lay.max_segments
-        outs = [((rows, S), torch.int32), ((rows, S), torch.uint8), ((rows, S), torch.int64)]
-        if mode == "pack":
-            outs += [((rows, S), torch.int32), ((lay.max_segments + 1,), torch.int32)]
-        fill = lay.max_segments if (mode == "pack" and self.token_rows == "fixed") else 0
-        token = [0 if mode == "pad" else 1, int(self.pad_id), S, reg["offsets"][0], reg["row_start"][0],
-                 reg["row_end"][0], reg["seg_offsets"][0], reg["tokens"][0], lay.header_stride, fill, lay.token_bytes]
-        return dict(kind=2, in_dt=_dtypes.code(torch.int32), out_dt=_dtypes.code(torch.int32), shuffle=False,
-                    batch=lay.batch, row_elems=1, seed=0, max_blocks=0, scale=[], bias=[], plane=0,
-                    n_data=[int(x.nData) for x in self.metadata_from_producer], widths=[], token=token,
-                    outputs=outs, token_mode=mode)
-
-    def _make_engine(self) -> None:
-        rec = self._engine_recipe()
-        if rec is None:
-            self._engine = None
-            return
-        import collections
-
-        from . import _native
-
-        st = self._stager
-        if "outputs" in rec:
-            self._eng_outputs = rec.pop("outputs")
-        else:
-            dt = rec.pop("out_dtype")
-            self._eng_outputs = [(sh, dt) for sh in rec.pop("out_shapes")]
-        self._eng_tokens = rec.pop("token_mode", None)
-        self._engine = _native.hip().BatchEngine(
-            st._native, n_producers=self.connection.n_producers, buffers=[b.data_ptr() for b in st.buffers],
-            ready=[e.cuda_event for e in st.ready_events], batch_stream=self._batch_stream.cuda_stream,
-            device=self.device.index, **rec)
-        # byte layout of one slot: every output 256-byte aligned, in order (a block holds K slots back to back)
-        self._eng_layout, size = [], 0
-        for sh, dt in self._eng_outputs:
-            self._eng_layout.append((sh, dt, size))
-            size += -(-math.prod(sh) * _dtypes.itemsize(dt) // 256) * 256
-        self._eng_slot_bytes = max(256, size)
-        self._eng_block = int(min(128, max(4, (512 << 20) // self._eng_slot_bytes)))
-        mode = self.native_dispatch
-        bpw_max = max(self.batches_per_window)
-        # whole-window launches: every window holds >= 2 batches, and consecutive slots of a block are one
-        # contiguous run per output where the kernel needs that (gather: no slot padding; split takes a slot
-        # stride; token windows get one pad/pack launch with a grid row per sub-batch)
-        whole_ok = (min(self.batches_per_window) > 1
-                    and (rec["kind"] != 0 or self._eng_slot_bytes == math.prod(self._eng_outputs[0][0])
-                         * _dtypes.itemsize(self._eng_outputs[0][1])))
-        if mode == "auto":
-            # small batches are host-bound: inline (no batch events, ~3 us of C++ per batch), or one launch per
-            # window when a window holds several small batches; a large batch kernel (25 us for 256 images) is
-            # worth overlapping with the previous step on the batch stream (GPU idle behind a train step 0.17%
-            # lookahead vs 0.71% inline, archive/profiles/r2_native_dispatch)
-            mode = "inline" if self._eng_slot_bytes < (16 << 20) else "lookahead"
-            if mode == "inline" and whole_ok and self._eng_slot_bytes * bpw_max <= (256 << 20):
-                mode = "window"
-        if mode == "window" and not whole_ok:
-            mode = "inline"
-        self._eng_whole = mode == "window"
-        if self._eng_whole:
-            self._eng_block = max(self._eng_block, bpw_max)  # a window's slots come from one block
-            self._engine.set_window_mode(True, self._eng_slot_bytes)
-        self._engine.inline = mode in ("inline", "window")
-        self._engine.set_batches_per_window([int(b) for b in self.batches_per_window])
-        # a window's ring buffer goes back to the stager at its last batch launch, one step before the
-        # consumer's release (profiles/r3_early_release); a later out-of-order fetch of that window raises
-        self._engine.early_release = True
-        # lookahead batches still pending at get(): the host waits for them (no device-side cross-queue
-        # barrier on the compute stream, profiles/r3_handoff) unless the exchange is on -- its kernels wait
-        # on peer ranks, and the host must never block on another rank's progress
-        self._engine.host_handoff = self._exchange_fn is None
-        self._eng_mode = mode
-        self._eng_slots: collections.deque = collections.deque()  # (slot id, outputs, block)
-        self._eng_next_id = 0
-        self._eng_rec = (None, None)  # (block, stream) of the last record_stream
-        self._eng_window = None
-        self._eng_given: dict = {}  # local batch -> (outputs, block, tags) of the current window (re-fetch)
-        self._eng_spare: dict = {}  # whole-window mode: slot id -> (outputs, block) built but not yet fetched
-        self._eng_streams: dict = {}  # torch stream id -> (Stream, raw hipStream_t)
-        self._eng_budget = 0
-        # the first blocks are allocated up front, outside any timed loop: >= 24 slots, so that in steady
-        # state every new block reuses a freed one from the caching allocator (no hipMalloc per block)
-        for _ in range(max(2, -(-24 // self._eng_block))):
-            self._engine_provide()
-
-    def _engine_provide(self) -> None:
-        """One allocation (on the batch stream) for a block of output slots; each slot is used once.
-        The K slots' views of an output come from ONE strided view + ``unbind`` (per-slot slicing cost
-        ~9 us per batch of host time on the box: three tensor ops per output per slot)."""
-        K = self._eng_block
-        with streams.on_stream(self._batch_stream), trace_range("ddl.engine.provide"):
-            block = torch.empty(K * self._eng_slot_bytes, dtype=torch.uint8, device=self.device)
-        base, sb, per_group, ptrs = block.data_ptr(), self._eng_slot_bytes, [], [[] for _ in range(K)]
-        for sh, dt, off in self._eng_layout:
-            isz = _dtypes.itemsize(dt)
-            inner = [1] * len(sh)
-            for d in range(len(sh) - 2, -1, -1):
-                inner[d] = inner[d + 1] * sh[d + 1]
-            per_group.append(block[off:].view(dt).as_strided((K,) + tuple(sh), (sb // isz,) + tuple(inner)).unbind(0))
-            for k in range(K):
-                ptrs[k].append(base + k * sb + off)
-        first = self._eng_next_id
-        self._eng_slots.extend(zip(range(first, first + K), zip(*per_group), [block] * K))
-        self._eng_next_id += K
-        self._engine.provide(ptrs)
-
-    def _engine_raise(self, code: int, producer: int, what: str) -> None:
-        from .exceptions import DDLError, DDLTimeoutError, PeerDeathError, ShutdownError
-
-        if code <= -10:
-            rc = -code - 10
-            if rc == 1:
-                raise ShutdownError(f"{what}: loader was shut down")
-            if rc == 2:
-                raise DDLTimeoutError(f"{what}: not staged within {self.timeout_s:.0f}s (producer {producer})")
-            pids = self.connection.producer_pids
-            pid = pids[producer] if 0 <= producer < len(pids) else None
-            if rc in (3, 4):
-                raise PeerDeathError(f"{what}: producer {producer} (pid {pid}) "
-                                     + ("reported a failure" if rc == 4 else "died"), producer, pid)
-            raise DDLError(f"{what}: {self._stager._native.error()}")
-        if code == -3:
-            raise DDLError(f"{what}: requested out of order after the window's last batch -- a window goes back "
-                           "to the prefetcher when its last batch is launched; within a window, fetch batches "
-                           "in order (a batch already fetched can be fetched again)")
-        raise DDLError(f"{what}: native batch engine error {code}")
-
-    def _engine_batch(self, local: int, bpw: int):
-        eng = self._engine
-        if self._eng_whole:
-            if local == 0:  # the window's bpw slots, after at most the skipped tail of a block
-                while eng.slots_left < bpw + self._eng_block:
-                    self._engine_provide()
-        else:
-            self._eng_budget -= 2  # a get takes at most 2 slots (the batch + a lookahead): query only when low
-            if self._eng_budget < 4:
-                if eng.slots_left < 4:
-                    self._engine_provide()
-                self._eng_budget = eng.slots_left
-        sid = torch._C._cuda_getCurrentStream(self.device.index)
-        hit = self._eng_streams.get(sid)
-        if hit is None:
-            st = streams.current(self.device.index)
-            hit = self._eng_streams[sid] = (st, st.cuda_stream)
-        cur, handle = hit
-        w = self.window
-        if self._eng_window == w:
-            again = self._eng_given.get(local)
-            if again is not None:  # fetched before in this window: the same outputs (slots are used once)
-                out, block, tags = again
-                if self._eng_rec[0] is not block or self._eng_rec[1] is not cur:
-                    block.record_stream(cur)
-                    self._eng_rec = (block, cur)
-                return self._engine_outputs(out, tags)
-        nxt = self.window_in_epoch + 1 < self.windows_per_epoch or self.epoch + 1 < self.n_epochs
-        if self._exchange_fn is not None:
-            posted = self._stager._posted
-            if w not in posted or (w + 1) not in posted:
-                self._ensure_posted(w)
-            # the engine's cross-window lookahead reads w + 1: only once its exchange is issued
-            nxt = nxt and (w + 1) in posted
-        if _TRACE_ENGINE:  # roctx range per native get (DDL_ROCTX=2: host timeline under rocprofv3)
-            with trace_range("ddl.engine.get"):
-                slot, prod, tags = eng.get(w, local, bpw, nxt, handle, self._timeout_ms)
-        else:
-            slot, prod, tags = eng.get(w, local, bpw, nxt, handle, self._timeout_ms)
-        if slot < 0:
-            self._engine_raise(slot, prod, f"batch {local} of window {w}")
-        if local == 0 and self._verify is not None:
-            self._verify_window(w, tags)
-        if self._eng_window != w:
-            self._eng_window = w
-            self._eng_given.clear()
-            self._eng_spare.clear()
-            self.metrics.windows += 1
-        spare = self._eng_spare.pop(slot, None) if self._eng_spare else None
-        if spare is not None:  # whole-window mode: a batch of this window fetched after a later one
-            out, block = spare
-        else:
-            q = self._eng_slots
-            while q[0][0] != slot:  # slots the engine skipped (dropped lookahead; whole-window: fetched later)
-                sid, o, b = q.popleft()
-                if self._eng_whole:
-                    self._eng_spare[sid] = (o, b)
-            _, out, block = q.popleft()
-        self._eng_given[local] = (out, block, tags)
-        if self._eng_rec[0] is not block or self._eng_rec[1] is not cur:
-            block.record_stream(cur)  # the compute stream uses this block from now on
-            self._eng_rec = (block, cur)
-        return self._engine_outputs(out, tags)
-
-    def _engine_outputs(self, out, tags):
-        if self._eng_tokens is None:
-            return out
-        n_tokens, n_rows, n_seg, max_seg = tags
-        if self._eng_tokens == "pad":
-            return {"input_ids": out[0], "attention_mask": out[1], "position_ids": out[2], "n_tokens": n_tokens}
-        if n_tokens > 0x7FFFFFFF:
-            raise ValueError(f"{n_tokens} tokens in one batch overflow int32 cu_seqlens")
-        if self.token_rows == "fixed":
-            return {"input_ids": out[0], "attention_mask": out[1], "position_ids": out[2], "segment_ids": out[3],
-                    "cu_seqlens": out[4][:n_seg + 1], "max_seqlen": max_seg, "n_tokens": n_tokens, "n_rows": n_rows}
-        return {"input_ids": out[0][:n_rows], "attention_mask": out[1][:n_rows], "position_ids": out[2][:n_rows],
-                "segment_ids": out[3][:n_rows], "cu_seqlens": out[4][:n_seg + 1], "max_seqlen": max_seg,
-                "n_tokens": n_tokens}
 
     # --------------------------------------------------------------- schedule
     def _schedule(self, w: int) -> tuple[int, int]:
@@ -1054,210 +790,9 @@ class DistributedDataLoader(DistributedDataloaderABC):
             self._update_len()
             self._begin_window()
 
-    def set_epoch(self, epoch: int) -> None:
-        """torch-style ``sampler.set_epoch``: position the loader at the START of ``epoch``.
-
-        A no-op when the cursor is already there (the usual ``for e in range(n): dl.set_epoch(e)``
-        loop); otherwise a live seek (producers repositioned, staging restarted), so batches and
-        their order are exactly those of ``epoch`` in an uninterrupted run. Called mid-epoch for
-        the current epoch, it restarts that epoch.
-        """
-        epoch = int(epoch)
-        if epoch == self.epoch and self.epoch_batch == 0 and not self._pending:
-            return
-        if not 0 <= epoch < self.n_epochs:
-            raise ValueError(f"epoch {epoch} outside [0, {self.n_epochs})")
-        if self.connection is None or self.connection.n_producers == 0:
-            self.epoch = epoch
-            return
-        if self.mode == "indexed" or self.mode == "split_along_epoch" or self.mode == "do_not_split_along_epoch":
-            w = epoch * self.windows_per_epoch
-            self._seek(window=w, window_in_epoch=0, epoch=epoch, batch=0, epoch_batch=0)
-
     def _can_continue(self) -> bool:
         return self.epoch < self.n_epochs
 
-    # ------------------------------------------------------------ checkpoint
-    def state_dict(self) -> dict:
-        """Checkpointable cursor. A batch already handed out by the auto-marking
-        iterator counts as consumed (resume continues with the next one).
-
-        ``kind="indexed"`` (world-size-invariant order): ``(seed, epoch,
-        global_batch_cursor)`` + the order's geometry -- resumable at ANY world
-        size with the same global batch. ``kind="window"``: epoch / window /
-        batch cursor of the producer-window schedule (same layout required).
-        """
-        consumed = self.epoch_batch + (1 if self._pending else 0)
-        base = {
-            "version": STATE_VERSION,
-            "seed": self.seed,
-            "epoch": self.epoch,
-            "batch_size": self.batch_size,
-            "world_size": self.env.world_size if self.env else self.n_instances,
-            "dtype": str(self.out_dtype or getattr(self, "window_dtype", torch.float32)).replace("torch.", ""),
-            "shuffle": self.shuffle,
-            "fraction_exchange": self.fraction_exchange,
-        }
-        if self.mode == "indexed":
-            extra = self.metadata_from_producer[0].extra if self.metadata_from_producer else {}
-            k = self.batches_per_window[0] if self.batches_per_window else 1
-            base.update({
-                "kind": "indexed",
-                "global_batch_cursor": consumed,
-                # the same position in samples of the epoch order (the epoch/sample-index format)
-                "global_sample_cursor": consumed * int(extra.get("global_batch") or 0),
-                "batches_per_epoch": self.windows_per_epoch * k,
-                "batches_per_window": k,
-                "global_batch": extra.get("global_batch"),
-                "n_samples": extra.get("n_samples"),
-                "order_seed": extra.get("order_seed"),
-                "drop_last": extra.get("order_drop_last"),
-            })
-            return base
-        base.update({
-            "kind": "window",
-            "mode": self.mode,
-            "window": self.window,
-            "window_in_epoch": self.window_in_epoch,
-            "batch": self.batch + (1 if self._pending else 0),
-            "epoch_batch": consumed,
-            "n_producers": self.connection.n_producers if self.connection else 0,
-            "n_slots": self.n_slots,
-        })
-        return base
-
-    def _apply_state(self, sd: dict) -> None:
-        if sd.get("version") != STATE_VERSION:
-            raise ValueError(f"unsupported loader state version {sd.get('version')}")
-        self.epoch = int(sd["epoch"])
-        if sd.get("seed") is not None:
-            self.seed = int(sd["seed"])
-        if sd.get("kind") == "indexed":
-            bpe = int(sd["batches_per_epoch"])
-            k = int(sd.get("batches_per_window", 1))  # global batches per window (token windows)
-            cur = batch_cursor(sd, sd.get("global_batch"))
-            if cur >= bpe:
-                self.epoch, cur = self.epoch + 1, 0
-            self.window = self.epoch * (bpe // k) + cur // k
-            self.window_in_epoch = cur // k
-            self.epoch_batch = cur
-            self.batch = cur % k
-            self._resume_check = sd
-            return
-        # exact resume, also mid-window: the producers restart at this window's round
-        # (deterministic content per round) and the cursor skips its consumed batches
-        self._resume_window_sd = sd
-        self.window = int(sd["window"])
-        self.window_in_epoch = int(sd["window_in_epoch"])
-        self.batch = int(sd.get("batch", 0))
-        self.epoch_batch = int(sd.get("epoch_batch", 0))
-
-    def load_state_dict(self, sd: dict) -> None:
-        """Restore a ``state_dict()`` on a LIVE loader (torch ``DataLoader``/``StatefulDataLoader`` style).
-
-        The staging ring is drained, the producers are repositioned to the checkpointed rounds
-        (``Connection.seek_producers``) and the cursor is rebuilt, so the next batch is exactly
-        the one an uninterrupted run would deliver after the checkpoint -- also mid-window, and
-        for ``kind="indexed"`` at a different world size (same global batch). Every rank of a
-        multi-rank job must call it at the same point (its exchange collectives restart from the
-        checkpointed window). Equivalent to constructing with ``resume_state=sd``.
-        """
-        if self._finalized:
-            raise RuntimeError("load_state_dict on a finished loader: construct a new one with resume_state=")
-        saved = (self.epoch, self.seed, self.window, self.window_in_epoch, self.batch, self.epoch_batch)
-        self._apply_state(sd)
-        try:
-            if self.connection is not None and self.connection.n_producers:
-                self._check_resume_layout(self.connection.n_producers)
-                if self.mode == "indexed":
-                    self._check_indexed_resume()
-        except Exception:
-            (self.epoch, self.seed, self.window, self.window_in_epoch, self.batch, self.epoch_batch) = saved
-            raise
-        if self.connection is None or self.connection.n_producers == 0:
-            return
-        self._seek(self.window, self.window_in_epoch, self.epoch, self.batch, self.epoch_batch)
-
-    def _check_resume_layout(self, n_producers: int) -> None:
-        """Window-kind checkpoints name producer rounds: the producer count must match (the slot
-        count may change -- content is a function of (producer, round), not of the slot)."""
-        sd = getattr(self, "_resume_window_sd", None)
-        if sd is None:
-            return
-        if int(sd.get("n_producers", n_producers)) != n_producers:
-            raise ShapeMismatchError((sd.get("n_producers"), n_producers),
-                                     f"window-kind checkpoint of {sd.get('n_producers')} producers cannot resume "
-                                     f"with {n_producers}: windows are (producer, round) pairs; use mode='indexed' "
-                                     "for a layout-independent order")
-        if sd.get("mode", self.mode) != self.mode:
-            raise ShapeMismatchError((sd.get("mode"), self.mode), "checkpoint window mode differs")
-
-    def _check_indexed_resume(self) -> None:
-        chk = getattr(self, "_resume_check", None)
-        if chk is None or not self.metadata_from_producer:
-            return
-        ex = self.metadata_from_producer[0].extra
-        dl_ck, dl_now = chk.get("drop_last"), ex.get("order_drop_last")
-        if dl_ck is not None and dl_now is not None and bool(dl_ck) != bool(dl_now):
-            raise ShapeMismatchError(("drop_last", dl_ck, dl_now),
-                                     f"checkpoint was saved with drop_last={bool(dl_ck)}, this loader has "
-                                     f"drop_last={bool(dl_now)} (the epoch has a different number of batches; "
-                                     "note ddl_amd.DataLoader's default is drop_last=False since round 3)")
-        for key in ("global_batch", "n_samples", "order_seed"):
-            if chk.get(key) is not None and ex.get(key) is not None and chk[key] != ex[key]:
-                raise ShapeMismatchError((key, chk[key], ex[key]),
-                                         f"checkpoint {key}={chk[key]} does not match the producers' {ex[key]}")
-        k = self.batches_per_window[0]
-        if int(chk["batches_per_epoch"]) != self.windows_per_epoch * k:
-            raise ShapeMismatchError(chk, "checkpoint batches_per_epoch does not match")
-        if int(chk.get("batches_per_window", 1)) != k:
-            raise ShapeMismatchError((chk.get("batches_per_window", 1), k),
-                                     "checkpoint batches_per_window differs from the producers' (the window "
-                                     "cursor would not map to the same global batches)")
-
-    def _seek(self, window: int, window_in_epoch: int, epoch: int, batch: int, epoch_batch: int) -> None:
-        """Live reposition: drain staging, move the producers, rebuild the cursor and the stager."""
-        if epoch >= self.n_epochs:
-            raise ValueError(f"cannot seek to epoch {epoch} of a {self.n_epochs}-epoch loader")
-        P = self.connection.n_producers
-        with trace_range("ddl.consumer.seek"):
-            # 1. stop every reader of the slots / ring buffers
-            if self._batch_stream is not None:
-                self._lookahead.clear()
-                self._win_done.clear()
-                self._batch_stream.synchronize()
-            if self._stager is not None:
-                self._stager.close()  # joins the native thread; copies and their slot hand-backs retire
-                self._drop_engine()
-            elif self._host_window is not None:
-                self._host_window = None  # seek_producers resets every slot, this one included
-            self._cur = None
-            self._pending = False
-            # 2. cursor
-            self.window, self.window_in_epoch, self.epoch = int(window), int(window_in_epoch), int(epoch)
-            self.batch, self.epoch_batch = int(batch), int(epoch_batch)
-            self.target_rank = self.window % P + 1
-            # 3. producers continue at the rounds of the new window schedule
-            self.connection.seek_producers([self._first_round(p, P, self.window) for p in range(P)])
-            # 4. a fresh staging ring starting at the new window
-            self.total_windows = self.n_epochs * self.windows_per_epoch - self.window
-            if self._stager is not None:
-                from .staging import WindowStager
-
-                old = self._stager
-                self.connection.remove_finalizer(old.close)
-                self._stager = WindowStager(self.connection, self.n_slots, self.total_windows, self.prefetch_depth,
-                                            self.device, old.max_window_bytes, post_copy=self._exchange_fn,
-                                            timeout_s=self.timeout_s, first_window=self.window,
-                                            meta_bytes=old.meta_bytes)
-                self.connection.add_finalizer(self._stager.close)
-                self.metrics.bytes_h2d += old.bytes_h2d
-                del old
-                if self._batch_stream is not None:
-                    self._make_engine()
-            self._update_len()
-            if self.batch == 0:
-                self._begin_window()
 
     # --------------------------------------------------------------- teardown
     def _finalize(self) -> None:
