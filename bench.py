@@ -69,7 +69,8 @@ def parse(argv=None):
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
     ap.add_argument("--window", type=int, default=256, help="samples per producer window")
     ap.add_argument("--producers", type=int, default=3)
-    ap.add_argument("--slots", type=int, default=1, help="windows per producer")
+    ap.add_argument("--slots", type=int, default=None,
+                    help="windows per producer (default: the producer's preferred_slots: 1, or 2 with --refill full)")
     ap.add_argument("--depth", type=int, default=4,
                     help="HBM prefetch depth (windows; 4 x 77 MB of HBM; the library default): deep enough that the "
                          "copy engine restarts "
@@ -80,7 +81,8 @@ def parse(argv=None):
                     help="producer work per round: stamp = one element per sample; full = rewrite every byte of "
                          "the window (a row permutation of the pristine window, as the reference's producers "
                          "shuffle theirs every round) with --producer-threads native host threads each")
-    ap.add_argument("--producer-threads", type=int, default=4)
+    ap.add_argument("--producer-threads", type=int, default=None,
+                    help="host threads per producer for --refill full (default 8; 4 for the cheap refills)")
     ap.add_argument("--shuffle", default="device", choices=["device", "none"])
     ap.add_argument("--exchange", type=float, default=None,
                     help="global-shuffle fraction per window over RCCL (default 0.5 when N>1, as the reference "
@@ -583,6 +585,8 @@ def main(argv=None) -> int:
                     "exchange_method": args.exchange_method if args.exchange > 0 else None,
                     "source_dtype": args.source_dtype,
                     "producer_refill": args.refill,
+                    "producer_slots": dl.n_slots,
+                    "producer_threads": producer.host_threads,
                     "dispatch": per_rank[0].get("dispatch", {}).get("mode"),
                 },
                 "delivered_samples_per_s": round(delivered, 1),

@@ -126,7 +126,7 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
         out_dtype: Any = None,
         shuffle: str = "none",
         seed: int = 0,
-        n_slots: int = 1,
+        n_slots: int | None = None,
         prefetch_depth: int = 4,
         mode: str = "window",
         normalize: dict | None = None,
@@ -159,7 +159,9 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
         self.n_instances = n_instances
         self.shuffle = shuffle
         self.seed = int(seed)
-        self.n_slots = int(n_slots)
+        # default: what the producer asks for (ProducerFunctionSkeleton.preferred_slots, 1 unless its rounds
+        # rewrite the whole window)
+        self.n_slots = int(n_slots if n_slots is not None else getattr(producer_function, "preferred_slots", 1))
         self.prefetch_depth = int(prefetch_depth)
         self.mode = "do_not_split_along_epoch" if mode == "window" else mode
         self.normalize = normalize

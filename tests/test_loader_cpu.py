@@ -266,3 +266,20 @@ class _OddProducer(IdProducer):
         if self.producer_index == 1:
             r.splits = (1, self.width - 1)
         return r
+
+
+def test_producer_preferred_slots(monkeypatch):
+    """n_slots defaults to the producer's preferred_slots: 2 for whole-window refills (one slot refilled while
+    the other is copied), 1 otherwise; an explicit n_slots wins."""
+    monkeypatch.setenv("DDL_DEVICE", "cpu")
+    from ddl_amd.models.producers import ImageWindowProducer
+
+    full, stamp = ImageWindowProducer(8, (3, 4, 4), "float32", refill="full"), ImageWindowProducer(8, (3, 4, 4))
+    assert (full.preferred_slots, full.host_threads) == (2, 8)
+    assert (stamp.preferred_slots, stamp.host_threads) == (1, 4)
+    with ddl_amd.start(n_producers=1) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(full, 4, conn, 2, env=env)
+        assert dl.n_slots == 2
+        seen = [x[0].clone() for x in dl]
+        assert len(seen) == 2
+        dl.close()

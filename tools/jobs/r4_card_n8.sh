@@ -8,6 +8,8 @@ TR="python -m torch.distributed.run --nnodes=1 --master-addr 127.0.0.1"
 run 200 refetch_test python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_loader_gpu.py tests/test_bench_gpu.py -k "refetch or native_dispatch_matches or held_batches or pressure"
 run 200 socket_dram python benchmarks/probe_socket_dram.py --json-out gpurun_out/socket_dram.json
 run 200 hbm_ceilings benchmarks/bin/hbm_ceilings 4
+run 200 bench_n1 python bench.py --steps 20 --warmup 5 --json-out gpurun_out/bench_n1.json
+run 200 bench_full_refill python bench.py --refill full --steps 100 --warmup 10 --order window --idle-steps 0 --json-out gpurun_out/bench_full.json
 run 400 n8_torchrun $TR --nproc-per-node 8 --master-port 29631 bench.py --gpus 8 --steps 20 --warmup 5 --json-out gpurun_out/n8_torchrun.json
 run 400 n8_self python bench.py --gpus 8 --steps 20 --warmup 5 --json-out gpurun_out/n8_self.json
 run 300 n4_torchrun $TR --nproc-per-node 4 --master-port 29632 bench.py --gpus 4 --steps 20 --warmup 5 --json-out gpurun_out/n4_torchrun.json
