@@ -42,9 +42,9 @@ from typing import Any, Iterator
 import torch
 
 from . import ops
-from .checkpoint import STATE_VERSION, CheckpointMixin  # noqa: F401  (STATE_VERSION: public name)
+from .checkpoint import CheckpointMixin
 from .connection import Connection
-from .engine_dispatch import _TRACE_ENGINE, NativeDispatchMixin  # noqa: F401
+from .engine_dispatch import NativeDispatchMixin
 from .datasetwrapper import ProducerFunctionSkeleton
 from .exceptions import ShapeMismatchError
 from .ops import _dtypes

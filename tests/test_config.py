@@ -65,7 +65,7 @@ def test_log_level_knob():
 def test_roctx_knob():
     code = "import ddl_amd.utils.tracing as t; print(t._ROCTX_ENABLED, t._roctx())"
     assert _py(code, DDL_ROCTX="0") == "False ()"
-    assert _py("import ddl_amd.dataloader as d; print(d._TRACE_ENGINE)", DDL_ROCTX="2") == "True"
+    assert _py("import ddl_amd.engine_dispatch as d; print(d._TRACE_ENGINE)", DDL_ROCTX="2") == "True"
 
 
 def test_numa_bind_and_cpu_partition_knobs(monkeypatch):
