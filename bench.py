@@ -196,8 +196,21 @@ def pressure_phase(args, env, dev, it, feed_per_rank: float, barrier, sync) -> d
     from ddl_amd.models.trainstep import CalibratedStep
     from ddl_amd.utils.tracing import ComputeIdleMeter, trace_range
 
+    from ddl_amd import ops
+
     r, B = args.pressure_ratio, args.batch
-    step = CalibratedStep(dev, step_ms=1000.0 * B / (r * feed_per_rank))
+    # the feed this phase runs against: re-measured here over >= 100 batches with the checksum consumer
+    # (phase 1's region can be as short as 20 steps, and the loader's state after phase 2 -- copy streams,
+    # ring -- is what the step will see); the step is sized from it, and its ratio is reported against it
+    acc = ops.ChecksumAccumulator(dev)
+    n_feed = max(args.steps, 100)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(n_feed):
+        acc.add(next(it)[0])
+    sync()
+    feed = B * n_feed / (time.perf_counter() - t0)
+    step = CalibratedStep(dev, step_ms=1000.0 * B / (r * feed))
     step.calibrate(next(it)[0])
     for _ in range(max(2, args.warmup // 2)):
         step(next(it)[0])
@@ -226,9 +239,10 @@ def pressure_phase(args, env, dev, it, feed_per_rank: float, barrier, sync) -> d
     res = meter.result()
     busy = res["busy_ms"] / max(1, res["steps"])
     cap = 1000.0 * B / busy
-    out = {"ratio_target": r, "ratio_measured": round(cap / feed_per_rank, 3), "steps": n,
+    out = {"ratio_target": r, "ratio_measured": round(cap / feed, 3), "steps": n,
+           "feed_samples_per_s": round(feed, 1), "phase1_feed_samples_per_s": round(feed_per_rank, 1),
            "step_ms": round(busy, 4), "gpu_idle_pct": res["gpu_idle_pct"],
-           "predicted_idle_pct": round(100.0 * max(0.0, 1.0 - feed_per_rank / cap), 3),
+           "predicted_idle_pct": round(100.0 * max(0.0, 1.0 - feed / cap), 3),
            "achieved_samples_per_s": B * n * env.world_size / el}
     if env.world_size > 1:
         t = torch.tensor([out["gpu_idle_pct"]], dtype=torch.float64)
@@ -366,7 +380,7 @@ def main(argv=None) -> int:
         args.exchange = 0.5 if n_world > 1 else 0.0
     total_steps = args.warmup + args.steps + (args.warmup // 2 + idle_steps if idle_steps else 0)
     if args.pressure_ratio > 0:
-        total_steps += 1 + max(2, args.warmup // 2) + 40 + max(args.steps, 100)
+        total_steps += 1 + max(2, args.warmup // 2) + 40 + 2 * max(args.steps, 100)
     bpw = args.window // args.batch
     if bpw < 1:
         raise SystemExit("--window must hold at least one --batch")

@@ -695,6 +695,9 @@ PYBIND11_MODULE(_ddl_hip, m) {
       py::arg("offsets"), py::arg("n"), py::arg("seq_len"), py::arg("max_segs"), py::arg("max_rows"),
       py::arg("seg_offsets"), py::arg("row_start"), py::arg("row_end"), py::arg("counts"), py::arg("scratch"),
       py::arg("stream"));
+  m.def("set_move_nt_stores", &ddl::set_move_nt_stores, py::arg("on"),
+        "raw row moves (same-dtype gather / scatter): non-temporal stores on or off, process-wide");
+  m.def("move_nt_stores", &ddl::move_nt_stores);
   m.def(
       "touch_pages",
       [](uintptr_t ptr, int64_t bytes, int64_t page, uintptr_t sink, int blocks, uintptr_t stream) {

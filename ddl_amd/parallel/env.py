@@ -72,6 +72,12 @@ def read_env(n_producers: int | None = None) -> DDLEnv:
     )
 
 
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def init_distributed(env: DDLEnv, backend: str | None = None, timeout_s: float = 600.0,
                      device: str | None = None) -> DDLEnv:
     """Create the DP (RCCL or gloo) group and a gloo control group; set the device.
@@ -104,7 +110,10 @@ def init_distributed(env: DDLEnv, backend: str | None = None, timeout_s: float =
     backend = backend or ("nccl" if use_gpu else "gloo")
     env.backend = backend
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ.setdefault("MASTER_PORT", "29500")
+    if "MASTER_PORT" not in os.environ:
+        # a 1-rank group has no peers to agree on a port with: take a free one (a fixed 29500 collides with
+        # any other job on the host); larger worlds keep torch's conventional default
+        os.environ["MASTER_PORT"] = str(_free_port()) if env.world_size == 1 else "29500"
     if not dist.is_initialized():
         kwargs = dict(backend=backend, rank=env.rank, world_size=env.world_size, timeout=timedelta(seconds=timeout_s))
         if backend == "nccl":

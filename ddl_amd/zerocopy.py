@@ -103,12 +103,12 @@ class ZeroCopyLoader(PrefetchedIndexedLoader):
                 self._reg_base = base
                 dptr = hip.host_device_pointer(base) + (addr - base)
             self.rows = ops.HostRows(self.cpu, dptr)
-            self.prefault_s = self._prefault(dptr) if prefault else 0.0
             self.prep_stream = streams.batch_stream(self.device)
             # prep_streams = 2: consecutive batches' gathers alternate between two streams, so the next one
             # starts while the previous one's last workgroups drain (the link idles in a lone kernel's tail)
             self._prep = [self.prep_stream] + [torch.cuda.Stream(self.device, priority=-1)
                                                for _ in range(max(1, int(prep_streams)) - 1)]
+            self.prefault_s = self._prefault(dptr) if prefault else 0.0
         else:
             self.rows = self.cpu
 

@@ -16,7 +16,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_bench_n1_reports_pressure_idle():
     """Phase 3 puts the loader-pressure idle into the credited line: a calibrated step at 0.9x the feed,
     its achieved ratio, and the idle % behind it next to the PatchMLP figure."""
-    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "DDL_BACKEND", "MASTER_PORT")}
     env["PYTHONPATH"] = REPO
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "20", "--warmup", "5",
                         "--order", "window"], capture_output=True, text=True, timeout=180, env=env)
