@@ -80,6 +80,9 @@ def _parse(argv=None):
     ap.add_argument("--read", default="all", choices=["all", "ids"],
                     help="tokens: the consumer reads every tensor of the batch (all) or only input_ids (ids, as "
                          "bench_tokens.py's feed phase)")
+    ap.add_argument("--max-ahead", type=int, default=None, help="DistributedDataLoader(max_ahead=) (A/B; default 16)")
+    ap.add_argument("--batch-priority", default="high", choices=["high", "normal"],
+                    help="priority of the loader's batch stream (A/B; the library uses high)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--markers", action="store_true", help="roctx markers around each step's fetch (trace_gaps)")
     return ap.parse_args(argv)
@@ -101,7 +104,8 @@ def _image_loader(a, env, conn, n_steps):
         ImageWindowProducer(a.window, (3, 224, 224), a.source_dtype, refill="stamp"), B, conn, n_epochs,
         env=env, device=torch.device(env.device), out_dtype=torch.bfloat16, shuffle="device", normalize=norm,
         native_dispatch=False if a.dispatch == "python" else a.dispatch,
-        **({"prefetch_depth": a.depth} if a.depth else {}))
+        **({"prefetch_depth": a.depth} if a.depth else {}),
+        **({"max_ahead": a.max_ahead} if a.max_ahead is not None else {}))
 
     def gen():
         while True:
@@ -173,6 +177,11 @@ def main(argv=None) -> int:
     from ddl_amd.utils.tracing import ComputeIdleMeter, trace_range
 
     ratios = [float(x) for x in a.ratios.split(",") if x]
+    if a.batch_priority == "normal":  # A/B: the loader's batch stream at normal priority
+        import ddl_amd.dataloader as _dl
+        from ddl_amd.utils import streams as _streams
+
+        _streams.batch_stream = _dl.streams.batch_stream = lambda device: torch.cuda.Stream(device)
     host_marks = a.markers
     n_steps = a.warmup + 2 * a.feed_steps + len(ratios) * (a.steps + a.warmup + a.tune_passes * a.tune_steps + 30)
     src = None

@@ -146,7 +146,7 @@ class ZeroCopyLoader(PrefetchedIndexedLoader):
 
     def stats(self) -> dict:
         return {"batches": self.batches, "source_bytes": self.nbytes, "max_blocks": self.max_blocks,
-                "prefault_s": round(getattr(self, "prefault_s", 0.0), 4),
+                "prefault_s": getattr(self, "prefault_s", 0.0),
                 "prep_streams": len(self._prep) if self.prep_stream is not None else 0}
 
     def close(self) -> None:
