@@ -62,6 +62,11 @@ def measure_d2d() -> float:
     for bpc in (2, 4, 8, 16):
         t = bench(lambda: hip.stream_copy(a.data_ptr(), b.data_ptr(), a.numel(), 256 * bpc, st), reps=20)
         best[f"stream_copy {bpc}x256 blocks"] = t
+    # one pass: every thread moves 4 x 16 B once (no grid-stride loop); the fastest copy shape measured at
+    # 4 GiB by benchmarks/hbm_ceilings.hip (5.69 TB/s), which also gives the read-only / write-only ceilings
+    one_shot = a.numel() // 16 // (256 * 4)
+    t = bench(lambda: hip.stream_copy(a.data_ptr(), b.data_ptr(), a.numel(), one_shot, st), reps=20)
+    best["stream_copy one pass"] = t
     for name, t in best.items():
         bps = 2 * a.numel() / t
         print(json.dumps({"kernel": f"roofline: {name} 1GiB", "us": round(t * 1e6, 2), "GBps": round(bps / 1e9, 1),
