@@ -297,6 +297,8 @@ PYBIND11_MODULE(_ddl_hip, m) {
       .def_property_readonly("bytes_landed", &ddl::NativeStager::bytes_landed)
       .def_property_readonly("wait_producer_s", &ddl::NativeStager::wait_producer_s)
       .def_property_readonly("free_waits", &ddl::NativeStager::free_waits)
+      .def_property_readonly("consumer_bound", &ddl::NativeStager::consumer_bound)
+      .def_property_readonly("policy_switches", &ddl::NativeStager::policy_switches)
       .def("copies_between", &ddl::NativeStager::copies_between, py::arg("t0_ns"), py::arg("t1_ns"),
            "(windows, bytes) of H2D copies enqueued in [t0_ns, t1_ns] (CLOCK_MONOTONIC) that have retired")
       .def(

@@ -147,6 +147,7 @@ void NativeStager::retire_loop() {
       if (device_ms(start_ev_[r.ev], &t_start) && device_ms(retire_ev_[r.ev], &t_end)) {
         done_log_.push_back(DoneRec{r.window, r.bytes, t_start, t_end, r.stream});
         if (done_log_.size() > kCopyLog) done_log_.pop_front();
+        note_link_gap(t_start, t_end);
       }
       retire_q_.pop_front();
       retired_upto_ = r.window + 1;
@@ -179,23 +180,36 @@ void NativeStager::fail(int code, int32_t producer, const std::string& msg) {
   retire_cv_.notify_all();
 }
 
-bool NativeStager::copy_in_flight(int i, int64_t w) const {
-  const int64_t lw = last_copy_[i];
-  // a retire event is re-recorded only after its window retired, so a copy kRetireEvents windows back is done
-  if (lw < 0 || w - lw >= kRetireEvents) return false;
-  return hipEventQuery(retire_ev_[static_cast<size_t>((lw - first_) % kRetireEvents)]) == hipErrorNotReady;
+void NativeStager::note_link_gap(double t_start, double t_end) {
+  // retire thread, copies in window order: how long the link sat idle before this copy (negative: it
+  // overlapped the previous one on the other engine)
+  if (link_end_ms_ >= 0.0) {
+    const double gap = t_start - link_end_ms_;
+    if (gap > kGapConsumerMs)
+      gap_run_ = gap_run_ > 0 ? gap_run_ + 1 : 1;
+    else if (gap < kGapLoaderMs)
+      gap_run_ = gap_run_ < 0 ? gap_run_ - 1 : -1;
+    const bool was = consumer_bound_.load(std::memory_order_relaxed);
+    if (!was && gap_run_ >= kGapRun) {
+      consumer_bound_.store(true, std::memory_order_relaxed);
+      policy_switches_ += 1;
+    } else if (was && gap_run_ <= -kGapRun) {
+      consumer_bound_.store(false, std::memory_order_relaxed);
+      policy_switches_ += 1;
+    }
+  }
+  link_end_ms_ = std::max(link_end_ms_, t_end);
 }
 
 int NativeStager::pick_copy_stream(int64_t w) const {
   if (copy_stream2_ == nullptr) return 0;
   if (copy_policy_ == 0) return static_cast<int>((w - first_) & 1);  // strict alternation
-  // auto: on kRingWaitRun windows in a row the stager waited for a ring buffer while the link went idle, so
-  // the consumer is slower than the link and the feed has slack: one stream (one SDMA engine), which shows a
-  // lower step-boundary idle below the crossover (profiles/r3_copy_policy). Otherwise (loader-bound)
-  // alternate, so two copies overlap and the link never waits for one to end (+2.5% feed). The run length
-  // keeps an isolated wait -- e.g. the one across a benchmark's opening synchronize -- from serialising the
-  // copies after it.
-  return ring_wait_run_ >= kRingWaitRun ? 0 : 1 - last_stream_;
+  // auto: while the consumer is the bottleneck (the link idles before copies, note_link_gap) one stream, i.e.
+  // one SDMA engine: below the crossover two concurrent copies raise the step-boundary idle (0.76% with one
+  // stream vs 1.4-2.0% alternating at r = 0.93-0.97, profiles/r4_third). Otherwise alternate, so two copies
+  // overlap and the link never waits for one to end (+1.8-2.5% feed, profiles/r2_copy_streams). Decided on
+  // the device clock: a copy queued behind a wait for its ring buffer is not "in flight" for the link.
+  return consumer_bound_.load(std::memory_order_relaxed) ? 0 : 1 - last_stream_;
 }
 
 void NativeStager::run() {
@@ -266,13 +280,7 @@ void NativeStager::run() {
     if (info.used_bytes > buffer_bytes_)
       return fail(-1, static_cast<int32_t>(p),
                   "window of " + std::to_string(info.used_bytes) + " B exceeds the staging buffer");
-    // stream choice as late as possible, when the engines' state is known (see pick_copy_stream)
-    // the consumer is the bottleneck when the stager had to wait for a ring buffer AND the link went idle
-    // meanwhile (no copy still in flight): a ring wait with copies in flight is the loader-bound steady state
-    // of a stager that runs ahead of the ring (e.g. 2 slots per producer)
-    const bool link_idle = !copy_in_flight(0, w) && (copy_stream2_ == nullptr || !copy_in_flight(1, w));
-    ring_wait_run_ = s1 - s0 > kRingWaitNs && link_idle ? ring_wait_run_ + 1 : 0;
-    const int si = pick_copy_stream(w);
+    const int si = pick_copy_stream(w);  // as late as possible: the latest link-gap verdict
     hipStream_t cs = si == 0 ? copy_stream_ : copy_stream2_;
     // the consumer's kernels reading this ring buffer (window w - depth) finish first; a free event that
     // has already completed needs no device-side wait (no cross-stream dependency on the compute stream)
@@ -280,7 +288,6 @@ void NativeStager::run() {
       if (hipStreamWaitEvent(cs, free_ev, 0) != hipSuccess) return fail(-1, -1, "hipStreamWaitEvent(free) failed");
       free_waits_ += 1;
     }
-    last_copy_[si] = w;
     last_stream_ = si;
     // start / retire events of w: a ring, so window w - kRetireEvents must have been retired before they are
     // re-recorded (never waits with depth < kRetireEvents ring buffers)

@@ -119,6 +119,8 @@ class NativeStager {
   double wait_producer_s() const { return wait_producer_ns_.load() * 1e-9; }
   // free-event waits actually enqueued on a copy stream (the rest had completed and were skipped)
   uint64_t free_waits() const { return free_waits_.load(); }
+  bool consumer_bound() const { return consumer_bound_.load(std::memory_order_relaxed); }
+  uint64_t policy_switches() const { return policy_switches_.load(); }
   // per staged window (first 4096): ns spent in each step of the stager loop -- waiting for the ring
   // (consumer release), enqueueing the free-event wait, waiting for the producer, enqueueing the copy,
   // waiting for a retire-event slot + recording the events
@@ -176,15 +178,22 @@ class NativeStager {
   // already running on another SDMA engine when one finishes (no per-copy gap on the link)
   hipStream_t copy_stream2_;
   // 0: windows strictly alternate between the two copy streams; 2 (default): auto, one stream while the
-  // stager waits on the consumer for ring buffers, alternation otherwise (pick_copy_stream)
+  // consumer is the bottleneck (the link idles before copies), alternation otherwise (pick_copy_stream)
   const int copy_policy_;
-  bool copy_in_flight(int i, int64_t w) const;
-  static constexpr int64_t kRingWaitNs = 50000;  // a ring wait longer than this: the consumer held the ring
-  static constexpr int kRingWaitRun = 3;  // ... with the link idle, this many windows in a row: consumer-bound
-  int ring_wait_run_ = 0;                 // consecutive such windows (stager thread)
-  int64_t last_copy_[2] = {-1, -1};  // last window copied on each stream (stager thread only)
+  // auto copy policy (pick_copy_stream): the consumer is the bottleneck when the LINK idles before copies,
+  // measured on the device clock by the retire thread: gap = a copy's start (its stream reached it, after
+  // any wait for its ring buffer) minus the end of every earlier copy. kGapRun windows in a row with a gap
+  // over kGapConsumerMs: one stream; kGapRun in a row under kGapLoaderMs: alternate (a lone SDMA engine's
+  // own turnaround between back-to-back copies is ~25 us, under the lower threshold).
+  static constexpr double kGapConsumerMs = 0.060, kGapLoaderMs = 0.040;
+  static constexpr int kGapRun = 3;
+  double link_end_ms_ = -1.0;  // end of the latest retired copy (retire thread)
+  int gap_run_ = 0;            // > 0: consecutive consumer-side gaps, < 0: consecutive loader-side (retire thread)
+  std::atomic<bool> consumer_bound_{false};
+  std::atomic<uint64_t> policy_switches_{0};
   int last_stream_ = 1;
   int pick_copy_stream(int64_t w) const;
+  void note_link_gap(double t_start, double t_end);  // retire thread
   const int device_;
   const std::vector<int32_t> peer_pids_;
   const int64_t timeout_ms_;

@@ -25,7 +25,7 @@ ddl/connection.py:89-92). This is the MI355X-native replacement of that gap
   read it (permute/cast/collate) finish first.
 
 HBM is plentiful on MI355X (288 GB): windows are staged whole, ``depth``
-windows deep (default 2 = double buffering against the training step), plus
+windows deep (default 4), plus
 two ring buffers for the exchange lookahead when the exchange is on.
 """
 
@@ -129,9 +129,9 @@ class WindowStager:
         # two copy streams (two SDMA engines): when copies run back to back the next one is already
         # running when one finishes, so the ~25 us gap per copy on one engine is gone (+1.8-2.5%,
         # profiles/r2_copy_streams, profiles/r3_copy_policy). copy_policy "auto" (default): alternate
-        # while the loader is the bottleneck, one stream while the stager waits on the consumer for ring
-        # buffers (below the crossover one engine shows a lower step-boundary idle); "alternate": strict
-        # alternation. DDL_COPY_STREAMS=1: one stream.
+        # while the loader is the bottleneck, one stream while the consumer is (the link idles before copies,
+        # measured on the device clock; below the crossover one engine halves the step-boundary idle,
+        # profiles/r4_third); "alternate": strict alternation. DDL_COPY_STREAMS=1: one stream.
         n_cs = int(os.environ.get("DDL_COPY_STREAMS", "2"))
         codes = {"alternate": 0, "auto": 2}
         copy_policy = copy_policy or COPY_POLICY
@@ -320,4 +320,6 @@ class WindowStager:
                 "windows_landed": self.windows_landed, "bytes_landed": self.bytes_landed,
                 "stager_wait_producer_s": float(self._native.wait_producer_s),
                 "copy_policy": self.copy_policy, "free_waits_enqueued": int(self._native.free_waits),
+                "copy_one_stream_now": bool(self._native.consumer_bound),
+                "copy_policy_switches": int(self._native.policy_switches),
                 "exchange_issue_wait_s": round(self.post_wait_s, 6)}
