@@ -183,7 +183,7 @@ def phase2(args, env, dev, it, idle_steps: int, barrier, sync) -> dict:
     return idle
 
 
-def pressure_phase(args, env, dev, it, feed_per_rank: float, barrier, sync) -> dict:
+def pressure_phase(args, env, dev, it, feed_per_rank: float, barrier, sync, dl=None) -> dict:
     """GPU idle % with the LOADER as the near-bottleneck: a calibrated step (reads the whole batch, then a
     bf16 GEMM chain, ``CalibratedStep``) sized so its capacity is ``--pressure-ratio`` x this rank's phase-1
     feed, re-sized twice from its busy time measured in this very loop, then timed. Behind the PatchMLP
@@ -226,14 +226,18 @@ def pressure_phase(args, env, dev, it, feed_per_rank: float, barrier, sync) -> d
         step.tune(tr["busy_ms"] / max(1, tr["steps"]))
     n = max(args.steps, 100)
     meter = ComputeIdleMeter()
+    stager = getattr(dl, "_stager", None)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
     t0 = time.perf_counter()
+    e0.record()
     with trace_range("bench.pressure"):
         for _ in range(n):
             (x,) = next(it)
             meter.step_begin()
             step(x)
             meter.step_end()
+        e1.record()
         sync()
     el = time.perf_counter() - t0
     res = meter.result()
@@ -244,6 +248,8 @@ def pressure_phase(args, env, dev, it, feed_per_rank: float, barrier, sync) -> d
            "step_ms": round(busy, 4), "gpu_idle_pct": res["gpu_idle_pct"],
            "predicted_idle_pct": round(100.0 * max(0.0, 1.0 - feed / cap), 3),
            "achieved_samples_per_s": B * n * env.world_size / el}
+    if stager is not None:  # how the window copies ran meanwhile (the auto policy's one-stream mode)
+        out["copies"] = stager.copy_summary(e0, e1)
     if env.world_size > 1:
         t = torch.tensor([out["gpu_idle_pct"]], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=env.control_group)
@@ -550,7 +556,7 @@ def main(argv=None) -> int:
         pressure = None
         if args.pressure_ratio > 0 and dev.type == "cuda":
             try:
-                pressure = pressure_phase(args, env, dev, it, value / env.world_size, barrier, sync)
+                pressure = pressure_phase(args, env, dev, it, value / env.world_size, barrier, sync, dl=dl)
             except Exception as e:  # the headline is still reported
                 import traceback
 

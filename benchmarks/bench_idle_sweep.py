@@ -81,6 +81,8 @@ def _parse(argv=None):
                     help="tokens: the consumer reads every tensor of the batch (all) or only input_ids (ids, as "
                          "bench_tokens.py's feed phase)")
     ap.add_argument("--max-ahead", type=int, default=None, help="DistributedDataLoader(max_ahead=) (A/B; default 16)")
+    ap.add_argument("--copy-policy", default=None, choices=["auto", "alternate"],
+                    help="copy-stream policy of the stager (A/B; default auto)")
     ap.add_argument("--batch-priority", default="high", choices=["high", "normal"],
                     help="priority of the loader's batch stream (A/B; the library uses high)")
     ap.add_argument("--json-out", default=None)
@@ -177,6 +179,10 @@ def main(argv=None) -> int:
     from ddl_amd.utils.tracing import ComputeIdleMeter, trace_range
 
     ratios = [float(x) for x in a.ratios.split(",") if x]
+    if a.copy_policy is not None:
+        from ddl_amd import staging as _staging
+
+        _staging.COPY_POLICY = a.copy_policy
     if a.batch_priority == "normal":  # A/B: the loader's batch stream at normal priority
         import ddl_amd.dataloader as _dl
         from ddl_amd.utils import streams as _streams
@@ -268,6 +274,8 @@ def main(argv=None) -> int:
                 nd0 = dl.stats().get("native_dispatch") or {}
                 seg0 = torch.cuda.memory_stats(dev).get("segment.all.allocated", 0)
                 torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
                 t2 = time.perf_counter()
                 with trace_range(f"sweep.p{i:02d}"):
                     for _ in range(a.steps):
@@ -279,6 +287,7 @@ def main(argv=None) -> int:
                         meter.step_begin()
                         step(batch)
                         meter.step_end()
+                    e1.record()
                     torch.cuda.synchronize()
                 t3 = time.perf_counter()
                 seg1 = torch.cuda.memory_stats(dev).get("segment.all.allocated", 0)
@@ -294,6 +303,8 @@ def main(argv=None) -> int:
                       "gpu_idle_pct": round(res["gpu_idle_pct"], 3), "predicted_idle_pct": round(pred, 3),
                       "error_pp": round(res["gpu_idle_pct"] - pred, 3),
                       "allocator_segments_created": seg1 - seg0}
+                if getattr(dl, "_stager", None) is not None:
+                    pt["copies"] = dl._stager.copy_summary(e0, e1)
                 if a.floor:  # the same step on one held batch, no loader calls: the meter's own floor
                     fm = ComputeIdleMeter()
                     torch.cuda.synchronize()

@@ -301,6 +301,19 @@ class WindowStager:
         "t0_ms", "t1_ms"}``; waits (bounded) for copies still in flight."""
         return dict(self._native.bytes_in_interval(e0.cuda_event, e1.cuda_event, int(timeout_s * 1000)))
 
+    def copy_summary(self, e0: torch.cuda.Event, e1: torch.cuda.Event) -> dict:
+        """How the window copies ran between two timing events: copies per stream, link busy % and the share
+        with two copies in flight, plus the auto policy's state (one stream now, switches so far)."""
+        pro = self.bytes_in_interval(e0, e1)
+        span = max(1e-9, pro.get("t1_ms", 0.0) - pro.get("t0_ms", 0.0))
+        out = {"copy_one_stream_now": bool(self._native.consumer_bound),
+               "copy_policy_switches": int(self._native.policy_switches)}
+        if pro.get("ok"):
+            out.update(copies_per_stream=list(pro["copies_per_stream"]),
+                       link_busy_pct=round(100.0 * pro["busy_ms"] / span, 2),
+                       two_copies_pct=round(100.0 * pro["overlap_ms"] / span, 2))
+        return out
+
     @property
     def windows_landed(self) -> int:
         """Windows whose H2D copy has retired (the data is in HBM)."""
