@@ -147,7 +147,7 @@ void NativeStager::retire_loop() {
       if (device_ms(start_ev_[r.ev], &t_start) && device_ms(retire_ev_[r.ev], &t_end)) {
         done_log_.push_back(DoneRec{r.window, r.bytes, t_start, t_end, r.stream});
         if (done_log_.size() > kCopyLog) done_log_.pop_front();
-        note_link_gap(t_start, t_end);
+        note_link_gap(r.stream, t_start, t_end);
       }
       retire_q_.pop_front();
       retired_upto_ = r.window + 1;
@@ -180,11 +180,15 @@ void NativeStager::fail(int code, int32_t producer, const std::string& msg) {
   retire_cv_.notify_all();
 }
 
-void NativeStager::note_link_gap(double t_start, double t_end) {
-  // retire thread, copies in window order: how long the link sat idle before this copy (negative: it
-  // overlapped the previous one on the other engine)
-  if (link_end_ms_ >= 0.0) {
-    const double gap = t_start - link_end_ms_;
+void NativeStager::note_link_gap(int stream, double t_start, double t_end) {
+  // retire thread, copies in window order: how long this copy's ENGINE sat idle before the copy started (its
+  // start event is recorded after the stream's wait for the copy's ring buffer). With the consumer the
+  // bottleneck every copy waits for its buffer; with the loader the bottleneck copies queue back to back on
+  // each engine. (The link as a whole is the wrong signal: two alternating copies that each wait for a
+  // buffer overlap and stretch, so the link looks ~95% busy while the consumer holds the ring.)
+  const int si = stream & 1;
+  if (engine_end_ms_[si] >= 0.0) {
+    const double gap = t_start - engine_end_ms_[si];
     if (gap > kGapConsumerMs)
       gap_run_ = gap_run_ > 0 ? gap_run_ + 1 : 1;
     else if (gap < kGapLoaderMs)
@@ -193,22 +197,22 @@ void NativeStager::note_link_gap(double t_start, double t_end) {
     if (!was && gap_run_ >= kGapRun) {
       consumer_bound_.store(true, std::memory_order_relaxed);
       policy_switches_ += 1;
-    } else if (was && gap_run_ <= -kGapRun) {
+    } else if (was && gap_run_ <= -kGapRunBack) {
       consumer_bound_.store(false, std::memory_order_relaxed);
       policy_switches_ += 1;
     }
   }
-  link_end_ms_ = std::max(link_end_ms_, t_end);
+  engine_end_ms_[si] = std::max(engine_end_ms_[si], t_end);
 }
 
 int NativeStager::pick_copy_stream(int64_t w) const {
   if (copy_stream2_ == nullptr) return 0;
   if (copy_policy_ == 0) return static_cast<int>((w - first_) & 1);  // strict alternation
-  // auto: while the consumer is the bottleneck (the link idles before copies, note_link_gap) one stream, i.e.
-  // one SDMA engine: below the crossover two concurrent copies raise the step-boundary idle (0.76% with one
-  // stream vs 1.4-2.0% alternating at r = 0.93-0.97, profiles/r4_third). Otherwise alternate, so two copies
-  // overlap and the link never waits for one to end (+1.8-2.5% feed, profiles/r2_copy_streams). Decided on
-  // the device clock: a copy queued behind a wait for its ring buffer is not "in flight" for the link.
+  // auto: while the consumer is the bottleneck (copies wait for their ring buffers, note_link_gap) one stream,
+  // i.e. one SDMA engine: below the crossover two concurrent copies triple the step-boundary idle (one stream
+  // 0.52 / 0.70% vs alternating 1.15-1.64 / 2.29-2.45% at r = 0.75 / 0.9, three runs each,
+  // profiles/r4_fifth). Otherwise alternate, so two copies overlap and the engines never wait for one
+  // another (+1.8-2.5% feed, profiles/r2_copy_streams). Decided on the device clock.
   return consumer_bound_.load(std::memory_order_relaxed) ? 0 : 1 - last_stream_;
 }
 

@@ -180,20 +180,19 @@ class NativeStager {
   // 0: windows strictly alternate between the two copy streams; 2 (default): auto, one stream while the
   // consumer is the bottleneck (the link idles before copies), alternation otherwise (pick_copy_stream)
   const int copy_policy_;
-  // auto copy policy (pick_copy_stream): the consumer is the bottleneck when the LINK idles before copies,
-  // measured on the device clock by the retire thread: gap = a copy's start (its stream reached it, after
-  // any wait for its ring buffer) minus the end of every earlier copy. kGapRun windows in a row with a gap
-  // over kGapConsumerMs: one stream; kGapRun in a row under kGapLoaderMs: alternate (a lone SDMA engine's
-  // own turnaround between back-to-back copies is ~25 us, under the lower threshold).
+  // auto copy policy (pick_copy_stream): the consumer is the bottleneck when copies wait for their ring
+  // buffers, measured on the device clock by the retire thread: gap = a copy's start (its stream reached it,
+  // after the wait for its buffer) minus the end of the previous copy on the same engine. kGapRun copies in a
+  // row with a gap over kGapConsumerMs: one stream; kGapRunBack in a row under kGapLoaderMs: alternate.
   static constexpr double kGapConsumerMs = 0.060, kGapLoaderMs = 0.040;
-  static constexpr int kGapRun = 3;
-  double link_end_ms_ = -1.0;  // end of the latest retired copy (retire thread)
-  int gap_run_ = 0;            // > 0: consecutive consumer-side gaps, < 0: consecutive loader-side (retire thread)
+  static constexpr int kGapRun = 3, kGapRunBack = 6;
+  double engine_end_ms_[2] = {-1.0, -1.0};  // end of the latest retired copy per stream (retire thread)
+  int gap_run_ = 0;  // > 0: consecutive consumer-side gaps, < 0: consecutive loader-side (retire thread)
   std::atomic<bool> consumer_bound_{false};
   std::atomic<uint64_t> policy_switches_{0};
   int last_stream_ = 1;
   int pick_copy_stream(int64_t w) const;
-  void note_link_gap(double t_start, double t_end);  // retire thread
+  void note_link_gap(int stream, double t_start, double t_end);  // retire thread
   const int device_;
   const std::vector<int32_t> peer_pids_;
   const int64_t timeout_ms_;
