@@ -181,28 +181,10 @@ void NativeStager::fail(int code, int32_t producer, const std::string& msg) {
 }
 
 void NativeStager::note_link_gap(int stream, double t_start, double t_end) {
-  // retire thread, copies in window order: how long this copy's ENGINE sat idle before the copy started (its
-  // start event is recorded after the stream's wait for the copy's ring buffer). With the consumer the
-  // bottleneck every copy waits for its buffer; with the loader the bottleneck copies queue back to back on
-  // each engine. (The link as a whole is the wrong signal: two alternating copies that each wait for a
-  // buffer overlap and stretch, so the link looks ~95% busy while the consumer holds the ring.)
-  const int si = stream & 1;
-  if (engine_end_ms_[si] >= 0.0) {
-    const double gap = t_start - engine_end_ms_[si];
-    if (gap > kGapConsumerMs)
-      gap_run_ = gap_run_ > 0 ? gap_run_ + 1 : 1;
-    else if (gap < kGapLoaderMs)
-      gap_run_ = gap_run_ < 0 ? gap_run_ - 1 : -1;
-    const bool was = consumer_bound_.load(std::memory_order_relaxed);
-    if (!was && gap_run_ >= kGapRun) {
-      consumer_bound_.store(true, std::memory_order_relaxed);
-      policy_switches_ += 1;
-    } else if (was && gap_run_ <= -kGapRunBack) {
-      consumer_bound_.store(false, std::memory_order_relaxed);
-      policy_switches_ += 1;
-    }
-  }
-  engine_end_ms_[si] = std::max(engine_end_ms_[si], t_end);
+  // retire thread, copies in window order (copy_mode.h: the per-engine wait-for-buffer gap)
+  const uint64_t before = copy_mode_.switches;
+  consumer_bound_.store(copy_mode_.note(stream, t_start, t_end), std::memory_order_relaxed);
+  if (copy_mode_.switches != before) policy_switches_ += 1;
 }
 
 int NativeStager::pick_copy_stream(int64_t w) const {

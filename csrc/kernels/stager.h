@@ -25,6 +25,8 @@
 // full interpreter switch interval (5 ms) by a Python-heavy training loop.
 #pragma once
 
+#include "copy_mode.h"
+
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -180,14 +182,8 @@ class NativeStager {
   // 0: windows strictly alternate between the two copy streams; 2 (default): auto, one stream while the
   // consumer is the bottleneck (the link idles before copies), alternation otherwise (pick_copy_stream)
   const int copy_policy_;
-  // auto copy policy (pick_copy_stream): the consumer is the bottleneck when copies wait for their ring
-  // buffers, measured on the device clock by the retire thread: gap = a copy's start (its stream reached it,
-  // after the wait for its buffer) minus the end of the previous copy on the same engine. kGapRun copies in a
-  // row with a gap over kGapConsumerMs: one stream; kGapRunBack in a row under kGapLoaderMs: alternate.
-  static constexpr double kGapConsumerMs = 0.060, kGapLoaderMs = 0.040;
-  static constexpr int kGapRun = 3, kGapRunBack = 6;
-  double engine_end_ms_[2] = {-1.0, -1.0};  // end of the latest retired copy per stream (retire thread)
-  int gap_run_ = 0;  // > 0: consecutive consumer-side gaps, < 0: consecutive loader-side (retire thread)
+  // auto copy policy (pick_copy_stream): one stream while copies wait for their ring buffers (copy_mode.h)
+  CopyModeTrigger copy_mode_;  // retire thread
   std::atomic<bool> consumer_bound_{false};
   std::atomic<uint64_t> policy_switches_{0};
   int last_stream_ = 1;
