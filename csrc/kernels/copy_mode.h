@@ -16,29 +16,31 @@
 namespace ddl {
 
 struct CopyModeTrigger {
-  static constexpr double kConsumerMs = 0.060;  // an engine waited longer than this for a buffer
-  static constexpr double kLoaderMs = 0.040;    // ... shorter than this (a lone engine's turnaround is ~25 us)
-  static constexpr int kRun = 3;                // consecutive consumer-side copies -> one stream
-  static constexpr int kRunBack = 6;            // consecutive loader-side copies -> alternate again
+  // the engines' mean wait per copy, an exponential average over the last ~5 copies (a run-length rule over
+  // single gaps flapped, profiles/r4_sixth). Each gap counts at most kCapMs: a one-off pause of the consumer
+  // (a synchronize, an epoch boundary) shows as a long gap on BOTH engines' next copies, and two capped gaps
+  // (2 x 0.2 x 0.15 ms < kConsumerMs) must not flip the policy; a steady consumer-bound feed waits on every
+  // copy (r = 0.9: ~150 us per copy on one engine, ~300 us per engine alternating).
+  static constexpr double kAlpha = 0.2;
+  static constexpr double kCapMs = 0.150;
+  static constexpr double kConsumerMs = 0.060;  // mean wait above this: one stream
+  static constexpr double kLoaderMs = 0.020;    // below this: alternate (back-to-back copies wait ~0)
 
   double engine_end[2] = {-1.0, -1.0};
-  int run = 0;  // > 0: consecutive consumer-side gaps, < 0: consecutive loader-side
+  double mean_gap = 0.0;  // ms
   bool consumer_bound = false;
   uint64_t switches = 0;
 
-  // One retired copy; returns the (possibly new) verdict.
+  // One retired copy (engine `stream`, device-clock [t_start, t_end] in ms); returns the (possibly new) verdict.
   bool note(int stream, double t_start, double t_end) {
     const int si = stream & 1;
     if (engine_end[si] >= 0.0) {
-      const double gap = t_start - engine_end[si];
-      if (gap > kConsumerMs)
-        run = run > 0 ? run + 1 : 1;
-      else if (gap < kLoaderMs)
-        run = run < 0 ? run - 1 : -1;
-      if (!consumer_bound && run >= kRun) {
+      const double gap = std::max(0.0, t_start - engine_end[si]);
+      mean_gap = (1.0 - kAlpha) * mean_gap + kAlpha * std::min(gap, kCapMs);
+      if (!consumer_bound && mean_gap > kConsumerMs) {
         consumer_bound = true;
         ++switches;
-      } else if (consumer_bound && run <= -kRunBack) {
+      } else if (consumer_bound && mean_gap < kLoaderMs) {
         consumer_bound = false;
         ++switches;
       }

@@ -246,7 +246,11 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
         if ma < 0:
             raise ValueError("max_ahead must be >= 0")
         self.max_ahead = ma
-        self._ahead_every = max(1, ma // 4)
+        # one event per batch (a ring, reused): the host is released one batch per finished step, so the
+        # copies it unblocks follow the step smoothly instead of in bursts of several windows (the stager's
+        # auto copy policy reads the copies' waits for ring buffers, csrc/kernels/copy_mode.h)
+        self._ahead_every = 1
+        self._ahead_ring: list = []
         # (batch count, event on the consumer's stream)
         self._ahead_q = collections.deque() if self.device.type == "cuda" and ma > 0 else None
         self._ahead_n = 0
@@ -488,7 +492,10 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
                 self.ahead_waits += 1
                 ev.synchronize()
         if n % self._ahead_every == 0:
-            ev = torch.cuda.Event()
+            ring = self._ahead_ring
+            if len(ring) < self.max_ahead + 2:  # an event is re-recorded only after it left the queue
+                ring.append(torch.cuda.Event())
+            ev = ring[n % len(ring)] if len(ring) == self.max_ahead + 2 else ring[-1]
             ev.record(torch.cuda.current_stream(self.device))
             q.append((n, ev))
 

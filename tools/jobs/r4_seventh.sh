@@ -1,4 +1,4 @@
-# Round 4, sixth box: the per-engine gap trigger of the auto copy policy across the crossover (it must switch
+# Round 4, seventh box: the EWMA per-engine wait trigger (per-batch run-ahead events) of the auto copy policy across the crossover (it must switch
 # to one stream below it and stay alternating above it), the driver bench x3 and the copy-policy GPU tests.
 source tools/gpu_job.sh
 unset DDL_BACKEND
