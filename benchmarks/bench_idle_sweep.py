@@ -44,6 +44,9 @@ def _parse(argv=None):
     ap.add_argument("--family", default="images", choices=["images", "tokens"])
     ap.add_argument("--source-dtype", default="bfloat16", choices=["bfloat16", "uint8"])
     ap.add_argument("--ratios", default=",".join(str(r) for r in RATIOS))
+    ap.add_argument("--step-ms", default=None,
+                    help="absolute step times in ms instead of ratios to the measured feed (compares loader variants "
+                         "whose feeds differ at the same step: a ratio to each one's own feed would not)")
     ap.add_argument("--feed-steps", type=int, default=300)
     ap.add_argument("--steps", type=int, default=150, help="timed steps per sweep point")
     ap.add_argument("--warmup", type=int, default=20)
@@ -255,8 +258,12 @@ def main(argv=None) -> int:
                 del blob
 
             # ---- sweep
+            step_ms_list = [float(x) for x in a.step_ms.split(",")] if a.step_ms else None
+            if step_ms_list:
+                ratios = [1000.0 * B / (ms * feed) for ms in step_ms_list]
             for i, r in enumerate(ratios):
-                step = CalibratedStep(dev, step_ms=1000.0 * B / (r * feed), read_keys=keys)
+                step = CalibratedStep(dev, step_ms=step_ms_list[i] if step_ms_list else 1000.0 * B / (r * feed),
+                                      read_keys=keys)
                 step.calibrate(next(it))
                 for _ in range(a.warmup):
                     step(next(it))
