@@ -216,7 +216,7 @@ def pressure_phase(args, env, dev, it, feed_per_rank: float, barrier, sync, dl=N
         step(next(it)[0])
     for _ in range(2):  # re-size from the busy time on the loader's batches (clocks, memory traffic)
         tm = ComputeIdleMeter()
-        for _ in range(20):
+        for _ in range(30):
             (x,) = next(it)
             tm.step_begin()
             step(x)
@@ -224,7 +224,7 @@ def pressure_phase(args, env, dev, it, feed_per_rank: float, barrier, sync, dl=N
         sync()
         tr = tm.result()
         step.tune(tr["busy_ms"] / max(1, tr["steps"]))
-    n = max(args.steps, 100)
+    n = max(args.steps, 300)
     meter = ComputeIdleMeter()
     stager = getattr(dl, "_stager", None)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -386,7 +386,7 @@ def main(argv=None) -> int:
         args.exchange = 0.5 if n_world > 1 else 0.0
     total_steps = args.warmup + args.steps + (args.warmup // 2 + idle_steps if idle_steps else 0)
     if args.pressure_ratio > 0:
-        total_steps += 1 + max(2, args.warmup // 2) + 40 + 2 * max(args.steps, 100)
+        total_steps += 1 + max(2, args.warmup // 2) + 60 + max(args.steps, 100) + max(args.steps, 300)
     bpw = args.window // args.batch
     if bpw < 1:
         raise SystemExit("--window must hold at least one --batch")

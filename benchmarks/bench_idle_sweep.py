@@ -84,6 +84,8 @@ def _parse(argv=None):
                     help="tokens: the consumer reads every tensor of the batch (all) or only input_ids (ids, as "
                          "bench_tokens.py's feed phase)")
     ap.add_argument("--max-ahead", type=int, default=None, help="DistributedDataLoader(max_ahead=) (A/B; default 16)")
+    ap.add_argument("--gather-blocks", type=int, default=0,
+                    help="grid cap of the loader's batch gather (A/B; 0 = uncapped, the library default)")
     ap.add_argument("--copy-policy", default=None, choices=["auto", "alternate"],
                     help="copy-stream policy of the stager (A/B; default auto)")
     ap.add_argument("--batch-priority", default="high", choices=["high", "normal"],
@@ -182,6 +184,10 @@ def main(argv=None) -> int:
     from ddl_amd.utils.tracing import ComputeIdleMeter, trace_range
 
     ratios = [float(x) for x in a.ratios.split(",") if x]
+    if a.gather_blocks:
+        from ddl_amd import engine_dispatch as _ed
+
+        _ed.GATHER_MAX_BLOCKS = a.gather_blocks
     if a.copy_policy is not None:
         from ddl_amd import staging as _staging
 

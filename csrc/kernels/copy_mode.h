@@ -17,15 +17,16 @@ namespace ddl {
 
 struct CopyModeTrigger {
   // the engines' mean wait per copy, an exponential average over the last ~5 copies (a run-length rule over
-  // single gaps flapped, profiles/r4_sixth). Each gap counts at most kCapMs: a one-off pause of the consumer
-  // (a synchronize, an epoch boundary) shows as a long gap on BOTH engines' next copies, and two capped gaps
-  // (2 x 0.2 x 0.15 ms < kConsumerMs) must not flip the policy; a steady consumer-bound feed waits on every
-  // copy (r = 0.9: ~150 us per copy on one engine, ~300 us per engine alternating).
+  // single gaps flapped, profiles/r4_sixth). The band is wide on purpose: one stream only once every engine
+  // waits ~0.3 ms per copy (alternating at r <= ~0.9; at equal step time one stream shows ~0.3-0.5 pp less
+  // idle there, profiles/r4_eighth), alternation again once one engine waits < 50 us (r >= ~0.965). Narrower
+  // bands (0.06 / 0.02 ms) flapped in the loader-bound headline, where producer turnarounds leave an engine
+  // idle now and then, and cost it 2-7% (profiles/r4_seventh). Each gap counts at most kCapMs: a one-off pause
+  // of the consumer (a synchronize) shows on both engines' next copies and must not flip the policy.
   static constexpr double kAlpha = 0.2;
-  static constexpr double kCapMs = 0.150;
-  static constexpr double kConsumerMs = 0.060;  // mean wait above this: one stream
-  static constexpr double kLoaderMs = 0.020;    // below this: alternate (back-to-back copies wait ~0)
-
+  static constexpr double kCapMs = 0.400;
+  static constexpr double kConsumerMs = 0.300;  // mean wait above this: one stream
+  static constexpr double kLoaderMs = 0.050;    // below this: alternate
   double engine_end[2] = {-1.0, -1.0};
   double mean_gap = 0.0;  // ms
   bool consumer_bound = false;

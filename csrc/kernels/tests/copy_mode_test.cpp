@@ -27,6 +27,16 @@ int main() {
     EXPECT(t.switches == 0);
   }
   {
+    // loader-bound with producer hiccups: every 10th copy on an engine starts 0.5 ms late -> no switch
+    ddl::CopyModeTrigger t;
+    double off = 0;
+    for (int w = 0; w < 300; ++w) {
+      if (w % 10 == 0) off += 0.5;
+      const double start = off + (w / 2) * 2 * copy + (w % 2) * copy;
+      EXPECT(!t.note(w % 2, start, start + 2 * copy));
+    }
+  }
+  {
     // a one-off pause of 5 ms in a loader-bound feed (both engines' next copies start late): no switch
     ddl::CopyModeTrigger t;
     double off = 0;
@@ -37,21 +47,21 @@ int main() {
     }
   }
   {
-    // consumer-bound at r = 0.9, alternating: a buffer frees every 1.52 ms; each copy starts when its buffer
-    // frees and overlaps the other engine's (the link looks busy, the engines wait)
+    // consumer-bound at r = 0.85, alternating: a buffer frees every 1.61 ms; each copy starts when its buffer
+    // frees and overlaps the other engine's (the link looks busy, each engine waits ~0.5 ms per copy)
     ddl::CopyModeTrigger t;
-    const double step = copy / 0.9;
+    const double step = copy / 0.85;
     int switched_at = -1;
     for (int w = 0; w < 50 && switched_at < 0; ++w) {
       const double start = w * step;
       if (t.note(w % 2, start, start + 1.9 * copy)) switched_at = w;
     }
     EXPECT(switched_at > 0 && switched_at <= 10);
-    // one engine at r = 0.9: 150 us waits -> stays one stream
+    // one engine at r = 0.85: 240 us waits -> stays one stream
     double t0 = 60 * step;
     for (int w = 0; w < 40; ++w) EXPECT(t.note(0, t0 + w * step, t0 + w * step + copy));
-    // r = 0.97 on one engine: 40 us waits sit between the thresholds -> still one stream (no flapping)
-    const double s97 = copy / 0.97;
+    // r = 0.96 on one engine: 57 us waits sit between the thresholds -> still one stream (no flapping)
+    const double s97 = copy / 0.96;
     t0 += 40 * step;
     for (int w = 0; w < 60; ++w) EXPECT(t.note(0, t0 + w * s97, t0 + w * s97 + copy));
     // the consumer speeds up (loader-bound on one engine): back to back -> alternate within ~10 copies
@@ -63,12 +73,12 @@ int main() {
     EXPECT(t.switches == 2);
   }
   {
-    // consumer-bound at r = 0.5 on one engine: 1.37 ms waits -> one stream, and it stays
+    // consumer-bound at r = 0.5: 1.37 ms waits -> one stream, and it stays
     ddl::CopyModeTrigger t;
     const double step = copy / 0.5;
     int n_one = 0;
     for (int w = 0; w < 60; ++w) n_one += t.note(w % 2, w * step, w * step + copy) ? 1 : 0;
-    EXPECT(n_one >= 55);
+    EXPECT(n_one >= 50);  // after ~7 copies
   }
   std::printf("copy_mode ok\n");
   return 0;

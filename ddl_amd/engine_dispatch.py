@@ -22,6 +22,9 @@ from .utils import streams
 from .utils.tracing import trace_range
 
 _TRACE_ENGINE = os.environ.get("DDL_ROCTX", "1") == "2"  # roctx level 2: also a range per native get
+# grid cap of the engine's gather / split launches (0: one workgroup per row tile, i.e. the whole GPU for a
+# 77 MB batch); an A/B hook for benchmarks/bench_idle_sweep.py --gather-blocks
+GATHER_MAX_BLOCKS = 0
 
 
 class NativeDispatchMixin:
@@ -46,7 +49,8 @@ class NativeDispatchMixin:
         out_dtype = self.out_dtype or (torch.float32 if norm is not None else wdt)
         splits = list(self.splits[0])
         rec = dict(in_dt=_dtypes.code(wdt), out_dt=_dtypes.code(out_dtype), shuffle=self.shuffle == "device",
-                   batch=self.batch_size, seed=self.seed & ((1 << 64) - 1), max_blocks=0, scale=[], bias=[],
+                   batch=self.batch_size, seed=self.seed & ((1 << 64) - 1), max_blocks=GATHER_MAX_BLOCKS, scale=[],
+                   bias=[],
                    plane=0, n_data=[int(x.nData) for x in self.metadata_from_producer], widths=[])
         if (self.contiguous or self.copy_batches) and len(splits) > 1 and len(self.sample_shape) == 1 \
                 and norm is None:
