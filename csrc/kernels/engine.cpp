@@ -292,6 +292,10 @@ int BatchEngine::launch(int64_t w, int64_t local, int64_t n_batches, const Stage
                ? pad_pack_tokens(sp, st)
                : (hipMemsetAsync(sp.cu_seqlens_out, 0, sizeof(int32_t), st) == hipSuccess ? 0 : -1);
     }
+  } else if (r_.kind == 3) {  // HWC image rows -> CHW, fused cast + per-channel affine (widths = {channels})
+    const int32_t c = r_.widths.empty() ? 1 : r_.widths[0];
+    rc = collate_hwc_to_chw(dst[0], r_.out_dt, src, r_.in_dt, n_batches * r_.batch, r_.row_elems / c, c, ri, r_.aff,
+                            st);
   } else if (r_.kind == 0) {
     // n_batches > 1: consecutive slots are contiguous for this kind (the caller enables whole-window mode
     // only when a slot is exactly one batch of output)

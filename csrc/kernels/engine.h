@@ -44,7 +44,8 @@
 namespace ddl {
 
 struct BatchRecipe {
-  int32_t kind = 0;       // 0: gather_rows (one output), 1: split_columns (n groups)
+  int32_t kind = 0;       // 0: gather_rows (one output), 1: split_columns (n groups), 2: token windows,
+                          // 3: HWC -> CHW image collate (widths = {channels}, row_elems = pixels x channels)
   int32_t in_dt = 0;      // window dtype code
   int32_t out_dt = 0;     // output dtype code
   int32_t shuffle = 0;    // 1: per-window-visit Feistel permutation of the rows

@@ -2,11 +2,12 @@
 
 The reference slices its batch out of the shared window on the host
 (``/root/reference/ddl/mpi_dataloader.py:179-198``). Here a batch is a gfx950 kernel launch over the
-staged HBM window (Feistel gather + cast / normalise, a contiguous column split, or a token pad/pack),
+staged HBM window (Feistel gather + cast / normalise, HWC -> CHW collate, a contiguous column split, or a
+token pad/pack),
 and the engine issues it from C++: inline on the caller's stream, one launch per window, or one batch
 ahead on the high-priority batch stream. The Python dispatch path (``native_dispatch=False``) builds the
-same batches with the same kernels; it serves the recipes the engine does not (augment, HWC collate,
-split views) and is the engine's test oracle.
+same batches with the same kernels; it serves the two recipes the engine does not (on-device augment, and
+zero-copy split views of the window) and is the engine's test oracle.
 """
 
 from __future__ import annotations
@@ -43,9 +44,9 @@ class NativeDispatchMixin:
         if self.collate is not None:
             return None
         norm = self.normalize
-        if norm is not None and norm.get("layout", "chw") == "hwc":
-            return None
         wdt = self.window_dtype
+        if norm is not None and norm.get("layout", "chw") == "hwc":
+            return self._hwc_recipe(norm, wdt)
         out_dtype = self.out_dtype or (torch.float32 if norm is not None else wdt)
         splits = list(self.splits[0])
         rec = dict(in_dt=_dtypes.code(wdt), out_dt=_dtypes.code(out_dtype), shuffle=self.shuffle == "device",
@@ -77,6 +78,23 @@ class NativeDispatchMixin:
         rec.update(kind=0, row_elems=int(math.prod(self.sample_shape)) if self.sample_shape else 1,
                    out_shapes=[(self.batch_size,) + tuple(self.sample_shape)], out_dtype=out_dtype)
         return rec
+
+    def _hwc_recipe(self, norm: dict, wdt) -> dict | None:
+        """HWC image rows ([H, W, C], e.g. decoded JPEGs) -> normalised CHW batches: the LDS-tiled collate kernel
+        (csrc/kernels/collate.hip) launched by the engine, like the gather."""
+        shape = tuple(self.sample_shape)
+        out_dtype = self.out_dtype or torch.float32
+        if (len(shape) < 2 or len(self.splits[0]) != 1 or out_dtype not in (torch.bfloat16, torch.float32)
+                or wdt not in (torch.uint8, torch.float32, torch.bfloat16)):
+            return None
+        c, pixels = int(shape[-1]), int(math.prod(shape[:-1]))
+        sc, bi = ops.norm_affine(c, norm.get("mean"), norm.get("std"), norm.get("scale"), norm.get("bias"),
+                                 ops.pixel_max(wdt))
+        return dict(kind=3, in_dt=_dtypes.code(wdt), out_dt=_dtypes.code(out_dtype), shuffle=self.shuffle == "device",
+                    batch=self.batch_size, seed=self.seed & ((1 << 64) - 1), max_blocks=0,
+                    scale=[float(x) for x in sc], bias=[float(x) for x in bi], plane=pixels,
+                    n_data=[int(x.nData) for x in self.metadata_from_producer], widths=[c],
+                    row_elems=c * pixels, out_shapes=[(self.batch_size, c) + shape[:-1]], out_dtype=out_dtype)
 
     def _token_recipe(self) -> dict | None:
         """Token windows (models/tokens.py): the pad/pack kernel straight from the staged window."""
@@ -135,7 +153,7 @@ class NativeDispatchMixin:
         # contiguous run per output where the kernel needs that (gather: no slot padding; split takes a slot
         # stride; token windows get one pad/pack launch with a grid row per sub-batch)
         whole_ok = (min(self.batches_per_window) > 1
-                    and (rec["kind"] != 0 or self._eng_slot_bytes == math.prod(self._eng_outputs[0][0])
+                    and (rec["kind"] not in (0, 3) or self._eng_slot_bytes == math.prod(self._eng_outputs[0][0])
                          * _dtypes.itemsize(self._eng_outputs[0][1])))
         if mode == "auto":
             # small batches are host-bound: inline (no batch events, ~3 us of C++ per batch), or one launch per

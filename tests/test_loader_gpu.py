@@ -277,7 +277,8 @@ def _collect(native, make, epochs=4, partial=None, **kw):
     return out, st
 
 
-@pytest.mark.parametrize("case", ["split_i32", "gather_cast_bf16", "images_u8_norm", "images_bf16_noshuffle_copy"])
+@pytest.mark.parametrize("case", ["split_i32", "gather_cast_bf16", "images_u8_norm", "images_bf16_noshuffle_copy",
+                                  "images_u8_hwc_norm"])
 def test_native_dispatch_matches_python_path(case):
     """The native batch engine (csrc/kernels/engine.cpp) delivers bit-identical batches to the Python
     dispatch path -- same Feistel order per window visit, same kernels -- including partial epochs
@@ -292,6 +293,10 @@ def test_native_dispatch_matches_python_path(case):
     elif case == "images_u8_norm":
         make = lambda: (ImageWindowProducer(32, (3, 16, 16), "uint8", seed=3), 8)  # noqa: E731
         kw = dict(kw, out_dtype=torch.bfloat16, normalize={"mean": [0.5, 0.4, 0.3], "std": [0.2, 0.25, 0.3]})
+    elif case == "images_u8_hwc_norm":  # decoded-JPEG layout: HWC uint8 -> normalised CHW bf16 (engine kind 3)
+        make = lambda: (ImageWindowProducer(32, (16, 16, 3), "uint8", seed=3), 8)  # noqa: E731
+        kw = dict(kw, out_dtype=torch.bfloat16,
+                  normalize={"mean": [0.5, 0.4, 0.3], "std": [0.2, 0.25, 0.3], "layout": "hwc"})
     else:
         make = lambda: (ImageWindowProducer(32, (3, 16, 16), "bfloat16", seed=3), 8)  # noqa: E731
         kw = dict(shuffle="none", copy_batches=True)
