@@ -8,3 +8,11 @@ run 200 bench_a python bench.py --steps 20 --warmup 5 --json-out gpurun_out/benc
 run 200 bench_b python bench.py --steps 20 --warmup 5 --json-out gpurun_out/bench_b.json
 export DDL_PRODUCER_MODE=thread
 run 300 trace_sweep rocprofv3 --kernel-trace --memory-copy-trace --marker-trace --output-format csv -d gpurun_out/trace -o sweep -- python3 benchmarks/bench_idle_sweep.py --step-ms 1.5,2.0 --steps 150 --feed-steps 100 --json-out gpurun_out/sweep_traced.jsonl
+unset DDL_PRODUCER_MODE
+S="python benchmarks/bench_idle_sweep.py --step-ms 1.5,1.7,2.0 --floor --steps 300 --feed-steps 200"
+for i in 1 2; do
+  run 200 g0_$i $S --json-out gpurun_out/g0_$i.jsonl
+  run 200 g32_$i $S --gather-blocks 32 --json-out gpurun_out/g32_$i.jsonl
+  run 200 g64_$i $S --gather-blocks 64 --json-out gpurun_out/g64_$i.jsonl
+  run 200 g128_$i $S --gather-blocks 128 --json-out gpurun_out/g128_$i.jsonl
+done
