@@ -86,8 +86,6 @@ def _parse(argv=None):
     ap.add_argument("--max-ahead", type=int, default=None, help="DistributedDataLoader(max_ahead=) (A/B; default 16)")
     ap.add_argument("--gather-blocks", type=int, default=0,
                     help="grid cap of the loader's batch gather (A/B; 0 = uncapped, the library default)")
-    ap.add_argument("--copy-policy", default=None, choices=["auto", "alternate"],
-                    help="copy-stream policy of the stager (A/B; default auto)")
     ap.add_argument("--batch-priority", default="high", choices=["high", "normal"],
                     help="priority of the loader's batch stream (A/B; the library uses high)")
     ap.add_argument("--json-out", default=None)
@@ -188,10 +186,6 @@ def main(argv=None) -> int:
         from ddl_amd import engine_dispatch as _ed
 
         _ed.GATHER_MAX_BLOCKS = a.gather_blocks
-    if a.copy_policy is not None:
-        from ddl_amd import staging as _staging
-
-        _staging.COPY_POLICY = a.copy_policy
     if a.batch_priority == "normal":  # A/B: the loader's batch stream at normal priority
         import ddl_amd.dataloader as _dl
         from ddl_amd.utils import streams as _streams

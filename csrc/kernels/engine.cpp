@@ -68,7 +68,8 @@ BatchEngine::BatchEngine(NativeStager* stager, BatchRecipe recipe, int32_t n_pro
       device_(device) {
   if (stager_ == nullptr || P_ < 1 || buffers_.empty() || ready_.size() != buffers_.size() ||
       static_cast<int32_t>(r_.n_data.size()) != P_ || r_.batch < 1 || (r_.kind == 1 && r_.widths.empty()) ||
-      r_.widths.size() > 8 || r_.kind < 0 || r_.kind > 2 || (r_.kind == 2 && r_.seq_len < 1))
+      r_.widths.size() > 8 || r_.kind < 0 || r_.kind > 3 || (r_.kind == 2 && r_.seq_len < 1) ||
+      (r_.kind == 3 && (r_.widths.size() != 1 || r_.widths[0] < 1 || r_.row_elems % r_.widths[0] != 0)))
     throw std::invalid_argument("BatchEngine: inconsistent arguments");
   if (hipSetDevice(device_) != hipSuccess) throw std::runtime_error("BatchEngine: hipSetDevice failed");
   batch_events_.resize(kBatchEvents);

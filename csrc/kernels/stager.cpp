@@ -27,7 +27,7 @@ NativeStager::NativeStager(const Arena* arena, int32_t n_producers, int32_t n_sl
                            std::vector<void*> buffers, uint64_t buffer_bytes, hipStream_t copy_stream, int device,
                            std::vector<int32_t> peer_pids, int64_t timeout_ms, std::vector<hipEvent_t> ready,
                            std::vector<hipEvent_t> copy_done, bool post_copy, int64_t meta_bytes,
-                           hipStream_t copy_stream2, int copy_policy)
+                           hipStream_t copy_stream2)
     : arena_(arena),
       P_(n_producers),
       n_slots_(n_slots),
@@ -37,7 +37,6 @@ NativeStager::NativeStager(const Arena* arena, int32_t n_producers, int32_t n_sl
       buffer_bytes_(buffer_bytes),
       copy_stream_(copy_stream),
       copy_stream2_(copy_stream2),
-      copy_policy_(copy_policy),
       device_(device),
       peer_pids_(std::move(peer_pids)),
       timeout_ms_(timeout_ms),
@@ -147,7 +146,6 @@ void NativeStager::retire_loop() {
       if (device_ms(start_ev_[r.ev], &t_start) && device_ms(retire_ev_[r.ev], &t_end)) {
         done_log_.push_back(DoneRec{r.window, r.bytes, t_start, t_end, r.stream});
         if (done_log_.size() > kCopyLog) done_log_.pop_front();
-        note_link_gap(r.stream, t_start, t_end);
       }
       retire_q_.pop_front();
       retired_upto_ = r.window + 1;
@@ -178,24 +176,6 @@ void NativeStager::fail(int code, int32_t producer, const std::string& msg) {
   }
   cv_.notify_all();
   retire_cv_.notify_all();
-}
-
-void NativeStager::note_link_gap(int stream, double t_start, double t_end) {
-  // retire thread, copies in window order (copy_mode.h: the per-engine wait-for-buffer gap)
-  const uint64_t before = copy_mode_.switches;
-  consumer_bound_.store(copy_mode_.note(stream, t_start, t_end), std::memory_order_relaxed);
-  if (copy_mode_.switches != before) policy_switches_ += 1;
-}
-
-int NativeStager::pick_copy_stream(int64_t w) const {
-  if (copy_stream2_ == nullptr) return 0;
-  if (copy_policy_ == 0) return static_cast<int>((w - first_) & 1);  // strict alternation
-  // auto: while the consumer is the bottleneck (copies wait for their ring buffers, note_link_gap) one stream,
-  // i.e. one SDMA engine: below the crossover two concurrent copies triple the step-boundary idle (one stream
-  // 0.52 / 0.70% vs alternating 1.15-1.64 / 2.29-2.45% at r = 0.75 / 0.9, three runs each,
-  // profiles/r4_fifth). Otherwise alternate, so two copies overlap and the engines never wait for one
-  // another (+1.8-2.5% feed, profiles/r2_copy_streams). Decided on the device clock.
-  return consumer_bound_.load(std::memory_order_relaxed) ? 0 : 1 - last_stream_;
 }
 
 void NativeStager::run() {
@@ -266,7 +246,12 @@ void NativeStager::run() {
     if (info.used_bytes > buffer_bytes_)
       return fail(-1, static_cast<int32_t>(p),
                   "window of " + std::to_string(info.used_bytes) + " B exceeds the staging buffer");
-    const int si = pick_copy_stream(w);  // as late as possible: the latest link-gap verdict
+    // two copy streams (two SDMA engines) strictly alternate: while one copy runs the next is already queued
+    // on the other engine, so the link never waits for a copy to end (+1.8-2.5% feed, profiles/r2_copy_streams).
+    // Switching to one engine while the consumer is the bottleneck was tried in round 4 (profiles/r4_fifth ..
+    // r4_tenth): -0.3-0.5 pp GPU idle near r = 0.9 at equal step time, but +0.06 pp behind a slow step and a
+    // trigger that either never fired or flapped and cost the link-bound feed 2-7%; alternation stays.
+    const int si = copy_stream2_ == nullptr ? 0 : 1 - last_stream_;
     hipStream_t cs = si == 0 ? copy_stream_ : copy_stream2_;
     // the consumer's kernels reading this ring buffer (window w - depth) finish first; a free event that
     // has already completed needs no device-side wait (no cross-stream dependency on the compute stream)

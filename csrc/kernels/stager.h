@@ -25,7 +25,6 @@
 // full interpreter switch interval (5 ms) by a Python-heavy training loop.
 #pragma once
 
-#include "copy_mode.h"
 
 #include <hip/hip_runtime.h>
 
@@ -80,7 +79,7 @@ class NativeStager {
                std::vector<void*> buffers, uint64_t buffer_bytes, hipStream_t copy_stream, int device,
                std::vector<int32_t> peer_pids, int64_t timeout_ms, std::vector<hipEvent_t> ready,
                std::vector<hipEvent_t> copy_done, bool post_copy, int64_t meta_bytes = 0,
-               hipStream_t copy_stream2 = nullptr, int copy_policy = 2);
+               hipStream_t copy_stream2 = nullptr);
   ~NativeStager();
 
   NativeStager(const NativeStager&) = delete;
@@ -121,8 +120,6 @@ class NativeStager {
   double wait_producer_s() const { return wait_producer_ns_.load() * 1e-9; }
   // free-event waits actually enqueued on a copy stream (the rest had completed and were skipped)
   uint64_t free_waits() const { return free_waits_.load(); }
-  bool consumer_bound() const { return consumer_bound_.load(std::memory_order_relaxed); }
-  uint64_t policy_switches() const { return policy_switches_.load(); }
   // per staged window (first 4096): ns spent in each step of the stager loop -- waiting for the ring
   // (consumer release), enqueueing the free-event wait, waiting for the producer, enqueueing the copy,
   // waiting for a retire-event slot + recording the events
@@ -179,16 +176,7 @@ class NativeStager {
   // optional second copy stream: windows alternate between the two, so the next window's copy is
   // already running on another SDMA engine when one finishes (no per-copy gap on the link)
   hipStream_t copy_stream2_;
-  // 0: windows strictly alternate between the two copy streams; 2 (default): auto, one stream while the
-  // consumer is the bottleneck (the link idles before copies), alternation otherwise (pick_copy_stream)
-  const int copy_policy_;
-  // auto copy policy (pick_copy_stream): one stream while copies wait for their ring buffers (copy_mode.h)
-  CopyModeTrigger copy_mode_;  // retire thread
-  std::atomic<bool> consumer_bound_{false};
-  std::atomic<uint64_t> policy_switches_{0};
   int last_stream_ = 1;
-  int pick_copy_stream(int64_t w) const;
-  void note_link_gap(int stream, double t_start, double t_end);  // retire thread
   const int device_;
   const std::vector<int32_t> peer_pids_;
   const int64_t timeout_ms_;

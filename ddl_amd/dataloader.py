@@ -247,8 +247,7 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
             raise ValueError("max_ahead must be >= 0")
         self.max_ahead = ma
         # one event per batch (a ring, reused): the host is released one batch per finished step, so the
-        # copies it unblocks follow the step smoothly instead of in bursts of several windows (the stager's
-        # auto copy policy reads the copies' waits for ring buffers, csrc/kernels/copy_mode.h)
+        # copies it unblocks follow the step smoothly instead of in bursts of several windows
         self._ahead_every = 1
         self._ahead_ring: list = []
         # (batch count, event on the consumer's stream)

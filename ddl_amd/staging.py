@@ -94,9 +94,6 @@ def warm_copy_engines(device: torch.device, n_engines: int = 4, nbytes: int = 51
     return time.perf_counter() - t0
 
 
-COPY_POLICY = "auto"  # the stager's default copy-stream policy ("alternate": strict alternation; tests A/B it)
-
-
 class WindowStager:
     """Python face of the native stager (``_ddl_hip.NativeStager``).
 
@@ -106,7 +103,7 @@ class WindowStager:
 
     def __init__(self, connection, n_slots: int, total_windows: int, depth: int, device: torch.device,
                  max_window_bytes: int, post_copy: Callable | None = None, timeout_s: float = 600.0,
-                 first_window: int = 0, meta_bytes: int = 0, copy_policy: str | None = None):
+                 first_window: int = 0, meta_bytes: int = 0):
         if depth < 1:
             raise ValueError("prefetch depth must be >= 1")
         hip, rt = _native.hip(), _native.runtime()
@@ -126,18 +123,11 @@ class WindowStager:
         # exchange) on a second stream, so window w's exchange overlaps window
         # w+1's DMA instead of idling the copy engine.
         self.copy_stream = torch.cuda.Stream(device=self.device)
-        # two copy streams (two SDMA engines): when copies run back to back the next one is already
-        # running when one finishes, so the ~25 us gap per copy on one engine is gone (+1.8-2.5%,
-        # profiles/r2_copy_streams, profiles/r3_copy_policy). copy_policy "auto" (default): alternate
-        # while the loader is the bottleneck, one stream while the consumer is (the link idles before copies,
-        # measured on the device clock; below the crossover one engine halves the step-boundary idle,
-        # profiles/r4_third); "alternate": strict alternation. DDL_COPY_STREAMS=1: one stream.
+        # two copy streams (two SDMA engines), strictly alternating: when copies run back to back the next one
+        # is already running when one finishes, so the ~25 us gap per copy on one engine is gone (+1.8-2.5%,
+        # profiles/r2_copy_streams). DDL_COPY_STREAMS=1: one stream. (Round 4 tried one engine while the
+        # consumer is the bottleneck and kept alternation: csrc/kernels/stager.cpp, profiles/r4_tenth.)
         n_cs = int(os.environ.get("DDL_COPY_STREAMS", "2"))
-        codes = {"alternate": 0, "auto": 2}
-        copy_policy = copy_policy or COPY_POLICY
-        if copy_policy not in codes:
-            raise ValueError(f"copy_policy must be one of {sorted(codes)}, not {copy_policy!r}")
-        policy = copy_policy
         self.copy_stream2 = torch.cuda.Stream(device=self.device) if n_cs >= 2 else None
         self.stream = torch.cuda.Stream(device=self.device) if post_copy is not None else self.copy_stream
         # The consumer posts window w+1's exchange when it enters window w (the fixed, rank-identical
@@ -163,9 +153,8 @@ class WindowStager:
             peer_pids=list(connection.producer_pids), timeout_ms=int(timeout_s * 1000),
             ready=[e.cuda_event for e in self.ready_events], copy_done=[e.cuda_event for e in self._copy_done],
             post_copy=post_copy is not None, meta_bytes=int(meta_bytes),
-            copy_stream2=self.copy_stream2.cuda_stream if self.copy_stream2 is not None else 0,
-            copy_policy=codes[policy])
-        self.copy_policy = policy if self.copy_stream2 is not None else "one stream"
+            copy_stream2=self.copy_stream2.cuda_stream if self.copy_stream2 is not None else 0)
+        self.copy_streams = 2 if self.copy_stream2 is not None else 1
         self.meta_bytes = int(meta_bytes)
 
     # -------------------------------------------------------------- consumer
@@ -303,11 +292,10 @@ class WindowStager:
 
     def copy_summary(self, e0: torch.cuda.Event, e1: torch.cuda.Event) -> dict:
         """How the window copies ran between two timing events: copies per stream, link busy % and the share
-        with two copies in flight, plus the auto policy's state (one stream now, switches so far)."""
+        with two copies in flight."""
         pro = self.bytes_in_interval(e0, e1)
         span = max(1e-9, pro.get("t1_ms", 0.0) - pro.get("t0_ms", 0.0))
-        out = {"copy_one_stream_now": bool(self._native.consumer_bound),
-               "copy_policy_switches": int(self._native.policy_switches)}
+        out: dict = {}
         if pro.get("ok"):
             out.update(copies_per_stream=list(pro["copies_per_stream"]),
                        link_busy_pct=round(100.0 * pro["busy_ms"] / span, 2),
@@ -332,7 +320,5 @@ class WindowStager:
         return {"bytes_h2d": self.bytes_h2d, "windows_staged": self.windows_staged,
                 "windows_landed": self.windows_landed, "bytes_landed": self.bytes_landed,
                 "stager_wait_producer_s": float(self._native.wait_producer_s),
-                "copy_policy": self.copy_policy, "free_waits_enqueued": int(self._native.free_waits),
-                "copy_one_stream_now": bool(self._native.consumer_bound),
-                "copy_policy_switches": int(self._native.policy_switches),
+                "copy_streams": self.copy_streams, "free_waits_enqueued": int(self._native.free_waits),
                 "exchange_issue_wait_s": round(self.post_wait_s, 6)}

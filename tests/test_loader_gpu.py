@@ -466,26 +466,23 @@ def test_stager_bytes_in_interval_is_pro_rata_and_additive():
         dl.close()
 
 
-@pytest.mark.parametrize("policy,streams", [("auto", "2"), ("alternate", "2"), ("auto", "1")])
-def test_copy_stream_policies_deliver_identical_batches(monkeypatch, policy, streams):
-    """The copy-stream policy only decides which SDMA stream each window copy runs on: every policy (and one
-    stream) delivers the same batches, bit for bit, including when the consumer is slow enough for `auto` to
-    switch to one stream (a sleep per batch makes the stager wait on the ring)."""
+@pytest.mark.parametrize("streams", ["2", "1"])
+def test_copy_streams_deliver_identical_batches(monkeypatch, streams):
+    """The copy streams only decide which SDMA engine each window copy runs on: two alternating streams and
+    one stream deliver the same batches, bit for bit, with a fast consumer and with a slow one (a sleep per
+    batch makes the stager wait on the ring)."""
     import time
 
     from ddl_amd.models.producers import ImageWindowProducer
 
-    def run(pol, n_cs, slow):
-        from ddl_amd import staging
-
-        monkeypatch.setattr(staging, "COPY_POLICY", pol)
+    def run(n_cs, slow):
         monkeypatch.setenv("DDL_COPY_STREAMS", n_cs)
         out = []
         with ddl_amd.start(n_producers=2) as (env, conn):
             dl = ddl_amd.DistributedDataLoader(ImageWindowProducer(32, (3, 16, 16), "bfloat16", seed=5), 8, conn, 6,
                                                env=env, device=torch.device("cuda"), out_dtype=torch.bfloat16,
                                                shuffle="device", seed=3, prefetch_depth=2)
-            assert dl.stats()["copy_policy"] == (pol if n_cs == "2" else "one stream")
+            assert dl.stats()["copy_streams"] == int(n_cs)
             for e in range(6):
                 for i in range(len(dl)):
                     (x,) = dl[i]
@@ -498,22 +495,10 @@ def test_copy_stream_policies_deliver_identical_batches(monkeypatch, policy, str
             dl.close()
         return torch.stack(out)
 
-    ref = run("alternate", "2", False)
+    ref = run("2", False)
     for slow in (False, True):
-        got = run(policy, streams, slow)
+        got = run(streams, slow)
         assert torch.equal(got, ref)
-
-
-def test_copy_policy_rejects_unknown(monkeypatch):
-    from ddl_amd.models.producers import ImageWindowProducer
-
-    from ddl_amd import staging
-
-    monkeypatch.setattr(staging, "COPY_POLICY", "adaptive")  # removed in round 4 (it serialised the copies)
-    with ddl_amd.start(n_producers=1) as (env, conn):
-        with pytest.raises(ValueError, match="copy_policy"):
-            ddl_amd.DistributedDataLoader(ImageWindowProducer(16, (3, 8, 8), "bfloat16"), 8, conn, 1, env=env,
-                                          device=torch.device("cuda"), out_dtype=torch.bfloat16)
 
 
 @pytest.mark.parametrize("mode", ["inline", "lookahead", "window"])
