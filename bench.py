@@ -257,7 +257,7 @@ def pressure_phase(args, env, dev, it, feed_per_rank: float, barrier, sync, dl=N
             retry = bool(t.item() > 0)
         if not retry:
             break
-        step.tune(busy)
+        step.correct(busy)
     out = {"ratio_target": r, "ratio_measured": round(cap / feed, 3), "steps": n, "attempts": attempts,
            "feed_samples_per_s": round(feed, 1), "phase1_feed_samples_per_s": round(feed_per_rank, 1),
            "step_ms": round(busy, 4), "gpu_idle_pct": res["gpu_idle_pct"],

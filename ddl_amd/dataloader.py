@@ -246,9 +246,9 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
         if ma < 0:
             raise ValueError("max_ahead must be >= 0")
         self.max_ahead = ma
-        # one event per batch (a ring, reused): the host is released one batch per finished step, so the
-        # copies it unblocks follow the step smoothly instead of in bursts of several windows
-        self._ahead_every = 1
+        # an event every max_ahead / 4 batches (one per batch raised the GPU idle behind a slow step from
+        # 0.12% to 0.17-0.18%: profiles/r4_eleventh); a small ring of them is reused
+        self._ahead_every = max(1, ma // 4)
         self._ahead_ring: list = []
         # (batch count, event on the consumer's stream)
         self._ahead_q = collections.deque() if self.device.type == "cuda" and ma > 0 else None
@@ -491,10 +491,11 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
                 self.ahead_waits += 1
                 ev.synchronize()
         if n % self._ahead_every == 0:
-            ring = self._ahead_ring
-            if len(ring) < self.max_ahead + 2:  # an event is re-recorded only after it left the queue
+            ring, k = self._ahead_ring, n // self._ahead_every
+            size = self.max_ahead // self._ahead_every + 2  # an event is re-recorded only after it left the queue
+            if len(ring) < size:
                 ring.append(torch.cuda.Event())
-            ev = ring[n % len(ring)] if len(ring) == self.max_ahead + 2 else ring[-1]
+            ev = ring[k % size] if len(ring) == size else ring[-1]
             ev.record(torch.cuda.current_stream(self.device))
             q.append((n, ev))
 

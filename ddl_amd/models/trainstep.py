@@ -179,7 +179,8 @@ class CalibratedStep:
 
     def _size(self, gemm_ms: float) -> None:
         m = self.a.shape[0]
-        work = max(0.0, self.step_ms - self.read_ms) / max(gemm_ms, 1e-6)  # in whole GEMMs
+        plan = getattr(self, "plan_ms", self.step_ms)
+        work = max(0.0, plan - self.read_ms) / max(gemm_ms, 1e-6)  # in whole GEMMs
         self.reps = int(work)
         self.tail_rows = min(m, int(round((work - self.reps) * m / 256)) * 256)
         if self.tail_rows == m:
@@ -190,6 +191,16 @@ class CalibratedStep:
         units = self.reps + self.tail_rows / self.a.shape[0]
         if units > 0 and busy_ms_per_step > self.read_ms:
             self.gemm_ms = (busy_ms_per_step - self.read_ms) / units
+            self._size(self.gemm_ms)
+        return self
+
+    def correct(self, busy_ms_per_step: float) -> "CalibratedStep":
+        """Multiplicative correction: the step measured ``busy_ms_per_step`` against its ``step_ms`` target, so
+        plan the chain for ``plan x target / measured`` (the GEMMs' time in the loop is not exactly linear in
+        their count -- the tail GEMM, clocks, the loader's traffic -- so re-sizing from a per-GEMM time alone
+        can settle off target)."""
+        if busy_ms_per_step > 0:
+            self.plan_ms = getattr(self, "plan_ms", self.step_ms) * self.step_ms / busy_ms_per_step
             self._size(self.gemm_ms)
         return self
 
