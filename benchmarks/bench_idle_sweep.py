@@ -84,6 +84,9 @@ def _parse(argv=None):
                     help="tokens: the consumer reads every tensor of the batch (all) or only input_ids (ids, as "
                          "bench_tokens.py's feed phase)")
     ap.add_argument("--max-ahead", type=int, default=None, help="DistributedDataLoader(max_ahead=) (A/B; default 16)")
+    ap.add_argument("--lead-diag", action="store_true",
+                    help="per step: how many enqueued steps the GPU had not finished when the host enqueued this one "
+                         "(0 = the host is late: the compute stream ran dry), and the host time of each fetch")
     ap.add_argument("--gather-blocks", type=int, default=0,
                     help="grid cap of the loader's batch gather (A/B; 0 = uncapped, the library default)")
     ap.add_argument("--batch-priority", default="high", choices=["high", "normal"],
@@ -285,12 +288,23 @@ def main(argv=None) -> int:
                 e0.record()
                 t2 = time.perf_counter()
                 with trace_range(f"sweep.p{i:02d}"):
-                    for _ in range(a.steps):
+                    leads, fetch_us = [], []
+                    for k in range(a.steps):
+                        tf = time.perf_counter()
                         if host_marks:  # --markers: the host's mark + get per step, for trace_gaps
                             with trace_range("sweep.get"):
                                 batch = next(it)
                         else:
                             batch = next(it)
+                        if a.lead_diag:
+                            fetch_us.append(1e6 * (time.perf_counter() - tf))
+                            # how many enqueued steps the GPU has not finished yet when this one is enqueued
+                            pairs, lead = meter._pairs, 0
+                            for j in range(len(pairs) - 1, max(-1, len(pairs) - 33), -1):
+                                if pairs[j][1].query():
+                                    break
+                                lead += 1
+                            leads.append(lead)
                         meter.step_begin()
                         step(batch)
                         meter.step_end()
@@ -312,6 +326,15 @@ def main(argv=None) -> int:
                       "allocator_segments_created": seg1 - seg0}
                 if getattr(dl, "_stager", None) is not None:
                     pt["copies"] = dl._stager.copy_summary(e0, e1)
+                if a.lead_diag and leads:
+                    import numpy as _np
+
+                    pt["host_lead_steps"] = {"p10": float(_np.percentile(leads, 10)), "p50": float(_np.median(leads)),
+                                             "p90": float(_np.percentile(leads, 90)),
+                                             "at_0": int(sum(1 for x in leads if x == 0))}
+                    pt["fetch_us"] = {"p50": round(float(_np.median(fetch_us)), 1),
+                                      "p90": round(float(_np.percentile(fetch_us, 90)), 1),
+                                      "max": round(max(fetch_us), 1)}
                 if a.floor:  # the same step on one held batch, no loader calls: the meter's own floor
                     fm = ComputeIdleMeter()
                     torch.cuda.synchronize()
