@@ -329,7 +329,8 @@ PYBIND11_MODULE(_ddl_hip, m) {
                        int64_t row_elems, uint64_t seed, std::vector<int64_t> n_data, std::vector<int32_t> widths,
                        std::vector<float> scale, std::vector<float> bias, int64_t plane, int64_t max_blocks,
                        int32_t n_producers, std::vector<uintptr_t> buffers, std::vector<uintptr_t> ready,
-                       uintptr_t batch_stream, int device, std::vector<int64_t> token) {
+                       uintptr_t batch_stream, int device, std::vector<int64_t> token, std::vector<double> augment,
+                       uint64_t aug_seed) {
              ddl::BatchRecipe r;
              r.kind = kind;
              r.in_dt = in_dt;
@@ -359,6 +360,22 @@ PYBIND11_MODULE(_ddl_hip, m) {
                if (r.token_bytes != 4 && r.token_bytes != 2)
                  throw std::invalid_argument("BatchEngine: tokens are 4 (int32) or 2 (uint16) bytes");
              }
+             if (kind == 4) {
+               if (augment.size() != 11)
+                 throw std::invalid_argument("BatchEngine: augment recipe needs 11 values");
+               r.aug_hwc = static_cast<int32_t>(augment[0]);
+               r.aug.in_h = static_cast<int32_t>(augment[1]);
+               r.aug.in_w = static_cast<int32_t>(augment[2]);
+               r.aug.channels = static_cast<int32_t>(augment[3]);
+               r.aug.out_h = static_cast<int32_t>(augment[4]);
+               r.aug.out_w = static_cast<int32_t>(augment[5]);
+               r.aug.scale_min = static_cast<float>(augment[6]);
+               r.aug.scale_max = static_cast<float>(augment[7]);
+               r.aug.ratio_min = static_cast<float>(augment[8]);
+               r.aug.ratio_max = static_cast<float>(augment[9]);
+               r.aug.flip_p = static_cast<float>(augment[10]);
+               r.aug_seed = aug_seed;
+             }
              std::vector<void*> bufs;
              for (auto b : buffers) bufs.push_back(as_ptr<void>(b));
              std::vector<hipEvent_t> rd;
@@ -370,9 +387,13 @@ PYBIND11_MODULE(_ddl_hip, m) {
            py::arg("batch"), py::arg("row_elems"), py::arg("seed"), py::arg("n_data"), py::arg("widths"),
            py::arg("scale"), py::arg("bias"), py::arg("plane"), py::arg("max_blocks"), py::arg("n_producers"),
            py::arg("buffers"), py::arg("ready"), py::arg("batch_stream"), py::arg("device"),
-           py::arg("token") = std::vector<int64_t>{}, py::keep_alive<1, 2>(),
+           py::arg("token") = std::vector<int64_t>{}, py::arg("augment") = std::vector<double>{},
+           py::arg("aug_seed") = 0, py::keep_alive<1, 2>(),
            "token = [mode (0 pad, 1 pack), pad_id, seq_len, byte offsets of offsets, row_start, row_end, "
            "seg_offsets, tokens] for kind 2")
+      .def("set_epoch_base", &ddl::BatchEngine::set_epoch_base, py::arg("window0"), py::arg("epoch0"),
+           py::arg("windows_per_epoch"),
+           "augment (kind 4): window window0 starts epoch epoch0; the crop seed of window w mixes in its epoch")
       .def(
           "provide",
           [](ddl::BatchEngine& e, const std::vector<std::vector<uintptr_t>>& slots) {

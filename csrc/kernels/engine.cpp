@@ -52,6 +52,9 @@ FeistelKeys host_feistel_keys(uint64_t seed, uint64_t key, uint64_t n) {
   return k;
 }
 
+// ddl_amd.dataloader._mix: splitmix64 finaliser over a * phi + b
+uint64_t mix2_host(uint64_t a, uint64_t b) { return mix64_host(a * 0x9E3779B97F4A7C15ull + b + 0x632BE59BD9B4E019ull); }
+
 uint64_t host_window_perm_key(uint64_t producer, uint64_t round) {
   const uint64_t z = producer * 0x9E3779B97F4A7C15ull + round + 0x632BE59BD9B4E019ull;
   return mix64_host(z) & ((1ull << 63) - 1);
@@ -68,7 +71,8 @@ BatchEngine::BatchEngine(NativeStager* stager, BatchRecipe recipe, int32_t n_pro
       device_(device) {
   if (stager_ == nullptr || P_ < 1 || buffers_.empty() || ready_.size() != buffers_.size() ||
       static_cast<int32_t>(r_.n_data.size()) != P_ || r_.batch < 1 || (r_.kind == 1 && r_.widths.empty()) ||
-      r_.widths.size() > 8 || r_.kind < 0 || r_.kind > 3 || (r_.kind == 2 && r_.seq_len < 1) ||
+      r_.widths.size() > 8 || r_.kind < 0 || r_.kind > 4 || (r_.kind == 2 && r_.seq_len < 1) ||
+      (r_.kind == 4 && (r_.aug.channels < 1 || r_.aug.out_h < 1 || r_.aug.out_w < 1 || r_.aug.in_h < 1)) ||
       (r_.kind == 3 && (r_.widths.size() != 1 || r_.widths[0] < 1 || r_.row_elems % r_.widths[0] != 0)))
     throw std::invalid_argument("BatchEngine: inconsistent arguments");
   if (hipSetDevice(device_) != hipSuccess) throw std::runtime_error("BatchEngine: hipSetDevice failed");
@@ -293,6 +297,16 @@ int BatchEngine::launch(int64_t w, int64_t local, int64_t n_batches, const Stage
                ? pad_pack_tokens(sp, st)
                : (hipMemsetAsync(sp.cu_seqlens_out, 0, sizeof(int32_t), st) == hipSuccess ? 0 : -1);
     }
+  } else if (r_.kind == 4) {  // RandomResizedCrop + flip + normalise + cast, crop boxes into output 1
+    if (n_batches != 1 || dst.size() < 2) return -1;
+    AugmentSpec a = r_.aug;
+    const int64_t epoch = r_.aug_e0 + (w - r_.aug_w0) / (r_.aug_wpe > 0 ? r_.aug_wpe : 1);
+    a.seed = mix2_host(r_.aug_seed, static_cast<uint64_t>(epoch));
+    a.sample_base = static_cast<int64_t>(mix2_host(static_cast<uint64_t>(info.producer), info.seq) &
+                                         ~0xFFFFFFFFull & ((1ull << 63) - 1));
+    a.sample_ids = nullptr;
+    rc = random_resized_crop(dst[0], r_.out_dt, src, r_.in_dt, r_.batch, a, r_.aug_hwc, ri, r_.aff,
+                             static_cast<int32_t*>(dst[1]), 0, st);
   } else if (r_.kind == 3) {  // HWC image rows -> CHW, fused cast + per-channel affine (widths = {channels})
     const int32_t c = r_.widths.empty() ? 1 : r_.widths[0];
     rc = collate_hwc_to_chw(dst[0], r_.out_dt, src, r_.in_dt, n_batches * r_.batch, r_.row_elems / c, c, ri, r_.aff,

@@ -45,7 +45,8 @@ namespace ddl {
 
 struct BatchRecipe {
   int32_t kind = 0;       // 0: gather_rows (one output), 1: split_columns (n groups), 2: token windows,
-                          // 3: HWC -> CHW image collate (widths = {channels}, row_elems = pixels x channels)
+                          // 3: HWC -> CHW image collate (widths = {channels}, row_elems = pixels x channels),
+                          // 4: RandomResizedCrop (augment)
   int32_t in_dt = 0;      // window dtype code
   int32_t out_dt = 0;     // output dtype code
   int32_t shuffle = 0;    // 1: per-window-visit Feistel permutation of the rows
@@ -66,6 +67,13 @@ struct BatchRecipe {
   int64_t header_stride = 0;  // bytes between the header blocks of consecutive sub-batches of a window
   int64_t token_fill_rows = 0;  // pack: fixed-shape batches of this many rows (0: exactly the packed rows)
   int64_t token_bytes = 4;      // 4: int32 tokens in the window, 2: uint16 (widened by the kernel)
+  // kind 4 (on-device RandomResizedCrop + flip + normalise + cast; outputs per slot: images, [batch, 5] int32
+  // crop boxes): the crop of a row is keyed by (seed mixed with the window's EPOCH, producer, producer round,
+  // source row) -- epoch(w) = aug_e0 + (w - aug_w0) / aug_wpe, set from the consumer's cursor
+  AugmentSpec aug{};
+  int32_t aug_hwc = 0;
+  uint64_t aug_seed = 0;
+  int64_t aug_w0 = 0, aug_e0 = 0, aug_wpe = 1;
 };
 
 class BatchEngine {
@@ -115,6 +123,11 @@ class BatchEngine {
   // one consumer step earlier, so the next window's copy is already enqueued when the lookahead looks
   // for it. release() then only drops the window's bookkeeping.
   void set_early_release(bool on) { early_ = on; }
+  void set_epoch_base(int64_t w0, int64_t e0, int64_t wpe) {
+    r_.aug_w0 = w0;
+    r_.aug_e0 = e0;
+    r_.aug_wpe = wpe > 0 ? wpe : 1;
+  }
   bool early_release() const { return early_; }
   // Batches per window of each producer's windows (lets the lookahead know that (w + 1, 0) is the last
   // batch of a one-batch window).

@@ -619,11 +619,14 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
         out_dtype = self.out_dtype or (torch.float32 if self.normalize is not None else wdt)
         if self.augment is not None:
             aug, norm = self.augment, self.normalize or {}
-            # crop randomness keyed by (seed, epoch) and the window row's identity (producer, round, row)
+            # crop randomness keyed by (seed, epoch OF THIS WINDOW) and the row's identity (producer, round, row);
+            # the window's epoch, not the cursor's: a lookahead batch of the next window is built a step early
+            w = sw.index if sw is not None else self.window
+            epoch = self.epoch + (w - (self.window - self.window_in_epoch)) // self.windows_per_epoch
             return (ops.random_resized_crop(
                 win, perm=perm, base=local * B, n_rows=B, size=aug.get("size", (224, 224)),
                 scale=aug.get("scale", (0.08, 1.0)), ratio=aug.get("ratio", (3.0 / 4.0, 4.0 / 3.0)),
-                flip_p=aug.get("flip_p", 0.5), seed=_mix(self.seed, self.epoch),
+                flip_p=aug.get("flip_p", 0.5), seed=_mix(self.seed, epoch),
                 sample_base=_mix(p, seq) & ~0xFFFFFFFF & ((1 << 63) - 1), layout=aug.get("layout", "chw"),
                 out_dtype=self.out_dtype or torch.bfloat16, mean=norm.get("mean"), std=norm.get("std")),)
         splits = list(self.splits[p])

@@ -37,10 +37,12 @@ class NativeDispatchMixin:
         augment. The global-shuffle exchange is compatible: it rewrites the staged window in place on the
         post-copy stream before the window's ready event, which is what the engine's launches wait on
         (``_ensure_posted`` issues it before the engine touches the window)."""
-        if not self.native_dispatch or self.augment is not None or self._batch_stream is None:
+        if not self.native_dispatch or self._batch_stream is None:
             return None
         if self.collate == "tokens":
             return self._token_recipe()
+        if self.augment is not None:
+            return self._augment_recipe()
         if self.collate is not None:
             return None
         norm = self.normalize
@@ -78,6 +80,32 @@ class NativeDispatchMixin:
         rec.update(kind=0, row_elems=int(math.prod(self.sample_shape)) if self.sample_shape else 1,
                    out_shapes=[(self.batch_size,) + tuple(self.sample_shape)], out_dtype=out_dtype)
         return rec
+
+    def _augment_recipe(self) -> dict | None:
+        """On-device RandomResizedCrop + flip + normalise + cast (csrc/kernels/augment.hip) launched by the engine.
+        Crops are keyed exactly as on the Python path: (seed mixed with the window's epoch, producer, producer
+        round, source row); the engine derives the epoch from the window index (``set_epoch_base``)."""
+        aug, norm = self.augment, self.normalize or {}
+        shape, wdt = tuple(self.sample_shape), self.window_dtype
+        layout = aug.get("layout", "chw")
+        out_dtype = self.out_dtype or torch.bfloat16
+        if (len(shape) != 3 or len(self.splits[0]) != 1 or out_dtype not in (torch.bfloat16, torch.float32)
+                or wdt not in (torch.uint8, torch.float32, torch.bfloat16)):
+            return None
+        c, h, w = (shape[2], shape[0], shape[1]) if layout == "hwc" else shape
+        oh, ow = aug.get("size", (224, 224))
+        sc, bi = ops.norm_affine(int(c), norm.get("mean"), norm.get("std"), None, None, ops.pixel_max(wdt))
+        scale, ratio = aug.get("scale", (0.08, 1.0)), aug.get("ratio", (3.0 / 4.0, 4.0 / 3.0))
+        return dict(kind=4, in_dt=_dtypes.code(wdt), out_dt=_dtypes.code(out_dtype), shuffle=self.shuffle == "device",
+                    batch=self.batch_size, seed=self.seed & ((1 << 64) - 1), max_blocks=0,
+                    scale=[float(x) for x in sc], bias=[float(x) for x in bi], plane=1,
+                    n_data=[int(x.nData) for x in self.metadata_from_producer], widths=[],
+                    row_elems=int(math.prod(shape)), aug_seed=self.seed & ((1 << 64) - 1),
+                    augment=[1.0 if layout == "hwc" else 0.0, float(h), float(w), float(c), float(oh), float(ow),
+                             float(scale[0]), float(scale[1]), float(ratio[0]), float(ratio[1]),
+                             float(aug.get("flip_p", 0.5))],
+                    outputs=[((self.batch_size, int(c), int(oh), int(ow)), out_dtype), ((self.batch_size, 5), torch.int32)],
+                    augment_outputs=True)
 
     def _hwc_recipe(self, norm: dict, wdt) -> dict | None:
         """HWC image rows ([H, W, C], e.g. decoded JPEGs) -> normalised CHW batches: the LDS-tiled collate kernel
@@ -136,10 +164,13 @@ class NativeDispatchMixin:
             dt = rec.pop("out_dtype")
             self._eng_outputs = [(sh, dt) for sh in rec.pop("out_shapes")]
         self._eng_tokens = rec.pop("token_mode", None)
+        self._eng_aug = rec.pop("augment_outputs", False)  # (images,) to the caller; the boxes stay in the slot
         self._engine = _native.hip().BatchEngine(
             st._native, n_producers=self.connection.n_producers, buffers=[b.data_ptr() for b in st.buffers],
             ready=[e.cuda_event for e in st.ready_events], batch_stream=self._batch_stream.cuda_stream,
             device=self.device.index, **rec)
+        if self._eng_aug:
+            self._engine.set_epoch_base(self.window - self.window_in_epoch, self.epoch, self.windows_per_epoch)
         # byte layout of one slot: every output 256-byte aligned, in order (a block holds K slots back to back)
         self._eng_layout, size = [], 0
         for sh, dt in self._eng_outputs:
@@ -152,7 +183,7 @@ class NativeDispatchMixin:
         # whole-window launches: every window holds >= 2 batches, and consecutive slots of a block are one
         # contiguous run per output where the kernel needs that (gather: no slot padding; split takes a slot
         # stride; token windows get one pad/pack launch with a grid row per sub-batch)
-        whole_ok = (min(self.batches_per_window) > 1
+        whole_ok = (min(self.batches_per_window) > 1 and rec["kind"] != 4  # augment: one launch per batch
                     and (rec["kind"] not in (0, 3) or self._eng_slot_bytes == math.prod(self._eng_outputs[0][0])
                          * _dtypes.itemsize(self._eng_outputs[0][1])))
         if mode == "auto":
@@ -300,7 +331,7 @@ class NativeDispatchMixin:
 
     def _engine_outputs(self, out, tags):
         if self._eng_tokens is None:
-            return out
+            return (out[0],) if self._eng_aug else out
         n_tokens, n_rows, n_seg, max_seg = tags
         if self._eng_tokens == "pad":
             return {"input_ids": out[0], "attention_mask": out[1], "position_ids": out[2], "n_tokens": n_tokens}

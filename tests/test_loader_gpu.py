@@ -278,7 +278,7 @@ def _collect(native, make, epochs=4, partial=None, **kw):
 
 
 @pytest.mark.parametrize("case", ["split_i32", "gather_cast_bf16", "images_u8_norm", "images_bf16_noshuffle_copy",
-                                  "images_u8_hwc_norm"])
+                                  "images_u8_hwc_norm", "images_u8_augment"])
 def test_native_dispatch_matches_python_path(case):
     """The native batch engine (csrc/kernels/engine.cpp) delivers bit-identical batches to the Python
     dispatch path -- same Feistel order per window visit, same kernels -- including partial epochs
@@ -293,6 +293,10 @@ def test_native_dispatch_matches_python_path(case):
     elif case == "images_u8_norm":
         make = lambda: (ImageWindowProducer(32, (3, 16, 16), "uint8", seed=3), 8)  # noqa: E731
         kw = dict(kw, out_dtype=torch.bfloat16, normalize={"mean": [0.5, 0.4, 0.3], "std": [0.2, 0.25, 0.3]})
+    elif case == "images_u8_augment":  # RandomResizedCrop + flip + normalise on the device (engine kind 4)
+        make = lambda: (ImageWindowProducer(32, (3, 20, 24), "uint8", seed=3), 8)  # noqa: E731
+        kw = dict(kw, out_dtype=torch.bfloat16, normalize={"mean": [0.5, 0.4, 0.3], "std": [0.2, 0.25, 0.3]},
+                  augment={"size": (16, 16), "scale": (0.3, 1.0), "flip_p": 0.5})
     elif case == "images_u8_hwc_norm":  # decoded-JPEG layout: HWC uint8 -> normalised CHW bf16 (engine kind 3)
         make = lambda: (ImageWindowProducer(32, (16, 16, 3), "uint8", seed=3), 8)  # noqa: E731
         kw = dict(kw, out_dtype=torch.bfloat16,
@@ -307,7 +311,8 @@ def test_native_dispatch_matches_python_path(case):
         nat, st = _collect(mode, make, partial=partial, **kw)
         # whole-window launches need contiguous slots: a gather whose batch is not a multiple of 256 bytes
         # (gather_cast_bf16: 32 B) falls back to inline
-        expect = "inline" if (mode == "window" and case == "gather_cast_bf16") else mode
+        # (augment: one launch per batch, never whole-window)
+        expect = "inline" if (mode == "window" and case in ("gather_cast_bf16", "images_u8_augment")) else mode
         assert st["native_dispatch"]["batches"] == len(nat) and st["native_dispatch"]["mode"] == expect
         assert len(nat) == len(ref) > 0
         for a, b in zip(nat, ref):
