@@ -102,7 +102,10 @@ BatchEngine::~BatchEngine() {
 
 void BatchEngine::provide(const std::vector<std::vector<void*>>& slots) {
   for (const auto& s : slots) {
-    const size_t need = r_.kind == 1 ? r_.widths.size() : r_.kind == 2 ? (r_.token_mode == 1 ? 5 : 3) : 1;
+    const size_t need = r_.kind == 1   ? r_.widths.size()
+                       : r_.kind == 2 ? (r_.token_mode == 1 ? 5 : 3)
+                       : r_.kind == 4 ? 2  // images + per-sample crop boxes
+                                      : 1;
     if (s.size() != need) throw std::invalid_argument("BatchEngine.provide: wrong number of outputs per slot");
     free_slots_.push_back(static_cast<int64_t>(slots_.size()));
     slots_.push_back(s);

@@ -104,7 +104,8 @@ class NativeDispatchMixin:
                     augment=[1.0 if layout == "hwc" else 0.0, float(h), float(w), float(c), float(oh), float(ow),
                              float(scale[0]), float(scale[1]), float(ratio[0]), float(ratio[1]),
                              float(aug.get("flip_p", 0.5))],
-                    outputs=[((self.batch_size, int(c), int(oh), int(ow)), out_dtype), ((self.batch_size, 5), torch.int32)],
+                    outputs=[((self.batch_size, int(c), int(oh), int(ow)), out_dtype),
+                             ((self.batch_size, 5), torch.int32)],
                     augment_outputs=True)
 
     def _hwc_recipe(self, norm: dict, wdt) -> dict | None:
