@@ -260,7 +260,7 @@ def pressure_phase(args, env, dev, it, feed_per_rank: float, barrier, sync, dl=N
         step.correct(busy)
     out = {"ratio_target": r, "ratio_measured": round(cap / feed, 3), "steps": n, "attempts": attempts,
            "feed_samples_per_s": round(feed, 1), "phase1_feed_samples_per_s": round(feed_per_rank, 1),
-           "step_ms": round(busy, 4), "gpu_idle_pct": res["gpu_idle_pct"],
+           "step_ms": round(busy, 4), "gpu_idle_pct": res["gpu_idle_pct"], "gaps_us": res.get("gaps_us"),
            "predicted_idle_pct": round(100.0 * max(0.0, 1.0 - feed / cap), 3),
            "achieved_samples_per_s": B * n * env.world_size / el}
     if stager is not None:  # how the window copies ran meanwhile (the auto policy's one-stream mode)

@@ -323,7 +323,7 @@ def main(argv=None) -> int:
                       "achieved_per_s": round(B * a.steps / (t3 - t2), 1),
                       "gpu_idle_pct": round(res["gpu_idle_pct"], 3), "predicted_idle_pct": round(pred, 3),
                       "error_pp": round(res["gpu_idle_pct"] - pred, 3),
-                      "allocator_segments_created": seg1 - seg0}
+                      "allocator_segments_created": seg1 - seg0, "gaps_us": res.get("gaps_us")}
                 if getattr(dl, "_stager", None) is not None:
                     pt["copies"] = dl._stager.copy_summary(e0, e1)
                 if a.lead_diag and leads:
@@ -344,7 +344,8 @@ def main(argv=None) -> int:
                             step(batch)
                             fm.step_end()
                         torch.cuda.synchronize()
-                    pt["floor_idle_pct"] = round(fm.result()["gpu_idle_pct"], 3)
+                    fr = fm.result()
+                    pt["floor_idle_pct"], pt["floor_gaps_us"] = round(fr["gpu_idle_pct"], 3), fr.get("gaps_us")
                     pt["error_vs_floor_pp"] = round(res["gpu_idle_pct"] - max(pred, pt["floor_idle_pct"]), 3)
                 if traffic is not None:  # the same floor loop, with the loader's copies running beside it
                     tm = ComputeIdleMeter()

@@ -126,4 +126,17 @@ class ComputeIdleMeter:
         busy = sum(s.elapsed_time(e) for s, e in self._pairs)
         wall = self._pairs[0][0].elapsed_time(self._pairs[-1][1])
         idle = 0.0 if wall <= 0 else max(0.0, 1.0 - busy / wall)
-        return {"gpu_idle_pct": 100.0 * idle, "busy_ms": busy, "wall_ms": wall, "steps": len(self._pairs)}
+        out = {"gpu_idle_pct": 100.0 * idle, "busy_ms": busy, "wall_ms": wall, "steps": len(self._pairs)}
+        if len(self._pairs) > 1:
+            # where the idle sits: many small gaps at every step boundary (device-side overhead) or a few
+            # long stalls (the feed running dry)
+            gaps = sorted(max(0.0, 1000.0 * a[1].elapsed_time(b[0])) for a, b in zip(self._pairs, self._pairs[1:]))
+            tot = sum(gaps)
+            top = gaps[-max(1, len(gaps) // 100):]
+
+            def pct(q: float) -> float:
+                return round(gaps[min(len(gaps) - 1, int(q * len(gaps)))], 1)
+
+            out["gaps_us"] = {"p50": pct(0.5), "p90": pct(0.9), "p99": pct(0.99), "max": round(gaps[-1], 1),
+                              "top1pct_share": round(sum(top) / tot, 3) if tot > 0 else 0.0}
+        return out

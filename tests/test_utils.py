@@ -307,3 +307,32 @@ def test_partition_after_spawn_leaves_the_consumer_process_alone():
     finally:
         child.kill()
         child.wait()
+
+
+def test_compute_idle_meter_gap_distribution():
+    """result() reports the idle and where it sits (per-boundary gaps), from the events' timestamps."""
+    from ddl_amd.utils.tracing import ComputeIdleMeter
+
+    class Ev:
+        def __init__(self, t_ms):
+            self.t = t_ms
+
+        def elapsed_time(self, other):
+            return other.t - self.t
+
+        def synchronize(self):
+            pass
+
+    m = ComputeIdleMeter.__new__(ComputeIdleMeter)
+    # 100 steps of 1 ms; 10 us gaps, except one 1 ms stall after step 50
+    t, pairs = 0.0, []
+    for i in range(100):
+        pairs.append((Ev(t), Ev(t + 1.0)))
+        t += 1.0 + (1.0 if i == 50 else 0.01)
+    m._pairs = pairs
+    r = m.result()
+    assert r["steps"] == 100 and abs(r["busy_ms"] - 100.0) < 1e-9
+    g = r["gaps_us"]
+    assert abs(g["p50"] - 10.0) < 0.1 and abs(g["max"] - 1000.0) < 0.1
+    assert abs(g["top1pct_share"] - 1000.0 / (1000.0 + 98 * 10.0)) < 1e-3
+    assert abs(r["gpu_idle_pct"] - 100.0 * (1.0 - 100.0 / (100.0 + 1.0 + 0.98))) < 1e-6
