@@ -87,6 +87,9 @@ def _parse(argv=None):
     ap.add_argument("--lead-diag", action="store_true",
                     help="per step: how many enqueued steps the GPU had not finished when the host enqueued this one "
                          "(0 = the host is late: the compute stream ran dry), and the host time of each fetch")
+    ap.add_argument("--ready-on-host", action="store_true",
+                    help="A/B: the host waits for each window's H2D copy before launching its batch kernels "
+                         "(no barrier packet on the batch queue)")
     ap.add_argument("--gather-blocks", type=int, default=0,
                     help="grid cap of the loader's batch gather (A/B; 0 = uncapped, the library default)")
     ap.add_argument("--batch-priority", default="high", choices=["high", "normal"],
@@ -185,10 +188,11 @@ def main(argv=None) -> int:
     from ddl_amd.utils.tracing import ComputeIdleMeter, trace_range
 
     ratios = [float(x) for x in a.ratios.split(",") if x]
-    if a.gather_blocks:
+    if a.gather_blocks or a.ready_on_host:
         from ddl_amd import engine_dispatch as _ed
 
         _ed.GATHER_MAX_BLOCKS = a.gather_blocks
+        _ed.READY_ON_HOST = a.ready_on_host
     if a.batch_priority == "normal":  # A/B: the loader's batch stream at normal priority
         import ddl_amd.dataloader as _dl
         from ddl_amd.utils import streams as _streams
@@ -367,7 +371,7 @@ def main(argv=None) -> int:
                 if nd1:  # per point: batches built ahead (lookahead hits), batches the compute stream waited for
                     pt["dispatch"] = {"mode": nd1.get("mode"),
                                       **{k: nd1.get(k, 0) - nd0.get(k, 0)
-                                         for k in ("batches", "lookahead_hits", "compute_waits")}}
+                                         for k in ("batches", "lookahead_hits", "compute_waits", "ready_host_waits")}}
                 points.append(pt)
                 print(json.dumps(pt), flush=True)
             stats = dl.stats()

@@ -268,7 +268,15 @@ int BatchEngine::launch(int64_t w, int64_t local, int64_t n_batches, const Stage
   const auto& dst = slots_[slot];
   const void* src = buffers_[info.buffer];
   uint64_t t0 = clock_ns();
-  if (ready_waited_ != w || ready_stream_ != st) {  // once per window and stream: its batches queue behind it
+  if (ready_host_) {  // the host waits for the copy (a no-op once it has retired)
+    const hipError_t q = hipEventQuery(ready_[info.buffer]);
+    if (q == hipErrorNotReady) {
+      if (hipEventSynchronize(ready_[info.buffer]) != hipSuccess) return -1;
+      ++ready_host_waits_;
+    } else if (q != hipSuccess) {
+      return -1;
+    }
+  } else if (ready_waited_ != w || ready_stream_ != st) {  // once per window and stream: its batches queue behind it
     if (hipStreamWaitEvent(st, ready_[info.buffer], 0) != hipSuccess) return -1;
     ready_waited_ = w;
     ready_stream_ = st;

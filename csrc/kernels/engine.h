@@ -139,6 +139,12 @@ class BatchEngine {
   // -- the usual case -- the host wait costs nothing.
   void set_host_handoff(bool on) { host_wait_ = on; }
   bool host_handoff() const { return host_wait_; }
+  // Dependency of a batch kernel on its window's H2D copy: false (default) makes the batch stream wait for
+  // the copy's ready event on the device; true makes the HOST wait for it before the launch, so the batch
+  // queue never holds a barrier packet on an unfinished copy.
+  void set_ready_on_host(bool on) { ready_host_ = on; }
+  bool ready_on_host() const { return ready_host_; }
+  uint64_t ready_host_waits() const { return ready_host_waits_; }  // launches whose copy the host waited for
 
   double wait_s() const { return wait_ns_ * 1e-9; }
   // host ns spent in get() in total, and inside HIP calls: kernel launches, event records, stream waits
@@ -214,6 +220,8 @@ class BatchEngine {
   int64_t bpw_of(const StagedInfo& info) const;
   bool early_ = true;
   bool host_wait_ = false;  // host hand-off of lookahead batches (set_host_handoff)
+  bool ready_host_ = false;  // host-side wait for a window's copy (set_ready_on_host)
+  uint64_t ready_host_waits_ = 0;
   std::vector<int64_t> bpw_;
   std::set<int64_t> handed_back_;  // windows whose buffer went back to the stager before release()
 };

@@ -849,6 +849,7 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
                 g, la, rec, sw = self._engine.timing_ns
                 n = max(1, int(self._engine.batches))
                 nd["compute_waits"] = int(self._engine.compute_waits)
+                nd["ready_host_waits"] = int(self._engine.ready_host_waits)
                 wait_ns = self._engine.wait_s * 1e9
                 nd["host_us_per_batch"] = {"get": round(g / n / 1e3, 2),
                                            "get_excl_staging_wait": round(max(0.0, g - wait_ns) / n / 1e3, 2),

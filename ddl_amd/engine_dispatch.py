@@ -26,6 +26,10 @@ _TRACE_ENGINE = os.environ.get("DDL_ROCTX", "1") == "2"  # roctx level 2: also a
 # grid cap of the engine's gather / split launches (0: one workgroup per row tile, i.e. the whole GPU for a
 # 77 MB batch); an A/B hook for benchmarks/bench_idle_sweep.py --gather-blocks
 GATHER_MAX_BLOCKS = 0
+# the host (not the batch stream) waits for a window's H2D copy before launching its batch kernels; an A/B
+# hook for benchmarks/bench_idle_sweep.py --ready-on-host (never with the exchange: the host must not wait
+# on peer ranks)
+READY_ON_HOST = False
 
 
 class NativeDispatchMixin:
@@ -210,6 +214,7 @@ class NativeDispatchMixin:
         # barrier on the compute stream, profiles/r3_handoff) unless the exchange is on -- its kernels wait
         # on peer ranks, and the host must never block on another rank's progress
         self._engine.host_handoff = self._exchange_fn is None
+        self._engine.ready_on_host = READY_ON_HOST and self._exchange_fn is None
         self._eng_mode = mode
         self._eng_slots: collections.deque = collections.deque()  # (slot id, outputs, block)
         self._eng_next_id = 0
