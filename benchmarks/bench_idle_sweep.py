@@ -90,6 +90,9 @@ def _parse(argv=None):
     ap.add_argument("--ready-on-host", action="store_true",
                     help="A/B: the host waits for each window's H2D copy before launching its batch kernels "
                          "(no barrier packet on the batch queue)")
+    ap.add_argument("--free-on-host", action="store_true",
+                    help="A/B: the stager thread waits for a ring buffer's free event on the host (no barrier "
+                         "packet on the copy stream)")
     ap.add_argument("--gather-blocks", type=int, default=0,
                     help="grid cap of the loader's batch gather (A/B; 0 = uncapped, the library default)")
     ap.add_argument("--batch-priority", default="high", choices=["high", "normal"],
@@ -193,6 +196,10 @@ def main(argv=None) -> int:
 
         _ed.GATHER_MAX_BLOCKS = a.gather_blocks
         _ed.READY_ON_HOST = a.ready_on_host
+    if a.free_on_host:
+        from ddl_amd import staging as _stg
+
+        _stg.FREE_ON_HOST = True
     if a.batch_priority == "normal":  # A/B: the loader's batch stream at normal priority
         import ddl_amd.dataloader as _dl
         from ddl_amd.utils import streams as _streams

@@ -256,7 +256,11 @@ void NativeStager::run() {
     // the consumer's kernels reading this ring buffer (window w - depth) finish first; a free event that
     // has already completed needs no device-side wait (no cross-stream dependency on the compute stream)
     if (free_ev != nullptr && hipEventQuery(free_ev) != hipSuccess) {
-      if (hipStreamWaitEvent(cs, free_ev, 0) != hipSuccess) return fail(-1, -1, "hipStreamWaitEvent(free) failed");
+      if (free_on_host_) {
+        if (hipEventSynchronize(free_ev) != hipSuccess) return fail(-1, -1, "hipEventSynchronize(free) failed");
+      } else if (hipStreamWaitEvent(cs, free_ev, 0) != hipSuccess) {
+        return fail(-1, -1, "hipStreamWaitEvent(free) failed");
+      }
       free_waits_ += 1;
     }
     last_stream_ = si;

@@ -120,6 +120,11 @@ class NativeStager {
   double wait_producer_s() const { return wait_producer_ns_.load() * 1e-9; }
   // free-event waits actually enqueued on a copy stream (the rest had completed and were skipped)
   uint64_t free_waits() const { return free_waits_.load(); }
+  // the stager thread waits for a pending free event on the host (true) instead of enqueueing the wait on
+  // the copy stream (false: a barrier packet that holds the copy stream's queue until the consumer's kernel
+  // has read the ring buffer). Set before start().
+  void set_free_on_host(bool on) { free_on_host_ = on; }
+  bool free_on_host() const { return free_on_host_; }
   // per staged window (first 4096): ns spent in each step of the stager loop -- waiting for the ring
   // (consumer release), enqueueing the free-event wait, waiting for the producer, enqueueing the copy,
   // waiting for a retire-event slot + recording the events
@@ -196,6 +201,7 @@ class NativeStager {
   std::string error_msg_;
   std::atomic<uint64_t> bytes_h2d_{0}, windows_staged_{0}, wait_producer_ns_{0};
   std::atomic<uint64_t> windows_landed_{0}, bytes_landed_{0}, free_waits_{0};
+  std::atomic<bool> free_on_host_{false};
   std::vector<std::vector<int64_t>> wait_log_;  // guarded by mu_
   struct CopyRec {
     int64_t window;

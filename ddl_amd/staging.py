@@ -44,6 +44,10 @@ from .exceptions import DDLError, DDLTimeoutError, NativeExtensionError, PeerDea
 from .utils import streams
 from .utils.tracing import trace_range
 
+# the stager thread waits for a ring buffer's free event on the host instead of enqueueing the wait on the copy
+# stream; an A/B hook for benchmarks/bench_idle_sweep.py --free-on-host
+FREE_ON_HOST = False
+
 
 @dataclasses.dataclass
 class StagedWindow:
@@ -154,6 +158,7 @@ class WindowStager:
             ready=[e.cuda_event for e in self.ready_events], copy_done=[e.cuda_event for e in self._copy_done],
             post_copy=post_copy is not None, meta_bytes=int(meta_bytes),
             copy_stream2=self.copy_stream2.cuda_stream if self.copy_stream2 is not None else 0)
+        self._native.free_on_host = FREE_ON_HOST
         self.copy_streams = 2 if self.copy_stream2 is not None else 1
         self.meta_bytes = int(meta_bytes)
 
@@ -321,4 +326,5 @@ class WindowStager:
                 "windows_landed": self.windows_landed, "bytes_landed": self.bytes_landed,
                 "stager_wait_producer_s": float(self._native.wait_producer_s),
                 "copy_streams": self.copy_streams, "free_waits_enqueued": int(self._native.free_waits),
+                "free_on_host": bool(self._native.free_on_host),
                 "exchange_issue_wait_s": round(self.post_wait_s, 6)}
