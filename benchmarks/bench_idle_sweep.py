@@ -87,12 +87,12 @@ def _parse(argv=None):
     ap.add_argument("--lead-diag", action="store_true",
                     help="per step: how many enqueued steps the GPU had not finished when the host enqueued this one "
                          "(0 = the host is late: the compute stream ran dry), and the host time of each fetch")
-    ap.add_argument("--ready-on-host", action="store_true",
-                    help="A/B: the host waits for each window's H2D copy before launching its batch kernels "
-                         "(no barrier packet on the batch queue)")
-    ap.add_argument("--free-on-host", action="store_true",
-                    help="A/B: the stager thread waits for a ring buffer's free event on the host (no barrier "
-                         "packet on the copy stream)")
+    ap.add_argument("--device-ready-wait", action="store_true",
+                    help="A/B: the batch stream waits for each window's H2D copy on the device (a barrier packet "
+                         "in its queue) instead of the host waiting before the launch")
+    ap.add_argument("--device-free-wait", action="store_true",
+                    help="A/B: the copy stream waits for a ring buffer's free event on the device instead of "
+                         "the stager thread waiting on the host")
     ap.add_argument("--gather-blocks", type=int, default=0,
                     help="grid cap of the loader's batch gather (A/B; 0 = uncapped, the library default)")
     ap.add_argument("--batch-priority", default="high", choices=["high", "normal"],
@@ -191,15 +191,15 @@ def main(argv=None) -> int:
     from ddl_amd.utils.tracing import ComputeIdleMeter, trace_range
 
     ratios = [float(x) for x in a.ratios.split(",") if x]
-    if a.gather_blocks or a.ready_on_host:
+    if a.gather_blocks or a.device_ready_wait:
         from ddl_amd import engine_dispatch as _ed
 
         _ed.GATHER_MAX_BLOCKS = a.gather_blocks
-        _ed.READY_ON_HOST = a.ready_on_host
-    if a.free_on_host:
+        _ed.READY_ON_HOST = not a.device_ready_wait
+    if a.device_free_wait:
         from ddl_amd import staging as _stg
 
-        _stg.FREE_ON_HOST = True
+        _stg.FREE_ON_HOST = False
     if a.batch_priority == "normal":  # A/B: the loader's batch stream at normal priority
         import ddl_amd.dataloader as _dl
         from ddl_amd.utils import streams as _streams

@@ -296,6 +296,7 @@ PYBIND11_MODULE(_ddl_hip, m) {
       .def_property_readonly("wait_producer_s", &ddl::NativeStager::wait_producer_s)
       .def_property_readonly("free_waits", &ddl::NativeStager::free_waits)
       .def_property("free_on_host", &ddl::NativeStager::free_on_host, &ddl::NativeStager::set_free_on_host)
+      .def_property("record_ready", &ddl::NativeStager::record_ready, &ddl::NativeStager::set_record_ready)
       .def("copies_between", &ddl::NativeStager::copies_between, py::arg("t0_ns"), py::arg("t1_ns"),
            "(windows, bytes) of H2D copies enqueued in [t0_ns, t1_ns] (CLOCK_MONOTONIC) that have retired")
       .def(

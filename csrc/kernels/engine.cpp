@@ -269,9 +269,10 @@ int BatchEngine::launch(int64_t w, int64_t local, int64_t n_batches, const Stage
   const void* src = buffers_[info.buffer];
   uint64_t t0 = clock_ns();
   if (ready_host_) {  // the host waits for the copy (a no-op once it has retired)
-    const hipError_t q = hipEventQuery(ready_[info.buffer]);
+    hipEvent_t ce = info.copy_event != nullptr ? info.copy_event : ready_[info.buffer];
+    const hipError_t q = hipEventQuery(ce);
     if (q == hipErrorNotReady) {
-      if (hipEventSynchronize(ready_[info.buffer]) != hipSuccess) return -1;
+      if (hipEventSynchronize(ce) != hipSuccess) return -1;
       ++ready_host_waits_;
     } else if (q != hipSuccess) {
       return -1;
@@ -472,8 +473,12 @@ int BatchEngine::release(int64_t w) {
           return -1;
       }
     }
-    if ((ready_waited_ != w || ready_stream_ != st) && hipStreamWaitEvent(st, ready_[b], 0) != hipSuccess)
+    if (ready_host_) {  // no batch read the window: its copy must still land before the buffer is reused
+      hipEvent_t ce = it->second.copy_event != nullptr ? it->second.copy_event : ready_[b];
+      if (hipEventSynchronize(ce) != hipSuccess) return -1;
+    } else if ((ready_waited_ != w || ready_stream_ != st) && hipStreamWaitEvent(st, ready_[b], 0) != hipSuccess) {
       return -1;
+    }
     ev = free_events_[b][free_next_[b]];
     free_next_[b] = (free_next_[b] + 1) % kFreeEvents;
     if (hipEventRecord(ev, st) != hipSuccess) return -1;

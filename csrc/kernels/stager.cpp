@@ -287,7 +287,8 @@ void NativeStager::run() {
       retire_q_.push_back(Retire{w, p, s, info.used_bytes, rev, si});
     }
     retire_cv_.notify_all();
-    if (hipEventRecord(post_copy_ ? copy_done_[b] : ready_[b], cs) != hipSuccess)
+    info.copy_event = retire_ev_[rev];
+    if ((post_copy_ || record_ready_) && hipEventRecord(post_copy_ ? copy_done_[b] : ready_[b], cs) != hipSuccess)
       return fail(-1, static_cast<int32_t>(p), "hipEventRecord failed");
     info.t_ready_host = mono_s();
     bytes_h2d_ += info.used_bytes;

@@ -52,6 +52,9 @@ struct StagedInfo {
   uint64_t used_bytes = 0;
   int64_t tag[4] = {0, 0, 0, 0};
   double t_ready_host = 0.0;  // CLOCK_MONOTONIC seconds when the copy was enqueued
+  // the copy's retire event (recorded right behind it; valid until the window is released): what a consumer
+  // that waits for the copy on the host waits on
+  hipEvent_t copy_event = nullptr;
   // the first meta_bytes of the window, copied on the host at staging time (before the slot goes back
   // to its producer): per-batch metadata of multi-batch windows (e.g. token counts per sub-batch)
   std::vector<int64_t> meta;
@@ -125,6 +128,11 @@ class NativeStager {
   // has read the ring buffer). Set before start().
   void set_free_on_host(bool on) { free_on_host_ = on; }
   bool free_on_host() const { return free_on_host_; }
+  // record the per-buffer ready event behind each copy (false: only the retire event is recorded, for a
+  // consumer that waits for copies on the host through StagedInfo::copy_event -- one marker per copy
+  // instead of two in the copy stream's queue). Needs depth < kRetireEvents; ignored with a post-copy stage.
+  void set_record_ready(bool on) { record_ready_ = on || depth_ >= kRetireEvents; }
+  bool record_ready() const { return record_ready_; }
   // per staged window (first 4096): ns spent in each step of the stager loop -- waiting for the ring
   // (consumer release), enqueueing the free-event wait, waiting for the producer, enqueueing the copy,
   // waiting for a retire-event slot + recording the events
@@ -201,7 +209,7 @@ class NativeStager {
   std::string error_msg_;
   std::atomic<uint64_t> bytes_h2d_{0}, windows_staged_{0}, wait_producer_ns_{0};
   std::atomic<uint64_t> windows_landed_{0}, bytes_landed_{0}, free_waits_{0};
-  std::atomic<bool> free_on_host_{false};
+  std::atomic<bool> free_on_host_{false}, record_ready_{true};
   std::vector<std::vector<int64_t>> wait_log_;  // guarded by mu_
   struct CopyRec {
     int64_t window;

@@ -26,10 +26,11 @@ _TRACE_ENGINE = os.environ.get("DDL_ROCTX", "1") == "2"  # roctx level 2: also a
 # grid cap of the engine's gather / split launches (0: one workgroup per row tile, i.e. the whole GPU for a
 # 77 MB batch); an A/B hook for benchmarks/bench_idle_sweep.py --gather-blocks
 GATHER_MAX_BLOCKS = 0
-# the host (not the batch stream) waits for a window's H2D copy before launching its batch kernels; an A/B
-# hook for benchmarks/bench_idle_sweep.py --ready-on-host (never with the exchange: the host must not wait
-# on peer ranks)
-READY_ON_HOST = False
+# the host (not the batch stream) waits for a window's H2D copy before launching its batch kernels, so no
+# queue holds a barrier packet on an unfinished copy: GPU idle below the crossover 2.4-2.5% -> 1.1% at
+# r = 0.9 (profiles/r4_sixteenth, r4_seventeenth). Never with the exchange (the host must not wait on peer
+# ranks). False is the A/B hook of benchmarks/bench_idle_sweep.py --device-ready-wait.
+READY_ON_HOST = True
 
 
 class NativeDispatchMixin:
@@ -215,6 +216,8 @@ class NativeDispatchMixin:
         # on peer ranks, and the host must never block on another rank's progress
         self._engine.host_handoff = self._exchange_fn is None
         self._engine.ready_on_host = READY_ON_HOST and self._exchange_fn is None
+        # then the copy's retire event is the only marker behind it in the copy stream's queue
+        self._stager._native.record_ready = not self._engine.ready_on_host
         self._eng_mode = mode
         self._eng_slots: collections.deque = collections.deque()  # (slot id, outputs, block)
         self._eng_next_id = 0

@@ -45,8 +45,9 @@ from .utils import streams
 from .utils.tracing import trace_range
 
 # the stager thread waits for a ring buffer's free event on the host instead of enqueueing the wait on the copy
-# stream; an A/B hook for benchmarks/bench_idle_sweep.py --free-on-host
-FREE_ON_HOST = False
+# stream (a barrier packet in its queue): GPU idle near r = 1 1.4-1.6% -> 0.9-1.0% (profiles/r4_seventeenth).
+# False is the A/B hook of benchmarks/bench_idle_sweep.py --device-free-wait.
+FREE_ON_HOST = True
 
 
 @dataclasses.dataclass
