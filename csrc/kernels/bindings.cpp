@@ -240,7 +240,8 @@ PYBIND11_MODULE(_ddl_hip, m) {
       .def(py::init([](uintptr_t arena, int32_t n_producers, int32_t n_slots, int64_t first, int64_t total,
                        std::vector<uintptr_t> buffers, uint64_t buffer_bytes, uintptr_t copy_stream, int device,
                        std::vector<int32_t> peer_pids, int64_t timeout_ms, std::vector<uintptr_t> ready,
-                       std::vector<uintptr_t> copy_done, bool post_copy, int64_t meta_bytes, uintptr_t copy_stream2) {
+                       std::vector<uintptr_t> copy_done, bool post_copy, int64_t meta_bytes, uintptr_t copy_stream2,
+                       bool direct_dma) {
              std::vector<void*> bufs;
              for (auto b : buffers) bufs.push_back(as_ptr<void>(b));
              std::vector<hipEvent_t> rd, cd;
@@ -249,12 +250,13 @@ PYBIND11_MODULE(_ddl_hip, m) {
              return std::make_unique<ddl::NativeStager>(
                  reinterpret_cast<const ddl::Arena*>(arena), n_producers, n_slots, first, total, std::move(bufs),
                  buffer_bytes, as_stream(copy_stream), device, std::move(peer_pids), timeout_ms, std::move(rd),
-                 std::move(cd), post_copy, meta_bytes, as_stream(copy_stream2));
+                 std::move(cd), post_copy, meta_bytes, as_stream(copy_stream2), direct_dma);
            }),
            py::arg("arena"), py::arg("n_producers"), py::arg("n_slots"), py::arg("first"), py::arg("total"),
            py::arg("buffers"), py::arg("buffer_bytes"), py::arg("copy_stream"), py::arg("device"),
            py::arg("peer_pids"), py::arg("timeout_ms"), py::arg("ready"), py::arg("copy_done"),
-           py::arg("post_copy"), py::arg("meta_bytes") = 0, py::arg("copy_stream2") = 0)
+           py::arg("post_copy"), py::arg("meta_bytes") = 0, py::arg("copy_stream2") = 0,
+           py::arg("direct_dma") = false)
       .def(
           "wait",
           [](ddl::NativeStager& st, int64_t w, int64_t timeout_ms) {
@@ -297,6 +299,10 @@ PYBIND11_MODULE(_ddl_hip, m) {
       .def_property_readonly("free_waits", &ddl::NativeStager::free_waits)
       .def_property("free_on_host", &ddl::NativeStager::free_on_host, &ddl::NativeStager::set_free_on_host)
       .def_property("record_ready", &ddl::NativeStager::record_ready, &ddl::NativeStager::set_record_ready)
+      .def_property_readonly("direct_dma", &ddl::NativeStager::direct_dma)
+      .def_property_readonly("direct_dma_reason", &ddl::NativeStager::direct_dma_reason)
+      .def("wait_copy", &ddl::NativeStager::wait_copy_window, py::arg("window"),
+           py::call_guard<py::gil_scoped_release>(), "host wait for staged window w's copy (direct-DMA mode)")
       .def("copies_between", &ddl::NativeStager::copies_between, py::arg("t0_ns"), py::arg("t1_ns"),
            "(windows, bytes) of H2D copies enqueued in [t0_ns, t1_ns] (CLOCK_MONOTONIC) that have retired")
       .def(

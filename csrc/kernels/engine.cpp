@@ -268,15 +268,16 @@ int BatchEngine::launch(int64_t w, int64_t local, int64_t n_batches, const Stage
   const auto& dst = slots_[slot];
   const void* src = buffers_[info.buffer];
   uint64_t t0 = clock_ns();
-  if (ready_host_) {  // the host waits for the copy (a no-op once it has retired)
-    hipEvent_t ce = info.copy_event != nullptr ? info.copy_event : ready_[info.buffer];
-    const hipError_t q = hipEventQuery(ce);
-    if (q == hipErrorNotReady) {
-      if (hipEventSynchronize(ce) != hipSuccess) return -1;
+  if (ready_host_) {  // the host waits for the copy (a no-op once it has landed)
+    const int q = NativeStager::copy_landed(info);
+    if (q == 0) {
+      if (NativeStager::wait_copy(info) != 0) return -1;
       ++ready_host_waits_;
-    } else if (q != hipSuccess) {
+    } else if (q < 0 && hipEventSynchronize(ready_[info.buffer]) != hipSuccess) {
       return -1;
     }
+  } else if (info.copy_signal != 0) {
+    return -1;  // a direct-DMA copy has no device-side event: the host must wait (ready_on_host)
   } else if (ready_waited_ != w || ready_stream_ != st) {  // once per window and stream: its batches queue behind it
     if (hipStreamWaitEvent(st, ready_[info.buffer], 0) != hipSuccess) return -1;
     ready_waited_ = w;
@@ -473,9 +474,11 @@ int BatchEngine::release(int64_t w) {
           return -1;
       }
     }
-    if (ready_host_) {  // no batch read the window: its copy must still land before the buffer is reused
-      hipEvent_t ce = it->second.copy_event != nullptr ? it->second.copy_event : ready_[b];
-      if (hipEventSynchronize(ce) != hipSuccess) return -1;
+    if (ready_host_ || it->second.copy_signal != 0) {
+      // no batch read the window: its copy must still land before the buffer is reused
+      const int q = NativeStager::copy_landed(it->second);
+      if (q == 0 && NativeStager::wait_copy(it->second) != 0) return -1;
+      if (q < 0 && hipEventSynchronize(ready_[b]) != hipSuccess) return -1;
     } else if ((ready_waited_ != w || ready_stream_ != st) && hipStreamWaitEvent(st, ready_[b], 0) != hipSuccess) {
       return -1;
     }

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <chrono>
 #include <climits>
+#include <cstdio>
 #include <set>
 
 namespace ddl {
@@ -27,7 +28,7 @@ NativeStager::NativeStager(const Arena* arena, int32_t n_producers, int32_t n_sl
                            std::vector<void*> buffers, uint64_t buffer_bytes, hipStream_t copy_stream, int device,
                            std::vector<int32_t> peer_pids, int64_t timeout_ms, std::vector<hipEvent_t> ready,
                            std::vector<hipEvent_t> copy_done, bool post_copy, int64_t meta_bytes,
-                           hipStream_t copy_stream2)
+                           hipStream_t copy_stream2, bool direct_dma)
     : arena_(arena),
       P_(n_producers),
       n_slots_(n_slots),
@@ -65,20 +66,26 @@ NativeStager::NativeStager(const Arena* arena, int32_t n_producers, int32_t n_sl
     throw std::runtime_error("NativeStager: epoch event failed");
   if (hipStreamCreateWithFlags(&anchor_stream_, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&anchor_ev_[0], hipEventBlockingSync) != hipSuccess ||
-      hipEventCreateWithFlags(&anchor_ev_[1], hipEventBlockingSync) != hipSuccess ||
-      hipEventRecord(anchor_ev_[0], anchor_stream_) != hipSuccess || hipEventSynchronize(anchor_ev_[0]) != hipSuccess)
+      hipEventCreateWithFlags(&anchor_ev_[1], hipEventBlockingSync) != hipSuccess)
     throw std::runtime_error("NativeStager: anchor event failed");
   {
-    float a0 = 0.f;
-    if (hipEventElapsedTime(&a0, epoch_ev_, anchor_ev_[0]) != hipSuccess)
-      throw std::runtime_error("NativeStager: anchor event failed");
-    anchor_ms_[0] = anchor_ms_[1] = a0;
-    // until the first re-anchor both slots name the construction-time anchor
-    if (hipEventRecord(anchor_ev_[1], anchor_stream_) != hipSuccess || hipEventSynchronize(anchor_ev_[1]) != hipSuccess ||
-        hipEventElapsedTime(&a0, epoch_ev_, anchor_ev_[1]) != hipSuccess)
-      throw std::runtime_error("NativeStager: anchor event failed");
-    anchor_ms_[1] = a0;
+    uint64_t f = 0;
+    if (hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &f) == HSA_STATUS_SUCCESS && f > 0)
+      sys_freq_ = static_cast<double>(f);
+    // two anchors a few us apart; the second is the current one until the first re-anchor
+    for (int k = 0; k < 2; ++k) {
+      float a = 0.f;
+      if (!record_anchor(k, &anchor_sys_[k]) || hipEventElapsedTime(&a, epoch_ev_, anchor_ev_[k]) != hipSuccess)
+        throw std::runtime_error("NativeStager: anchor event failed");
+      anchor_ms_[k] = a;
+    }
     anchor_cur_ = 1;
+  }
+  if (direct_dma) {
+    if (post_copy_)
+      direct_reason_ = "a post-copy stage (the exchange) waits for copies on the device";
+    else
+      direct_ = init_direct(copy_stream2_ != nullptr ? 2 : 1);
   }
   thread_ = std::thread([this] { run(); });
   retire_thread_ = std::thread([this] { retire_loop(); });
@@ -92,6 +99,161 @@ NativeStager::~NativeStager() {
   for (auto e : anchor_ev_)
     if (e != nullptr) hipEventDestroy(e);
   if (anchor_stream_ != nullptr) hipStreamDestroy(anchor_stream_);
+  for (auto sg : copy_sig_) hsa_signal_destroy(sg);
+}
+
+bool NativeStager::init_direct(int n_engines) {
+  // the HSA agent of HIP device `device_` (matched by PCI location: HIP_VISIBLE_DEVICES renumbers HIP devices
+  // only), and the CPU agent nearest to it as the source agent
+  char bus[64] = {0};
+  unsigned dom = 0, b = 0, d = 0, f = 0;
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus), device_) != hipSuccess ||
+      std::sscanf(bus, "%x:%x:%x.%x", &dom, &b, &d, &f) != 4) {
+    direct_reason_ = "no PCI location for the device";
+    return false;
+  }
+  struct Find {
+    uint32_t dom, bdf;
+    hsa_agent_t gpu, cpu;
+    bool have_gpu, have_cpu;
+  } fd{dom, (b << 8) | (d << 3) | f, {}, {}, false, false};
+  hsa_iterate_agents(
+      [](hsa_agent_t a, void* data) -> hsa_status_t {
+        auto* fd = static_cast<Find*>(data);
+        hsa_device_type_t t;
+        if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+        if (t == HSA_DEVICE_TYPE_CPU && !fd->have_cpu) {
+          fd->cpu = a;
+          fd->have_cpu = true;
+        } else if (t == HSA_DEVICE_TYPE_GPU && !fd->have_gpu) {
+          uint32_t bdf = 0, dm = 0;
+          if (hsa_agent_get_info(a, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_BDFID), &bdf) == HSA_STATUS_SUCCESS &&
+              hsa_agent_get_info(a, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_DOMAIN), &dm) == HSA_STATUS_SUCCESS &&
+              bdf == fd->bdf && dm == fd->dom) {
+            fd->gpu = a;
+            fd->have_gpu = true;
+          }
+        }
+        return HSA_STATUS_SUCCESS;
+      },
+      &fd);
+  if (!fd.have_gpu || !fd.have_cpu) {
+    direct_reason_ = std::string("no HSA agent for ") + bus;
+    return false;
+  }
+  gpu_agent_ = fd.gpu;
+  cpu_agent_ = fd.cpu;
+  hsa_agent_t near{};
+  if (hsa_agent_get_info(gpu_agent_, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_NEAREST_CPU), &near) ==
+          HSA_STATUS_SUCCESS &&
+      near.handle != 0)
+    cpu_agent_ = near;
+  // the arena is locked for the GPU (hipHostRegister): its GPU-side address range
+  const char* probe = reinterpret_cast<const char*>(arena_->slot_data(0, 0));
+  hsa_amd_pointer_info_t pi{};
+  pi.size = sizeof(pi);
+  if (hsa_amd_pointer_info(probe, &pi, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
+      (pi.type != HSA_EXT_POINTER_TYPE_LOCKED && pi.type != HSA_EXT_POINTER_TYPE_HSA) ||
+      pi.agentBaseAddress == nullptr || pi.sizeInBytes == 0) {
+    direct_reason_ = "the arena is not locked for the GPU";
+    return false;
+  }
+  arena_agent_base_ = static_cast<const char*>(pi.agentBaseAddress);
+  arena_host_base_ = pi.hostBaseAddress != nullptr ? static_cast<const char*>(pi.hostBaseAddress) : arena_agent_base_;
+  arena_span_ = pi.sizeInBytes;
+  // SDMA engines for host -> this GPU: the idle ones first, else the runtime's recommendation
+  uint32_t mask = 0;
+  if (hsa_amd_memory_copy_engine_status(gpu_agent_, cpu_agent_, &mask) != HSA_STATUS_SUCCESS || mask == 0) {
+    mask = 0;
+    if (hsa_amd_memory_get_preferred_copy_engine(gpu_agent_, cpu_agent_, &mask) != HSA_STATUS_SUCCESS) mask = 0;
+  }
+  int got = 0;
+  for (uint32_t bit = 1; bit != 0 && got < n_engines; bit <<= 1)
+    if (mask & bit) dma_engine_[got++] = bit;
+  if (got == 0) {
+    direct_reason_ = "no SDMA engine available for host -> device copies";
+    return false;
+  }
+  if (got == 1) dma_engine_[1] = dma_engine_[0];
+  if (hsa_amd_profiling_async_copy_enable(true) != HSA_STATUS_SUCCESS) {
+    direct_reason_ = "async-copy profiling unavailable";
+    return false;
+  }
+  copy_sig_.resize(kRetireEvents);
+  for (auto& sg : copy_sig_)
+    if (hsa_signal_create(0, 0, nullptr, &sg) != HSA_STATUS_SUCCESS) {
+      direct_reason_ = "hsa_signal_create failed";
+      return false;
+    }
+  // bring each engine up now (its first copy in a process stalls ~10 ms), not on the first window
+  const size_t n = static_cast<size_t>(std::min<uint64_t>(4096, buffer_bytes_));
+  for (int k = 0; k < (dma_engine_[1] != dma_engine_[0] ? 2 : 1); ++k) {
+    hsa_signal_store_screlease(copy_sig_[0], 1);
+    if (hsa_amd_memory_async_copy_on_engine(buffers_[0], gpu_agent_, arena_agent_base_ + (probe - arena_host_base_),
+                                            cpu_agent_, n, 0, nullptr, copy_sig_[0],
+                                            static_cast<hsa_amd_sdma_engine_id_t>(dma_engine_[k]),
+                                            false) != HSA_STATUS_SUCCESS) {
+      hsa_signal_store_screlease(copy_sig_[0], 0);
+      direct_reason_ = "hsa_amd_memory_async_copy_on_engine failed";
+      return false;
+    }
+    while (hsa_signal_wait_scacquire(copy_sig_[0], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED) >= 1) {
+    }
+  }
+  return true;
+}
+
+bool NativeStager::record_anchor(int slot, uint64_t* sys_tick) {
+  // record on the idle anchor stream and SPIN until it completes, bracketed by the HSA system clock: the
+  // completion lies inside [t0, t1]; retry (the last record counts) until the bracket is under 50 us
+  for (int k = 0; k < 4; ++k) {
+    uint64_t t0 = 0, t1 = 0;
+    hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP, &t0);
+    if (hipEventRecord(anchor_ev_[slot], anchor_stream_) != hipSuccess) return false;
+    hipError_t q;
+    while ((q = hipEventQuery(anchor_ev_[slot])) == hipErrorNotReady) {
+    }
+    if (q != hipSuccess) return false;
+    hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP, &t1);
+    *sys_tick = t0 + (t1 - t0) / 2;
+    if (static_cast<double>(t1 - t0) < 50e-6 * sys_freq_) break;
+  }
+  return true;
+}
+
+double NativeStager::sys_ms(uint64_t tick, int a) const {
+  return anchor_ms_[a] + 1e3 * static_cast<double>(static_cast<int64_t>(tick - anchor_sys_[a])) / sys_freq_;
+}
+
+bool NativeStager::retired_now(int ev) const {
+  if (direct_) return hsa_signal_load_scacquire(copy_sig_[ev]) < 1;
+  return hipEventQuery(retire_ev_[ev]) == hipSuccess;
+}
+
+int NativeStager::copy_landed(const StagedInfo& info) {
+  if (info.copy_signal != 0) return hsa_signal_load_scacquire(hsa_signal_t{info.copy_signal}) < 1 ? 1 : 0;
+  if (info.copy_event != nullptr) {
+    const hipError_t q = hipEventQuery(info.copy_event);
+    return q == hipSuccess ? 1 : q == hipErrorNotReady ? 0 : -1;
+  }
+  return -1;
+}
+
+int NativeStager::wait_copy(const StagedInfo& info) {
+  if (info.copy_signal != 0) {
+    const hsa_signal_t sg{info.copy_signal};
+    while (hsa_signal_wait_scacquire(sg, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED) >= 1) {
+    }
+    return 0;
+  }
+  if (info.copy_event != nullptr) return hipEventSynchronize(info.copy_event) == hipSuccess ? 0 : -1;
+  return -1;
+}
+
+int NativeStager::wait_copy_window(int64_t w) {
+  StagedInfo info;
+  if (!peek(w, &info)) return 0;
+  return wait_copy(info);
 }
 
 bool NativeStager::device_ms(hipEvent_t e, double* out) const {
@@ -114,10 +276,11 @@ void NativeStager::reanchor() {
   std::lock_guard<std::mutex> lk(mu_);
   const int nxt = anchor_cur_ ^ 1;
   float d = 0.f;
-  if (hipEventRecord(anchor_ev_[nxt], anchor_stream_) != hipSuccess || hipEventSynchronize(anchor_ev_[nxt]) != hipSuccess ||
-      hipEventElapsedTime(&d, anchor_ev_[anchor_cur_], anchor_ev_[nxt]) != hipSuccess)
+  uint64_t sys = 0;
+  if (!record_anchor(nxt, &sys) || hipEventElapsedTime(&d, anchor_ev_[anchor_cur_], anchor_ev_[nxt]) != hipSuccess)
     return;  // keep the current anchor (times stay correct, only coarser)
   anchor_ms_[nxt] = anchor_ms_[anchor_cur_] + d;
+  anchor_sys_[nxt] = sys;
   anchor_cur_ = nxt;
 }
 
@@ -131,8 +294,13 @@ void NativeStager::retire_loop() {
       if (retire_q_.empty()) return;  // stopped and drained
       r = retire_q_.front();
     }
-    if (hipEventSynchronize(retire_ev_[r.ev]) != hipSuccess) return fail(-1, static_cast<int32_t>(r.producer),
-                                                                         "hipEventSynchronize(retire) failed");
+    if (direct_) {
+      while (hsa_signal_wait_scacquire(copy_sig_[r.ev], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
+                                       HSA_WAIT_STATE_BLOCKED) >= 1) {
+      }
+    } else if (hipEventSynchronize(retire_ev_[r.ev]) != hipSuccess) {
+      return fail(-1, static_cast<int32_t>(r.producer), "hipEventSynchronize(retire) failed");
+    }
     bytes_landed_.fetch_add(r.bytes, std::memory_order_relaxed);
     windows_landed_.fetch_add(1, std::memory_order_release);
     arena_->set_state(r.producer, r.slot, kEmpty);  // slot back to its producer (release store + futex wake)
@@ -143,7 +311,19 @@ void NativeStager::retire_loop() {
     {
       std::lock_guard<std::mutex> lk(mu_);
       double t_start = 0.0, t_end = 0.0;  // ms since construction, GPU clock
-      if (device_ms(start_ev_[r.ev], &t_start) && device_ms(retire_ev_[r.ev], &t_end)) {
+      bool timed = false;
+      if (direct_) {
+        hsa_amd_profiling_async_copy_time_t t{};
+        if (r.bytes > 0 && hsa_amd_profiling_get_async_copy_time(copy_sig_[r.ev], &t) == HSA_STATUS_SUCCESS &&
+            t.end >= t.start && t.start != 0) {
+          t_start = sys_ms(t.start, anchor_cur_);
+          t_end = sys_ms(t.end, anchor_cur_);
+          timed = true;
+        }
+      } else {
+        timed = device_ms(start_ev_[r.ev], &t_start) && device_ms(retire_ev_[r.ev], &t_end);
+      }
+      if (timed) {
         done_log_.push_back(DoneRec{r.window, r.bytes, t_start, t_end, r.stream});
         if (done_log_.size() > kCopyLog) done_log_.pop_front();
       }
@@ -159,7 +339,7 @@ void NativeStager::settle(int64_t timeout_ms) {
   std::unique_lock<std::mutex> lk(mu_);
   while (!retire_q_.empty() && error_code_ == 0 && !stop_) {
     const int64_t front = retire_q_.front().window;
-    if (hipEventQuery(retire_ev_[retire_q_.front().ev]) != hipSuccess) return;  // still in flight: not landed
+    if (!retired_now(retire_q_.front().ev)) return;  // still in flight: not landed
     if (!retire_cv_.wait_until(lk, deadline, [&] {
           return stop_ || error_code_ != 0 || retire_q_.empty() || retire_q_.front().window != front;
         }))
@@ -256,7 +436,7 @@ void NativeStager::run() {
     // the consumer's kernels reading this ring buffer (window w - depth) finish first; a free event that
     // has already completed needs no device-side wait (no cross-stream dependency on the compute stream)
     if (free_ev != nullptr && hipEventQuery(free_ev) != hipSuccess) {
-      if (free_on_host_) {
+      if (free_on_host_ || direct_) {
         if (hipEventSynchronize(free_ev) != hipSuccess) return fail(-1, -1, "hipEventSynchronize(free) failed");
       } else if (hipStreamWaitEvent(cs, free_ev, 0) != hipSuccess) {
         return fail(-1, -1, "hipStreamWaitEvent(free) failed");
@@ -272,23 +452,46 @@ void NativeStager::run() {
       retire_cv_.wait(lk, [&] { return stop_ || error_code_ != 0 || w - kRetireEvents < retired_upto_; });
       if (stop_ || error_code_ != 0) return;
     }
-    if (hipEventRecord(start_ev_[rev], cs) != hipSuccess)  // the stream reaches the copy: it can start
+    if (!direct_ && hipEventRecord(start_ev_[rev], cs) != hipSuccess)  // the stream reaches the copy: it can start
       return fail(-1, static_cast<int32_t>(p), "hipEventRecord(start) failed");
     const uint64_t enq_ns = now_ns();  // before the call: the copy cannot start earlier
-    if (info.used_bytes > 0 &&
-        hipMemcpyAsync(buffers_[b], arena_->slot_data(p, s), info.used_bytes, hipMemcpyHostToDevice, cs) !=
-            hipSuccess)
+    if (direct_) {
+      // straight onto SDMA engine `si`: no AQL packet anywhere waits for this copy
+      const hsa_signal_t sg = copy_sig_[rev];
+      hsa_signal_store_screlease(sg, 1);
+      info.copy_signal = sg.handle;
+      if (info.used_bytes > 0) {
+        const char* src = reinterpret_cast<const char*>(arena_->slot_data(p, s));
+        if (src < arena_host_base_ || src + info.used_bytes > arena_host_base_ + arena_span_) {
+          hsa_signal_store_screlease(sg, 0);
+          return fail(-1, static_cast<int32_t>(p), "slot outside the GPU-locked arena range");
+        }
+        if (hsa_amd_memory_async_copy_on_engine(buffers_[b], gpu_agent_, arena_agent_base_ + (src - arena_host_base_),
+                                                cpu_agent_, info.used_bytes, 0, nullptr, sg,
+                                                static_cast<hsa_amd_sdma_engine_id_t>(dma_engine_[si]),
+                                                false) != HSA_STATUS_SUCCESS) {
+          hsa_signal_store_screlease(sg, 0);
+          return fail(-1, static_cast<int32_t>(p), "hsa_amd_memory_async_copy_on_engine H2D failed");
+        }
+      } else {
+        hsa_signal_store_screlease(sg, 0);
+      }
+    } else if (info.used_bytes > 0 &&
+               hipMemcpyAsync(buffers_[b], arena_->slot_data(p, s), info.used_bytes, hipMemcpyHostToDevice, cs) !=
+                   hipSuccess) {
       return fail(-1, static_cast<int32_t>(p), "hipMemcpyAsync H2D failed");
+    }
     const int64_t s4 = ns();
-    if (hipEventRecord(retire_ev_[rev], cs) != hipSuccess)
+    if (!direct_ && hipEventRecord(retire_ev_[rev], cs) != hipSuccess)
       return fail(-1, static_cast<int32_t>(p), "hipEventRecord(retire) failed");
     {
       std::lock_guard<std::mutex> lk(mu_);
       retire_q_.push_back(Retire{w, p, s, info.used_bytes, rev, si});
     }
     retire_cv_.notify_all();
-    info.copy_event = retire_ev_[rev];
-    if ((post_copy_ || record_ready_) && hipEventRecord(post_copy_ ? copy_done_[b] : ready_[b], cs) != hipSuccess)
+    if (!direct_) info.copy_event = retire_ev_[rev];
+    if (!direct_ && (post_copy_ || record_ready_) &&
+        hipEventRecord(post_copy_ ? copy_done_[b] : ready_[b], cs) != hipSuccess)
       return fail(-1, static_cast<int32_t>(p), "hipEventRecord failed");
     info.t_ready_host = mono_s();
     bytes_h2d_ += info.used_bytes;
@@ -360,7 +563,7 @@ std::pair<uint64_t, uint64_t> NativeStager::copies_between(uint64_t t0_ns, uint6
   std::lock_guard<std::mutex> lk(mu_);
   std::set<int64_t> done;
   for (const Retire& r : retire_q_)
-    if (hipEventQuery(retire_ev_[r.ev]) == hipSuccess) done.insert(r.window);
+    if (retired_now(r.ev)) done.insert(r.window);
   uint64_t n = 0, bytes = 0;
   for (const CopyRec& c : copy_log_) {
     if (c.enq_ns >= t0_ns && c.enq_ns <= t1_ns && (c.window < retired_upto_ || done.count(c.window) != 0)) {

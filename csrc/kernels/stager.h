@@ -27,6 +27,8 @@
 
 
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 
 #include <atomic>
 #include <condition_variable>
@@ -55,6 +57,8 @@ struct StagedInfo {
   // the copy's retire event (recorded right behind it; valid until the window is released): what a consumer
   // that waits for the copy on the host waits on
   hipEvent_t copy_event = nullptr;
+  // direct-DMA mode: the copy's HSA completion signal (handle; 0 in stream mode)
+  uint64_t copy_signal = 0;
   // the first meta_bytes of the window, copied on the host at staging time (before the slot goes back
   // to its producer): per-batch metadata of multi-batch windows (e.g. token counts per sub-batch)
   std::vector<int64_t> meta;
@@ -82,7 +86,7 @@ class NativeStager {
                std::vector<void*> buffers, uint64_t buffer_bytes, hipStream_t copy_stream, int device,
                std::vector<int32_t> peer_pids, int64_t timeout_ms, std::vector<hipEvent_t> ready,
                std::vector<hipEvent_t> copy_done, bool post_copy, int64_t meta_bytes = 0,
-               hipStream_t copy_stream2 = nullptr);
+               hipStream_t copy_stream2 = nullptr, bool direct_dma = false);
   ~NativeStager();
 
   NativeStager(const NativeStager&) = delete;
@@ -133,6 +137,20 @@ class NativeStager {
   // instead of two in the copy stream's queue). Needs depth < kRetireEvents; ignored with a post-copy stage.
   void set_record_ready(bool on) { record_ready_ = on || depth_ >= kRetireEvents; }
   bool record_ready() const { return record_ready_; }
+  // Direct-DMA mode (asked for with direct_dma, granted unless a post-copy stage is set or the HSA setup fails:
+  // direct_dma_reason() says why): window copies go straight to SDMA engines through ROCr
+  // (hsa_amd_memory_async_copy_on_engine, one HSA completion signal per copy) instead of through HIP copy
+  // streams. No AQL queue then holds a packet that waits on a copy: every consumer of a window waits for its
+  // copy on the HOST (copy_landed / wait_copy; the engine's ready_on_host), and the free-event wait is always
+  // on the host. Copy times come from ROCr's async-copy profiling, mapped onto the anchor events' clock.
+  bool direct_dma() const { return direct_; }
+  std::string direct_dma_reason() const { return direct_reason_; }
+  // 1: the window's copy has landed; 0: in flight; -1: no handle in `info` (or a HIP error)
+  static int copy_landed(const StagedInfo& info);
+  // host wait for the window's copy (0 ok, -1 no handle / error)
+  static int wait_copy(const StagedInfo& info);
+  // wait_copy for staged window w (0 also when w is not staged: nothing to wait for)
+  int wait_copy_window(int64_t w);
   // per staged window (first 4096): ns spent in each step of the stager loop -- waiting for the ring
   // (consumer release), enqueueing the free-event wait, waiting for the producer, enqueueing the copy,
   // waiting for a retire-event slot + recording the events
@@ -210,6 +228,21 @@ class NativeStager {
   std::atomic<uint64_t> bytes_h2d_{0}, windows_staged_{0}, wait_producer_ns_{0};
   std::atomic<uint64_t> windows_landed_{0}, bytes_landed_{0}, free_waits_{0};
   std::atomic<bool> free_on_host_{false}, record_ready_{true};
+  // direct-DMA state (set in the constructor, read-only afterwards)
+  bool direct_ = false;
+  std::string direct_reason_;
+  hsa_agent_t gpu_agent_{}, cpu_agent_{};
+  uint32_t dma_engine_[2] = {0, 0};
+  std::vector<hsa_signal_t> copy_sig_;  // kRetireEvents, like the retire events
+  const char* arena_host_base_ = nullptr;
+  const char* arena_agent_base_ = nullptr;
+  size_t arena_span_ = 0;
+  double sys_freq_ = 1e9;              // HSA system timestamp ticks per second
+  uint64_t anchor_sys_[2] = {0, 0};    // each anchor event's completion on the HSA system clock (guarded by mu_)
+  bool init_direct(int n_engines);     // constructor; false + direct_reason_ when not possible
+  bool record_anchor(int slot, uint64_t* sys_tick);  // record + spin-wait an anchor; its HSA system time
+  bool retired_now(int ev) const;      // copy `ev` has completed (event or signal)
+  double sys_ms(uint64_t tick, int anchor) const;  // HSA system tick -> ms on the anchors' clock (mu_ held)
   std::vector<std::vector<int64_t>> wait_log_;  // guarded by mu_
   struct CopyRec {
     int64_t window;

@@ -138,7 +138,7 @@ def build_hip(force: bool = False, jobs: int = 8) -> str:
             list(ex.map(lambda j: _run(j[0]), jobs_list))
     if force or jobs_list or _newer(out, objs):
         cmd = [hipcc, "-shared", "-fPIC", *objs, "-o", out + ".tmp", f"-L{torch_lib}", f"-Wl,-rpath,{torch_lib}",
-               "-l:libamdhip64.so", "-lpthread", "-lrt"]
+               "-l:libamdhip64.so", "-l:libhsa-runtime64.so", "-lpthread", "-lrt"]
         _run(cmd)
         os.replace(out + ".tmp", out)
     return out

@@ -556,7 +556,7 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
     def _enqueue_batch(self, sw, p: int, s: int, local: int):
         """Build batch ``local`` of window ``sw`` on the batch stream; returns (outputs, ready event)."""
         bs = self._batch_stream
-        bs.wait_event(self._stager.ready_events[sw.buffer])
+        self._stager.wait_ready(sw, bs)
         with streams.on_stream(bs):
             out = self._batch_from_window(sw, p, s, local)
             ev = torch.cuda.Event()
@@ -712,7 +712,7 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
                 if sw is not None and sw.index == self.window:
                     # a window no batch was built from (skipped at a partial epoch end) can still have
                     # its exchange running on the post-copy stream: the free event must follow it too
-                    stream.wait_event(self._stager.ready_events[sw.buffer])
+                    self._stager.wait_ready(sw, stream)
             self._stager.release(self.window, stream)
             self._cur = None
         elif self._host_window == self.window:

@@ -215,7 +215,8 @@ class NativeDispatchMixin:
         # barrier on the compute stream, profiles/r3_handoff) unless the exchange is on -- its kernels wait
         # on peer ranks, and the host must never block on another rank's progress
         self._engine.host_handoff = self._exchange_fn is None
-        self._engine.ready_on_host = READY_ON_HOST and self._exchange_fn is None
+        # (a direct-DMA copy has no device-side event at all: then the host always waits)
+        self._engine.ready_on_host = (READY_ON_HOST or self._stager.direct_dma) and self._exchange_fn is None
         # then the copy's retire event is the only marker behind it in the copy stream's queue
         self._stager._native.record_ready = not self._engine.ready_on_host
         self._eng_mode = mode

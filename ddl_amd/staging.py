@@ -42,12 +42,16 @@ import torch
 from . import _native
 from .exceptions import DDLError, DDLTimeoutError, NativeExtensionError, PeerDeathError, ShutdownError
 from .utils import streams
+from .utils.logging import logger
 from .utils.tracing import trace_range
 
 # the stager thread waits for a ring buffer's free event on the host instead of enqueueing the wait on the copy
 # stream (a barrier packet in its queue): GPU idle near r = 1 1.4-1.6% -> 0.9-1.0% (profiles/r4_seventeenth).
 # False is the A/B hook of benchmarks/bench_idle_sweep.py --device-free-wait.
 FREE_ON_HOST = True
+# window copies go straight to SDMA engines through ROCr (NativeStager direct-DMA mode) instead of HIP copy
+# streams, so no AQL queue holds a packet waiting on a copy; an A/B hook for bench_idle_sweep.py --direct-dma
+DIRECT_DMA = False
 
 
 @dataclasses.dataclass
@@ -158,7 +162,11 @@ class WindowStager:
             peer_pids=list(connection.producer_pids), timeout_ms=int(timeout_s * 1000),
             ready=[e.cuda_event for e in self.ready_events], copy_done=[e.cuda_event for e in self._copy_done],
             post_copy=post_copy is not None, meta_bytes=int(meta_bytes),
-            copy_stream2=self.copy_stream2.cuda_stream if self.copy_stream2 is not None else 0)
+            copy_stream2=self.copy_stream2.cuda_stream if self.copy_stream2 is not None else 0,
+            direct_dma=bool(DIRECT_DMA and post_copy is None))
+        self.direct_dma = bool(self._native.direct_dma)
+        if DIRECT_DMA and post_copy is None and not self.direct_dma:
+            logger.info("direct-DMA staging unavailable (%s): HIP copy streams", self._native.direct_dma_reason)
         self._native.free_on_host = FREE_ON_HOST
         self.copy_streams = 2 if self.copy_stream2 is not None else 1
         self.meta_bytes = int(meta_bytes)
@@ -180,8 +188,18 @@ class WindowStager:
         if self.post_copy is not None:
             self._post(w)  # normally already posted by post() at the previous window's hand-back
         sw = self._wait_staged(w)
-        streams.current(self.device.index).wait_event(self.ready_events[sw.buffer])
+        self.wait_ready(sw, streams.current(self.device.index))
         return sw
+
+    def wait_ready(self, sw: StagedWindow, stream) -> None:
+        """Order ``stream`` after window ``sw``'s copy: a device-side event wait, or in direct-DMA mode (no HIP
+        event behind the copy) a host wait for the copy's completion signal."""
+        if self.direct_dma:
+            rc = self._native.wait_copy(sw.index)
+            if rc != 0:
+                raise DDLError(f"window {sw.index}: waiting for its copy failed ({self._native.error()})")
+        else:
+            stream.wait_event(self.ready_events[sw.buffer])
 
     def peek(self, w: int) -> StagedWindow | None:
         """Window ``w`` if it is already staged AND its post-copy work (exchange) is
@@ -327,5 +345,5 @@ class WindowStager:
                 "windows_landed": self.windows_landed, "bytes_landed": self.bytes_landed,
                 "stager_wait_producer_s": float(self._native.wait_producer_s),
                 "copy_streams": self.copy_streams, "free_waits_enqueued": int(self._native.free_waits),
-                "free_on_host": bool(self._native.free_on_host),
+                "free_on_host": bool(self._native.free_on_host), "direct_dma": self.direct_dma,
                 "exchange_issue_wait_s": round(self.post_wait_s, 6)}
