@@ -138,7 +138,7 @@ bool NativeStager::init_direct(int n_engines) {
       },
       &fd);
   if (!fd.have_gpu || !fd.have_cpu) {
-    direct_reason_ = std::string("no HSA agent for ") + bus;
+    direct_reason_ = std::string("no HSA agent for ") + bus + (fd.have_cpu ? "" : " (no CPU agent)");
     return false;
   }
   gpu_agent_ = fd.gpu;
@@ -152,10 +152,11 @@ bool NativeStager::init_direct(int n_engines) {
   const char* probe = reinterpret_cast<const char*>(arena_->slot_data(0, 0));
   hsa_amd_pointer_info_t pi{};
   pi.size = sizeof(pi);
-  if (hsa_amd_pointer_info(probe, &pi, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
-      (pi.type != HSA_EXT_POINTER_TYPE_LOCKED && pi.type != HSA_EXT_POINTER_TYPE_HSA) ||
+  const hsa_status_t pst = hsa_amd_pointer_info(probe, &pi, nullptr, nullptr, nullptr);
+  if (pst != HSA_STATUS_SUCCESS || (pi.type != HSA_EXT_POINTER_TYPE_LOCKED && pi.type != HSA_EXT_POINTER_TYPE_HSA) ||
       pi.agentBaseAddress == nullptr || pi.sizeInBytes == 0) {
-    direct_reason_ = "the arena is not locked for the GPU";
+    direct_reason_ = "the arena is not locked for the GPU (pointer_info status " + std::to_string(pst) + ", type " +
+                     std::to_string(static_cast<int>(pi.type)) + ", size " + std::to_string(pi.sizeInBytes) + ")";
     return false;
   }
   arena_agent_base_ = static_cast<const char*>(pi.agentBaseAddress);
@@ -171,7 +172,7 @@ bool NativeStager::init_direct(int n_engines) {
   for (uint32_t bit = 1; bit != 0 && got < n_engines; bit <<= 1)
     if (mask & bit) dma_engine_[got++] = bit;
   if (got == 0) {
-    direct_reason_ = "no SDMA engine available for host -> device copies";
+    direct_reason_ = "no SDMA engine available for host -> device copies (mask " + std::to_string(mask) + ")";
     return false;
   }
   if (got == 1) dma_engine_[1] = dma_engine_[0];

@@ -346,4 +346,5 @@ class WindowStager:
                 "stager_wait_producer_s": float(self._native.wait_producer_s),
                 "copy_streams": self.copy_streams, "free_waits_enqueued": int(self._native.free_waits),
                 "free_on_host": bool(self._native.free_on_host), "direct_dma": self.direct_dma,
+                "direct_dma_reason": self._native.direct_dma_reason,
                 "exchange_issue_wait_s": round(self.post_wait_s, 6)}
