@@ -153,15 +153,28 @@ bool NativeStager::init_direct(int n_engines) {
   hsa_amd_pointer_info_t pi{};
   pi.size = sizeof(pi);
   const hsa_status_t pst = hsa_amd_pointer_info(probe, &pi, nullptr, nullptr, nullptr);
-  if (pst != HSA_STATUS_SUCCESS || (pi.type != HSA_EXT_POINTER_TYPE_LOCKED && pi.type != HSA_EXT_POINTER_TYPE_HSA) ||
-      pi.agentBaseAddress == nullptr || pi.sizeInBytes == 0) {
-    direct_reason_ = "the arena is not locked for the GPU (pointer_info status " + std::to_string(pst) + ", type " +
-                     std::to_string(static_cast<int>(pi.type)) + ", size " + std::to_string(pi.sizeInBytes) + ")";
-    return false;
+  if (pst == HSA_STATUS_SUCCESS && (pi.type == HSA_EXT_POINTER_TYPE_LOCKED || pi.type == HSA_EXT_POINTER_TYPE_HSA) &&
+      pi.agentBaseAddress != nullptr && pi.sizeInBytes != 0) {
+    arena_agent_base_ = static_cast<const char*>(pi.agentBaseAddress);
+    arena_host_base_ = pi.hostBaseAddress != nullptr ? static_cast<const char*>(pi.hostBaseAddress) : arena_agent_base_;
+    arena_span_ = pi.sizeInBytes;
+  } else {
+    // registered by HIP (hipHostRegister, mapped) outside ROCr's lock table: HIP names the device address of
+    // the whole arena; both ends must map contiguously
+    const char* base = reinterpret_cast<const char*>(arena_->base());
+    const size_t span = static_cast<size_t>(arena_->total_bytes());
+    void *d0 = nullptr, *d1 = nullptr;
+    if (span == 0 || hipHostGetDevicePointer(&d0, const_cast<char*>(base), 0) != hipSuccess ||
+        hipHostGetDevicePointer(&d1, const_cast<char*>(base + span - 1), 0) != hipSuccess || d0 == nullptr ||
+        static_cast<const char*>(d1) != static_cast<const char*>(d0) + (span - 1)) {
+      direct_reason_ = "the arena is not mapped for the GPU (pointer_info type " +
+                       std::to_string(static_cast<int>(pi.type)) + ", no contiguous hipHostGetDevicePointer)";
+      return false;
+    }
+    arena_host_base_ = base;
+    arena_agent_base_ = static_cast<const char*>(d0);
+    arena_span_ = span;
   }
-  arena_agent_base_ = static_cast<const char*>(pi.agentBaseAddress);
-  arena_host_base_ = pi.hostBaseAddress != nullptr ? static_cast<const char*>(pi.hostBaseAddress) : arena_agent_base_;
-  arena_span_ = pi.sizeInBytes;
   // SDMA engines for host -> this GPU: the idle ones first, else the runtime's recommendation
   uint32_t mask = 0;
   if (hsa_amd_memory_copy_engine_status(gpu_agent_, cpu_agent_, &mask) != HSA_STATUS_SUCCESS || mask == 0) {
