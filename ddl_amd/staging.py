@@ -50,8 +50,10 @@ from .utils.tracing import trace_range
 # False is the A/B hook of benchmarks/bench_idle_sweep.py --device-free-wait.
 FREE_ON_HOST = True
 # window copies go straight to SDMA engines through ROCr (NativeStager direct-DMA mode) instead of HIP copy
-# streams, so no AQL queue holds a packet waiting on a copy; an A/B hook for bench_idle_sweep.py --direct-dma
-DIRECT_DMA = False
+# streams, so no AQL queue holds a packet waiting on a copy: GPU idle at r = 0.9 1.25% -> 0.78%, feed-bound
+# rate 187.9k -> 191.4k samples/s (profiles/r4_twentieth). Not with a post-copy stage (the exchange waits for
+# copies on the device). False is the A/B hook of bench_idle_sweep.py --stream-copies.
+DIRECT_DMA = True
 
 
 @dataclasses.dataclass
