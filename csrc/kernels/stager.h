@@ -6,21 +6,26 @@
 // training loop WITHOUT the Python GIL:
 //
 //   wait until the ring buffer for window w is free (consumer released w-depth;
-//   its free event -> hipStreamWaitEvent on the copy stream)
+//   its free event, waited for on the host)
 //   futex-wait for producer p = w % P to publish slot s = (w / P) % n_slots
-//   READY -> HELD; hipMemcpyAsync H2D (SDMA) from the pinned arena
-//   hipEventRecord(retire event of w) ; hipEventRecord(ready or copy_done)
+//   READY -> HELD; H2D copy from the pinned arena straight onto SDMA engine
+//   w % 2 through ROCr (direct DMA: hsa_amd_memory_async_copy_on_engine, one
+//   completion signal per copy) -- or, with a post-copy stage (the exchange),
+//   hipMemcpyAsync on a copy stream + retire / ready (copy_done) events
 //   publish "window w staged"
 //
 // A second std::thread retires windows in order: it blocks on each window's
-// retire event (hipEventSynchronize, blocking-sync event) and then hands the
-// slot back to its producer (EMPTY + futex wake) and counts the landed bytes.
+// completion signal (or retire event) and then hands the slot back to its
+// producer (EMPTY + futex wake) and counts the landed bytes. In direct-DMA mode
+// no AQL packet anywhere waits on a copy: consumers wait for it on the host
+// (copy_landed / wait_copy), which costs no device time while the host runs
+// ahead, whereas a queue holding such a packet delayed the compute stream at
+// every step boundary (profiles/r4_fifteenth .. r4_twentieth).
 // (A hipLaunchHostFunc per window did the same from HIP's callback thread, but
 // a host function on the copy stream also stalls the NEXT copy until it has
 // run: ~43 us of idle SDMA per 1.37 ms window, measured in the r2 trace.)
 //
-// The consumer thread only waits on a condition variable (GIL released) and
-// makes its compute stream wait on the ready event on the device. A Python
+// The consumer thread only waits on a condition variable (GIL released). A Python
 // staging thread needed the GIL for every window and could be held off for a
 // full interpreter switch interval (5 ms) by a Python-heavy training loop.
 #pragma once
