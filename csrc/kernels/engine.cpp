@@ -276,8 +276,6 @@ int BatchEngine::launch(int64_t w, int64_t local, int64_t n_batches, const Stage
     } else if (q < 0 && hipEventSynchronize(ready_[info.buffer]) != hipSuccess) {
       return -1;
     }
-  } else if (info.copy_signal != 0) {
-    return -1;  // a direct-DMA copy has no device-side event: the host must wait (ready_on_host)
   } else if (ready_waited_ != w || ready_stream_ != st) {  // once per window and stream: its batches queue behind it
     if (hipStreamWaitEvent(st, ready_[info.buffer], 0) != hipSuccess) return -1;
     ready_waited_ = w;
@@ -474,7 +472,7 @@ int BatchEngine::release(int64_t w) {
           return -1;
       }
     }
-    if (ready_host_ || it->second.copy_signal != 0) {
+    if (ready_host_) {
       // no batch read the window: its copy must still land before the buffer is reused
       const int q = NativeStager::copy_landed(it->second);
       if (q == 0 && NativeStager::wait_copy(it->second) != 0) return -1;

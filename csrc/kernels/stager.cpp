@@ -81,12 +81,7 @@ NativeStager::NativeStager(const Arena* arena, int32_t n_producers, int32_t n_sl
     }
     anchor_cur_ = 1;
   }
-  if (direct_dma) {
-    if (post_copy_)
-      direct_reason_ = "a post-copy stage (the exchange) waits for copies on the device";
-    else
-      direct_ = init_direct(copy_stream2_ != nullptr ? 2 : 1);
-  }
+  if (direct_dma) direct_ = init_direct(copy_stream2_ != nullptr ? 2 : 1);
   thread_ = std::thread([this] { run(); });
   retire_thread_ = std::thread([this] { retire_loop(); });
 }

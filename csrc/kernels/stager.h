@@ -142,12 +142,13 @@ class NativeStager {
   // instead of two in the copy stream's queue). Needs depth < kRetireEvents; ignored with a post-copy stage.
   void set_record_ready(bool on) { record_ready_ = on || depth_ >= kRetireEvents; }
   bool record_ready() const { return record_ready_; }
-  // Direct-DMA mode (asked for with direct_dma, granted unless a post-copy stage is set or the HSA setup fails:
-  // direct_dma_reason() says why): window copies go straight to SDMA engines through ROCr
+  // Direct-DMA mode (asked for with direct_dma, granted unless the HSA setup fails: direct_dma_reason() says
+  // why): window copies go straight to SDMA engines through ROCr
   // (hsa_amd_memory_async_copy_on_engine, one HSA completion signal per copy) instead of through HIP copy
   // streams. No AQL queue then holds a packet that waits on a copy: every consumer of a window waits for its
-  // copy on the HOST (copy_landed / wait_copy; the engine's ready_on_host), and the free-event wait is always
-  // on the host. Copy times come from ROCr's async-copy profiling, mapped onto the anchor events' clock.
+  // copy on the HOST (copy_landed / wait_copy; the engine's ready_on_host; with a post-copy stage, the consumer
+  // before it enqueues that stage, whose ready event the engine then waits on), and the free-event wait is
+  // always on the host. Copy times come from ROCr's async-copy profiling, mapped onto the anchor events' clock.
   bool direct_dma() const { return direct_; }
   std::string direct_dma_reason() const { return direct_reason_; }
   // 1: the window's copy has landed; 0: in flight; -1: no handle in `info` (or a HIP error)

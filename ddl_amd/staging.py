@@ -51,8 +51,9 @@ from .utils.tracing import trace_range
 FREE_ON_HOST = True
 # window copies go straight to SDMA engines through ROCr (NativeStager direct-DMA mode) instead of HIP copy
 # streams, so no AQL queue holds a packet waiting on a copy: GPU idle at r = 0.9 1.25% -> 0.78%, feed-bound
-# rate 187.9k -> 191.4k samples/s (profiles/r4_twentieth). Not with a post-copy stage (the exchange waits for
-# copies on the device). False is the A/B hook of bench_idle_sweep.py --stream-copies.
+# rate 187.9k -> 191.4k samples/s (profiles/r4_twentieth). With a post-copy stage (the exchange) the consumer
+# waits for the copy on the host before it enqueues the stage. False is the A/B hook of bench_idle_sweep.py
+# --stream-copies.
 DIRECT_DMA = True
 
 
@@ -165,9 +166,9 @@ class WindowStager:
             ready=[e.cuda_event for e in self.ready_events], copy_done=[e.cuda_event for e in self._copy_done],
             post_copy=post_copy is not None, meta_bytes=int(meta_bytes),
             copy_stream2=self.copy_stream2.cuda_stream if self.copy_stream2 is not None else 0,
-            direct_dma=bool(DIRECT_DMA and post_copy is None))
+            direct_dma=bool(DIRECT_DMA))
         self.direct_dma = bool(self._native.direct_dma)
-        if DIRECT_DMA and post_copy is None and not self.direct_dma:
+        if DIRECT_DMA and not self.direct_dma:
             logger.info("direct-DMA staging unavailable (%s): HIP copy streams", self._native.direct_dma_reason)
         self._native.free_on_host = FREE_ON_HOST
         self.copy_streams = 2 if self.copy_stream2 is not None else 1
@@ -194,9 +195,10 @@ class WindowStager:
         return sw
 
     def wait_ready(self, sw: StagedWindow, stream) -> None:
-        """Order ``stream`` after window ``sw``'s copy: a device-side event wait, or in direct-DMA mode (no HIP
-        event behind the copy) a host wait for the copy's completion signal."""
-        if self.direct_dma:
+        """Order ``stream`` after window ``sw``'s copy (and its post-copy stage): a device-side event wait, or in
+        direct-DMA mode without a post-copy stage (no HIP event behind the copy) a host wait for the copy's
+        completion signal."""
+        if self.direct_dma and self.post_copy is None:
             rc = self._native.wait_copy(sw.index)
             if rc != 0:
                 raise DDLError(f"window {sw.index}: waiting for its copy failed ({self._native.error()})")
@@ -226,7 +228,11 @@ class WindowStager:
         t0 = time.perf_counter()
         sw = self._wait_staged(w)
         self.post_wait_s += time.perf_counter() - t0
-        self.stream.wait_event(self._copy_done[sw.buffer])
+        if self.direct_dma:  # no HIP event behind the copy: the host waits for it, then enqueues the stage
+            if self._native.wait_copy(w) != 0:
+                raise DDLError(f"window {w}: waiting for its copy failed ({self._native.error()})")
+        else:
+            self.stream.wait_event(self._copy_done[sw.buffer])
         with streams.on_stream(self.stream), trace_range("ddl.stage.post_copy"):
             self.post_copy(sw.data, w, {"seq": sw.seq, "used_bytes": sw.nbytes, "tag": list(sw.tags)})
         self.ready_events[sw.buffer].record(self.stream)
