@@ -507,6 +507,8 @@ def main(argv=None) -> int:
             "h2d_two_copies_pct": (round(100.0 * pro["overlap_ms"] / max(1e-9, pro["t1_ms"] - pro["t0_ms"]), 2)
                                    if pro is not None and pro["ok"] else None),
             "h2d_copies_per_stream": list(pro["copies_per_stream"]) if pro is not None and pro["ok"] else None,
+            # window copies straight onto SDMA engines through ROCr (True) or on HIP copy streams
+            "h2d_direct_dma": bool(getattr(getattr(dl, "_stager", None), "direct_dma", False)),
             "h2d_bytes_whole_windows_enqueued_and_retired_in_region": b_in,
             "h2d_bytes_landed_any_enqueue_time": b_land1 - b_land0,
             "h2d_enqueued_bytes_timed": bytes_enq1 - bytes_enq0,
