@@ -23,15 +23,7 @@ __all__ = [
     "ops",
 ]
 
-import os as _os
-
-# AQL queues in device memory: the command processor then reads each stream's packets from HBM instead of over
-# the PCIe link that the window copies keep busy (GPU idle behind a step at 0.9x the feed 0.79 -> 0.68%,
-# profiles/r4_twentythird). ROCr reads this when HIP initialises, so it takes effect when ddl_amd is imported
-# before the process's first GPU call; HSA_ALLOCATE_QUEUE_DEV_MEM=0 keeps the queues in host memory.
-_os.environ.setdefault("HSA_ALLOCATE_QUEUE_DEV_MEM", "1")
-
-from . import ops  # noqa: E402
+from . import ops
 from .datapusher import DataProducerOnInitReturn
 from .dataloader import DistributedDataLoader
 from .datasetwrapper import ProducerFunctionSkeleton

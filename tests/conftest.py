@@ -7,9 +7,6 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if REPO not in sys.path:
     sys.path.insert(0, REPO)
 os.environ.setdefault("PYTHONPATH", REPO)
-# what `import ddl_amd` sets (ddl_amd/__init__.py), applied before collection initialises HIP below, so the GPU
-# tests run with the runtime configuration the library gives a training process
-os.environ.setdefault("HSA_ALLOCATE_QUEUE_DEV_MEM", "1")
 
 
 def pytest_configure(config):

@@ -109,17 +109,3 @@ def test_verify_order_knob(monkeypatch):
             dl.close()
     finally:
         src.close()
-
-
-@pytest.mark.parametrize("preset", [None, "0"])
-def test_import_sets_device_memory_queues_unless_set(preset):
-    """Importing ddl_amd asks ROCr for AQL queues in device memory (HSA_ALLOCATE_QUEUE_DEV_MEM=1, read when HIP
-    initialises) and leaves a value the user set alone."""
-    env = {k: v for k, v in os.environ.items() if k != "HSA_ALLOCATE_QUEUE_DEV_MEM"}
-    env["DDL_AMD_NO_AUTOBUILD"] = "1"
-    if preset is not None:
-        env["HSA_ALLOCATE_QUEUE_DEV_MEM"] = preset
-    r = subprocess.run([sys.executable, "-c", "import os, ddl_amd; print(os.environ['HSA_ALLOCATE_QUEUE_DEV_MEM'])"],
-                       capture_output=True, text=True, env=env, cwd=str(ROOT), timeout=120)
-    assert r.returncode == 0, r.stderr[-2000:]
-    assert r.stdout.strip().splitlines()[-1] == (preset or "1")
