@@ -1,10 +1,12 @@
 """Run a benchmark script with the library's A/B hooks flipped (no environment knobs for them).
 
-    python benchmarks/ab_run.py [--stream-copies] [--device-ready-wait] [--device-free-wait] -- SCRIPT [ARGS...]
+    python benchmarks/ab_run.py [--stream-copies] [--device-ready-wait] [--device-free-wait] [--alternate-engines]
+                                -- SCRIPT [ARGS...]
 
 --stream-copies      window copies on HIP copy streams (staging.DIRECT_DMA = False)
 --device-ready-wait  batch kernels wait for their window's copy on the device (engine_dispatch.READY_ON_HOST = False)
 --device-free-wait   copy streams wait for free ring buffers on the device (staging.FREE_ON_HOST = False)
+--alternate-engines  direct-DMA copies always alternate over two SDMA engines (staging.ENGINE_POLICY = False)
 """
 
 import argparse
@@ -24,6 +26,7 @@ def main() -> None:
     ap.add_argument("--stream-copies", action="store_true")
     ap.add_argument("--device-ready-wait", action="store_true")
     ap.add_argument("--device-free-wait", action="store_true")
+    ap.add_argument("--alternate-engines", action="store_true")
     a = ap.parse_args(argv[:cut])
     script, rest = argv[cut + 1], argv[cut + 2:]
     sys.path.insert(0, REPO)
@@ -31,6 +34,7 @@ def main() -> None:
 
     staging.DIRECT_DMA = not a.stream_copies
     staging.FREE_ON_HOST = not a.device_free_wait
+    staging.ENGINE_POLICY = not a.alternate_engines
     engine_dispatch.READY_ON_HOST = not a.device_ready_wait
     sys.argv = [script] + rest
     runpy.run_path(script, run_name="__main__")

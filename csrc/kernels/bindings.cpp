@@ -300,6 +300,8 @@ PYBIND11_MODULE(_ddl_hip, m) {
       .def_property("free_on_host", &ddl::NativeStager::free_on_host, &ddl::NativeStager::set_free_on_host)
       .def_property("record_ready", &ddl::NativeStager::record_ready, &ddl::NativeStager::set_record_ready)
       .def_property_readonly("direct_dma", &ddl::NativeStager::direct_dma)
+      .def_property("engine_policy", &ddl::NativeStager::engine_policy, &ddl::NativeStager::set_engine_policy)
+      .def_property_readonly("single_engine_copies", &ddl::NativeStager::single_engine_copies)
       .def_property_readonly("direct_dma_reason", &ddl::NativeStager::direct_dma_reason)
       .def("wait_copy", &ddl::NativeStager::wait_copy_window, py::arg("window"),
            py::call_guard<py::gil_scoped_release>(), "host wait for staged window w's copy (direct-DMA mode)")

@@ -378,8 +378,10 @@ void NativeStager::run() {
     const int b = static_cast<int>((w - first_) % depth_);
     hipEvent_t free_ev = nullptr;
     const int64_t s0 = ns();
+    bool ring_full = false;  // the consumer had not released this window's ring buffer yet
     {
       std::unique_lock<std::mutex> lk(mu_);
+      ring_full = !(w - depth_ < released_upto_);
       cv_.wait(lk, [&] { return stop_ || w - depth_ < released_upto_; });
       if (stop_) return;
       free_ev = free_events_[b];
@@ -435,16 +437,20 @@ void NativeStager::run() {
     if (info.used_bytes > buffer_bytes_)
       return fail(-1, static_cast<int32_t>(p),
                   "window of " + std::to_string(info.used_bytes) + " B exceeds the staging buffer");
-    // two copy streams (two SDMA engines) strictly alternate: while one copy runs the next is already queued
-    // on the other engine, so the link never waits for a copy to end (+1.8-2.5% feed, profiles/r2_copy_streams).
-    // Switching to one engine while the consumer is the bottleneck was tried in round 4 (profiles/r4_fifth ..
-    // r4_tenth): -0.3-0.5 pp GPU idle near r = 0.9 at equal step time, but +0.06 pp behind a slow step and a
-    // trigger that either never fired or flapped and cost the link-bound feed 2-7%; alternation stays.
-    const int si = copy_stream2_ == nullptr ? 0 : 1 - last_stream_;
-    hipStream_t cs = si == 0 ? copy_stream_ : copy_stream2_;
     // the consumer's kernels reading this ring buffer (window w - depth) finish first; a free event that
-    // has already completed needs no device-side wait (no cross-stream dependency on the compute stream)
-    if (free_ev != nullptr && hipEventQuery(free_ev) != hipSuccess) {
+    // has already completed needs no wait at all
+    const bool free_pending = free_ev != nullptr && hipEventQuery(free_ev) != hipSuccess;
+    // two SDMA engines alternate: while one copy runs the next is already queued on the other engine, so the
+    // link never waits for a copy to end (+1.8-2.5% feed, profiles/r2_copy_streams). With direct DMA, a window
+    // whose ring buffer the consumer had not freed yet (the consumer is the bottleneck: no copy is urgent)
+    // goes to the engine of the previous copy instead -- one engine reading the host at a time disturbs the
+    // compute stream less (profiles/r4_twentieth: 0.57% vs 0.78% idle at r = 0.9). On HIP copy streams the
+    // same switch cost a 24 us gap per copy and flapped (profiles/r4_fifth .. r4_tenth); there they alternate.
+    const bool one_engine = direct_ && engine_policy_ && (ring_full || free_pending);
+    const int si = copy_stream2_ == nullptr ? 0 : one_engine ? last_stream_ : 1 - last_stream_;
+    if (one_engine && copy_stream2_ != nullptr) single_engine_copies_ += 1;
+    hipStream_t cs = si == 0 ? copy_stream_ : copy_stream2_;
+    if (free_pending) {
       if (free_on_host_ || direct_) {
         if (hipEventSynchronize(free_ev) != hipSuccess) return fail(-1, -1, "hipEventSynchronize(free) failed");
       } else if (hipStreamWaitEvent(cs, free_ev, 0) != hipSuccess) {

@@ -55,6 +55,10 @@ FREE_ON_HOST = True
 # waits for the copy on the host before it enqueues the stage. False is the A/B hook of bench_idle_sweep.py
 # --stream-copies.
 DIRECT_DMA = True
+# direct DMA: a window whose ring buffer the consumer had not freed yet stays on the previous copy's SDMA engine
+# (one engine reading the host while the consumer is the bottleneck); False (alternate always) is the A/B hook
+# of bench_idle_sweep.py --alternate-engines
+ENGINE_POLICY = True
 
 
 @dataclasses.dataclass
@@ -167,6 +171,7 @@ class WindowStager:
             post_copy=post_copy is not None, meta_bytes=int(meta_bytes),
             copy_stream2=self.copy_stream2.cuda_stream if self.copy_stream2 is not None else 0,
             direct_dma=bool(DIRECT_DMA))
+        self._native.engine_policy = ENGINE_POLICY
         self.direct_dma = bool(self._native.direct_dma)
         if DIRECT_DMA and not self.direct_dma:
             logger.info("direct-DMA staging unavailable (%s): HIP copy streams", self._native.direct_dma_reason)
@@ -355,4 +360,5 @@ class WindowStager:
                 "copy_streams": self.copy_streams, "free_waits_enqueued": int(self._native.free_waits),
                 "free_on_host": bool(self._native.free_on_host), "direct_dma": self.direct_dma,
                 "direct_dma_reason": self._native.direct_dma_reason,
+                "single_engine_copies": int(self._native.single_engine_copies),
                 "exchange_issue_wait_s": round(self.post_wait_s, 6)}
