@@ -93,9 +93,9 @@ def _parse(argv=None):
     ap.add_argument("--device-free-wait", action="store_true",
                     help="A/B: the copy stream waits for a ring buffer's free event on the device instead of "
                          "the stager thread waiting on the host")
-    ap.add_argument("--alternate-engines", action="store_true",
-                    help="A/B: direct-DMA copies always alternate over the two SDMA engines (no one-engine placement "
-                         "while the consumer is the bottleneck)")
+    ap.add_argument("--one-engine-when-full", action="store_true",
+                    help="A/B: a direct-DMA copy whose ring buffer was not free yet stays on the previous copy's SDMA "
+                         "engine (one engine while the consumer is the bottleneck)")
     ap.add_argument("--stream-copies", action="store_true",
                     help="A/B: window copies on HIP copy streams instead of straight onto SDMA engines through ROCr")
     ap.add_argument("--gather-blocks", type=int, default=0,
@@ -201,12 +201,12 @@ def main(argv=None) -> int:
 
         _ed.GATHER_MAX_BLOCKS = a.gather_blocks
         _ed.READY_ON_HOST = not a.device_ready_wait
-    if a.device_free_wait or a.stream_copies or a.alternate_engines:
+    if a.device_free_wait or a.stream_copies or a.one_engine_when_full:
         from ddl_amd import staging as _stg
 
         _stg.FREE_ON_HOST = not a.device_free_wait
         _stg.DIRECT_DMA = not a.stream_copies
-        _stg.ENGINE_POLICY = not a.alternate_engines
+        _stg.ENGINE_POLICY = a.one_engine_when_full
     if a.batch_priority == "normal":  # A/B: the loader's batch stream at normal priority
         import ddl_amd.dataloader as _dl
         from ddl_amd.utils import streams as _streams

@@ -151,7 +151,7 @@ class NativeStager {
   // always on the host. Copy times come from ROCr's async-copy profiling, mapped onto the anchor events' clock.
   bool direct_dma() const { return direct_; }
   // direct DMA: a copy whose ring buffer was not free yet (consumer-bound) stays on the previous copy's engine
-  // instead of alternating (true, default). Copies placed that way so far: single_engine_copies().
+  // instead of alternating (default false). Copies placed that way so far: single_engine_copies().
   void set_engine_policy(bool on) { engine_policy_ = on; }
   bool engine_policy() const { return engine_policy_; }
   uint64_t single_engine_copies() const { return single_engine_copies_.load(); }
@@ -238,7 +238,7 @@ class NativeStager {
   std::string error_msg_;
   std::atomic<uint64_t> bytes_h2d_{0}, windows_staged_{0}, wait_producer_ns_{0};
   std::atomic<uint64_t> windows_landed_{0}, bytes_landed_{0}, free_waits_{0};
-  std::atomic<bool> free_on_host_{false}, record_ready_{true}, engine_policy_{true};
+  std::atomic<bool> free_on_host_{false}, record_ready_{true}, engine_policy_{false};
   std::atomic<uint64_t> single_engine_copies_{0};
   // direct-DMA state (set in the constructor, read-only afterwards)
   bool direct_ = false;

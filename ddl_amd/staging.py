@@ -56,9 +56,9 @@ FREE_ON_HOST = True
 # --stream-copies.
 DIRECT_DMA = True
 # direct DMA: a window whose ring buffer the consumer had not freed yet stays on the previous copy's SDMA engine
-# (one engine reading the host while the consumer is the bottleneck); False (alternate always) is the A/B hook
-# of bench_idle_sweep.py --alternate-engines
-ENGINE_POLICY = True
+# (one engine reading the host while the consumer is the bottleneck) instead of alternating; an A/B hook of
+# bench_idle_sweep.py --one-engine-when-full (off: the measured default alternates always)
+ENGINE_POLICY = False
 
 
 @dataclasses.dataclass
