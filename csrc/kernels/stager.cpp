@@ -378,11 +378,11 @@ void NativeStager::run() {
     const int b = static_cast<int>((w - first_) % depth_);
     hipEvent_t free_ev = nullptr;
     const int64_t s0 = ns();
-    bool ring_full = false;  // the consumer had not released this window's ring buffer yet
+    int64_t backlog = 0;  // windows whose copy has landed but the consumer has not released yet
     {
       std::unique_lock<std::mutex> lk(mu_);
-      ring_full = !(w - depth_ < released_upto_);
       cv_.wait(lk, [&] { return stop_ || w - depth_ < released_upto_; });
+      backlog = retired_upto_ - released_upto_;
       if (stop_) return;
       free_ev = free_events_[b];
     }
@@ -441,12 +441,13 @@ void NativeStager::run() {
     // has already completed needs no wait at all
     const bool free_pending = free_ev != nullptr && hipEventQuery(free_ev) != hipSuccess;
     // two SDMA engines alternate: while one copy runs the next is already queued on the other engine, so the
-    // link never waits for a copy to end (+1.8-2.5% feed, profiles/r2_copy_streams). With direct DMA, a window
-    // whose ring buffer the consumer had not freed yet (the consumer is the bottleneck: no copy is urgent)
-    // goes to the engine of the previous copy instead -- one engine reading the host at a time disturbs the
-    // compute stream less (profiles/r4_twentieth: 0.57% vs 0.78% idle at r = 0.9). On HIP copy streams the
-    // same switch cost a 24 us gap per copy and flapped (profiles/r4_fifth .. r4_tenth); there they alternate.
-    const bool one_engine = direct_ && engine_policy_ && (ring_full || free_pending);
+    // link never waits for a copy to end (+1.8-2.5% feed, profiles/r2_copy_streams). With direct DMA and the
+    // engine policy, a copy made while the consumer holds >= 2 LANDED windows (the consumer is the bottleneck:
+    // no copy is urgent) goes to the engine of the previous copy instead -- one engine reading the host at a
+    // time disturbs the compute stream less (profiles/r4_twentieth: 0.57% vs 0.78% idle at r = 0.9). A ring
+    // that is full of copies still in flight means the link is the bottleneck: alternate (profiles/
+    // r4_twentyeighth). On HIP copy streams a switch cost a 24 us gap per copy (profiles/r4_fifth .. r4_tenth).
+    const bool one_engine = direct_ && engine_policy_ && backlog >= 2;
     const int si = copy_stream2_ == nullptr ? 0 : one_engine ? last_stream_ : 1 - last_stream_;
     if (one_engine && copy_stream2_ != nullptr) single_engine_copies_ += 1;
     hipStream_t cs = si == 0 ? copy_stream_ : copy_stream2_;

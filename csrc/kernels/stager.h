@@ -150,8 +150,8 @@ class NativeStager {
   // before it enqueues that stage, whose ready event the engine then waits on), and the free-event wait is
   // always on the host. Copy times come from ROCr's async-copy profiling, mapped onto the anchor events' clock.
   bool direct_dma() const { return direct_; }
-  // direct DMA: a copy whose ring buffer was not free yet (consumer-bound) stays on the previous copy's engine
-  // instead of alternating (default false). Copies placed that way so far: single_engine_copies().
+  // direct DMA: a copy made while the consumer holds >= 2 landed, unreleased windows (consumer-bound) stays on
+  // the previous copy's engine instead of alternating (default false). Copies placed that way: single_engine_copies().
   void set_engine_policy(bool on) { engine_policy_ = on; }
   bool engine_policy() const { return engine_policy_; }
   uint64_t single_engine_copies() const { return single_engine_copies_.load(); }

@@ -55,7 +55,7 @@ FREE_ON_HOST = True
 # waits for the copy on the host before it enqueues the stage. False is the A/B hook of bench_idle_sweep.py
 # --stream-copies.
 DIRECT_DMA = True
-# direct DMA: a window whose ring buffer the consumer had not freed yet stays on the previous copy's SDMA engine
+# direct DMA: a copy made while the consumer holds >= 2 landed windows stays on the previous copy's SDMA engine
 # (one engine reading the host while the consumer is the bottleneck) instead of alternating; an A/B hook of
 # bench_idle_sweep.py --one-engine-when-full (off: the measured default alternates always)
 ENGINE_POLICY = False
