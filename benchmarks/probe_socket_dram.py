@@ -43,6 +43,8 @@ def _parse(argv=None):
     ap.add_argument("--dma-threads", type=int, default=6, help="host read threads emulating 3 more GPUs' DMA")
     ap.add_argument("--refill-threads", type=int, default=8, help="threads of the refill host pool (4 ranks)")
     ap.add_argument("--target-gbps", type=float, default=56.0)
+    ap.add_argument("--stream-stores", default="on", choices=["on", "off"],
+                    help="refill copies with non-temporal stores (the runtime default) or plain memcpy")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
 
@@ -82,6 +84,7 @@ def main(argv=None) -> int:
     node = bind_to_gpu_numa(0, 1)
     cpus = sorted(os.sched_getaffinity(0))
     rt = _native.runtime()
+    rt.set_stream_stores(a.stream_stores == "on")
     wb = int(a.window_mb * 1e6) // 4096 * 4096
     dev = torch.device("cuda", 0)
 
@@ -150,6 +153,7 @@ def main(argv=None) -> int:
     summary = {
         "probe": "socket DRAM headroom (one socket's share of an 8-rank job, emulated on the GPU's node)",
         "gpu_numa_node": gpu_numa_node(0), "bound_node": node, "cpus": len(cpus),
+        "stream_stores": bool(rt.stream_stores()),
         "page_nodes": nodes,
         "demand_gbps": {"stamp": 4 * t, "full": 12 * t},
         "target_per_gpu_gbps": t,

@@ -161,6 +161,10 @@ void gather_rows(uint8_t* dst, const uint8_t* src, uint64_t row_bytes, const int
                  uint64_t n, uint64_t src_rows, int n_threads);
 // Parallel memcpy (large contiguous copies: window replication).
 void parallel_copy(uint8_t* dst, const uint8_t* src, uint64_t bytes, int n_threads);
+// Host copies into windows (gather_rows, gather_ragged, parallel_copy, copy_spans) use streaming stores for
+// every run of >= 1 KiB (default on): no read-for-ownership of the destination, which an SDMA engine reads next.
+void set_stream_stores(bool on);
+bool stream_stores();
 // Many independent copies dst[i] <- src[i] (sizes[i] bytes) on the worker pool, split into
 // ~1 MiB tasks of consecutive spans: the packing step of map-style dataset producers, where
 // Python collects one span per sample field and the bytes move without the GIL.

@@ -287,6 +287,9 @@ PYBIND11_MODULE(_ddl_runtime, m) {
       },
       py::arg("keys"), py::arg("half_bits"), py::arg("n"), py::arg("pos0"), py::arg("gb"), py::arg("lb"),
       py::arg("shard_rows"), py::arg("world"), py::arg("rank"), py::arg("lo"));
+  m.def("set_stream_stores", &ddl::set_stream_stores, py::arg("on"),
+        "host window copies with streaming (non-temporal) stores (default on); off: plain memcpy");
+  m.def("stream_stores", &ddl::stream_stores);
   m.def(
       "parallel_copy",
       [](uintptr_t dst, uintptr_t src, uint64_t bytes, int n_threads) {

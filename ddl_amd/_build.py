@@ -10,6 +10,11 @@ Two shared objects are produced next to this file:
   module links against the HIP runtime bundled in torch/lib so a single HIP
   runtime lives in the process.
 
+Each shared object embeds a SHA-256 of its source inputs (``source_hash``; the marker
+``ddl-source-hash=<hex>`` in a generated translation unit). ``_native`` compares it with the tree
+before importing, so an edit under ``csrc/`` without a rebuild is rebuilt (or, with
+``DDL_AMD_NO_AUTOBUILD=1``, reported) instead of silently running the old binary.
+
 Usage: ``python -m ddl_amd._build [--only runtime|hip] [--force] [-j N]``.
 """
 
@@ -17,6 +22,7 @@ from __future__ import annotations
 
 import argparse
 import glob
+import hashlib
 import os
 import shutil
 import subprocess
@@ -70,6 +76,72 @@ def _run(cmd: list[str]) -> None:
         sys.stderr.write(proc.stdout)
 
 
+HASH_MARKER = b"ddl-source-hash="
+
+
+def runtime_inputs() -> list[str]:
+    srcs = [os.path.join(CSRC, "runtime", f) for f in ("arena.cpp", "fileio.cpp", "numa.cpp", "bindings.cpp")]
+    return srcs + [os.path.join(CSRC, "runtime", h) for h in ("arena.h", "feistel.h", "fileio.h", "numa.h")]
+
+
+def hip_inputs() -> list[str]:
+    """Every file compiled into ``_ddl_hip``: the kernels, the host C++ (stager, engine, bindings, the
+    arena), and the headers they include."""
+    return sorted(_kernel_sources() + glob.glob(os.path.join(CSRC, "kernels", "*.h")) +
+                  [os.path.join(CSRC, "kernels", f) for f in ("bindings.cpp", "stager.cpp", "engine.cpp")] +
+                  [os.path.join(CSRC, "runtime", f) for f in ("arena.cpp", "arena.h", "feistel.h")])
+
+
+def sources_present() -> bool:
+    """The csrc tree is here (an installed package without it cannot be checked)."""
+    return os.path.isdir(os.path.join(CSRC, "runtime")) and os.path.isdir(os.path.join(CSRC, "kernels"))
+
+
+def source_hash(paths: list[str]) -> str:
+    """SHA-256 over the inputs' paths (relative to csrc/) and contents, and the target architecture."""
+    h = hashlib.sha256(ARCH.encode())
+    for p in sorted(paths):
+        h.update(os.path.relpath(p, CSRC).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    return h.hexdigest()
+
+
+def embedded_hash(target: str) -> str | None:
+    """The source hash a built shared object carries, or None (missing file, or built without one)."""
+    try:
+        with open(target, "rb") as f:
+            data = f.read()
+    except OSError:
+        return None
+    i = data.find(HASH_MARKER)
+    if i < 0:
+        return None
+    h = data[i + len(HASH_MARKER):i + len(HASH_MARKER) + 64]
+    return h.decode() if len(h) == 64 else None
+
+
+def is_stale(which: str) -> bool:
+    """``which`` ("runtime" / "hip") is missing, or was built from other sources than the tree's."""
+    target, inputs = (runtime_target(), runtime_inputs()) if which == "runtime" else (hip_target(), hip_inputs())
+    if not os.path.exists(target):
+        return True
+    if not sources_present():
+        return False
+    return embedded_hash(target) != source_hash(inputs)
+
+
+def _hash_source(name: str, digest: str) -> str:
+    """A translation unit that carries ``digest`` in the shared object (kept by ``used``)."""
+    os.makedirs(BUILD, exist_ok=True)
+    path = os.path.join(BUILD, f"{name}_source_hash.cpp")
+    with open(path, "w") as f:
+        f.write(f'__attribute__((used)) extern const char ddl_{name}_source_hash[] = '
+                f'"{HASH_MARKER.decode()}{digest}";\n')
+    return path
+
+
 def runtime_target() -> str:
     return os.path.join(PKG_DIR, "_ddl_runtime" + EXT_SUFFIX)
 
@@ -79,11 +151,13 @@ def hip_target() -> str:
 
 
 def build_runtime(force: bool = False, extra_flags: list[str] | None = None) -> str:
-    srcs = [os.path.join(CSRC, "runtime", f) for f in ("arena.cpp", "fileio.cpp", "numa.cpp", "bindings.cpp")]
-    deps = srcs + [os.path.join(CSRC, "runtime", h) for h in ("arena.h", "feistel.h", "fileio.h", "numa.h")]
+    deps = runtime_inputs()
+    srcs = [d for d in deps if d.endswith(".cpp")]
     out = runtime_target()
-    if not force and not _newer(out, deps):
+    digest = source_hash(deps)
+    if not force and not _newer(out, deps) and embedded_hash(out) == digest:
         return out
+    srcs.append(_hash_source("runtime", digest))
     cxx = os.environ.get("CXX", "g++")
     cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wno-unused-function"]
     cmd += [f"-I{p}" for p in _py_includes()]
@@ -132,11 +206,17 @@ def build_hip(force: bool = False, jobs: int = 8) -> str:
         cmd = [hipcc, "-c", binding, "-o", bobj] + common
         cmd += [f"-I{p}" for p in _py_includes()] + ["-fvisibility=hidden"]
         jobs_list.append((cmd, bobj))
+    digest = source_hash(hip_inputs())
+    stale = embedded_hash(out) != digest
+    if force or stale or jobs_list:
+        hobj = os.path.join(BUILD, "hip_source_hash.o")
+        jobs_list.append(([hipcc, "-c", _hash_source("hip", digest), "-o", hobj, "-fPIC"], hobj))
+    objs.append(os.path.join(BUILD, "hip_source_hash.o"))
 
     if jobs_list:
         with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
             list(ex.map(lambda j: _run(j[0]), jobs_list))
-    if force or jobs_list or _newer(out, objs):
+    if force or jobs_list or stale or _newer(out, objs):
         cmd = [hipcc, "-shared", "-fPIC", *objs, "-o", out + ".tmp", f"-L{torch_lib}", f"-Wl,-rpath,{torch_lib}",
                "-l:libamdhip64.so", "-l:libhsa-runtime64.so", "-lpthread", "-lrt"]
         _run(cmd)

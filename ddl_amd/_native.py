@@ -4,9 +4,10 @@
 consumer hand slots over through it). ``hip()`` returns the gfx950 kernel
 module. On a GPU host a missing/broken HIP extension is an error, never a
 silent fallback to eager PyTorch: ``hip()`` raises ``NativeExtensionError``.
-If an extension is missing it is built in-tree once (under a file lock, so
-concurrently starting producer processes do not race); set
-``DDL_AMD_NO_AUTOBUILD=1`` to disable.
+If an extension is missing, or STALE -- the source hash it embeds differs from
+the ``csrc/`` tree's (``_build.is_stale``) -- it is (re)built in-tree before the
+import (under a file lock, so concurrently starting producer processes do not
+race); with ``DDL_AMD_NO_AUTOBUILD=1`` either case raises instead.
 """
 
 from __future__ import annotations
@@ -38,10 +39,28 @@ def _build_locked(which: str) -> None:
             fcntl.flock(lk, fcntl.LOCK_UN)
 
 
+def _check_fresh(name: str, which: str) -> None:
+    """Rebuild a stale extension before it is imported (a loaded module cannot be replaced), or raise with
+    ``DDL_AMD_NO_AUTOBUILD``. A missing one is left to the import below."""
+    from . import _build
+
+    target = _build.runtime_target() if which == "runtime" else _build.hip_target()
+    if not os.path.exists(target) or not _build.is_stale(which):
+        return
+    if os.environ.get("DDL_AMD_NO_AUTOBUILD"):
+        raise NativeExtensionError(
+            f"ddl_amd.{name} is stale: built from other sources than csrc/ holds; run `python -m ddl_amd._build`")
+    try:
+        _build_locked(which)
+    except Exception as e:  # pragma: no cover - depends on toolchain
+        raise NativeExtensionError(f"ddl_amd.{name} is stale and failed to rebuild: {e}") from e
+
+
 def _load(name: str, which: str) -> ModuleType:
     with _lock:
         if name in _cache:
             return _cache[name]
+        _check_fresh(name, which)
         try:
             mod = importlib.import_module(f"ddl_amd.{name}")
         except ImportError as first:
@@ -57,7 +76,11 @@ def _load(name: str, which: str) -> ModuleType:
 
 
 def runtime() -> ModuleType:
-    return _load("_ddl_runtime", "runtime")
+    first = "_ddl_runtime" not in _cache
+    mod = _load("_ddl_runtime", "runtime")
+    if first and os.environ.get("DDL_STREAM_STORES", "1") == "0":  # producer processes inherit the setting
+        mod.set_stream_stores(False)
+    return mod
 
 
 def hip() -> ModuleType:

@@ -87,6 +87,39 @@ def test_no_autobuild_knob(monkeypatch):
         nat._load("_ddl_does_not_exist", "runtime")
 
 
+def test_stream_stores_knob():
+    code = "from ddl_amd import _native; print(_native.runtime().stream_stores())"
+    assert _py(code, DDL_STREAM_STORES="0") == "False"
+    assert _py(code, DDL_STREAM_STORES="1") == "True"
+
+
+def test_stream_store_copies_are_exact():
+    """Every host window copy gives the same bytes with and without streaming stores, for unaligned
+    destinations and lengths around the 1 KiB switch and the 16 / 64-byte store blocks."""
+    import numpy as np
+
+    from ddl_amd import _native
+
+    rt = _native.runtime()
+    rng = np.random.default_rng(0)
+    src = rng.integers(0, 256, size=1 << 20, dtype=np.uint8)
+    try:
+        for nt in (True, False):
+            rt.set_stream_stores(nt)
+            for row in (1, 17, 1023, 1024, 1025, 4099, 65536 + 48):
+                n = min(64, src.size // row)
+                idx = rng.permutation(n).astype(np.int64)
+                dst = np.zeros(n * row + 3, dtype=np.uint8)
+                rt.gather_rows(dst.ctypes.data + 3, src.ctypes.data, row, idx, n, 4)
+                want = src[: n * row].reshape(n, row)[idx].reshape(-1)
+                assert np.array_equal(dst[3:], want), (nt, row)
+            dst = np.zeros(src.size + 5, dtype=np.uint8)
+            rt.parallel_copy(dst.ctypes.data + 5, src.ctypes.data, src.size, 3)
+            assert np.array_equal(dst[5:], src)
+    finally:
+        rt.set_stream_stores(True)
+
+
 def test_verify_order_knob(monkeypatch):
     """DDL_VERIFY_ORDER=1 turns on the per-window order check of indexed loaders by default."""
     import numpy as np
