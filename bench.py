@@ -420,7 +420,8 @@ def main(argv=None) -> int:
             producer, args.batch, conn, n_epochs, args.exchange, args.exchange_method, env.rank, env.world_size,
             env=env, device=dev, out_dtype=torch.bfloat16, shuffle=args.shuffle, seed=args.seed,
             n_slots=args.slots, prefetch_depth=args.depth, normalize=norm,
-            native_dispatch=False if args.dispatch == "python" else args.dispatch)
+            native_dispatch=False if args.dispatch == "python" else args.dispatch,
+            copy_timing=True)  # device times of every window copy: the pro-rata H2D accounting below
         acc = ops.ChecksumAccumulator(dev)  # one streaming launch per batch
 
         def batches():
@@ -480,7 +481,7 @@ def main(argv=None) -> int:
         w_land1, b_land1 = _landed(dl)
         bytes_enq1 = dl._stager.bytes_h2d if dl._stager is not None else 0
         # CPU rehearsal: the host path has no H2D; every delivered window counts
-        n_in, b_in = cb if cb is not None else (w_land1 - w_land0, 0)
+        n_in, b_in = cb[:2] if cb is not None else (w_land1 - w_land0, 0)
         pro = dl._stager.bytes_in_interval(ev0, ev1) if dl._stager is not None and ev0 is not None else None
         if pro is not None and pro["ok"]:
             # the device interval is the region as the GPU saw it; its length next to the host's is a check

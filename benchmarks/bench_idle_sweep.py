@@ -87,19 +87,8 @@ def _parse(argv=None):
     ap.add_argument("--lead-diag", action="store_true",
                     help="per step: how many enqueued steps the GPU had not finished when the host enqueued this one "
                          "(0 = the host is late: the compute stream ran dry), and the host time of each fetch")
-    ap.add_argument("--device-ready-wait", action="store_true",
-                    help="A/B: the batch stream waits for each window's H2D copy on the device (a barrier packet "
-                         "in its queue) instead of the host waiting before the launch")
-    ap.add_argument("--device-free-wait", action="store_true",
-                    help="A/B: the copy stream waits for a ring buffer's free event on the device instead of "
-                         "the stager thread waiting on the host")
-    ap.add_argument("--one-engine-when-full", action="store_true",
-                    help="A/B: a direct-DMA copy whose ring buffer was not free yet stays on the previous copy's SDMA "
-                         "engine (one engine while the consumer is the bottleneck)")
     ap.add_argument("--stream-copies", action="store_true",
                     help="A/B: window copies on HIP copy streams instead of straight onto SDMA engines through ROCr")
-    ap.add_argument("--gather-blocks", type=int, default=0,
-                    help="grid cap of the loader's batch gather (A/B; 0 = uncapped, the library default)")
     ap.add_argument("--batch-priority", default="high", choices=["high", "normal"],
                     help="priority of the loader's batch stream (A/B; the library uses high)")
     ap.add_argument("--json-out", default=None)
@@ -124,7 +113,7 @@ def _image_loader(a, env, conn, n_steps):
         env=env, device=torch.device(env.device), out_dtype=torch.bfloat16, shuffle="device", normalize=norm,
         native_dispatch=False if a.dispatch == "python" else a.dispatch,
         **({"prefetch_depth": a.depth} if a.depth else {}),
-        **({"max_ahead": a.max_ahead} if a.max_ahead is not None else {}))
+        **({"max_ahead": a.max_ahead} if a.max_ahead is not None else {}), copy_timing=True)
 
     def gen():
         while True:
@@ -177,7 +166,7 @@ def _token_loader(a, env, conn, n_steps, src):
                                                           batches_per_window=a.tokens_k), B, conn,
                                        n_epochs, mode="indexed", env=env, collate="tokens", auto_mark=True,
                                        n_slots=2,
-                                       **({"prefetch_depth": a.depth} if a.depth else {}))
+                                       copy_timing=True, **({"prefetch_depth": a.depth} if a.depth else {}))
 
     def gen():
         while True:
@@ -196,17 +185,10 @@ def main(argv=None) -> int:
     from ddl_amd.utils.tracing import ComputeIdleMeter, trace_range
 
     ratios = [float(x) for x in a.ratios.split(",") if x]
-    if a.gather_blocks or a.device_ready_wait:
-        from ddl_amd import engine_dispatch as _ed
-
-        _ed.GATHER_MAX_BLOCKS = a.gather_blocks
-        _ed.READY_ON_HOST = not a.device_ready_wait
-    if a.device_free_wait or a.stream_copies or a.one_engine_when_full:
+    if a.stream_copies:
         from ddl_amd import staging as _stg
 
-        _stg.FREE_ON_HOST = not a.device_free_wait
-        _stg.DIRECT_DMA = not a.stream_copies
-        _stg.ENGINE_POLICY = a.one_engine_when_full
+        _stg.DIRECT_DMA = False
     if a.batch_priority == "normal":  # A/B: the loader's batch stream at normal priority
         import ddl_amd.dataloader as _dl
         from ddl_amd.utils import streams as _streams

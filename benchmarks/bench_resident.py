@@ -25,8 +25,6 @@ def main(argv=None):
     ap.add_argument("--depths", default="1,2,4")
     ap.add_argument("--augment", action="store_true",
                     help="RandomResizedCrop(224) + flip + normalise on the device instead of the plain gather")
-    ap.add_argument("--nt-stores", action="store_true",
-                    help="non-temporal stores in the raw row moves (hip.set_move_nt_stores A/B)")
     a = ap.parse_args(argv)
 
     import torch
@@ -60,10 +58,6 @@ def main(argv=None):
                 dist.barrier(group=env.control_group)
             norm = {"mean": [0.485, 0.456, 0.406], "std": [0.229, 0.224, 0.225]} if a.dtype == "uint8" else None
             dev = torch.device(env.device)
-            if dev.type == "cuda":
-                from ddl_amd import _native
-
-                _native.hip().set_move_nt_stores(a.nt_stores)
             for depth in [int(x) for x in a.depths.split(",")]:
                 dl = ResidentGlobalLoader(src, a.batch * env.world_size, env, seed=1, depth=depth,
                                           out_dtype=torch.bfloat16, normalize=norm,

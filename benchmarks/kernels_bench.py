@@ -222,11 +222,6 @@ def out_of_cache(dev) -> None:
     outs = [torch.empty(B, C, H, W, dtype=torch.bfloat16, device=dev) for _ in range(4)]
     fns = [lambda o=o, k=k: ops.gather_rows(win, perm=p, base=k * B, n_rows=B, out=o) for k, o in enumerate(outs)]
     report("OOC permute_gather bf16->bf16 1024 rows (rotating)", rotating(fns), 2 * B * img * 2, rows=B)
-    from ddl_amd import _native
-
-    _native.hip().set_move_nt_stores(True)
-    report("OOC permute_gather bf16->bf16 1024 rows (rotating), nt stores", rotating(fns), 2 * B * img * 2, rows=B)
-    _native.hip().set_move_nt_stores(False)
     idxs = [torch.from_numpy(p(np.arange(k * B, (k + 1) * B))).to(dev) for k in range(4)]
     fns = [lambda o=o, ix=ix: ops.scatter_rows(win.view(n, -1), o.view(B, -1), ix) for o, ix in zip(outs, idxs)]
     report("OOC scatter_rows bf16 1024 rows (rotating)", rotating(fns), 2 * B * img * 2, rows=B)

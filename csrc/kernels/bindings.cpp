@@ -241,7 +241,7 @@ PYBIND11_MODULE(_ddl_hip, m) {
                        std::vector<uintptr_t> buffers, uint64_t buffer_bytes, uintptr_t copy_stream, int device,
                        std::vector<int32_t> peer_pids, int64_t timeout_ms, std::vector<uintptr_t> ready,
                        std::vector<uintptr_t> copy_done, bool post_copy, int64_t meta_bytes, uintptr_t copy_stream2,
-                       bool direct_dma) {
+                       bool direct_dma, bool copy_timing) {
              std::vector<void*> bufs;
              for (auto b : buffers) bufs.push_back(as_ptr<void>(b));
              std::vector<hipEvent_t> rd, cd;
@@ -250,13 +250,13 @@ PYBIND11_MODULE(_ddl_hip, m) {
              return std::make_unique<ddl::NativeStager>(
                  reinterpret_cast<const ddl::Arena*>(arena), n_producers, n_slots, first, total, std::move(bufs),
                  buffer_bytes, as_stream(copy_stream), device, std::move(peer_pids), timeout_ms, std::move(rd),
-                 std::move(cd), post_copy, meta_bytes, as_stream(copy_stream2), direct_dma);
+                 std::move(cd), post_copy, meta_bytes, as_stream(copy_stream2), direct_dma, copy_timing);
            }),
            py::arg("arena"), py::arg("n_producers"), py::arg("n_slots"), py::arg("first"), py::arg("total"),
            py::arg("buffers"), py::arg("buffer_bytes"), py::arg("copy_stream"), py::arg("device"),
            py::arg("peer_pids"), py::arg("timeout_ms"), py::arg("ready"), py::arg("copy_done"),
            py::arg("post_copy"), py::arg("meta_bytes") = 0, py::arg("copy_stream2") = 0,
-           py::arg("direct_dma") = false)
+           py::arg("direct_dma") = false, py::arg("copy_timing") = false)
       .def(
           "wait",
           [](ddl::NativeStager& st, int64_t w, int64_t timeout_ms) {
@@ -300,13 +300,30 @@ PYBIND11_MODULE(_ddl_hip, m) {
       .def_property("free_on_host", &ddl::NativeStager::free_on_host, &ddl::NativeStager::set_free_on_host)
       .def_property("record_ready", &ddl::NativeStager::record_ready, &ddl::NativeStager::set_record_ready)
       .def_property_readonly("direct_dma", &ddl::NativeStager::direct_dma)
-      .def_property("engine_policy", &ddl::NativeStager::engine_policy, &ddl::NativeStager::set_engine_policy)
-      .def_property_readonly("single_engine_copies", &ddl::NativeStager::single_engine_copies)
       .def_property_readonly("direct_dma_reason", &ddl::NativeStager::direct_dma_reason)
+      .def_property_readonly("error_code", &ddl::NativeStager::error_code)
       .def("wait_copy", &ddl::NativeStager::wait_copy_window, py::arg("window"),
-           py::call_guard<py::gil_scoped_release>(), "host wait for staged window w's copy (direct-DMA mode)")
-      .def("copies_between", &ddl::NativeStager::copies_between, py::arg("t0_ns"), py::arg("t1_ns"),
-           "(windows, bytes) of H2D copies enqueued in [t0_ns, t1_ns] (CLOCK_MONOTONIC) that have retired")
+           py::call_guard<py::gil_scoped_release>(),
+           "host wait for staged window w's copy, bounded by the stager's timeout: 0 landed, 2 timed out (the "
+           "stager has failed: error()), 1 closed, -1 error")
+      .def(
+          "set_copy_timing", [](ddl::NativeStager& st, bool on) { return st.set_copy_timing(on); }, py::arg("on"),
+          "device times for every direct-DMA copy (ROCr async-copy profiling: a process-wide switch, reference "
+          "counted over stagers); False if ROCr refuses")
+      .def_property_readonly("copy_timing", &ddl::NativeStager::copy_timing)
+      .def("set_anchor_every", &ddl::NativeStager::set_anchor_every, py::arg("n"))
+      .def_property_readonly("reanchors", &ddl::NativeStager::reanchors)
+      .def("inject_stuck_copy", &ddl::NativeStager::inject_stuck_copy, py::arg("window"),
+           "fault injection: window w's copy never reads as landed (its completion signal is armed one too high)")
+      .def(
+          "copies_between",
+          [](const ddl::NativeStager& st, uint64_t t0, uint64_t t1) {
+            const ddl::CopiesBetween c = st.copies_between(t0, t1);
+            return py::make_tuple(c.windows, c.bytes, c.complete);
+          },
+          py::arg("t0_ns"), py::arg("t1_ns"),
+          "(windows, bytes, complete) of H2D copies enqueued in [t0_ns, t1_ns] (CLOCK_MONOTONIC) that have "
+          "retired; complete is False when older copy records were dropped")
       .def(
           "bytes_in_interval",
           [](ddl::NativeStager& st, uintptr_t e0, uintptr_t e1, int64_t timeout_ms) {
@@ -325,6 +342,8 @@ PYBIND11_MODULE(_ddl_hip, m) {
             d["busy_ms"] = r.busy_ms;
             d["overlap_ms"] = r.overlap_ms;
             d["copies_per_stream"] = py::make_tuple(r.copies_per_stream[0], r.copies_per_stream[1]);
+            d["untimed"] = r.untimed;
+            d["truncated"] = r.truncated;
             return d;
           },
           py::arg("e0"), py::arg("e1"), py::arg("timeout_ms") = 2000,
@@ -726,9 +745,6 @@ PYBIND11_MODULE(_ddl_hip, m) {
       py::arg("offsets"), py::arg("n"), py::arg("seq_len"), py::arg("max_segs"), py::arg("max_rows"),
       py::arg("seg_offsets"), py::arg("row_start"), py::arg("row_end"), py::arg("counts"), py::arg("scratch"),
       py::arg("stream"));
-  m.def("set_move_nt_stores", &ddl::set_move_nt_stores, py::arg("on"),
-        "raw row moves (same-dtype gather / scatter): non-temporal stores on or off, process-wide");
-  m.def("move_nt_stores", &ddl::move_nt_stores);
   m.def(
       "touch_pages",
       [](uintptr_t ptr, int64_t bytes, int64_t page, uintptr_t sink, int blocks, uintptr_t stream) {

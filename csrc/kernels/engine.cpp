@@ -140,7 +140,8 @@ int BatchEngine::enqueue(int64_t w, int64_t local, const StagedInfo& info, Pendi
   if (!on_caller) st = bs_;  // inline mode: the caller's stream (the null stream is a valid one), no event
   const int64_t slot = free_slots_.front();
   free_slots_.pop_front();
-  if (launch(w, local, 1, info, slot, st) != 0) return -1;
+  const int lrc = launch(w, local, 1, info, slot, st);
+  if (lrc != 0) return lrc == kCopyWaitFailed ? lrc : -1;
   if (on_caller) {  // every stream that read the window: its free event must follow all of them
     auto& v = read_streams_[w];
     if (std::find(v.begin(), v.end(), st) == v.end()) v.push_back(st);
@@ -212,7 +213,8 @@ int BatchEngine::enqueue_window(int64_t w, int64_t bpw, const StagedInfo& info, 
   }
   const int64_t s0 = free_slots_.front();
   for (int64_t j = 0; j < bpw; ++j) free_slots_.pop_front();
-  if (launch(w, 0, bpw, info, s0, st) != 0) return -1;
+  const int lrc = launch(w, 0, bpw, info, s0, st);
+  if (lrc != 0) return lrc == kCopyWaitFailed ? lrc : -1;
   const uint64_t t2 = clock_ns();
   // the launch is the window buffer's only reader: its free event goes right behind it
   const int b = info.buffer;
@@ -268,10 +270,10 @@ int BatchEngine::launch(int64_t w, int64_t local, int64_t n_batches, const Stage
   const auto& dst = slots_[slot];
   const void* src = buffers_[info.buffer];
   uint64_t t0 = clock_ns();
-  if (ready_host_) {  // the host waits for the copy (a no-op once it has landed)
+  if (ready_host_) {  // the host waits for the copy (a no-op once it has landed), bounded by the loader timeout
     const int q = NativeStager::copy_landed(info);
     if (q == 0) {
-      if (NativeStager::wait_copy(info) != 0) return -1;
+      if (stager_->wait_copy(info) != 0) return kCopyWaitFailed;
       ++ready_host_waits_;
     } else if (q < 0 && hipEventSynchronize(ready_[info.buffer]) != hipSuccess) {
       return -1;
@@ -475,7 +477,7 @@ int BatchEngine::release(int64_t w) {
     if (ready_host_) {
       // no batch read the window: its copy must still land before the buffer is reused
       const int q = NativeStager::copy_landed(it->second);
-      if (q == 0 && NativeStager::wait_copy(it->second) != 0) return -1;
+      if (q == 0 && stager_->wait_copy(it->second) != 0) return kCopyWaitFailed;
       if (q < 0 && hipEventSynchronize(ready_[b]) != hipSuccess) return -1;
     } else if ((ready_waited_ != w || ready_stream_ != st) && hipStreamWaitEvent(st, ready_[b], 0) != hipSuccess) {
       return -1;

@@ -78,6 +78,7 @@ struct BatchRecipe {
 
 class BatchEngine {
  public:
+  static constexpr int kCopyWaitFailed = -4;
   // `stager` outlives the engine; `ready` are the stager's per-ring-buffer events
   // (recorded when a window's H2D copy retires); `buffers` the ring buffers.
   BatchEngine(NativeStager* stager, BatchRecipe recipe, int32_t n_producers, std::vector<void*> buffers,
@@ -93,7 +94,9 @@ class BatchEngine {
   // Batch `local` of window `w` (bpw batches; next_ok: a window w+1 follows in this run).
   // Returns its slot id (>= 0), or a negative code: -(10 + stager wait code) when the window
   // could not be acquired (see NativeStager::wait; *failed_producer names the producer),
-  // -1 HIP error, -2 no free output slot. `tags` (if not null) receives the window's 4 publish tags.
+  // -1 HIP error, -2 no free output slot, kCopyWaitFailed (-4) the host wait for the window's H2D copy failed
+  // or timed out (the stager's error_code() / error() say which). `tags` (if not null) receives the window's
+  // 4 publish tags.
   int64_t get(int64_t w, int64_t local, int64_t bpw, bool next_ok, hipStream_t compute, int64_t timeout_ms,
               int32_t* failed_producer, int64_t* tags = nullptr);
   // Make window w available without building a batch (skipped windows at a partial epoch end).

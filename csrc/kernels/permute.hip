@@ -25,12 +25,12 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kUnroll = 4;
 
 // ------------------------------ raw byte moves ------------------------------
-// Store policy of the raw row moves: streaming (non-temporal) stores measured +7.8% out of cache on the
-// 1024-image gather (5.39 vs 5.00 TB/s, benchmarks/hbm_ceilings.hip); plain stores leave the batch in the
-// 256 MB MALL for a consumer that reads it right away. set_move_nt_stores() picks (A/B from Python).
-bool g_move_nt = false;
+// Store policy of the raw row moves: plain stores, which leave the batch in the 256 MB MALL for a consumer
+// that reads it right away. Streaming stores measured +7.8% on the isolated 1024-image gather (5.39 vs 5.00
+// TB/s) but 5.49M vs 5.74M samples/s in the HBM-resident loader, which reads the batch right after it is
+// written (profiles/r4_second/resident_*.json): plain stores only.
 
-template <typename U, bool NT>
+template <typename U>
 __global__ void __launch_bounds__(kThreads) move_rows_chunked(uint8_t* __restrict__ dst,
                                                               const uint8_t* __restrict__ src,
                                                               int64_t units_per_row, int64_t chunks_per_row,
@@ -57,10 +57,7 @@ __global__ void __launch_bounds__(kThreads) move_rows_chunked(uint8_t* __restric
   for (int k = 0; k < kUnroll; ++k) {
     const int64_t u = u0 + k * kThreads;
     if (u < units_per_row) {
-      if constexpr (NT)
-        __builtin_nontemporal_store(v[k], d + u);
-      else
-        d[u] = v[k];
+      d[u] = v[k];
     }
   }
   }
@@ -310,14 +307,9 @@ void launch_move(void* dst, const void* src, int64_t n_rows, int64_t row_bytes, 
   const int64_t units = row_bytes / static_cast<int64_t>(sizeof(U));
   if (units >= kThreads) {
     const int64_t chunks = (units + kThreads * kUnroll - 1) / (kThreads * kUnroll);
-    if (g_move_nt)
-      hipLaunchKernelGGL((move_rows_chunked<U, true>), tile_grid(n_rows * chunks, max_blocks), dim3(kThreads), 0, st,
-                         static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), units, chunks, n_rows * chunks,
-                         ri, scatter);
-    else
-      hipLaunchKernelGGL((move_rows_chunked<U, false>), tile_grid(n_rows * chunks, max_blocks), dim3(kThreads), 0, st,
-                         static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), units, chunks, n_rows * chunks,
-                         ri, scatter);
+    hipLaunchKernelGGL(move_rows_chunked<U>, tile_grid(n_rows * chunks, max_blocks), dim3(kThreads), 0, st,
+                       static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), units, chunks, n_rows * chunks,
+                       ri, scatter);
   } else {
     hipLaunchKernelGGL(move_rows_flat<U>, dim3(flat_grid_capped(n_rows * units, max_blocks)), dim3(kThreads), 0, st,
                        static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), units, n_rows * units, ri,
@@ -402,8 +394,6 @@ int gather_rows(void* dst, int32_t out_dt, const void* src, int32_t in_dt, int64
   return static_cast<int>(hipGetLastError());
 }
 
-void set_move_nt_stores(bool on) { g_move_nt = on; }
-bool move_nt_stores() { return g_move_nt; }
 
 int feistel_indices(int64_t* out, int64_t count, int64_t base, const FeistelKeys& keys, hipStream_t st) {
   if (count <= 0) return 0;

@@ -10,6 +10,8 @@
 #include <chrono>
 #include <climits>
 #include <cstdio>
+#include <cmath>
+#include <limits>
 #include <set>
 
 namespace ddl {
@@ -21,6 +23,24 @@ double mono_s() {
   return static_cast<double>(ts.tv_sec) + 1e-9 * static_cast<double>(ts.tv_nsec);
 }
 
+int64_t ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// a polling wait's pause: spin-yield for the first iterations (a copy or kernel a few us from done), then sleep
+void poll_pause(int* spins) {
+  if (++*spins < 64)
+    std::this_thread::yield();
+  else
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+}
+
+// ROCr's async-copy profiling is one switch for the whole process: on while any stager asks for copy times
+std::mutex g_prof_mu;
+int g_prof_users = 0;
+
+constexpr int64_t kSliceMs = 5;  // bounded waits check stop / failures this often
+
 
 }  // namespace
 
@@ -28,7 +48,7 @@ NativeStager::NativeStager(const Arena* arena, int32_t n_producers, int32_t n_sl
                            std::vector<void*> buffers, uint64_t buffer_bytes, hipStream_t copy_stream, int device,
                            std::vector<int32_t> peer_pids, int64_t timeout_ms, std::vector<hipEvent_t> ready,
                            std::vector<hipEvent_t> copy_done, bool post_copy, int64_t meta_bytes,
-                           hipStream_t copy_stream2, bool direct_dma)
+                           hipStream_t copy_stream2, bool direct_dma, bool copy_timing)
     : arena_(arena),
       P_(n_producers),
       n_slots_(n_slots),
@@ -64,24 +84,28 @@ NativeStager::NativeStager(const Arena* arena, int32_t n_producers, int32_t n_sl
   if (hipEventCreateWithFlags(&epoch_ev_, hipEventBlockingSync) != hipSuccess ||
       hipEventRecord(epoch_ev_, copy_stream_) != hipSuccess || hipEventSynchronize(epoch_ev_) != hipSuccess)
     throw std::runtime_error("NativeStager: epoch event failed");
-  if (hipStreamCreateWithFlags(&anchor_stream_, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&anchor_ev_[0], hipEventBlockingSync) != hipSuccess ||
-      hipEventCreateWithFlags(&anchor_ev_[1], hipEventBlockingSync) != hipSuccess)
-    throw std::runtime_error("NativeStager: anchor event failed");
+  if (hipStreamCreateWithFlags(&anchor_stream_, hipStreamNonBlocking) != hipSuccess)
+    throw std::runtime_error("NativeStager: anchor stream failed");
+  for (auto& e : anchor_ev_)
+    if (hipEventCreateWithFlags(&e, hipEventBlockingSync) != hipSuccess)
+      throw std::runtime_error("NativeStager: anchor event failed");
   {
     uint64_t f = 0;
     if (hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &f) == HSA_STATUS_SUCCESS && f > 0)
       sys_freq_ = static_cast<double>(f);
-    // two anchors a few us apart; the second is the current one until the first re-anchor
+    // two anchors a few us apart; the second is the current one until the first re-anchor (an idle stream
+    // at construction: up to a second for each)
     for (int k = 0; k < 2; ++k) {
       float a = 0.f;
-      if (!record_anchor(k, &anchor_sys_[k]) || hipEventElapsedTime(&a, epoch_ev_, anchor_ev_[k]) != hipSuccess)
+      if (!record_anchor(k, &anchor_sys_[k], 1000000) ||
+          hipEventElapsedTime(&a, epoch_ev_, anchor_ev_[k]) != hipSuccess)
         throw std::runtime_error("NativeStager: anchor event failed");
       anchor_ms_[k] = a;
     }
     anchor_cur_ = 1;
   }
   if (direct_dma) direct_ = init_direct(copy_stream2_ != nullptr ? 2 : 1);
+  if (copy_timing && !set_copy_timing(true)) throw std::runtime_error("NativeStager: async-copy profiling refused");
   thread_ = std::thread([this] { run(); });
   retire_thread_ = std::thread([this] { retire_loop(); });
 }
@@ -94,7 +118,9 @@ NativeStager::~NativeStager() {
   for (auto e : anchor_ev_)
     if (e != nullptr) hipEventDestroy(e);
   if (anchor_stream_ != nullptr) hipStreamDestroy(anchor_stream_);
-  for (auto sg : copy_sig_) hsa_signal_destroy(sg);
+  set_copy_timing(false);
+  for (size_t k = 0; k < copy_sig_.size(); ++k)
+    if (!sig_leaked_[k]) hsa_signal_destroy(copy_sig_[k]);
 }
 
 bool NativeStager::init_direct(int n_engines) {
@@ -184,16 +210,16 @@ bool NativeStager::init_direct(int n_engines) {
     return false;
   }
   if (got == 1) dma_engine_[1] = dma_engine_[0];
-  if (hsa_amd_profiling_async_copy_enable(true) != HSA_STATUS_SUCCESS) {
-    direct_reason_ = "async-copy profiling unavailable";
-    return false;
-  }
-  copy_sig_.resize(kRetireEvents);
-  for (auto& sg : copy_sig_)
+  copy_sig_.reserve(kRetireEvents);
+  for (int k = 0; k < kRetireEvents; ++k) {
+    hsa_signal_t sg{};
     if (hsa_signal_create(0, 0, nullptr, &sg) != HSA_STATUS_SUCCESS) {
       direct_reason_ = "hsa_signal_create failed";
       return false;
     }
+    copy_sig_.push_back(sg);
+    sig_leaked_.push_back(false);
+  }
   // bring each engine up now (its first copy in a process stalls ~10 ms), not on the first window
   const size_t n = static_cast<size_t>(std::min<uint64_t>(4096, buffer_bytes_));
   for (int k = 0; k < (dma_engine_[1] != dma_engine_[0] ? 2 : 1); ++k) {
@@ -206,21 +232,83 @@ bool NativeStager::init_direct(int n_engines) {
       direct_reason_ = "hsa_amd_memory_async_copy_on_engine failed";
       return false;
     }
-    while (hsa_signal_wait_scacquire(copy_sig_[0], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED) >= 1) {
+    if (wait_signal(copy_sig_[0], 10000, false) != 0) {  // bounded: a dead engine leaves HIP copy streams
+      sig_leaked_[0] = true;
+      direct_reason_ = "the SDMA engine warm-up copy did not complete within 10 s";
+      return false;
     }
   }
   return true;
 }
 
-bool NativeStager::record_anchor(int slot, uint64_t* sys_tick) {
+int NativeStager::wait_signal(hsa_signal_t sg, int64_t timeout_ms, bool stop_aware) const {
+  const uint64_t slice = static_cast<uint64_t>(sys_freq_ * static_cast<double>(kSliceMs) * 1e-3);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    if (hsa_signal_wait_scacquire(sg, HSA_SIGNAL_CONDITION_LT, 1, slice, HSA_WAIT_STATE_BLOCKED) < 1) return 0;
+    if (copy_stuck_.load()) return -1;
+    if (stop_aware && stopping_.load()) return kShutdown;
+    if (timeout_ms >= 0 && ms_since(t0) >= timeout_ms) return kTimeout;
+  }
+}
+
+int NativeStager::wait_event(hipEvent_t ev, int64_t timeout_ms, bool stop_aware) const {
+  const auto t0 = std::chrono::steady_clock::now();
+  int spins = 0;
+  for (;;) {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) return 0;
+    if (q != hipErrorNotReady) return -1;
+    if (copy_stuck_.load()) return -1;
+    if (stop_aware && stopping_.load()) return kShutdown;
+    if (timeout_ms >= 0 && ms_since(t0) >= timeout_ms) return kTimeout;
+    poll_pause(&spins);
+  }
+}
+
+void NativeStager::copy_timed_out(const StagedInfo& info, int64_t waited_ms) {
+  char eng[32];
+  std::snprintf(eng, sizeof(eng), "0x%x", info.engine);
+  copy_stuck_ = true;
+  fail(kTimeout, info.producer,
+       "window " + std::to_string(info.window) + ": its H2D copy (" + std::to_string(info.used_bytes) +
+           " B from producer " + std::to_string(info.producer) + " slot " + std::to_string(info.slot) + ", " +
+           (direct_ ? std::string("SDMA engine ") + eng : std::string("HIP copy stream ") + std::to_string(info.engine)) +
+           ") did not complete within " + std::to_string(waited_ms) + " ms");
+}
+
+bool NativeStager::set_copy_timing(bool on) {
+  if (!direct_) {  // stream copies are timed by their own HIP events
+    copy_timing_ = on;
+    return true;
+  }
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  if (on == copy_timing_.load()) return true;
+  if (on) {
+    if (g_prof_users == 0 && hsa_amd_profiling_async_copy_enable(true) != HSA_STATUS_SUCCESS) return false;
+    ++g_prof_users;
+  } else if (--g_prof_users == 0) {
+    hsa_amd_profiling_async_copy_enable(false);
+  }
+  copy_timing_ = on;
+  return true;
+}
+
+bool NativeStager::record_anchor(int slot, uint64_t* sys_tick, int64_t spin_us) {
   // record on the idle anchor stream and SPIN until it completes, bracketed by the HSA system clock: the
-  // completion lies inside [t0, t1]; retry (the last record counts) until the bracket is under 50 us
+  // completion lies inside [t0, t1]; retry (the last record counts) until the bracket is under 50 us. The
+  // anchor stream may share a hardware queue with the compute stream (GPU_MAX_HW_QUEUES): a marker queued
+  // behind a step's kernels is given up after spin_us (false: the caller keeps its current anchor)
   for (int k = 0; k < 4; ++k) {
     uint64_t t0 = 0, t1 = 0;
     hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP, &t0);
     if (hipEventRecord(anchor_ev_[slot], anchor_stream_) != hipSuccess) return false;
+    const auto w0 = std::chrono::steady_clock::now();
     hipError_t q;
     while ((q = hipEventQuery(anchor_ev_[slot])) == hipErrorNotReady) {
+      if (std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - w0).count() >
+          spin_us)
+        return false;
     }
     if (q != hipSuccess) return false;
     hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP, &t1);
@@ -249,14 +337,13 @@ int NativeStager::copy_landed(const StagedInfo& info) {
 }
 
 int NativeStager::wait_copy(const StagedInfo& info) {
-  if (info.copy_signal != 0) {
-    const hsa_signal_t sg{info.copy_signal};
-    while (hsa_signal_wait_scacquire(sg, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED) >= 1) {
-    }
-    return 0;
-  }
-  if (info.copy_event != nullptr) return hipEventSynchronize(info.copy_event) == hipSuccess ? 0 : -1;
-  return -1;
+  if (info.copy_signal == 0 && info.copy_event == nullptr) return -1;
+  const auto t0 = std::chrono::steady_clock::now();
+  const int rc = info.copy_signal != 0 ? wait_signal(hsa_signal_t{info.copy_signal}, timeout_ms_, true)
+                                       : wait_event(info.copy_event, timeout_ms_, true);
+  if (rc == kTimeout) copy_timed_out(info, ms_since(t0));
+  if (rc == -1 && copy_stuck_.load()) return kTimeout;  // another waiter timed out first (on this copy or one before)
+  return rc;
 }
 
 int NativeStager::wait_copy_window(int64_t w) {
@@ -269,28 +356,64 @@ bool NativeStager::device_ms(hipEvent_t e, double* out) const {
   // relative to the current anchor; an event older than it (a copy in flight across a re-anchor) is measured
   // from the previous one, which precedes every copy still in flight by construction
   float d = 0.f;
-  const int c = anchor_cur_;
+  const int c = anchor_cur_, prev = (anchor_cur_ + 2) % 3;
   if (hipEventElapsedTime(&d, anchor_ev_[c], e) == hipSuccess && d >= 0.f) {
     *out = anchor_ms_[c] + d;
     return true;
   }
-  if (hipEventElapsedTime(&d, anchor_ev_[c ^ 1], e) != hipSuccess) return false;
-  *out = anchor_ms_[c ^ 1] + d;
+  if (hipEventElapsedTime(&d, anchor_ev_[prev], e) != hipSuccess) return false;
+  *out = anchor_ms_[prev] + d;
   return true;
 }
 
-void NativeStager::reanchor() {
+bool NativeStager::reanchor() {
   // the idle anchor stream: the new event completes at once; its time since construction is the old
-  // anchor's plus a short (sub-second) float interval
-  std::lock_guard<std::mutex> lk(mu_);
-  const int nxt = anchor_cur_ ^ 1;
+  // anchor's plus a short (sub-second) float interval. Recorded into the slot no reader uses (neither the
+  // current nor the previous anchor), without mu_: the consumer's wait / peek / release never wait on it
+  int cur;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    cur = anchor_cur_;
+  }
+  const int nxt = (cur + 1) % 3;
   float d = 0.f;
   uint64_t sys = 0;
-  if (!record_anchor(nxt, &sys) || hipEventElapsedTime(&d, anchor_ev_[anchor_cur_], anchor_ev_[nxt]) != hipSuccess)
-    return;  // keep the current anchor (times stay correct, only coarser)
-  anchor_ms_[nxt] = anchor_ms_[anchor_cur_] + d;
+  if (!record_anchor(nxt, &sys, 2000) || hipEventElapsedTime(&d, anchor_ev_[cur], anchor_ev_[nxt]) != hipSuccess)
+    return false;  // keep the current anchor (times stay correct, only coarser)
+  std::lock_guard<std::mutex> lk(mu_);
+  anchor_ms_[nxt] = anchor_ms_[cur] + d;
   anchor_sys_[nxt] = sys;
   anchor_cur_ = nxt;
+  reanchors_ += 1;
+  return true;
+}
+
+int NativeStager::wait_retired(const Retire& r) {
+  // bounded by the loader's timeout; once close() began, by at most kCloseGraceMs more (a copy in flight must
+  // land before the caller frees the ring, but a dead engine must not hang close())
+  auto wait = [&](int64_t t, bool stop_aware) {
+    return direct_ ? wait_signal(copy_sig_[r.ev], t, stop_aware) : wait_event(retire_ev_[r.ev], t, stop_aware);
+  };
+  const auto t0 = std::chrono::steady_clock::now();
+  int rc = wait(timeout_ms_, true);
+  if (rc == kShutdown) {
+    const int64_t left = timeout_ms_ < 0 ? kCloseGraceMs : std::max<int64_t>(0, timeout_ms_ - ms_since(t0));
+    rc = wait(std::min(left, kCloseGraceMs), false);
+  }
+  if (rc == kTimeout) {
+    if (direct_) sig_leaked_[r.ev] = true;  // the engine may still write it: never destroyed
+    StagedInfo info;
+    info.window = r.window;
+    info.producer = static_cast<int32_t>(r.producer);
+    info.slot = static_cast<int32_t>(r.slot);
+    info.used_bytes = r.bytes;
+    info.engine = direct_ ? dma_engine_[r.stream] : static_cast<uint32_t>(r.stream);
+    copy_timed_out(info, ms_since(t0));
+  } else if (rc != 0 && !copy_stuck_.load()) {
+    fail(-1, static_cast<int32_t>(r.producer), "waiting for the H2D copy of window " + std::to_string(r.window) +
+                                                   " failed");
+  }
+  return rc;
 }
 
 void NativeStager::retire_loop() {
@@ -303,38 +426,40 @@ void NativeStager::retire_loop() {
       if (retire_q_.empty()) return;  // stopped and drained
       r = retire_q_.front();
     }
-    if (direct_) {
-      while (hsa_signal_wait_scacquire(copy_sig_[r.ev], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
-                                       HSA_WAIT_STATE_BLOCKED) >= 1) {
-      }
-    } else if (hipEventSynchronize(retire_ev_[r.ev]) != hipSuccess) {
-      return fail(-1, static_cast<int32_t>(r.producer), "hipEventSynchronize(retire) failed");
-    }
+    if (wait_retired(r) != 0) return;  // the stager failed (the copy never landed): its slot stays held
     bytes_landed_.fetch_add(r.bytes, std::memory_order_relaxed);
     windows_landed_.fetch_add(1, std::memory_order_release);
     arena_->set_state(r.producer, r.slot, kEmpty);  // slot back to its producer (release store + futex wake)
-    if (++retires_since_anchor_ >= kAnchorEvery) {
-      retires_since_anchor_ = 0;
-      reanchor();
-    }
+    if (++retires_since_anchor_ >= anchor_every_.load())
+      retires_since_anchor_ = reanchor() ? 0 : std::max<int64_t>(0, anchor_every_.load() - 64);  // retry soon
+    uint64_t seen_tick = 0;  // untimed direct copies: when the retire thread saw the copy land (an upper bound)
+    if (direct_ && !r.timed) hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP, &seen_tick);
     {
       std::lock_guard<std::mutex> lk(mu_);
       double t_start = 0.0, t_end = 0.0;  // ms since construction, GPU clock
       bool timed = false;
       if (direct_) {
         hsa_amd_profiling_async_copy_time_t t{};
-        if (r.bytes > 0 && hsa_amd_profiling_get_async_copy_time(copy_sig_[r.ev], &t) == HSA_STATUS_SUCCESS &&
-            t.end >= t.start && t.start != 0) {
+        if (r.timed && r.bytes > 0 &&
+            hsa_amd_profiling_get_async_copy_time(copy_sig_[r.ev], &t) == HSA_STATUS_SUCCESS && t.end >= t.start &&
+            t.start != 0) {
           t_start = sys_ms(t.start, anchor_cur_);
           t_end = sys_ms(t.end, anchor_cur_);
           timed = true;
+        } else if (r.bytes > 0) {
+          if (seen_tick == 0) hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP, &seen_tick);
+          t_start = std::numeric_limits<double>::quiet_NaN();
+          t_end = sys_ms(seen_tick, anchor_cur_);
         }
       } else {
         timed = device_ms(start_ev_[r.ev], &t_start) && device_ms(retire_ev_[r.ev], &t_end);
       }
-      if (timed) {
-        done_log_.push_back(DoneRec{r.window, r.bytes, t_start, t_end, r.stream});
-        if (done_log_.size() > kCopyLog) done_log_.pop_front();
+      if (timed || (direct_ && r.bytes > 0)) {
+        done_log_.push_back(DoneRec{r.window, r.bytes, t_start, t_end, r.stream, timed});
+        if (done_log_.size() > kCopyLog) {
+          done_trim_end_ms_ = std::max(done_trim_end_ms_, done_log_.front().t_end_ms);
+          done_log_.pop_front();
+        }
       }
       retire_q_.pop_front();
       retired_upto_ = r.window + 1;
@@ -378,11 +503,9 @@ void NativeStager::run() {
     const int b = static_cast<int>((w - first_) % depth_);
     hipEvent_t free_ev = nullptr;
     const int64_t s0 = ns();
-    int64_t backlog = 0;  // windows whose copy has landed but the consumer has not released yet
     {
       std::unique_lock<std::mutex> lk(mu_);
       cv_.wait(lk, [&] { return stop_ || w - depth_ < released_upto_; });
-      backlog = retired_upto_ - released_upto_;
       if (stop_) return;
       free_ev = free_events_[b];
     }
@@ -441,19 +564,19 @@ void NativeStager::run() {
     // has already completed needs no wait at all
     const bool free_pending = free_ev != nullptr && hipEventQuery(free_ev) != hipSuccess;
     // two SDMA engines alternate: while one copy runs the next is already queued on the other engine, so the
-    // link never waits for a copy to end (+1.8-2.5% feed, profiles/r2_copy_streams). With direct DMA and the
-    // engine policy, a copy made while the consumer holds >= 2 LANDED windows (the consumer is the bottleneck:
-    // no copy is urgent) goes to the engine of the previous copy instead -- one engine reading the host at a
-    // time disturbs the compute stream less (profiles/r4_twentieth: 0.57% vs 0.78% idle at r = 0.9). A ring
-    // that is full of copies still in flight means the link is the bottleneck: alternate (profiles/
-    // r4_twentyeighth). On HIP copy streams a switch cost a 24 us gap per copy (profiles/r4_fifth .. r4_tenth).
-    const bool one_engine = direct_ && engine_policy_ && backlog >= 2;
-    const int si = copy_stream2_ == nullptr ? 0 : one_engine ? last_stream_ : 1 - last_stream_;
-    if (one_engine && copy_stream2_ != nullptr) single_engine_copies_ += 1;
+    // link never waits for a copy to end (+1.8-2.5% feed, archive/profiles/r2_copy_streams). (Round 4 measured
+    // one engine while the consumer is the bottleneck: less GPU idle there, a lower link-bound rate; the
+    // alternation stayed.)
+    const int si = copy_stream2_ == nullptr ? 0 : 1 - last_stream_;
     hipStream_t cs = si == 0 ? copy_stream_ : copy_stream2_;
     if (free_pending) {
       if (free_on_host_ || direct_) {
-        if (hipEventSynchronize(free_ev) != hipSuccess) return fail(-1, -1, "hipEventSynchronize(free) failed");
+        // polled, not hipEventSynchronize: the free event follows the consumer's reads of the buffer (with the
+        // exchange, collectives that depend on peer ranks too), so it is consumer-paced and unbounded -- but
+        // close() must still end this wait
+        const int rc = wait_event(free_ev, -1, true);
+        if (rc == kShutdown) return;
+        if (rc != 0) return fail(-1, -1, "waiting for the free event of ring buffer " + std::to_string(b) + " failed");
       } else if (hipStreamWaitEvent(cs, free_ev, 0) != hipSuccess) {
         return fail(-1, -1, "hipStreamWaitEvent(free) failed");
       }
@@ -474,8 +597,9 @@ void NativeStager::run() {
     if (direct_) {
       // straight onto SDMA engine `si`: no AQL packet anywhere waits for this copy
       const hsa_signal_t sg = copy_sig_[rev];
-      hsa_signal_store_screlease(sg, 1);
+      hsa_signal_store_screlease(sg, stuck_window_.load() == w ? 2 : 1);  // 2: fault injection, never lands
       info.copy_signal = sg.handle;
+      info.engine = dma_engine_[si];
       if (info.used_bytes > 0) {
         const char* src = reinterpret_cast<const char*>(arena_->slot_data(p, s));
         if (src < arena_host_base_ || src + info.used_bytes > arena_host_base_ + arena_span_) {
@@ -492,17 +616,18 @@ void NativeStager::run() {
       } else {
         hsa_signal_store_screlease(sg, 0);
       }
-    } else if (info.used_bytes > 0 &&
-               hipMemcpyAsync(buffers_[b], arena_->slot_data(p, s), info.used_bytes, hipMemcpyHostToDevice, cs) !=
-                   hipSuccess) {
-      return fail(-1, static_cast<int32_t>(p), "hipMemcpyAsync H2D failed");
+    } else {
+      info.engine = static_cast<uint32_t>(si);
+      if (info.used_bytes > 0 &&
+          hipMemcpyAsync(buffers_[b], arena_->slot_data(p, s), info.used_bytes, hipMemcpyHostToDevice, cs) != hipSuccess)
+        return fail(-1, static_cast<int32_t>(p), "hipMemcpyAsync H2D failed");
     }
     const int64_t s4 = ns();
     if (!direct_ && hipEventRecord(retire_ev_[rev], cs) != hipSuccess)
       return fail(-1, static_cast<int32_t>(p), "hipEventRecord(retire) failed");
     {
       std::lock_guard<std::mutex> lk(mu_);
-      retire_q_.push_back(Retire{w, p, s, info.used_bytes, rev, si});
+      retire_q_.push_back(Retire{w, p, s, info.used_bytes, rev, si, !direct_ || copy_timing_.load()});
     }
     retire_cv_.notify_all();
     if (!direct_) info.copy_event = retire_ev_[rev];
@@ -518,7 +643,10 @@ void NativeStager::run() {
       staged_[w] = info;
       if (wait_log_.size() < 4096) wait_log_.push_back({w, s1 - s0, s2 - s1, s3 - s2, s4 - s3, s5 - s4, s0});
       copy_log_.push_back(CopyRec{w, enq_ns, info.used_bytes});
-      if (copy_log_.size() > kCopyLog) copy_log_.pop_front();
+      if (copy_log_.size() > kCopyLog) {
+        copy_trim_ns_ = std::max(copy_trim_ns_, copy_log_.front().enq_ns);
+        copy_log_.pop_front();
+      }
     }
     cv_.notify_all();
   }
@@ -562,6 +690,7 @@ void NativeStager::release(int64_t w, hipEvent_t free_event) {
 }
 
 void NativeStager::close() {
+  stopping_ = true;
   {
     std::lock_guard<std::mutex> lk(mu_);
     stop_ = true;
@@ -573,21 +702,22 @@ void NativeStager::close() {
   if (retire_thread_.joinable()) retire_thread_.join();
 }
 
-std::pair<uint64_t, uint64_t> NativeStager::copies_between(uint64_t t0_ns, uint64_t t1_ns) const {
+CopiesBetween NativeStager::copies_between(uint64_t t0_ns, uint64_t t1_ns) const {
   // complete NOW: retired by the retire thread, or its retire event already signalled (the retire thread
   // lags the device by its wake-up); call right at the end of the region, before any settle()
   std::lock_guard<std::mutex> lk(mu_);
   std::set<int64_t> done;
   for (const Retire& r : retire_q_)
     if (retired_now(r.ev)) done.insert(r.window);
-  uint64_t n = 0, bytes = 0;
+  CopiesBetween out;
+  out.complete = copy_trim_ns_ < t0_ns;
   for (const CopyRec& c : copy_log_) {
     if (c.enq_ns >= t0_ns && c.enq_ns <= t1_ns && (c.window < retired_upto_ || done.count(c.window) != 0)) {
-      ++n;
-      bytes += c.bytes;
+      ++out.windows;
+      out.bytes += c.bytes;
     }
   }
-  return {n, bytes};
+  return out;
 }
 
 InIntervalBytes NativeStager::bytes_in_interval(hipEvent_t e0, hipEvent_t e1, int64_t timeout_ms) {
@@ -607,7 +737,12 @@ InIntervalBytes NativeStager::bytes_in_interval(hipEvent_t e0, hipEvent_t e1, in
       }))
     return out;
   std::vector<std::pair<double, int>> edges;  // clipped [start, end] of every overlapping copy: +1 / -1
+  out.truncated = done_trim_end_ms_ > T0;  // a dropped record may overlap the interval
   for (const DoneRec& d : done_log_) {
+    if (!d.timed) {  // landed at or before t_end_ms: it may overlap the interval unless it ended before it
+      if (d.t_end_ms >= T0) out.untimed = true;
+      continue;
+    }
     const double a = std::max(d.t_start_ms, T0);
     const double b = std::min(d.t_end_ms, T1);
     if (b <= a) continue;
@@ -628,13 +763,18 @@ InIntervalBytes NativeStager::bytes_in_interval(hipEvent_t e0, hipEvent_t e1, in
     if (live >= 1) out.busy_ms += dt;
     if (live >= 2) out.overlap_ms += dt;
   }
-  out.ok = true;
+  out.ok = !out.untimed && !out.truncated;
   return out;
 }
 
 std::string NativeStager::error() const {
   std::lock_guard<std::mutex> lk(mu_);
   return error_msg_;
+}
+
+int NativeStager::error_code() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return error_code_;
 }
 
 }  // namespace ddl

@@ -215,7 +215,7 @@ class CheckpointMixin:
                 self._stager = WindowStager(self.connection, self.n_slots, self.total_windows, self.prefetch_depth,
                                             self.device, old.max_window_bytes, post_copy=self._exchange_fn,
                                             timeout_s=self.timeout_s, first_window=self.window,
-                                            meta_bytes=old.meta_bytes)
+                                            meta_bytes=old.meta_bytes, copy_timing=old.copy_timing)
                 self.connection.add_finalizer(self._stager.close)
                 self.metrics.bytes_h2d += old.bytes_h2d
                 del old

@@ -145,6 +145,7 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
         token_rows: str = "exact",
         verify_order: bool | None = None,
         max_ahead: int | None = None,
+        copy_timing: bool = False,
     ):
         if mode not in MODES:
             raise ValueError(f"unknown mode {mode!r}; one of {MODES}")
@@ -189,6 +190,9 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
             raise ValueError("token_rows must be 'exact' or 'fixed'")
         self.token_rows = token_rows
         self.debug_checksum = debug_checksum
+        # device times of every window copy from the first one (WindowStager.copy_timing: bytes_in_interval and
+        # copy_summary need them; direct DMA takes them from a process-wide ROCr switch, so off by default)
+        self.copy_timing = bool(copy_timing)
         self.metrics = LoaderMetrics()
         self.timeout_s = timeout_s if timeout_s is not None else (connection.timeout_s if connection else 600.0)
         self._timeout_ms = int(self.timeout_s * 1000)
@@ -328,7 +332,8 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
             meta_bytes = max(int(x.extra.get("meta_bytes", 0)) for x in md)
             self._stager = WindowStager(connection, self.n_slots, self.total_windows, self.prefetch_depth,
                                         self.device, max_bytes, post_copy=self._exchange_fn,
-                                        timeout_s=self.timeout_s, first_window=self.window, meta_bytes=meta_bytes)
+                                        timeout_s=self.timeout_s, first_window=self.window, meta_bytes=meta_bytes,
+                                        copy_timing=self.copy_timing)
             connection.add_finalizer(self._stager.close)  # stop the native thread before the arena is unpinned
             if self._produces_copy():
                 self._batch_stream = streams.batch_stream(self.device)

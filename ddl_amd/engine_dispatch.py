@@ -23,14 +23,6 @@ from .utils import streams
 from .utils.tracing import trace_range
 
 _TRACE_ENGINE = os.environ.get("DDL_ROCTX", "1") == "2"  # roctx level 2: also a range per native get
-# grid cap of the engine's gather / split launches (0: one workgroup per row tile, i.e. the whole GPU for a
-# 77 MB batch); an A/B hook for benchmarks/bench_idle_sweep.py --gather-blocks
-GATHER_MAX_BLOCKS = 0
-# the host (not the batch stream) waits for a window's H2D copy before launching its batch kernels, so no
-# queue holds a barrier packet on an unfinished copy: GPU idle below the crossover 2.4-2.5% -> 1.1% at
-# r = 0.9 (profiles/r4_sixteenth, r4_seventeenth). Never with the exchange (the host must not wait on peer
-# ranks). False is the A/B hook of benchmarks/bench_idle_sweep.py --device-ready-wait.
-READY_ON_HOST = True
 
 
 class NativeDispatchMixin:
@@ -57,7 +49,7 @@ class NativeDispatchMixin:
         out_dtype = self.out_dtype or (torch.float32 if norm is not None else wdt)
         splits = list(self.splits[0])
         rec = dict(in_dt=_dtypes.code(wdt), out_dt=_dtypes.code(out_dtype), shuffle=self.shuffle == "device",
-                   batch=self.batch_size, seed=self.seed & ((1 << 64) - 1), max_blocks=GATHER_MAX_BLOCKS, scale=[],
+                   batch=self.batch_size, seed=self.seed & ((1 << 64) - 1), max_blocks=0, scale=[],
                    bias=[],
                    plane=0, n_data=[int(x.nData) for x in self.metadata_from_producer], widths=[])
         if (self.contiguous or self.copy_batches) and len(splits) > 1 and len(self.sample_shape) == 1 \
@@ -215,8 +207,11 @@ class NativeDispatchMixin:
         # barrier on the compute stream, profiles/r3_handoff) unless the exchange is on -- its kernels wait
         # on peer ranks, and the host must never block on another rank's progress
         self._engine.host_handoff = self._exchange_fn is None
-        # (a direct-DMA copy has no device-side event at all: then the host always waits)
-        self._engine.ready_on_host = (READY_ON_HOST or self._stager.direct_dma) and self._exchange_fn is None
+        # the host (not the batch stream) waits for a window's H2D copy before launching its batch kernels
+        # (bounded by the loader timeout), so no queue holds a barrier packet on an unfinished copy: GPU idle
+        # below the crossover 2.4-2.5% -> 1.1% at r = 0.9 (archive/profiles/r4_sixteenth, r4_seventeenth). Not
+        # with the exchange: the batch stream waits on the post-copy stage's ready event instead
+        self._engine.ready_on_host = self._exchange_fn is None
         # then the copy's retire event is the only marker behind it in the copy stream's queue
         self._stager._native.record_ready = not self._engine.ready_on_host
         self._eng_mode = mode
@@ -269,6 +264,9 @@ class NativeDispatchMixin:
                 raise PeerDeathError(f"{what}: producer {producer} (pid {pid}) "
                                      + ("reported a failure" if rc == 4 else "died"), producer, pid)
             raise DDLError(f"{what}: {self._stager._native.error()}")
+        if code == -4:  # the host wait for the window's H2D copy failed (the stager's error names it)
+            err = self._stager._native.error() or "waiting for the window's H2D copy failed"
+            raise (DDLTimeoutError if self._stager._native.error_code == 2 else DDLError)(f"{what}: {err}")
         if code == -3:
             raise DDLError(f"{what}: requested out of order after the window's last batch -- a window goes back "
                            "to the prefetcher when its last batch is launched; within a window, fetch batches "

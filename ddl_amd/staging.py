@@ -7,22 +7,28 @@ ddl/connection.py:89-92). This is the MI355X-native replacement of that gap
 
 * a native C++ stager thread (``csrc/kernels/stager.cpp``, no GIL) walks the
   consumer's window schedule ahead of the training loop: it futex-waits for
-  producer ``p`` to publish slot ``s``, enqueues ``hipMemcpyAsync`` H2D from
-  the pinned arena into HBM ring buffer ``w % n_buffers`` on the **prefetch stream**,
-  then enqueues (``hipLaunchHostFunc``) the hand-back of the slot to its
-  producer, so the producer refills it the moment the DMA retires -- the
-  consumer thread is never involved;
+  producer ``p`` to publish slot ``s`` and copies it from the pinned arena into
+  HBM ring buffer ``w % n_buffers`` straight on an SDMA engine through ROCr
+  (direct DMA; two engines alternate). A second native thread retires the copies
+  in order and hands each slot back to its producer the moment its DMA lands --
+  the consumer thread is never involved. Without direct DMA (ROCr refuses: see
+  ``direct_dma_reason``) the copies run on two HIP copy streams instead;
 * optional post-copy device work (the cross-GPU global shuffle exchange over
   RCCL, ``parallel/shuffle.py``) on a second stream. Collectives must be
   issued in the same order and number on every rank, so they are NOT issued
   by the stager (whose progress depends on producer timing): the consumer
   thread issues window w+1's exchange when it starts window w (``get``),
-  i.e. one window ahead, deterministically;
-* a ``ready`` event per buffer; the compute stream waits on it *on the device*
-  (``hipStreamWaitEvent``) -- the host never blocks on a copy;
+  i.e. one window ahead, deterministically -- after a host wait for w+1's copy
+  (no HIP event follows a direct-DMA copy);
+* consumers wait for a copy on the host (``wait_ready``: a bounded wait on its
+  completion signal), so no AQL queue holds a packet waiting on a copy; with a
+  post-copy stage the compute stream waits on the stage's ``ready`` event;
 * a buffer is recycled only after a ``free`` event recorded on the compute
   stream when the consumer moved past the window, so in-flight kernels that
   read it (permute/cast/collate) finish first.
+
+Every host wait is bounded by the loader's ``timeout_s``: a copy that never lands raises
+``DDLTimeoutError`` naming the window and SDMA engine, and ``close()`` never hangs on one.
 
 HBM is plentiful on MI355X (288 GB): windows are staged whole, ``depth``
 windows deep (default 4), plus
@@ -32,7 +38,6 @@ two ring buffers for the exchange lookahead when the exchange is on.
 from __future__ import annotations
 
 import dataclasses
-import os
 import sys
 import time
 from typing import Callable
@@ -45,20 +50,12 @@ from .utils import streams
 from .utils.logging import logger
 from .utils.tracing import trace_range
 
-# the stager thread waits for a ring buffer's free event on the host instead of enqueueing the wait on the copy
-# stream (a barrier packet in its queue): GPU idle near r = 1 1.4-1.6% -> 0.9-1.0% (profiles/r4_seventeenth).
-# False is the A/B hook of benchmarks/bench_idle_sweep.py --device-free-wait.
-FREE_ON_HOST = True
 # window copies go straight to SDMA engines through ROCr (NativeStager direct-DMA mode) instead of HIP copy
 # streams, so no AQL queue holds a packet waiting on a copy: GPU idle at r = 0.9 1.25% -> 0.78%, feed-bound
-# rate 187.9k -> 191.4k samples/s (profiles/r4_twentieth). With a post-copy stage (the exchange) the consumer
-# waits for the copy on the host before it enqueues the stage. False is the A/B hook of bench_idle_sweep.py
-# --stream-copies.
+# rate 187.9k -> 191.4k samples/s (archive/profiles/r4_twentieth). With a post-copy stage (the exchange) the
+# consumer waits for the copy on the host before it enqueues the stage. False: HIP copy streams (tests compare
+# the two paths).
 DIRECT_DMA = True
-# direct DMA: a copy made while the consumer holds >= 2 landed windows stays on the previous copy's SDMA engine
-# (one engine reading the host while the consumer is the bottleneck) instead of alternating; an A/B hook of
-# bench_idle_sweep.py --one-engine-when-full (off: the measured default alternates always)
-ENGINE_POLICY = False
 
 
 @dataclasses.dataclass
@@ -90,9 +87,6 @@ def warm_copy_engines(device: torch.device, n_engines: int = 4, nbytes: int = 51
     Here ``n_engines`` copies of ``nbytes`` are enqueued on separate streams back to back, each
     long enough to keep its engine busy while the next one comes up. Returns the seconds spent.
     """
-    import os
-    import time
-
     key = (device.type, device.index)
     if key in _SDMA_WARM or device.type != "cuda":
         return 0.0
@@ -119,7 +113,7 @@ class WindowStager:
 
     def __init__(self, connection, n_slots: int, total_windows: int, depth: int, device: torch.device,
                  max_window_bytes: int, post_copy: Callable | None = None, timeout_s: float = 600.0,
-                 first_window: int = 0, meta_bytes: int = 0):
+                 first_window: int = 0, meta_bytes: int = 0, copy_timing: bool = False):
         if depth < 1:
             raise ValueError("prefetch depth must be >= 1")
         hip, rt = _native.hip(), _native.runtime()
@@ -139,12 +133,10 @@ class WindowStager:
         # exchange) on a second stream, so window w's exchange overlaps window
         # w+1's DMA instead of idling the copy engine.
         self.copy_stream = torch.cuda.Stream(device=self.device)
-        # two copy streams (two SDMA engines), strictly alternating: when copies run back to back the next one
-        # is already running when one finishes, so the ~25 us gap per copy on one engine is gone (+1.8-2.5%,
-        # profiles/r2_copy_streams). DDL_COPY_STREAMS=1: one stream. (Round 4 tried one engine while the
-        # consumer is the bottleneck and kept alternation: csrc/kernels/stager.cpp, profiles/r4_tenth.)
-        n_cs = int(os.environ.get("DDL_COPY_STREAMS", "2"))
-        self.copy_stream2 = torch.cuda.Stream(device=self.device) if n_cs >= 2 else None
+        # two copy streams / SDMA engines, strictly alternating: when copies run back to back the next one is
+        # already running when one finishes, so the ~25 us gap per copy on one engine is gone (+1.8-2.5%,
+        # archive/profiles/r2_copy_streams)
+        self.copy_stream2 = torch.cuda.Stream(device=self.device)
         self.stream = torch.cuda.Stream(device=self.device) if post_copy is not None else self.copy_stream
         # The consumer posts window w+1's exchange when it enters window w (the fixed, rank-identical
         # issue point of the collective, parallel/order.py), so two windows are held at once (w being
@@ -169,14 +161,15 @@ class WindowStager:
             peer_pids=list(connection.producer_pids), timeout_ms=int(timeout_s * 1000),
             ready=[e.cuda_event for e in self.ready_events], copy_done=[e.cuda_event for e in self._copy_done],
             post_copy=post_copy is not None, meta_bytes=int(meta_bytes),
-            copy_stream2=self.copy_stream2.cuda_stream if self.copy_stream2 is not None else 0,
-            direct_dma=bool(DIRECT_DMA))
-        self._native.engine_policy = ENGINE_POLICY
+            copy_stream2=self.copy_stream2.cuda_stream, direct_dma=bool(DIRECT_DMA), copy_timing=bool(copy_timing))
         self.direct_dma = bool(self._native.direct_dma)
         if DIRECT_DMA and not self.direct_dma:
             logger.info("direct-DMA staging unavailable (%s): HIP copy streams", self._native.direct_dma_reason)
-        self._native.free_on_host = FREE_ON_HOST
-        self.copy_streams = 2 if self.copy_stream2 is not None else 1
+        # the stream fallback too waits for a pending free ring buffer on the host (polled, close() interrupts
+        # it) instead of a barrier packet in the copy stream's queue: GPU idle near r = 1 1.4-1.6% -> 0.9-1.0%
+        # (archive/profiles/r4_seventeenth)
+        self._native.free_on_host = True
+        self.copy_streams = 2
         self.meta_bytes = int(meta_bytes)
 
     # -------------------------------------------------------------- consumer
@@ -202,13 +195,23 @@ class WindowStager:
     def wait_ready(self, sw: StagedWindow, stream) -> None:
         """Order ``stream`` after window ``sw``'s copy (and its post-copy stage): a device-side event wait, or in
         direct-DMA mode without a post-copy stage (no HIP event behind the copy) a host wait for the copy's
-        completion signal."""
+        completion signal, bounded by ``timeout_s``."""
         if self.direct_dma and self.post_copy is None:
-            rc = self._native.wait_copy(sw.index)
-            if rc != 0:
-                raise DDLError(f"window {sw.index}: waiting for its copy failed ({self._native.error()})")
+            self._wait_copy(sw.index)
         else:
             stream.wait_event(self.ready_events[sw.buffer])
+
+    def _wait_copy(self, w: int) -> None:
+        """Host wait for window ``w``'s H2D copy (the stager's bounded wait; GIL released)."""
+        rc = self._native.wait_copy(w)
+        if rc == 0:
+            return
+        if rc == 2:
+            raise DDLTimeoutError(self._native.error() or f"window {w}: its H2D copy did not land within "
+                                                          f"{self.timeout_s:.0f}s")
+        if rc == 1:
+            raise ShutdownError(f"window {w}: loader was shut down while waiting for its copy")
+        raise DDLError(f"window {w}: waiting for its copy failed ({self._native.error()})")
 
     def peek(self, w: int) -> StagedWindow | None:
         """Window ``w`` if it is already staged AND its post-copy work (exchange) is
@@ -234,8 +237,7 @@ class WindowStager:
         sw = self._wait_staged(w)
         self.post_wait_s += time.perf_counter() - t0
         if self.direct_dma:  # no HIP event behind the copy: the host waits for it, then enqueues the stage
-            if self._native.wait_copy(w) != 0:
-                raise DDLError(f"window {w}: waiting for its copy failed ({self._native.error()})")
+            self._wait_copy(w)
         else:
             self.stream.wait_event(self._copy_done[sw.buffer])
         with streams.on_stream(self.stream), trace_range("ddl.stage.post_copy"):
@@ -296,8 +298,7 @@ class WindowStager:
         self._closed = True
         self._native.close()
         self.copy_stream.synchronize()
-        if self.copy_stream2 is not None:
-            self.copy_stream2.synchronize()
+        self.copy_stream2.synchronize()
         self.stream.synchronize()
         # drop the ring (a live seek builds a new stager; batches handed out keep their own refs) and any
         # token-collate views cached over it (models/tokens.py), which would otherwise keep it allocated
@@ -320,11 +321,25 @@ class WindowStager:
         """After a device synchronize: wait until every completed copy has been counted as landed."""
         self._native.settle(int(timeout_s * 1000))
 
+    @property
+    def copy_timing(self) -> bool:
+        """Device times for every window copy, which ``bytes_in_interval`` / ``copy_summary`` need. Direct DMA
+        takes them from ROCr's async-copy profiling, a PROCESS-WIDE switch (it timestamps every async copy of
+        the process, torch's and RCCL's included), so it is off unless set here; turn it on before the copies
+        to be measured. Stream-mode copies are always timed."""
+        return bool(self._native.copy_timing)
+
+    @copy_timing.setter
+    def copy_timing(self, on: bool) -> None:
+        if not self._native.set_copy_timing(bool(on)):
+            raise DDLError("ROCr refused async-copy profiling: no device times for direct-DMA copies")
+
     def bytes_in_interval(self, e0: torch.cuda.Event, e1: torch.cuda.Event, timeout_s: float = 2.0) -> dict:
         """H2D bytes that crossed PCIe between two recorded timing events (``enable_timing=True``), on the
-        GPU clock: each copy is timed on the device (start and retire events) and counts with the share of
-        its bytes whose [start, end] lies between the events. ``{"ok", "bytes", "windows", "copies",
-        "t0_ms", "t1_ms"}``; waits (bounded) for copies still in flight."""
+        GPU clock: each copy is timed on the device and counts with the share of its bytes whose [start, end]
+        lies between the events. ``{"ok", "bytes", "windows", "copies", "t0_ms", "t1_ms", "untimed",
+        "truncated"}``; waits (bounded) for copies still in flight. ``ok`` is False when a copy that may
+        overlap the interval was not timed (``copy_timing`` off when it ran) or its record was dropped."""
         return dict(self._native.bytes_in_interval(e0.cuda_event, e1.cuda_event, int(timeout_s * 1000)))
 
     def copy_summary(self, e0: torch.cuda.Event, e1: torch.cuda.Event) -> dict:
@@ -360,5 +375,4 @@ class WindowStager:
                 "copy_streams": self.copy_streams, "free_waits_enqueued": int(self._native.free_waits),
                 "free_on_host": bool(self._native.free_on_host), "direct_dma": self.direct_dma,
                 "direct_dma_reason": self._native.direct_dma_reason,
-                "single_engine_copies": int(self._native.single_engine_copies),
                 "exchange_issue_wait_s": round(self.post_wait_s, 6)}

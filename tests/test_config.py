@@ -2,7 +2,7 @@
 
 Knobs covered elsewhere: DDL_BACKEND (test_multirank_*), DDL_DEVICE (everywhere), DDL_PRODUCERS_PER_RANK
 (test_utils), DDL_PRODUCER_MODE / DDL_FAULT_PRODUCER (test_loader_cpu), DDL_HOSTNAME (test_multirank_cpu),
-DDL_COPY_STREAMS (test_loader_gpu), DDL_FAULT_RANK (test_job_abort). The rest are tested here.
+DDL_FAULT_RANK (test_job_abort). The rest are tested here.
 """
 
 import os

@@ -1,0 +1,121 @@
+"""Direct-DMA staging on the card: bit-exact batches and bounded waits.
+
+Window copies go straight onto SDMA engines through ROCr (``csrc/kernels/stager.cpp``); every consumer of a
+window waits for its copy's completion signal on the host. These tests hold the delivered batches to the
+PRODUCER'S BYTES (``ops.ref_gather_rows`` over the window the producer wrote, in the window's Feistel
+order), which is the reference's batch semantics -- a slice of the producer's window
+(``/root/reference/ddl/mpi_dataloader.py:179-198``) -- plus the device shuffle; and they check that a copy that
+never lands fails the loader within its timeout instead of hanging it (the reference's consumer blocks in
+``Recv`` forever, ``/root/reference/ddl/connection.py:154``).
+"""
+
+import time
+
+import pytest
+import torch
+
+import ddl_amd
+from ddl_amd import Marker, ops
+from ddl_amd.dataloader import window_perm_key
+from ddl_amd.permutation import FeistelPermutation
+from tests.helpers import IdProducer
+
+pytestmark = pytest.mark.gpu
+
+N, WIDTH, B, P, SEED = 64, 8, 16, 2, 3
+
+
+def producer_window(p: int, rnd: int) -> torch.Tensor:
+    """The window producer ``p`` writes in round ``rnd`` (IdProducer._write, rank 0), int32 [N, WIDTH]."""
+    t = torch.empty(N, WIDTH, dtype=torch.int32)
+    prod = IdProducer(N, WIDTH)
+    prod.rank_global, prod.producer_index = 0, p
+    prod._write(t, rnd)
+    return t
+
+
+def expected_batch(w: int, local: int) -> torch.Tensor:
+    p, rnd = w % P, w // P  # round-robin schedule, one slot per producer
+    perm = FeistelPermutation(N, SEED, window_perm_key(p, rnd))
+    return ops.ref_gather_rows(producer_window(p, rnd), perm=perm, base=local * B, n_rows=B)
+
+
+@pytest.mark.parametrize("dispatch", ["lookahead", "inline", "python"])
+@pytest.mark.parametrize("slow", [False, True])
+def test_direct_dma_batches_equal_the_producers_bytes(dispatch, slow):
+    """Every batch, fast or slow consumer (the ring refills a 2-buffer ring many times), through the native
+    engine and the Python dispatch path, equals the producer's window rows in the window's order, bitwise."""
+    with ddl_amd.start(n_producers=P) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(IdProducer(N, WIDTH), B, conn, 8, env=env, device=torch.device("cuda"),
+                                           shuffle="device", seed=SEED, prefetch_depth=2, copy_batches=True,
+                                           native_dispatch=dispatch if dispatch != "python" else False)
+        st = dl.stats()
+        assert st["direct_dma"], st.get("direct_dma_reason")
+        w = 0
+        for e in range(8):
+            for i in range(len(dl)):
+                a, b = dl[i]
+                got = torch.cat([a, b], 1).cpu()
+                assert torch.equal(got, expected_batch(w, i)), (w, i)
+                if slow:
+                    time.sleep(0.003)
+                dl.mark(Marker.END_OF_BATCH)
+            w += 1
+            if e < 7:
+                dl.mark(Marker.END_OF_EPOCH)
+        dl._stager.settle()
+        st = dl.stats()
+        assert st["bytes_landed"] == st["bytes_h2d"] == 8 * N * WIDTH * 4
+        dl.close()
+
+
+@pytest.mark.parametrize("dispatch", ["lookahead", "python"])
+def test_stuck_copy_raises_within_the_timeout_and_close_returns(dispatch):
+    """A window copy whose completion signal never drops (fault injection: armed one too high, what a hung
+    SDMA engine looks like) fails the consumer with DDLTimeoutError naming the window and the engine within
+    the loader's timeout, and close() returns promptly -- no wait anywhere is unbounded."""
+    from ddl_amd.exceptions import DDLTimeoutError
+
+    timeout_s = 3.0
+    with ddl_amd.start(n_producers=P) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(IdProducer(N, WIDTH), B, conn, 8, env=env, device=torch.device("cuda"),
+                                           shuffle="device", seed=SEED, prefetch_depth=2, copy_batches=True,
+                                           timeout_s=timeout_s,
+                                           native_dispatch=dispatch if dispatch != "python" else False)
+        if not dl._stager.direct_dma:
+            pytest.skip(f"no direct DMA here: {dl.stats()['direct_dma_reason']}")
+        dl._stager._native.inject_stuck_copy(3)  # windows 0 and 1 fill the 2-buffer ring; 3 is not staged yet
+        t0 = time.monotonic()
+        with pytest.raises(DDLTimeoutError) as ei:
+            for e in range(8):
+                for i in range(len(dl)):
+                    if e == 2 and i == 0:
+                        t0 = time.monotonic()  # window 3's copy is enqueued from here on (window 1 released)
+                    dl[i]
+                    dl.mark(Marker.END_OF_BATCH)
+                dl.mark(Marker.END_OF_EPOCH)
+        waited = time.monotonic() - t0
+        msg = str(ei.value)
+        assert "window 3" in msg and "SDMA engine" in msg and "did not complete" in msg, msg
+        assert waited < timeout_s + 5.0, waited
+        t1 = time.monotonic()
+        dl.close()
+        assert time.monotonic() - t1 < 15.0
+
+
+def test_direct_dma_copy_timing_is_off_unless_asked():
+    """ROCr's async-copy profiling is process-wide: a loader turns it on only with copy_timing=True, and its
+    stager turns it off again when it is done with it (reference counted)."""
+    with ddl_amd.start(n_producers=P) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(IdProducer(N, WIDTH), B, conn, 2, env=env, device=torch.device("cuda"),
+                                           prefetch_depth=2, copy_batches=True)
+        st = dl._stager
+        assert not st.copy_timing
+        st.copy_timing = True
+        assert st.copy_timing
+        st.copy_timing = False
+        assert not st.copy_timing
+        for _ in dl:
+            dl.mark(Marker.END_OF_BATCH)
+        dl.mark(Marker.END_OF_EPOCH)
+        dl.close()

@@ -418,17 +418,19 @@ def test_stager_counts_the_copies_of_a_time_window():
                 dl.mark(Marker.END_OF_EPOCH)
         torch.cuda.synchronize()
         t1 = rt.now_ns()
-        n, b = st._native.copies_between(t0, t1)
-        assert n == st.windows_staged == 4 and b == st.bytes_h2d == n * 64 * 8 * 4
-        assert st._native.copies_between(t1 + 1, t1 + 2) == (0, 0)
+        n, b, complete = st._native.copies_between(t0, t1)
+        assert complete and n == st.windows_staged == 4 and b == st.bytes_h2d == n * 64 * 8 * 4
+        assert st._native.copies_between(t1 + 1, t1 + 2) == (0, 0, True)
         dl.close()
 
 
-def test_stager_bytes_in_interval_is_pro_rata_and_additive():
+@pytest.mark.parametrize("anchor_every", [None, 3])
+def test_stager_bytes_in_interval_is_pro_rata_and_additive(anchor_every):
     """bytes_in_interval(e0, e1): the H2D bytes that crossed PCIe between two timing events, from the
     device times of every copy (bench.py's landed count). An interval around the whole run holds every byte;
     splitting it at an event in the middle splits the bytes exactly (pro rata per copy, nothing lost or
-    counted twice); an interval after the run holds none."""
+    counted twice); an interval after the run holds none. With the device clock re-anchored every 3 retires
+    (instead of every 4096) the same holds across the re-anchors."""
     from ddl_amd.models.producers import ImageWindowProducer
 
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
@@ -437,8 +439,12 @@ def test_stager_bytes_in_interval_is_pro_rata_and_additive():
         e0.record()
         dl = ddl_amd.DistributedDataLoader(ImageWindowProducer(64, (3, 64, 64), "bfloat16", refill="stamp"), 32,
                                            conn, 6, env=env, device=torch.device("cuda"),
-                                           out_dtype=torch.bfloat16, shuffle="device", prefetch_depth=2)
+                                           out_dtype=torch.bfloat16, shuffle="device", prefetch_depth=2,
+                                           copy_timing=True)
         st = dl._stager
+        assert st.copy_timing
+        if anchor_every:
+            st._native.set_anchor_every(anchor_every)
         n_batches = 0
         em = None
         for e in range(6):
@@ -468,83 +474,46 @@ def test_stager_bytes_in_interval_is_pro_rata_and_additive():
         e3.record()
         after = st.bytes_in_interval(e2, e3)
         assert after["ok"] and after["bytes"] == 0.0 and after["copies"] == 0
+        if anchor_every:
+            assert st._native.reanchors >= 2
         dl.close()
 
 
-@pytest.mark.parametrize("streams", ["2", "1"])
-def test_copy_streams_deliver_identical_batches(monkeypatch, streams):
-    """The copy streams only decide which SDMA engine each window copy runs on: two alternating streams and
-    one stream deliver the same batches, bit for bit, with a fast consumer and with a slow one (a sleep per
-    batch makes the stager wait on the ring)."""
-    import time
-
+def test_untimed_direct_copies_make_the_interval_unusable():
+    """Direct-DMA copy times come from a process-wide ROCr switch that is off unless a loader asks for it
+    (copy_timing): without it an interval that the copies overlap reports ok=False (untimed), never a
+    silent zero; after the run, an interval no copy overlaps is fine."""
     from ddl_amd.models.producers import ImageWindowProducer
 
-    def run(n_cs, slow):
-        monkeypatch.setenv("DDL_COPY_STREAMS", n_cs)
-        out = []
-        with ddl_amd.start(n_producers=2) as (env, conn):
-            dl = ddl_amd.DistributedDataLoader(ImageWindowProducer(32, (3, 16, 16), "bfloat16", seed=5), 8, conn, 6,
-                                               env=env, device=torch.device("cuda"), out_dtype=torch.bfloat16,
-                                               shuffle="device", seed=3, prefetch_depth=2)
-            assert dl.stats()["copy_streams"] == int(n_cs)
-            for e in range(6):
-                for i in range(len(dl)):
-                    (x,) = dl[i]
-                    out.append(x.float().sum(dim=(1, 2, 3)).cpu())
-                    if slow:
-                        time.sleep(0.002)
-                    dl.mark(Marker.END_OF_BATCH)
-                if e < 5:
-                    dl.mark(Marker.END_OF_EPOCH)
-            dl.close()
-        return torch.stack(out)
-
-    ref = run("2", False)
-    for slow in (False, True):
-        got = run(streams, slow)
-        assert torch.equal(got, ref)
-
-
-@pytest.mark.parametrize("dispatch", ["lookahead", "inline", "python"])
-def test_direct_dma_delivers_identical_batches(monkeypatch, dispatch):
-    """Direct-DMA staging (window copies straight onto SDMA engines through ROCr, host waits on their completion
-    signals) delivers the same batches, bit for bit, as HIP copy streams -- through the native engine (lookahead
-    and inline) and the Python dispatch path, with a fast and a slow consumer, over a 2-buffer ring that is
-    refilled many times."""
-    import time
-
-    from ddl_amd import staging
-    from ddl_amd.models.producers import ImageWindowProducer
-
-    def run(direct, slow):
-        monkeypatch.setattr(staging, "DIRECT_DMA", direct)
-        out = []
-        with ddl_amd.start(n_producers=2) as (env, conn):
-            dl = ddl_amd.DistributedDataLoader(ImageWindowProducer(32, (3, 16, 16), "bfloat16", seed=5), 8, conn, 6,
-                                               env=env, device=torch.device("cuda"), out_dtype=torch.bfloat16,
-                                               shuffle="device", seed=3, prefetch_depth=2,
-                                               native_dispatch=dispatch if dispatch != "python" else False)
-            st = dl.stats()
-            assert st["direct_dma"] is direct, st.get("direct_dma_reason")
-            for e in range(6):
-                for i in range(len(dl)):
-                    (x,) = dl[i]
-                    out.append(x.float().sum(dim=(1, 2, 3)).cpu())
-                    if slow:
-                        time.sleep(0.002)
-                    dl.mark(Marker.END_OF_BATCH)
-                if e < 5:
-                    dl.mark(Marker.END_OF_EPOCH)
-            st = dl.stats()
-            dl.close()
-        return torch.stack(out), st
-
-    ref, _ = run(False, False)
-    for slow in (False, True):
-        got, st = run(True, slow)
-        assert torch.equal(got, ref)
-        assert st["direct_dma"] and st.get("bytes_landed", 1) != 0
+    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    with ddl_amd.start(n_producers=2) as (env, conn):
+        e0 = ev()
+        e0.record()
+        dl = ddl_amd.DistributedDataLoader(ImageWindowProducer(64, (3, 32, 32), "bfloat16", refill="stamp"), 32,
+                                           conn, 3, env=env, device=torch.device("cuda"),
+                                           out_dtype=torch.bfloat16, shuffle="device", prefetch_depth=2)
+        st = dl._stager
+        if not st.direct_dma:
+            pytest.skip(f"no direct DMA here: {st.stats()['direct_dma_reason']}")
+        assert not st.copy_timing
+        for e in range(3):
+            for i in range(len(dl)):
+                dl[i]
+                dl.mark(Marker.END_OF_BATCH)
+            if e < 2:
+                dl.mark(Marker.END_OF_EPOCH)
+        torch.cuda.synchronize()
+        e1 = ev()
+        e1.record()
+        e1.synchronize()
+        r = st.bytes_in_interval(e0, e1)
+        assert not r["ok"] and r["untimed"]
+        st.settle()  # the retire thread has seen every copy land (an untimed copy's end is when it saw it)
+        e2, e3 = ev(), ev()
+        e2.record()
+        e3.record()
+        assert st.bytes_in_interval(e2, e3)["ok"]
+        dl.close()
 
 
 @pytest.mark.parametrize("mode", ["inline", "lookahead", "window"])

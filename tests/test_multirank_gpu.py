@@ -27,7 +27,9 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GPU_GLOO = {"DDL_DEVICE": "", "DDL_BACKEND": "gloo"}  # "" = not forced to the CPU
 
 
-def _exchange_rank_gpu(rank, world, method, fraction):
+def _exchange_rank_gpu(rank, world, method, fraction, slow=0.0):
+    import time
+
     import ddl_amd
     from ddl_amd import Marker
     from tests.helpers import IdProducer
@@ -36,28 +38,34 @@ def _exchange_rank_gpu(rank, world, method, fraction):
     with ddl_amd.start(n_producers=2) as (env, conn):
         assert env.device.startswith("cuda"), env.device
         dl = ddl_amd.DistributedDataLoader(IdProducer(64, 6), 16, conn, 3, fraction, method, env=env,
-                                           copy_batches=True, seed=1, device=torch.device(env.device))
+                                           copy_batches=True, seed=1, device=torch.device(env.device),
+                                           prefetch_depth=2)
         assert dl._exchange_fn is not None
+        direct = dl.stats()["direct_dma"]
         for _ in range(3):
             rows = []
             for a, b in dl:
                 assert a.is_cuda and b.is_cuda
                 rows.append(torch.cat([a, b], 1).cpu())
+                if slow:  # the consumer is the bottleneck: the ring fills, the stager waits on free events
+                    time.sleep(slow)
                 dl.mark(Marker.END_OF_BATCH)
             dl.mark(Marker.END_OF_EPOCH)
             eps.append(torch.cat(rows).numpy())
         n_ex = dl._exchange_fn.n_exchange
         dl.close()
-    return eps, n_ex
+    return eps, n_ex, direct
 
 
 @pytest.mark.timeout(240)
-@pytest.mark.parametrize("world", [2, 4])
-def test_exchange_conserves_rows_on_device(world):
-    """The all-to-all window exchange between ranks whose windows live in HBM: every (rank,
-    producer, row) of every round is delivered exactly once over all ranks, and each rank holds
-    exactly the foreign rows the exchange plan says."""
-    res = run_ranks(_exchange_rank_gpu, world, "alltoall", 0.5, timeout=200, env=GPU_GLOO)
+@pytest.mark.parametrize("world,slow", [(2, 0.0), (4, 0.0), (2, 0.01)])
+def test_exchange_conserves_rows_on_device(world, slow):
+    """The all-to-all window exchange between ranks whose windows live in HBM, on direct-DMA staging (the
+    consumer host-waits each copy's completion signal before it enqueues the exchange), with a fast and a
+    slow consumer: every (rank, producer, row) of every round is delivered exactly once over all ranks, and
+    each rank holds exactly the foreign rows the exchange plan says."""
+    res = run_ranks(_exchange_rank_gpu, world, "alltoall", 0.5, slow, timeout=200, env=GPU_GLOO)
+    assert all(r[2] for r in res), "direct-DMA staging not in use"
     n_ex = res[0][1]
     assert n_ex > 0
     for e in range(3):
