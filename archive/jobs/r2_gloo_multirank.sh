@@ -1,5 +1,5 @@
 # Multi-rank GPU data path on the one-GPU box: RCCL refuses two ranks on one card
-# (profiles/r1_rccl_probe), so the DP group is gloo (DDL_BACKEND=gloo; its all-to-all on
+# (archive/profiles/r1_rccl_probe), so the DP group is gloo (DDL_BACKEND=gloo; its all-to-all on
 # device tensors bounces through host memory). Every rank still runs the full device path:
 # producers -> pinned shm -> H2D ring -> exchange -> gfx950 gather -> DDP train step.
 source tools/gpu_job.sh

@@ -75,7 +75,7 @@ def parse(argv=None):
                     help="HBM prefetch depth (windows; 4 x 77 MB of HBM; the library default): deep enough that the "
                          "copy engine restarts "
                          "without a gap after the barrier + synchronize that opens the timed region "
-                         "(profiles/r3_variance: 20-step spread 176.7-188.1k at depth 2-3, 187.5-188.1k at 4)")
+                         "(archive/profiles/r3_variance: 20-step spread 176.7-188.1k at depth 2-3, 187.5-188.1k at 4)")
     ap.add_argument("--source-dtype", default="bfloat16", choices=["bfloat16", "uint8", "float32"])
     ap.add_argument("--refill", default="stamp", choices=["stamp", "full"],
                     help="producer work per round: stamp = one element per sample; full = rewrite every byte of "

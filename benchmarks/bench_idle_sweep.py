@@ -205,7 +205,7 @@ def main(argv=None) -> int:
         src = SharedTokenSource.synthetic(f"ddl_amd_sweep_{os.getpid()}", 8192, 256, 4096, seed=1)
         src.bind_to_node(gpu_numa_node(0))  # next to the producers (bound to the GPU's node)
     # tokens: 6 producers x 4 gather threads x 2 slots -- the host-bound feed then has headroom, so it is
-    # consumer-bound and stable from run to run (profiles/r3_tokens)
+    # consumer-bound and stable from run to run (archive/profiles/r3_tokens)
     producers = a.producers or (3 if a.family == "images" else 6)
     points = []
     try:

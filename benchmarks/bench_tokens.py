@@ -44,7 +44,7 @@ def main(argv=None):
     ap.add_argument("--token-dtype", default="auto", choices=["auto", "int32", "uint16"],
                     help="token ids in the corpus and on the wire: auto = uint16 when every id is < 65536 (the "
                          "synthetic GPT-2-sized vocabulary is), else int32; uint16 ships 2 B per token over PCIe "
-                         "and the pack kernel widens it to int32 input_ids (profiles/r3_tok16)")
+                         "and the pack kernel widens it to int32 input_ids (archive/profiles/r3_tok16)")
     a = ap.parse_args(argv)
 
     import torch

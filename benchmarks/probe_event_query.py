@@ -3,7 +3,7 @@
 
 The stager's adaptive copy policy asked "has the last copy on stream 0 retired?" with hipEventQuery and
 found it retired for 192 of 199 copies while two copies overlapped under strict alternation on the same
-box (profiles/r3_copy_policy). This probe records events right after work that takes milliseconds and
+box (archive/profiles/r3_copy_policy). This probe records events right after work that takes milliseconds and
 queries them at once:
 
 * after a 1 GiB pinned H2D copy (SDMA) on a side stream;

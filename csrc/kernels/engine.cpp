@@ -35,7 +35,7 @@ constexpr int kFreeEvents = 4;
 
 // Flags of the engine's synchronisation events (batch-ready, free, join): no timing. Device-scope release
 // (hipEventReleaseToDevice) and no system fence were A/B'd against the default and showed no measured effect
-// (profiles/r3_idle_residual), so the default system-scope release stays.
+// (archive/profiles/r3_idle_residual), so the default system-scope release stays.
 unsigned event_flags() { return static_cast<unsigned>(hipEventDisableTiming); }
 
 }  // namespace

@@ -138,7 +138,7 @@ class BatchEngine {
   // Hand-off of a lookahead batch whose kernel is still pending at get(): false (default) makes the
   // compute stream wait for its event on the device; true makes the HOST wait for it
   // (hipEventSynchronize). A device-side cross-queue wait costs the compute stream ~25 us per step on
-  // MI355X when it follows an H2D-fed kernel (profiles/r3_handoff); when the host runs ahead of the GPU
+  // MI355X when it follows an H2D-fed kernel (archive/profiles/r3_handoff); when the host runs ahead of the GPU
   // -- the usual case -- the host wait costs nothing.
   void set_host_handoff(bool on) { host_wait_ = on; }
   bool host_handoff() const { return host_wait_; }

@@ -251,7 +251,7 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
             raise ValueError("max_ahead must be >= 0")
         self.max_ahead = ma
         # an event every max_ahead / 4 batches (one per batch raised the GPU idle behind a slow step from
-        # 0.12% to 0.17-0.18%: profiles/r4_eleventh); a small ring of them is reused
+        # 0.12% to 0.17-0.18%: archive/profiles/r4_eleventh); a small ring of them is reused
         self._ahead_every = max(1, ma // 4)
         self._ahead_ring: list = []
         # (batch count, event on the consumer's stream)

@@ -28,7 +28,7 @@ class ProducerFunctionSkeleton:
     # Pinned slots per producer the loader uses when its ``n_slots`` is not given. One slot suffices when a
     # round is cheap (the slot is back with its producer as soon as its H2D copy retires); a producer that
     # rewrites its whole window every round sets 2, so one slot is refilled while the other is copied
-    # (profiles/r3_full_refill: 141k -> 175-178k samples/s).
+    # (archive/profiles/r3_full_refill: 141k -> 175-178k samples/s).
     preferred_slots: int = 1
 
     def __init__(self, *args: Any, **kwargs: Any) -> None:

@@ -201,10 +201,10 @@ class NativeDispatchMixin:
         self._engine.inline = mode in ("inline", "window")
         self._engine.set_batches_per_window([int(b) for b in self.batches_per_window])
         # a window's ring buffer goes back to the stager at its last batch launch, one step before the
-        # consumer's release (profiles/r3_early_release); a later out-of-order fetch of that window raises
+        # consumer's release (archive/profiles/r3_early_release); a later out-of-order fetch of that window raises
         self._engine.early_release = True
         # lookahead batches still pending at get(): the host waits for them (no device-side cross-queue
-        # barrier on the compute stream, profiles/r3_handoff) unless the exchange is on -- its kernels wait
+        # barrier on the compute stream, archive/profiles/r3_handoff) unless the exchange is on -- its kernels wait
         # on peer ranks, and the host must never block on another rank's progress
         self._engine.host_handoff = self._exchange_fn is None
         # the host (not the batch stream) waits for a window's H2D copy before launching its batch kernels

@@ -101,7 +101,7 @@ class ImageWindowProducer(ProducerFunctionSkeleton):
         self.seed = seed
         self.refill = refill
         # a full refill rewrites 77 MB per round: 8 host threads and 2 slots hold the link (53.7 GB/s vs
-        # 42.5 GB/s with 4 threads and one slot, profiles/r3_full_refill)
+        # 42.5 GB/s with 4 threads and one slot, archive/profiles/r3_full_refill)
         self.host_threads = int(host_threads) if host_threads is not None else (8 if refill == "full" else 4)
         self.preferred_slots = 2 if refill == "full" else 1
         self._base: torch.Tensor | None = None

@@ -1,6 +1,6 @@
 """Several DP ranks on the GPU box's one card: the multi-process device data path on hardware.
 
-RCCL refuses two ranks on one GPU ("Duplicate GPU detected", ``profiles/r1_rccl_probe``), so
+RCCL refuses two ranks on one GPU ("Duplicate GPU detected", ``archive/profiles/r1_rccl_probe``), so
 these runs build the DP group on gloo (``DDL_BACKEND=gloo``; gloo's all-to-all and all-reduce
 take device tensors and bounce them through host memory). Everything else is the production
 path of each rank: its own producer processes and pinned arena, H2D staging on the copy
