@@ -235,7 +235,7 @@ def build_benchmarks(force: bool = False) -> list[str]:
         deps = [src, *glob.glob(os.path.join(CSRC, "kernels", "*.h"))]
         if force or _newer(target, deps):
             _run([_hipcc(), "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-I", os.path.join(CSRC, "kernels"),
-                  src, "-o", target])
+                  src, "-o", target, "-lhsa-runtime64"])
         out.append(target)
     return out
 

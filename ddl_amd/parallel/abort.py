@@ -40,6 +40,11 @@ from typing import Any, Callable
 from ..utils.logging import logger
 
 PEER_ABORT_EXIT = 75  # exit status of a rank torn down because ANOTHER rank failed
+# A rank is declared dead when its heartbeat has not moved for this long. The heartbeat is bumped by a Python
+# daemon thread, so it needs the GIL: a HEALTHY rank whose main thread holds the GIL longer than this in one
+# call (a long C extension call that does not release it, unpickling a huge object) is indistinguishable from
+# a hung one and takes the job down with PEER_ABORT_EXIT. The loader's own waits all release the GIL. Raise it
+# (``start(peer_timeout_s=)``, ``distributed_dataloader(peer_timeout_s=)``) for such workloads.
 DEFAULT_PEER_TIMEOUT_S = 60.0
 
 
@@ -53,10 +58,16 @@ def _store_client(prefix: str, timeout_s: float):
         port = int(os.environ["MASTER_PORT"])
         store = dist.TCPStore(host, port, is_master=False, timeout=timedelta(seconds=timeout_s),
                               wait_for_workers=False)
-    except Exception:
-        from torch.distributed.distributed_c10d import _get_default_store
+    except Exception as first:
+        # a job not rendezvoused over MASTER_ADDR / MASTER_PORT: the default group's store (private torch API)
+        try:
+            from torch.distributed.distributed_c10d import _get_default_store
 
-        store = _get_default_store()
+            store = _get_default_store()
+        except Exception as e:
+            raise RuntimeError("JobWatchdog needs a store for its side channel: no TCPStore at MASTER_ADDR:"
+                               f"MASTER_PORT ({first}) and no default process-group store ({e}); pass "
+                               "abort_on_error=False to run without the job-wide abort") from e
     return dist.PrefixStore(prefix, store)
 
 

@@ -77,7 +77,8 @@ def start(n_producers: int | None = None, init_dist: bool = True, backend: str |
     failure on any rank ends the whole job, as the reference's ``Abort(1)`` does
     (``/root/reference/ddl/ddl_env.py:25-30``): the failing rank publishes the error and exits 1, its
     peers exit ``PEER_ABORT_EXIT`` within a fraction of a second, and a rank that dies silently is
-    declared dead after ``peer_timeout_s`` without a heartbeat (``parallel/abort.py``).
+    declared dead after ``peer_timeout_s`` without a heartbeat (``parallel/abort.py``; the heartbeat needs
+    the GIL, so a rank holding it longer than that in one call counts as hung).
     """
     configure()
     env = read_env(n_producers)
@@ -97,7 +98,7 @@ def start(n_producers: int | None = None, init_dist: bool = True, backend: str |
 
             was = dist.is_available() and dist.is_initialized()
             init_distributed(env, backend, timeout_s=timeout_s, device=device)
-            created_pg = not was and env.world_size > 1
+            created_pg = not was and dist.is_initialized()  # a named backend builds a group at world size 1 too
             if abort_on_error and env.world_size > 1 and env.control_group is not None:
                 watchdog = JobWatchdog(env.rank, env.world_size, peer_timeout_s=peer_timeout_s,
                                        on_abort=conn.kill if conn is not None else None).start()
@@ -127,18 +128,20 @@ def start(n_producers: int | None = None, init_dist: bool = True, backend: str |
 
 def distributed_dataloader(func: Callable | None = None, *, n_producers: int | None = None, init_dist: bool = True,
                            backend: str | None = None, timeout_s: float = DEFAULT_TIMEOUT_S,
-                           abort_on_error: bool = True):
+                           abort_on_error: bool = True, peer_timeout_s: float = DEFAULT_PEER_TIMEOUT_S):
     """Decorator: run ``func(*args, env, conn, **kwargs)`` as this rank's consumer with its producers.
 
     Usable bare (``@distributed_dataloader``) or with options
     (``@distributed_dataloader(n_producers=4)``). The number of producers per
-    rank defaults to ``$DDL_PRODUCERS_PER_RANK`` or 3.
+    rank defaults to ``$DDL_PRODUCERS_PER_RANK`` or 3. ``timeout_s``, ``abort_on_error`` and
+    ``peer_timeout_s``: as for ``start``.
     """
 
     def deco(f: Callable) -> Callable:
         @functools.wraps(f)
         def wrapper(*args: Any, **kwargs: Any) -> Any:
-            with start(n_producers, init_dist, backend, timeout_s, abort_on_error=abort_on_error) as (env, conn):
+            with start(n_producers, init_dist, backend, timeout_s, abort_on_error=abort_on_error,
+                       peer_timeout_s=peer_timeout_s) as (env, conn):
                 return f(*args, env, conn, **kwargs)
 
         return wrapper

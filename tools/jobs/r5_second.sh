@@ -1,7 +1,8 @@
 # Round 5, second box: streaming-store A/B (socket DRAM probe, full-refill bench), multi-rank GPU tests, and
-# the 4- and 8-rank device path over gloo on the one card (final direct-DMA tree).
+# a per-row SDMA gather probe for the indexed order, the 4- and 8-rank device path over gloo on the one card (final direct-DMA tree).
 source tools/gpu_job.sh
 unset DDL_BACKEND
+run 200 sdma_rowgather benchmarks/bin/probe_sdma_rowgather 256 4096 60
 run 200 socket_nt python benchmarks/probe_socket_dram.py --dma-threads 12 --refill-threads 16 --stream-stores on --json-out gpurun_out/socket_nt.json
 run 200 socket_plain python benchmarks/probe_socket_dram.py --dma-threads 12 --refill-threads 16 --stream-stores off --json-out gpurun_out/socket_plain.json
 run 250 refill_nt python bench.py --refill full --steps 100 --warmup 10 --idle-steps 0 --order window --pressure-ratio 0 --json-out gpurun_out/refill_nt.json
