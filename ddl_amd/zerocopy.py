@@ -67,8 +67,8 @@ class ZeroCopyLoader(PrefetchedIndexedLoader):
         self.out_dtype = _dtypes.to_torch_dtype(out_dtype) if out_dtype is not None else self.src_dtype
         self.normalize = normalize
         if max_blocks is None:
-            # measured grid caps (archive/profiles/r1_zerocopy, archive/profiles/r2_misc): a same-width copy is PCIe-bound
-            # and peaks at 32 workgroups (bf16: 188k vs 182k samples/s at 64); a widening uint8 -> bf16
+            # measured grid caps (archive/profiles/r1_zerocopy, archive/profiles/r2_misc): a same-width copy is
+            # PCIe-bound and peaks at 32 workgroups (bf16: 188k vs 182k samples/s at 64); a widening uint8 -> bf16
             # gather writes twice the bytes it reads and keeps improving up to the full grid
             src_bytes = torch.empty((), dtype=self.src_dtype).element_size()
             out_bytes = torch.empty((), dtype=self.out_dtype).element_size()
