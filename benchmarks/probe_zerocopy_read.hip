@@ -11,8 +11,9 @@
 //   wave4k     one wave per 4 KB: 4 x 16 B per lane, 64 lanes, a wave's loads cover 4 KB contiguous
 //   row        one workgroup per row, looping over the row in 16 KB steps (no grid-stride across rows)
 // for several grid caps (workgroups), and two streams alternating launches (the next batch starts while the
-// previous one's last workgroups drain). Bandwidth = bytes read from the host per second (best of 3 passes
-// of 30 launches, HIP events). Output: one JSON object per line.
+// previous one's last workgroups drain). Bandwidth = bytes read from the host per second over one pass of 60
+// launches (HIP events); every configuration is measured `reps` times, round-robin over the configurations so
+// drift of the box hits all alike; median / min / max. Output: one JSON object per configuration.
 //
 // Build: python -m ddl_amd._build --only benchmarks
 #include <hip/hip_runtime.h>
@@ -122,7 +123,7 @@ __global__ void __launch_bounds__(kThreads) gather_row(u32x4* __restrict__ dst, 
 int main(int argc, char** argv) {
   const int batch = 256;
   const int n_src = argc > 1 ? std::atoi(argv[1]) : 4096;
-  const int launches = 30;
+  const int launches = 60;
   CHECK(hipSetDevice(0));
   u32x4* src = nullptr;
   CHECK(hipHostMalloc(reinterpret_cast<void**>(&src), static_cast<size_t>(n_src) * kRow, hipHostMallocMapped));
@@ -162,36 +163,47 @@ int main(int argc, char** argv) {
                          static_cast<int64_t>(batch));
   };
   const char* names[4] = {"tile16", "tile16_nt", "wave4k", "row"};
-  const int grids[] = {16, 24, 32, 48, 64, 128, 256};
-  for (int kind = 0; kind < 4; ++kind) {
-    for (int blocks : grids) {
-      if (kind == 3 && blocks > batch) continue;
-      for (int n_st = 1; n_st <= 2; ++n_st) {
-        float best = 1e30f;
-        for (int pass = 0; pass < 3; ++pass) {
-          for (int k = 0; k < 2; ++k) launch(kind, blocks, k, st[0]);  // warm
-          CHECK(hipStreamSynchronize(st[0]));
-          CHECK(hipEventRecord(e0, st[0]));
-          CHECK(hipStreamWaitEvent(st[1], e0, 0));
-          for (int k = 0; k < launches; ++k) launch(kind, blocks, k, st[n_st == 2 ? (k & 1) : 0]);
-          if (n_st == 2) {
-            CHECK(hipEventRecord(join, st[1]));
-            CHECK(hipStreamWaitEvent(st[0], join, 0));
-          }
-          CHECK(hipEventRecord(e1, st[0]));
-          CHECK(hipEventSynchronize(e1));
-          float ms = 0.f;
-          CHECK(hipEventElapsedTime(&ms, e0, e1));
-          best = std::min(best, ms);
-        }
-        const double gbps = static_cast<double>(launches) * batch * kRow / (best * 1e-3) / 1e9;
-        std::printf("{\"probe\": \"zerocopy_read\", \"kernel\": \"%s\", \"workgroups\": %d, \"streams\": %d, "
-                    "\"gbps\": %.2f, \"samples_per_s\": %.1f}\n",
-                    names[kind], kind == 3 ? std::min(blocks, batch) : blocks, n_st, gbps, gbps * 1e9 / kRow);
-        std::fflush(stdout);
+  // (kernel, workgroups, streams), measured round-robin over `reps` rounds so box drift hits every config
+  // alike; each measurement: one pass of `launches` back-to-back batches
+  struct Cfg {
+    int kind, blocks, streams;
+    std::vector<double> gbps;
+  };
+  std::vector<Cfg> cfgs;
+  for (int kind : {0, 2, 3})
+    for (int blocks : {16, 24, 32, 48, 64})
+      for (int n_st = 1; n_st <= 2; ++n_st) cfgs.push_back({kind, blocks, n_st, {}});
+  cfgs.push_back({1, 32, 1, {}});
+  cfgs.push_back({1, 32, 2, {}});
+  const int reps = argc > 2 ? std::atoi(argv[2]) : 5;
+  for (int rep = 0; rep < reps; ++rep) {
+    for (auto& c : cfgs) {
+      for (int k = 0; k < 2; ++k) launch(c.kind, c.blocks, k, st[0]);  // warm
+      CHECK(hipStreamSynchronize(st[0]));
+      CHECK(hipEventRecord(e0, st[0]));
+      CHECK(hipStreamWaitEvent(st[1], e0, 0));
+      for (int k = 0; k < launches; ++k) launch(c.kind, c.blocks, k, st[c.streams == 2 ? (k & 1) : 0]);
+      if (c.streams == 2) {
+        CHECK(hipEventRecord(join, st[1]));
+        CHECK(hipStreamWaitEvent(st[0], join, 0));
       }
+      CHECK(hipEventRecord(e1, st[0]));
+      CHECK(hipEventSynchronize(e1));
+      float ms = 0.f;
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      c.gbps.push_back(static_cast<double>(launches) * batch * kRow / (ms * 1e-3) / 1e9);
     }
   }
+  for (auto& c : cfgs) {
+    std::vector<double> g = c.gbps;
+    std::sort(g.begin(), g.end());
+    std::printf("{\"probe\": \"zerocopy_read\", \"kernel\": \"%s\", \"workgroups\": %d, \"streams\": %d, "
+                "\"gbps_median\": %.2f, \"gbps_min\": %.2f, \"gbps_max\": %.2f, \"reps\": %d, "
+                "\"samples_per_s_median\": %.1f}\n",
+                names[c.kind], c.kind == 3 ? std::min(c.blocks, batch) : c.blocks, c.streams, g[g.size() / 2],
+                g.front(), g.back(), static_cast<int>(g.size()), g[g.size() / 2] * 1e9 / kRow);
+  }
+  std::fflush(stdout);
   CHECK(hipHostFree(src));
   for (auto p : dst) CHECK(hipFree(p));
   CHECK(hipFree(rows));
