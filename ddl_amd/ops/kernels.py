@@ -191,8 +191,10 @@ def gather_rows(src, index: torch.Tensor | None = None, *, perm: FeistelPermutat
     return out
 
 
-def scatter_rows(dst: torch.Tensor, src: torch.Tensor, index: torch.Tensor, *, stream=None) -> torch.Tensor:
-    """dst[index[r]] = src[r] (same dtype). Used to put exchanged rows back."""
+def scatter_rows(dst: torch.Tensor, src: torch.Tensor, index: torch.Tensor, *, stream=None,
+                 max_blocks: int = 0) -> torch.Tensor:
+    """dst[index[r]] = src[r] (same dtype). Used to put exchanged rows back. ``max_blocks`` > 0 caps the
+    grid, as for ``gather_rows``."""
     if dst.dtype != src.dtype or dst.shape[1:] != src.shape[1:]:
         raise ValueError("scatter_rows: dst/src row mismatch")
     if index.numel() != src.shape[0]:
@@ -204,7 +206,7 @@ def scatter_rows(dst: torch.Tensor, src: torch.Tensor, index: torch.Tensor, *, s
     _native.hip().gather_rows(
         dst=dst.data_ptr(), out_dt=_dtypes.code(dst.dtype), src=src.data_ptr(), in_dt=_dtypes.code(src.dtype),
         n_rows=src.shape[0], row_elems=row_elems, scale=[], bias=[], plane=0, scatter=True,
-        stream=_stream_handle(stream), **_index_kw(index, None, 0))
+        stream=_stream_handle(stream), max_blocks=int(max_blocks), **_index_kw(index, None, 0))
     return dst
 
 

@@ -32,9 +32,12 @@ def test_native_module_is_loaded():
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.uint8, torch.float16])
-@pytest.mark.parametrize("row_shape", [(9,), (3, 224, 224), (7,), (1024,)])
+@pytest.mark.parametrize("row_shape", [(9,), (3, 224, 224), (7,), (1024,), (3, 17, 19)])
 @pytest.mark.parametrize("how", ["identity", "index", "perm"])
-def test_gather_rows_same_dtype_bitwise(dtype, row_shape, how):
+@pytest.mark.parametrize("max_blocks", [0, 5, 32])
+def test_gather_rows_same_dtype_bitwise(dtype, row_shape, how, max_blocks):
+    """Every same-dtype move (16 / 4 / 1-byte units; uncapped tiles, and the capped grid's wave-granular
+    pieces of the zero-copy gather, move_rows_waves) equals index_select bitwise."""
     n = 300
     g = torch.Generator().manual_seed(1)
     src = (torch.rand((n, *row_shape), generator=g) * 200).to(dtype)
@@ -52,9 +55,23 @@ def test_gather_rows_same_dtype_bitwise(dtype, row_shape, how):
         kw = dict(base=5, n_rows=100)
         dk = kw
     ref = ops.ref_gather_rows(src, **kw)
-    out = ops.gather_rows(d, **dk)
+    out = ops.gather_rows(d, max_blocks=max_blocks, **dk)
     torch.cuda.synchronize()
     assert torch.equal(out.cpu(), ref)
+
+
+@pytest.mark.parametrize("max_blocks", [0, 3, 32])
+def test_scatter_rows_capped_grid(max_blocks):
+    """The exchange's receive side with 16-byte rows wide enough for the wave-granular capped kernel."""
+    n, w = 96, 2048
+    src_rows = torch.randn(40, w)
+    dst = torch.zeros(n, w)
+    idx = torch.randperm(n)[:40]
+    ref = dst.clone().index_copy_(0, idx, src_rows)
+    d = dst.to(_dev())
+    ops.scatter_rows(d, src_rows.to(_dev()), idx.to(_dev()), max_blocks=max_blocks)
+    torch.cuda.synchronize()
+    assert torch.equal(d.cpu(), ref)
 
 
 @pytest.mark.parametrize("src_dtype", [torch.float32, torch.float16, torch.bfloat16])
