@@ -15,10 +15,16 @@
 // launches (HIP events); every configuration is measured `reps` times, round-robin over the configurations so
 // drift of the box hits all alike; median / min / max. Output: one JSON object per configuration.
 //
+// Usage: probe_zerocopy_read [n_src rows] [rounds] [hostmalloc|shm|anon4k|anonthp]
 // Build: python -m ddl_amd._build --only benchmarks
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <cstring>
+#include <string>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -124,12 +130,39 @@ int main(int argc, char** argv) {
   const int batch = 256;
   const int n_src = argc > 1 ? std::atoi(argv[1]) : 4096;
   const int launches = 60;
+  // where the source lives: "hostmalloc" (hipHostMalloc), "shm" (a POSIX shm segment registered with
+  // hipHostRegister: what SharedArraySource + ZeroCopyLoader use), "anon4k" / "anonthp" (anonymous memory with
+  // transparent huge pages off / on, registered)
+  const std::string mem = argc > 3 ? argv[3] : "hostmalloc";
   CHECK(hipSetDevice(0));
+  const size_t bytes = static_cast<size_t>(n_src) * kRow;
+  const size_t map_bytes = (bytes + (2u << 20) - 1) / (2u << 20) * (2u << 20);
   u32x4* src = nullptr;
-  CHECK(hipHostMalloc(reinterpret_cast<void**>(&src), static_cast<size_t>(n_src) * kRow, hipHostMallocMapped));
+  bool registered = false;
+  int shm_fd = -1;
+  std::string shm_name = "/ddl_probe_zc_" + std::to_string(getpid());
+  if (mem == "hostmalloc") {
+    CHECK(hipHostMalloc(reinterpret_cast<void**>(&src), bytes, hipHostMallocMapped));
+  } else {
+    void* p = MAP_FAILED;
+    if (mem == "shm") {
+      shm_fd = shm_open(shm_name.c_str(), O_CREAT | O_RDWR, 0600);
+      if (shm_fd < 0 || ftruncate(shm_fd, static_cast<off_t>(map_bytes)) != 0) return 4;
+      p = mmap(nullptr, map_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, shm_fd, 0);
+    } else {
+      p = mmap(nullptr, map_bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+      if (p != MAP_FAILED) madvise(p, map_bytes, mem == "anonthp" ? MADV_HUGEPAGE : MADV_NOHUGEPAGE);
+    }
+    if (p == MAP_FAILED) return 4;
+    src = static_cast<u32x4*>(p);
+  }
   {
     auto* b = reinterpret_cast<uint8_t*>(src);
-    for (int64_t i = 0; i < static_cast<int64_t>(n_src) * kRow; i += 4096) b[i] = static_cast<uint8_t>(i >> 12);
+    for (int64_t i = 0; i < static_cast<int64_t>(bytes); i += 4096) b[i] = static_cast<uint8_t>(i >> 12);
+  }
+  if (mem != "hostmalloc") {
+    CHECK(hipHostRegister(src, map_bytes, hipHostRegisterMapped));
+    registered = true;
   }
   u32x4* dsrc = nullptr;
   CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&dsrc), src, 0));
@@ -170,11 +203,9 @@ int main(int argc, char** argv) {
     std::vector<double> gbps;
   };
   std::vector<Cfg> cfgs;
-  for (int kind : {0, 2, 3})
+  for (int kind : {0, 2})
     for (int blocks : {16, 24, 32, 48, 64})
       for (int n_st = 1; n_st <= 2; ++n_st) cfgs.push_back({kind, blocks, n_st, {}});
-  cfgs.push_back({1, 32, 1, {}});
-  cfgs.push_back({1, 32, 2, {}});
   const int reps = argc > 2 ? std::atoi(argv[2]) : 5;
   for (int rep = 0; rep < reps; ++rep) {
     for (auto& c : cfgs) {
@@ -197,14 +228,23 @@ int main(int argc, char** argv) {
   for (auto& c : cfgs) {
     std::vector<double> g = c.gbps;
     std::sort(g.begin(), g.end());
-    std::printf("{\"probe\": \"zerocopy_read\", \"kernel\": \"%s\", \"workgroups\": %d, \"streams\": %d, "
+    std::printf("{\"probe\": \"zerocopy_read\", \"mem\": \"%s\", \"kernel\": \"%s\", \"workgroups\": %d, \"streams\": %d, "
                 "\"gbps_median\": %.2f, \"gbps_min\": %.2f, \"gbps_max\": %.2f, \"reps\": %d, "
                 "\"samples_per_s_median\": %.1f}\n",
-                names[c.kind], c.kind == 3 ? std::min(c.blocks, batch) : c.blocks, c.streams, g[g.size() / 2],
+                mem.c_str(), names[c.kind], c.kind == 3 ? std::min(c.blocks, batch) : c.blocks, c.streams, g[g.size() / 2],
                 g.front(), g.back(), static_cast<int>(g.size()), g[g.size() / 2] * 1e9 / kRow);
   }
   std::fflush(stdout);
-  CHECK(hipHostFree(src));
+  if (registered) {
+    CHECK(hipHostUnregister(src));
+    munmap(src, map_bytes);
+    if (shm_fd >= 0) {
+      close(shm_fd);
+      shm_unlink(shm_name.c_str());
+    }
+  } else {
+    CHECK(hipHostFree(src));
+  }
   for (auto p : dst) CHECK(hipFree(p));
   CHECK(hipFree(rows));
   return 0;
