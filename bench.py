@@ -274,20 +274,82 @@ def pressure_phase(args, env, dev, it, feed_per_rank: float, barrier, sync, dl=N
     return out
 
 
-def indexed_phase(args, env, dev, barrier, sync) -> dict:
-    """The world-size-invariant order: every global batch is positions [g*GB, (g+1)*GB) of the epoch's
-    Feistel permutation over a node-shared source, rank r taking its contiguous slice (the union over
-    ranks is the same batch at any N). ``ZeroCopyLoader`` gathers the rank's slice straight from the
-    pinned, device-mapped source over PCIe into a bf16 batch (no producers, no host copies), depth 2
-    ahead on its own stream. Same phase structure as the headline: feed rate (checksum consumer,
-    timed exactly like phase 1) then GPU idle % behind the PatchMLP step."""
+def _timed_feed(args, env, it, acc, barrier, sync, label: str) -> tuple[float, float]:
+    """Warmup, then exactly ``args.steps`` checksum-consumed batches bracketed by barrier + synchronize;
+    (samples/s over all ranks from the max elapsed time, ms per step)."""
     import torch
     import torch.distributed as dist
 
+    from ddl_amd.utils.tracing import trace_range
+
+    for _ in range(args.warmup):
+        acc.add(next(it))
+    barrier()
+    t0 = time.perf_counter()
+    with trace_range(label):
+        for _ in range(args.steps):
+            acc.add(next(it))
+        sync()
+    el = time.perf_counter() - t0
+    barrier()
+    if env.world_size > 1:
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=env.control_group)
+        el = float(t.item())
+    return args.batch * args.steps * env.world_size / el, 1000 * el / args.steps
+
+
+def _idle_behind_step(args, env, dev, it, barrier, sync) -> float | None:
+    """GPU idle % behind the PatchMLP step (phase 2's measurement) on the batches of ``it``."""
+    import torch
+    import torch.distributed as dist
+
+    from ddl_amd.models.trainstep import TrainStep
+    from ddl_amd.utils.tracing import ComputeIdleMeter
+
+    idle_steps = args.steps if args.idle_steps < 0 else args.idle_steps
+    if not idle_steps or dev.type != "cuda":
+        return None
+    step = TrainStep(dev, dim=args.model_dim, depth=args.model_depth,
+                     process_group=env.process_group if env.world_size > 1 else None)
+    for _ in range(max(1, args.warmup // 2)):
+        step(next(it))
+    meter = ComputeIdleMeter()
+    barrier()
+    for _ in range(idle_steps):
+        x = next(it)
+        meter.step_begin()
+        step(x)
+        meter.step_end()
+    sync()
+    idle = meter.result()["gpu_idle_pct"]
+    if env.world_size > 1:
+        t = torch.tensor([idle], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=env.control_group)
+        idle = float(t.item())
+    return round(idle, 3)
+
+
+def indexed_phase(args, env, dev, barrier, sync, spare=None) -> dict:
+    """The world-size-invariant order: every global batch is positions [g*GB, (g+1)*GB) of the epoch's
+    Feistel permutation over a node-shared source, rank r taking its contiguous slice (the union over
+    ranks is the same batch at any N). Two paths deliver it, each timed like the headline (checksum
+    consumer, barrier + synchronize around exactly ``--steps`` batches), then GPU idle % behind the
+    PatchMLP step:
+
+    * ``value`` -- producers (``IndexedProducer`` on the spare producer set ``spare``, spawned with the
+      headline's): each window is one local batch gathered on the host in the epoch order (native
+      streaming-store gather) and staged like the headline's windows (direct DMA);
+    * ``zero_copy`` -- ``ZeroCopyLoader``: a gfx950 kernel gathers the rank's slice straight from the
+      pinned, device-mapped source over PCIe (no producers, no host copies; no host DRAM writes, which
+      matters when four ranks share a socket).
+    """
+    import torch
+
+    import ddl_amd
     from ddl_amd import ops
     from ddl_amd.models.datasets import numa_local_source
-    from ddl_amd.models.trainstep import TrainStep
-    from ddl_amd.utils.tracing import ComputeIdleMeter, trace_range
+    from ddl_amd.models.producers import IndexedProducer
     from ddl_amd.zerocopy import ZeroCopyLoader
 
     shape = (3, 224, 224)
@@ -298,67 +360,55 @@ def indexed_phase(args, env, dev, barrier, sync) -> dict:
         t.view(torch.uint8).fill_(0x3C)
         t.view(n, -1)[:, 0] = torch.arange(n, dtype=torch.float32).to(torch.bfloat16)
 
+    def forever(dl):  # batches as one tensor (a window loader yields a tuple of column groups)
+        while True:
+            for b in dl:
+                yield b[0] if isinstance(b, (tuple, list)) else b
+
     # one replica per NUMA node of the node's GPUs: no GPU gathers across the socket link
     src, node, _ = numa_local_source(name, n, shape, torch.bfloat16, env, fill=fill)
+    out = {"order": "indexed (EpochOrder, world-size-invariant) from a NUMA-local bf16 replica of the "
+                    "node-shared source", "source_samples": n}
     try:
         pages = src.page_nodes(64)
-        dl = ZeroCopyLoader(src, args.batch * env.world_size, env, seed=args.seed, out_dtype=torch.bfloat16,
-                            device=dev, prefault=not args.index_no_prefault)
-
-        def gen():
-            while True:
-                yield from dl
-
-        it = gen()
+        out["numa"] = {"gpu_node": node, "source_pages_on_gpu_node_pct":
+                       round(100.0 * sum(1 for p in pages if p == node) / max(1, len(pages)), 1)
+                       if node is not None else None}
         acc = ops.ChecksumAccumulator(dev)
-        for _ in range(args.warmup):
-            acc.add(next(it))
-        barrier()
-        t0 = time.perf_counter()
-        with trace_range("bench.indexed"):
-            for _ in range(args.steps):
-                acc.add(next(it))
-            sync()
-        t1 = time.perf_counter()
-        barrier()
-        el = t1 - t0
-        if env.world_size > 1:
-            t = torch.tensor([el], dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=env.control_group)
-            el = float(t.item())
-        out = {"order": "indexed (EpochOrder, world-size-invariant), zero-copy gather from a NUMA-local pinned "
-                        "bf16 replica of the node-shared source",
-               "prefault_s": dl.stats().get("prefault_s"),
-               "value": round(args.batch * args.steps * env.world_size / el, 1), "ms_per_step":
-               round(1000 * el / args.steps, 4), "source_samples": n,
-               "numa": {"gpu_node": node, "source_pages_on_gpu_node_pct":
-                        round(100.0 * sum(1 for p in pages if p == node) / max(1, len(pages)), 1)
-                        if node is not None else None}}
         idle_steps = args.steps if args.idle_steps < 0 else args.idle_steps
-        if idle_steps and dev.type == "cuda":
-            step = TrainStep(dev, dim=args.model_dim, depth=args.model_depth,
-                             process_group=env.process_group if env.world_size > 1 else None)
-            for _ in range(max(1, args.warmup // 2)):
-                step(next(it))
-            meter = ComputeIdleMeter()
-            barrier()
-            for _ in range(idle_steps):
-                x = next(it)
-                meter.step_begin()
-                step(x)
-                meter.step_end()
-            sync()
-            res = meter.result()
-            idle = res["gpu_idle_pct"]
-            if env.world_size > 1:
-                t = torch.tensor([idle], dtype=torch.float64)
-                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=env.control_group)
-                idle = float(t.item())
-            out["gpu_idle_pct"] = round(idle, 3)
-        dl.close()
+        if spare is not None:
+            gb = args.batch * env.world_size
+            bpe = n // gb
+            total = args.warmup + args.steps + (max(1, args.warmup // 2) + idle_steps if idle_steps else 0)
+            dl = ddl_amd.DistributedDataLoader(
+                IndexedProducer(src, gb, seed=args.seed, host_threads=8), args.batch, spare,
+                math.ceil(total / bpe) + 2, mode="indexed", env=env, device=dev, n_slots=2, auto_mark=True)
+            it = forever(dl)
+            rate, ms = _timed_feed(args, env, it, acc, barrier, sync, "bench.indexed")
+            st = dl.stats()
+            out.update({"path": "producers (IndexedProducer: host gather in the epoch order, 2 slots x 8 "
+                                "threads, direct-DMA staging)",
+                        "value": round(rate, 1), "ms_per_step": round(ms, 4),
+                        "h2d_direct_dma": bool(st.get("direct_dma", False))})
+            out["gpu_idle_pct"] = _idle_behind_step(args, env, dev, it, barrier, sync)
+            dl.close()
+        zc = ZeroCopyLoader(src, args.batch * env.world_size, env, seed=args.seed, out_dtype=torch.bfloat16,
+                            device=dev, prefault=not args.index_no_prefault)
+        it = forever(zc)
+        rate, ms = _timed_feed(args, env, it, acc, barrier, sync, "bench.indexed_zero_copy")
+        zres = {"path": "zero-copy gfx950 gather over PCIe from the pinned, device-mapped source",
+                "value": round(rate, 1), "ms_per_step": round(ms, 4), "prefault_s": zc.stats().get("prefault_s")}
+        if spare is None:
+            zres["gpu_idle_pct"] = _idle_behind_step(args, env, dev, it, barrier, sync)
+            out.update(zres)
+        else:
+            out["zero_copy"] = zres
+        zc.close()
         return out
     finally:
         if env.world_size > 1:
+            import torch.distributed as dist
+
             dist.barrier(group=env.control_group)  # every rank has unmapped its view before the unlink
         src.close()
 
@@ -409,7 +459,9 @@ def main(argv=None) -> int:
     shape = (3, 224, 224)
     sample_bytes = math.prod(shape) * torch.empty((), dtype=getattr(torch, args.source_dtype)).element_size()
 
-    with ddl_amd.start(n_producers=args.producers) as (env, conn):
+    # the indexed phase's producers are spawned with the headline's, before anything touches the GPU
+    spares = 1 if args.order == "window+indexed" and args.producers > 0 else 0
+    with ddl_amd.start(n_producers=args.producers, spare_connections=spares) as (env, conn):
         dev = torch.device(env.device)
         producer = ImageWindowProducer(args.window, shape, args.source_dtype, seed=args.seed, refill=args.refill,
                                        host_threads=args.producer_threads)
@@ -585,7 +637,8 @@ def main(argv=None) -> int:
         indexed = None
         if args.order == "window+indexed":
             try:
-                indexed = indexed_phase(args, env, dev, barrier, sync)
+                indexed = indexed_phase(args, env, dev, barrier, sync,
+                                        spare=conn.spares[0] if conn is not None and conn.spares else None)
             except Exception as e:  # the headline is still reported
                 import traceback
 

@@ -25,7 +25,6 @@ def main(argv=None):
     ap.add_argument("--blocks", default="16,32,64,128,0")
     ap.add_argument("--prep-streams", default="1", help="comma list: gather streams per loader (1, 2)")
     ap.add_argument("--train-steps", type=int, default=100)
-    ap.add_argument("--capped-waves", action="store_true", help="TEMPORARY A/B: wave-granular capped gather")
     a = ap.parse_args(argv)
 
     import torch
@@ -38,10 +37,6 @@ def main(argv=None):
     from ddl_amd.utils.tracing import ComputeIdleMeter
     from ddl_amd.zerocopy import ZeroCopyLoader
 
-    if a.capped_waves:
-        from ddl_amd import _native
-
-        _native.hip().set_capped_waves(True)
     shape = (3, 224, 224)
     dt = torch.uint8 if a.dtype == "uint8" else torch.bfloat16
     name = f"ddl_amd_benchzc_{os.environ.get('MASTER_PORT', '0')}"

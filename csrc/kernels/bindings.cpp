@@ -570,7 +570,6 @@ PYBIND11_MODULE(_ddl_hip, m) {
       py::arg("iters") = 20000, "Host microseconds per call of the HIP stream/event APIs on the batch path");
 
   // --------------------------------------------------------------- kernels
-  m.def("set_capped_waves", &ddl::set_capped_waves, py::arg("on"), "TEMPORARY round-5 A/B of the capped gather");
   m.def(
       "gather_rows",
       [](uintptr_t dst, int out_dt, uintptr_t src, int in_dt, int64_t n_rows, int64_t row_elems, int mode,

@@ -15,7 +15,6 @@ namespace ddl {
 // dst[source_row(ri, r), :] = src[r, :]       (scatter=1, same dtype only)
 // max_blocks > 0 caps the grid (grid-stride over tiles), e.g. to keep a
 // zero-copy gather out of pinned host memory on a few CUs.
-void set_capped_waves(bool on);  // TEMPORARY round-5 A/B (permute.hip)
 int gather_rows(void* dst, int32_t out_dt, const void* src, int32_t in_dt, int64_t n_rows, int64_t row_elems,
                 const RowIndex& ri, const Affine& aff, int scatter, int64_t max_blocks, hipStream_t st);
 // out[i] = feistel_perm(base + i), i < count

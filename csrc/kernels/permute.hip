@@ -63,48 +63,6 @@ __global__ void __launch_bounds__(kThreads) move_rows_chunked(uint8_t* __restric
   }
 }
 
-// Capped grids (zero-copy gathers out of pinned host memory, ddl_amd/zerocopy.py): the unit of work is one
-// WAVE's contiguous piece of a row -- 64 lanes x kUnroll units, 4 KB with 16-byte units -- not a workgroup's
-// 16 KB tile. Each wave walks its own pieces (grid-stride over pieces, 4 waves per workgroup), so the few
-// workgroups the kernel may occupy keep every wave's loads in flight on its own stretch of a host row instead
-// of four waves interleaving 1 KB stripes of one tile. Measured on the loader's pattern (256 random 301 KB rows
-// per launch, back to back): 57.2 GB/s at 24-32 workgroups against 53.4 GB/s for the 16 KB tiling
-// (benchmarks/probe_zerocopy_read.hip, profiles/r5_fourth/).
-bool g_capped_waves = false;  // TEMPORARY round-5 A/B: capped grids use move_rows_waves (set_capped_waves)
-
-template <typename U>
-__global__ void __launch_bounds__(kThreads) move_rows_waves(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
-                                                            int64_t units_per_row, int64_t pieces_per_row,
-                                                            int64_t n_pieces, RowIndex ri, int scatter) {
-  constexpr int kWave = 64;
-  constexpr int kPiece = kWave * kUnroll;  // units per wave piece
-  const int lane = static_cast<int>(threadIdx.x) & (kWave - 1);
-  const int64_t waves = static_cast<int64_t>(gridDim.x) * (kThreads / kWave);
-  for (int64_t p = static_cast<int64_t>(blockIdx.x) * (kThreads / kWave) + (threadIdx.x / kWave); p < n_pieces;
-       p += waves) {
-    // pieces < 2^31 (host-checked): 32-bit division
-    const int64_t row = static_cast<uint32_t>(p) / static_cast<uint32_t>(pieces_per_row);
-    const int64_t piece = static_cast<uint32_t>(p) - static_cast<uint32_t>(row) * static_cast<uint32_t>(pieces_per_row);
-    const int64_t mapped = source_row(ri, row);
-    const int64_t srow = scatter ? row : mapped;
-    const int64_t drow = scatter ? mapped : row;
-    const U* s = reinterpret_cast<const U*>(src) + srow * units_per_row;
-    U* d = reinterpret_cast<U*>(dst) + drow * units_per_row;
-    const int64_t u0 = piece * kPiece + lane;
-    U v[kUnroll];
-#pragma unroll
-    for (int k = 0; k < kUnroll; ++k) {
-      const int64_t u = u0 + k * kWave;
-      if (u < units_per_row) v[k] = s[u];
-    }
-#pragma unroll
-    for (int k = 0; k < kUnroll; ++k) {
-      const int64_t u = u0 + k * kWave;
-      if (u < units_per_row) d[u] = v[k];
-    }
-  }
-}
-
 template <typename U>
 __global__ void __launch_bounds__(kThreads) move_rows_flat(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
                                                            int64_t units_per_row, int64_t total_units, RowIndex ri,
@@ -347,14 +305,7 @@ template <typename U>
 void launch_move(void* dst, const void* src, int64_t n_rows, int64_t row_bytes, const RowIndex& ri, int scatter,
                  int64_t max_blocks, hipStream_t st) {
   const int64_t units = row_bytes / static_cast<int64_t>(sizeof(U));
-  const int64_t ppr = (units + 64 * kUnroll - 1) / (64 * kUnroll);  // wave pieces per row
-  const int64_t n_pieces = n_rows * ppr;
-  if (g_capped_waves && max_blocks > 0 && units >= kThreads && n_pieces < (int64_t{1} << 31)) {  // move_rows_waves
-    const int64_t g = std::min<int64_t>(max_blocks, (n_pieces + (kThreads / 64) - 1) / (kThreads / 64));
-    hipLaunchKernelGGL(move_rows_waves<U>, dim3(static_cast<unsigned>(g)), dim3(kThreads), 0, st,
-                       static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), units, ppr, n_pieces, ri,
-                       scatter);
-  } else if (units >= kThreads) {
+  if (units >= kThreads) {
     const int64_t chunks = (units + kThreads * kUnroll - 1) / (kThreads * kUnroll);
     hipLaunchKernelGGL(move_rows_chunked<U>, tile_grid(n_rows * chunks, max_blocks), dim3(kThreads), 0, st,
                        static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), units, chunks, n_rows * chunks,
@@ -409,8 +360,6 @@ __global__ void __launch_bounds__(kThreads) feistel_fill(int64_t* __restrict__ o
 }
 
 }  // namespace
-
-void set_capped_waves(bool on) { g_capped_waves = on; }
 
 int gather_rows(void* dst, int32_t out_dt, const void* src, int32_t in_dt, int64_t n_rows, int64_t row_elems,
                 const RowIndex& ri, const Affine& aff, int scatter, int64_t max_blocks, hipStream_t st) {

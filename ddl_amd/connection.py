@@ -76,6 +76,8 @@ class _Pipe:
                         f"{self.name}: connection lost while waiting for {expect!r} ({e!r})") from None
                 if tag == "error":
                     raise PeerDeathError(f"{self.name} failed:\n{payload}")
+                if tag == "shutdown" and expect != "shutdown":  # the consumer closed before using this producer
+                    raise ShutdownError(f"{self.name}: shut down while waiting for {expect!r}")
                 if tag != expect:
                     raise RuntimeError(f"{self.name}: protocol error, expected {expect!r} got {tag!r}")
                 return payload
@@ -118,6 +120,7 @@ class Connection:
         self.processes = list(procs)
         self.arena = None
         self.cpu_layout: dict | None = None  # consumer / producer CPU split (utils/numa.partition_after_spawn)
+        self.spares: list["Connection"] = []  # more producer sets spawned with this one (start(spare_connections=))
         self._finalizers: list = []
         self.window_shapes: list[tuple[int, ...]] = []
         self.window_dtypes: list[torch.dtype] = []

@@ -31,7 +31,7 @@ import numpy as np
 import torch
 
 from .connection import ProducerConnection
-from .exceptions import ShapeMismatchError
+from .exceptions import ShapeMismatchError, ShutdownError
 from .ops import _dtypes
 from .types import MetaData_Consumer_To_Producer, MetaData_Producer_To_Consumer, WorkerInfo
 from .utils import faults
@@ -232,6 +232,8 @@ def producer_main(pipe, producer_index: int, consumer_pid: int, rank: int, world
     try:
         pusher = DataPusher(conn, rank_global=rank, world_size=world_size)
         pusher.push_data()
+    except ShutdownError:  # closed before any loader used this producer (e.g. an unused spare connection)
+        logger.debug("producer %d: shut down before a loader used it", producer_index)
     except BaseException as e:  # report, then exit non-zero
         logger.error("producer %d failed: %r", producer_index, e)
         conn.report_error(e)

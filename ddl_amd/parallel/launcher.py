@@ -69,7 +69,8 @@ def spawn_producers(env: DDLEnv, timeout_s: float = DEFAULT_TIMEOUT_S, env_overr
 def start(n_producers: int | None = None, init_dist: bool = True, backend: str | None = None,
           timeout_s: float = DEFAULT_TIMEOUT_S, env_overrides: dict | None = None,
           device: str | None = None, abort_on_error: bool = True,
-          peer_timeout_s: float = DEFAULT_PEER_TIMEOUT_S) -> Iterator[tuple[DDLEnv, Connection | None]]:
+          peer_timeout_s: float = DEFAULT_PEER_TIMEOUT_S,
+          spare_connections: int = 0) -> Iterator[tuple[DDLEnv, Connection | None]]:
     """Context-manager form of the launcher: ``with start() as (env, conn): ...``.
 
     ``timeout_s`` bounds every wait: the shm hand-offs with the producers AND the process groups'
@@ -79,6 +80,12 @@ def start(n_producers: int | None = None, init_dist: bool = True, backend: str |
     peers exit ``PEER_ABORT_EXIT`` within a fraction of a second, and a rank that dies silently is
     declared dead after ``peer_timeout_s`` without a heartbeat (``parallel/abort.py``; the heartbeat needs
     the GIL, so a rank holding it longer than that in one call counts as hung).
+
+    ``spare_connections``: that many more independent sets of ``n_producers`` producers, spawned with the
+    first (before anything touches the GPU -- a process must never be spawned from a GPU-initialised
+    parent), as ``conn.spares``: one per later ``DistributedDataLoader`` of the same program (an evaluation
+    loader after the training loader, a second order). A producer set serves one loader; an unused spare
+    shuts down cleanly at exit.
     """
     configure()
     env = read_env(n_producers)
@@ -87,9 +94,16 @@ def start(n_producers: int | None = None, init_dist: bool = True, backend: str |
     # before spawning: the producers inherit the rank's CPU slice of its GPU's NUMA node
     node = bind_to_gpu_numa(env.local_rank, env.local_world_size)
     conn = spawn_producers(env, timeout_s, env_overrides) if env.n_producers > 0 else None
+    spares = [spawn_producers(env, timeout_s, env_overrides) for _ in range(int(spare_connections))] \
+        if conn is not None else []
+    if conn is not None:
+        conn.spares = spares
     if conn is not None and node is not None:  # a GPU host: split the slice between consumer and producers
-        pids = [p for p in conn.producer_pids if p and p != os.getpid()]  # thread-mode producers: none
-        conn.cpu_layout = partition_after_spawn(pids, len(pids)) if len(pids) == env.n_producers else None
+        every = [conn, *spares]
+        pids = [p for c in every for p in c.producer_pids if p and p != os.getpid()]  # thread mode: none
+        layout = partition_after_spawn(pids, len(pids)) if len(pids) == env.n_producers * len(every) else None
+        for c in every:
+            c.cpu_layout = layout
     created_pg = False
     watchdog = None
     try:
@@ -101,15 +115,19 @@ def start(n_producers: int | None = None, init_dist: bool = True, backend: str |
             created_pg = not was and dist.is_initialized()  # a named backend builds a group at world size 1 too
             if abort_on_error and env.world_size > 1 and env.control_group is not None:
                 watchdog = JobWatchdog(env.rank, env.world_size, peer_timeout_s=peer_timeout_s,
-                                       on_abort=conn.kill if conn is not None else None).start()
+                                       on_abort=(lambda: [c.kill() for c in (conn, *spares)]) if conn is not None
+                                       else None).start()
         yield env, conn
     except BaseException as e:
         if watchdog is not None and not (isinstance(e, SystemExit) and e.code in (None, 0)):
-            abort_on_exception(watchdog, e, cleanup=conn.kill if conn is not None else None)
+            abort_on_exception(watchdog, e, cleanup=(lambda: [c.kill() for c in (conn, *spares)]) if conn is not None
+                               else None)
         raise
     finally:
         if watchdog is not None:
             watchdog.finishing()
+        for c in spares:
+            c.finalize()
         if conn is not None:
             conn.finalize()
         if created_pg:

@@ -36,8 +36,8 @@ def test_native_module_is_loaded():
 @pytest.mark.parametrize("how", ["identity", "index", "perm"])
 @pytest.mark.parametrize("max_blocks", [0, 5, 32])
 def test_gather_rows_same_dtype_bitwise(dtype, row_shape, how, max_blocks):
-    """Every same-dtype move (16 / 4 / 1-byte units; uncapped tiles, and the capped grid's wave-granular
-    pieces of the zero-copy gather, move_rows_waves) equals index_select bitwise."""
+    """Every same-dtype move (16 / 4 / 1-byte units; uncapped and capped grids -- the zero-copy gather runs
+    capped) equals index_select bitwise."""
     n = 300
     g = torch.Generator().manual_seed(1)
     src = (torch.rand((n, *row_shape), generator=g) * 200).to(dtype)

@@ -283,3 +283,20 @@ def test_producer_preferred_slots(monkeypatch):
         seen = [x[0].clone() for x in dl]
         assert len(seen) == 2
         dl.close()
+
+
+def test_spare_connections_serve_later_loaders_and_unused_ones_exit_cleanly():
+    """``start(spare_connections=)`` spawns more producer sets up front (before the GPU is touched): a second
+    loader after the first runs on ``conn.spares[0]`` (its own producers, its own arena) and delivers every row
+    exactly once; a spare that no loader used exits with status 0 at the end (no error report)."""
+    with ddl_amd.start(n_producers=2, spare_connections=2) as (env, conn):
+        assert len(conn.spares) == 2 and all(s.n_producers == 2 for s in conn.spares)
+        first = ddl_amd.DistributedDataLoader(IdProducer(32, 4), 8, conn, 2, env=env)
+        a = _epochs(first, 2)
+        second = ddl_amd.DistributedDataLoader(IdProducer(48, 4), 8, conn.spares[0], 2, env=env)
+        b = _epochs(second, 2)
+        for rows, n in ((a, 32), (b, 48)):
+            for ep in rows:
+                assert sorted(ep[:, 2].tolist()) == list(range(n))  # column 2: the row id inside the window
+        unused = conn.spares[1].processes
+    assert all(p.exitcode == 0 for p in unused), [p.exitcode for p in unused]
