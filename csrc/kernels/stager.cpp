@@ -27,9 +27,10 @@ int64_t ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
 }
 
-// a polling wait's pause: spin-yield for the first iterations (a copy or kernel a few us from done), then sleep
-void poll_pause(int* spins) {
-  if (++*spins < 64)
+// a polling wait's pause: spin-yield for the first 500 us (the event is usually a kernel or copy that is about
+// to finish: the wait must add no latency there, as hipEventSynchronize's spin did), then sleep 20 us
+void poll_pause(std::chrono::steady_clock::time_point t0) {
+  if (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(500))
     std::this_thread::yield();
   else
     std::this_thread::sleep_for(std::chrono::microseconds(20));
@@ -254,7 +255,6 @@ int NativeStager::wait_signal(hsa_signal_t sg, int64_t timeout_ms, bool stop_awa
 
 int NativeStager::wait_event(hipEvent_t ev, int64_t timeout_ms, bool stop_aware) const {
   const auto t0 = std::chrono::steady_clock::now();
-  int spins = 0;
   for (;;) {
     const hipError_t q = hipEventQuery(ev);
     if (q == hipSuccess) return 0;
@@ -262,7 +262,7 @@ int NativeStager::wait_event(hipEvent_t ev, int64_t timeout_ms, bool stop_aware)
     if (copy_stuck_.load()) return -1;
     if (stop_aware && stopping_.load()) return kShutdown;
     if (timeout_ms >= 0 && ms_since(t0) >= timeout_ms) return kTimeout;
-    poll_pause(&spins);
+    poll_pause(t0);
   }
 }
 

@@ -119,3 +119,33 @@ def test_direct_dma_copy_timing_is_off_unless_asked():
             dl.mark(Marker.END_OF_BATCH)
         dl.mark(Marker.END_OF_EPOCH)
         dl.close()
+
+
+def test_close_interrupts_a_pending_free_event_wait():
+    """The stager waits for a ring buffer's free event (recorded behind the consumer's reads) by polling, so
+    close() ends that wait at once even while the consumer's stream is still busy: here a ~3 s spin kernel
+    sits in front of window 0's free event while the stager wants its buffer back for window 2."""
+    with ddl_amd.start(n_producers=P) as (env, conn):
+        # calibrate the spin kernel (its clock is the shader clock): cycles per second
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        torch.cuda._sleep(int(1e8))
+        e1.record()
+        e1.synchronize()
+        cycles_per_s = 1e8 / max(1e-4, e0.elapsed_time(e1) / 1e3)
+        dl = ddl_amd.DistributedDataLoader(IdProducer(N, WIDTH), B, conn, 8, env=env, device=torch.device("cuda"),
+                                           shuffle="device", seed=SEED, prefetch_depth=2, copy_batches=True,
+                                           native_dispatch=False)
+        for i in range(len(dl)):
+            dl[i]
+            if i + 1 < len(dl):
+                dl.mark(Marker.END_OF_BATCH)
+        torch.cuda._sleep(int(3.0 * cycles_per_s))  # ~3 s of spinning ahead of window 0's free event
+        dl.mark(Marker.END_OF_BATCH)  # window 0 released behind the spin: its free event stays pending
+        time.sleep(0.3)  # the stager is now waiting for that free event (window 2 needs buffer 0)
+        assert not torch.cuda.current_stream().query(), "the spin kernel finished too early for this test"
+        t0 = time.monotonic()
+        dl._stager._native.close()
+        assert time.monotonic() - t0 < 1.0
+        assert not torch.cuda.current_stream().query()  # the wait was interrupted, not satisfied
+        dl.close()
