@@ -149,3 +149,46 @@ def test_close_interrupts_a_pending_free_event_wait():
         assert time.monotonic() - t0 < 1.0
         assert not torch.cuda.current_stream().query()  # the wait was interrupted, not satisfied
         dl.close()
+
+
+@pytest.mark.timeout(300)
+def test_long_run_reanchors_and_flags_trimmed_copy_logs():
+    """Past 4096 retires the stager re-anchors its device clock (off its lock), and past the 16,384 copies its
+    logs keep, an interval or window that starts before the oldest kept record says so (``truncated`` /
+    ``complete=False``) instead of undercounting; a recent interval still counts exactly."""
+    from ddl_amd import _native
+
+    rt = _native.runtime()
+    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    n_win = 20000
+    with ddl_amd.start(n_producers=P) as (env, conn):
+        e0 = ev()
+        e0.record()
+        t0_ns = rt.now_ns()
+        dl = ddl_amd.DistributedDataLoader(IdProducer(64, 64), 64, conn, n_win, env=env, device=torch.device("cuda"),
+                                           prefetch_depth=4, copy_batches=True, copy_timing=True)
+        em = None
+        for e in range(n_win):
+            if e == n_win - 200:
+                torch.cuda.synchronize()
+                em = ev()
+                em.record()
+            dl[0]
+            dl.mark(Marker.END_OF_BATCH)
+            if e + 1 < n_win:
+                dl.mark(Marker.END_OF_EPOCH)
+        torch.cuda.synchronize()
+        e1 = ev()
+        e1.record()
+        e1.synchronize()
+        st = dl._stager
+        st.settle()
+        assert st._native.reanchors >= 3, st._native.reanchors
+        whole = st.bytes_in_interval(e0, e1)
+        assert not whole["ok"] and whole["truncated"]
+        recent = st.bytes_in_interval(em, e1)
+        assert recent["ok"] and not recent["truncated"] and recent["bytes"] > 0
+        assert recent["bytes"] <= 200 * 64 * 64 * 4 + 1e-6
+        _, _, complete = st._native.copies_between(t0_ns, rt.now_ns())
+        assert not complete
+        dl.close()
