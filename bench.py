@@ -102,6 +102,8 @@ def parse(argv=None):
                          "next to the headline in the JSON line ('indexed')")
     ap.add_argument("--index-samples", type=int, default=4096,
                     help="indexed order: samples in the node-shared synthetic source")
+    ap.add_argument("--index-threads", type=int, default=8,
+                    help="indexed order: host gather threads per producer (IndexedProducer host_threads)")
     ap.add_argument("--index-no-prefault", action="store_true",
                     help="indexed order: skip the one-word-per-page touch of the mapped source (A/B)")
     ap.add_argument("--dispatch", default="auto", choices=["auto", "inline", "lookahead", "python"],
@@ -381,15 +383,20 @@ def indexed_phase(args, env, dev, barrier, sync, spare=None) -> dict:
             bpe = n // gb
             total = args.warmup + args.steps + (max(1, args.warmup // 2) + idle_steps if idle_steps else 0)
             dl = ddl_amd.DistributedDataLoader(
-                IndexedProducer(src, gb, seed=args.seed, host_threads=8), args.batch, spare,
+                IndexedProducer(src, gb, seed=args.seed, host_threads=args.index_threads), args.batch, spare,
                 math.ceil(total / bpe) + 2, mode="indexed", env=env, device=dev, n_slots=2, auto_mark=True)
             it = forever(dl)
+            w0 = dl.stats().get("stager_wait_producer_s", 0.0)
             rate, ms = _timed_feed(args, env, it, acc, barrier, sync, "bench.indexed")
             st = dl.stats()
-            out.update({"path": "producers (IndexedProducer: host gather in the epoch order, 2 slots x 8 "
-                                "threads, direct-DMA staging)",
+            out.update({"path": f"producers (IndexedProducer: host gather in the epoch order, 2 slots x "
+                                f"{args.index_threads} threads, direct-DMA staging)",
                         "value": round(rate, 1), "ms_per_step": round(ms, 4),
-                        "h2d_direct_dma": bool(st.get("direct_dma", False))})
+                        "h2d_direct_dma": bool(st.get("direct_dma", False)),
+                        # the stager's waits for producers over warmup + timed steps (diagnostic)
+                        "stager_wait_producer_s": round(st.get("stager_wait_producer_s", 0.0) - w0, 4),
+                        "producer_fill_us_per_round": [round(p["fill_ns_total"] / max(1, p["rounds"]) / 1e3, 1)
+                                                       for p in st.get("producers", [])]})
             out["gpu_idle_pct"] = _idle_behind_step(args, env, dev, it, barrier, sync)
             dl.close()
         zc = ZeroCopyLoader(src, args.batch * env.world_size, env, seed=args.seed, out_dtype=torch.bfloat16,

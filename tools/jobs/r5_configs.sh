@@ -8,3 +8,8 @@ run 250 tokens_idle python benchmarks/bench_tokens.py --batch 2048 --steps 2000 
 run 250 resident python benchmarks/bench_resident.py --steps 300 --warmup 30 --depths 1,2,4
 run 200 bench_u8 python bench.py --steps 100 --warmup 10 --source-dtype uint8 --idle-steps 0 --pressure-ratio 0 --order window --json-out gpurun_out/bench_u8.json
 run 400 sweep python benchmarks/bench_idle_sweep.py --ratios 0.5,0.75,0.9,1.25 --floor --json-out gpurun_out/sweep.jsonl
+for t in 4 8; do
+  for rep in 1 2; do
+    run 200 idx_t${t}_$rep python bench.py --steps 20 --warmup 5 --idle-steps 0 --pressure-ratio 0 --index-threads $t --json-out gpurun_out/idx_t${t}_$rep.json
+  done
+done
