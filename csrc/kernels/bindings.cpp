@@ -466,7 +466,8 @@ PYBIND11_MODULE(_ddl_hip, m) {
             return py::make_tuple(rc, fp);
           },
           py::arg("window"), py::arg("timeout_ms"))
-      .def("release", &ddl::BatchEngine::release, py::arg("window"))
+      .def("release", &ddl::BatchEngine::release, py::arg("window"), py::call_guard<py::gil_scoped_release>(),
+           "hand window w back to the stager (0 ok; -4: the bounded wait for its copy failed, -1 HIP error)")
       .def("reset", &ddl::BatchEngine::reset)
       .def_property("inline", &ddl::BatchEngine::is_inline, &ddl::BatchEngine::set_inline)
       .def("set_window_mode", &ddl::BatchEngine::set_window_mode, py::arg("on"), py::arg("slot_stride"))

@@ -686,10 +686,9 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
 
     def _release_window(self) -> None:
         if self._engine is not None:
-            if self._engine.release(self.window) != 0:
-                from .exceptions import DDLError
-
-                raise DDLError(f"native batch engine: releasing window {self.window} failed")
+            rc = self._engine.release(self.window)
+            if rc != 0:
+                self._engine_raise(rc, -1, f"releasing window {self.window}")
             if self._exchange_fn is not None:
                 self._stager.forget(self.window)  # the Python face's record of the posted window
             if self._eng_window == self.window:

@@ -154,3 +154,39 @@ def test_exchange_loader_live_load_state_dict(rccl_env, dispatch):
         assert len(got) == len(ref)
         for a, b in zip(got, ref):
             assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dispatch", ["auto", False])
+def test_exchange_stuck_copy_raises_within_the_timeout(rccl_env, dispatch):
+    """With the exchange on, the consumer host-waits for window w+1's copy before it enqueues w+1's
+    all-to-all (direct DMA: no HIP event follows the copy). That wait is bounded too: a copy whose completion
+    signal never drops (fault injection) raises DDLTimeoutError naming the window within the loader's
+    timeout, and close() returns."""
+    import time
+
+    import ddl_amd
+    from ddl_amd import Marker
+    from ddl_amd.exceptions import DDLTimeoutError
+    from ddl_amd.parallel import launcher
+    from tests.helpers import IdProducer
+
+    conn = launcher.spawn_producers(ddl_amd.parallel.read_env(2), mode="thread")
+    try:
+        dl = ddl_amd.DistributedDataLoader(IdProducer(64, 8), 16, conn, 8, 0.5, "alltoall", env=rccl_env,
+                                           shuffle="device", copy_batches=True, seed=2, prefetch_depth=2,
+                                           timeout_s=3.0, native_dispatch=dispatch)
+        if not dl._stager.direct_dma:
+            pytest.skip("no direct DMA here")
+        dl._stager._native.inject_stuck_copy(4)  # not staged yet: the 3-buffer ring holds windows 0..2
+        t0 = time.monotonic()
+        with pytest.raises(DDLTimeoutError, match="window 4"):
+            for _ in range(8):
+                for _ in dl:
+                    dl.mark(Marker.END_OF_BATCH)
+                dl.mark(Marker.END_OF_EPOCH)
+        assert time.monotonic() - t0 < 3.0 + 8.0
+        t1 = time.monotonic()
+        dl.close()
+        assert time.monotonic() - t1 < 15.0
+    finally:
+        conn.finalize()
