@@ -43,8 +43,11 @@ def test_alltoall_exchange_on_device_conserves_window(rccl_env):
     assert sh.calls == 1
 
 
-def test_loader_with_exchange_enabled_on_gpu(rccl_env, monkeypatch):
-    """The stager runs the exchange on its post-copy stream; batches stay exactly-once."""
+@pytest.mark.parametrize("method", ["alltoall", "sendrecv_replace"])
+def test_loader_with_exchange_enabled_on_gpu(rccl_env, monkeypatch, method):
+    """The stager runs the exchange on its post-copy stream; batches stay exactly-once -- with the
+    all-to-all and with the reference's two-partner pattern (``sendrecv_replace``: grouped isend / irecv,
+    here to the rank itself) through RCCL."""
     import ddl_amd
     from ddl_amd import Marker
     from ddl_amd.parallel import launcher
@@ -52,7 +55,7 @@ def test_loader_with_exchange_enabled_on_gpu(rccl_env, monkeypatch):
 
     conn = launcher.spawn_producers(ddl_amd.parallel.read_env(2), mode="thread")
     try:
-        dl = ddl_amd.DistributedDataLoader(IdProducer(64, 8), 16, conn, 4, 0.5, "alltoall", env=rccl_env,
+        dl = ddl_amd.DistributedDataLoader(IdProducer(64, 8), 16, conn, 4, 0.5, method, env=rccl_env,
                                            shuffle="device", copy_batches=True, seed=2)
         assert dl._exchange_fn is not None and dl._stager.stream is not dl._stager.copy_stream
         for e in range(4):
