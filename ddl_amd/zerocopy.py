@@ -105,7 +105,9 @@ class ZeroCopyLoader(PrefetchedIndexedLoader):
             self.rows = ops.HostRows(self.cpu, dptr)
             self.prep_stream = streams.batch_stream(self.device)
             # prep_streams = 2: consecutive batches' gathers alternate between two streams, so the next one
-            # starts while the previous one's last workgroups drain (the link idles in a lone kernel's tail)
+            # starts while the previous one's last workgroups drain (the link idles in a lone kernel's tail).
+            # Not the default: two gathers in flight over the link were erratic on MI355X (16 workgroups:
+            # 171-190k samples/s; 24-32: 20k-185k, profiles/r5_zerocopy/) against a steady 188k with one
             self._prep = [self.prep_stream] + [torch.cuda.Stream(self.device, priority=-1)
                                                for _ in range(max(1, int(prep_streams)) - 1)]
             self.prefault_s = self._prefault(dptr) if prefault else 0.0
