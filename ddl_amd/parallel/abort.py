@@ -16,10 +16,14 @@ through the (possibly blocked) collectives: a client of the job's rendezvous ``T
 * **Abort -> exit.** Every other rank's watchdog sees the key within ``poll_s``, logs it, stops its
   producer workers and exits with ``PEER_ABORT_EXIT`` (``os._exit``: the main thread may be blocked in
   a collective that will never complete).
-* **Silent death.** Each rank bumps a heartbeat counter; rank r watches rank ``(r + 1) % W`` only (O(W)
-  store traffic). A counter that has not moved for ``peer_timeout_s`` (SIGKILL, OOM kill, a hang with
-  the GIL held) makes the watcher publish the abort for it. An unreachable store (its host rank died)
-  is an abort too.
+* **Death.** Each rank has a ``DeathWatch``: a small child process, spawned before the rank touches the
+  GPU, that holds one end of a pipe to the rank. When the rank dies without a clean shutdown (SIGKILL,
+  OOM kill, a crash in native code) the pipe reaches EOF and the child publishes the abort at once, so
+  the peers exit within ``poll_s`` -- not after ``peer_timeout_s``. It needs no GIL and no heartbeat.
+* **Silent hang.** Each rank bumps a heartbeat counter; rank r watches rank ``(r + 1) % W`` only (O(W)
+  store traffic). A counter that has not moved for ``peer_timeout_s`` (a hang with the GIL held, a
+  SIGSTOPped process) makes the watcher publish the abort for it. An unreachable store (its host rank
+  died) is an abort too.
 * **Clean exit.** ``stop()`` marks the rank done (watchers of a finished rank stop checking it) before
   the final barrier, so a slow rank is never mistaken for a dead one once its neighbour finished.
 
@@ -46,6 +50,10 @@ PEER_ABORT_EXIT = 75  # exit status of a rank torn down because ANOTHER rank fai
 # a hung one and takes the job down with PEER_ABORT_EXIT. The loader's own waits all release the GIL. Raise it
 # (``start(peer_timeout_s=)``, ``distributed_dataloader(peer_timeout_s=)``) for such workloads.
 DEFAULT_PEER_TIMEOUT_S = 60.0
+
+
+def _job_key() -> str:
+    return os.environ.get("TORCHELASTIC_RUN_ID") or os.environ.get("MASTER_PORT", "0")
 
 
 def _store_client(prefix: str, timeout_s: float):
@@ -82,7 +90,7 @@ class JobWatchdog:
         self.poll_s = float(poll_s)
         self.on_abort = on_abort
         self._exit = exit_fn or os._exit
-        key = job_key or os.environ.get("TORCHELASTIC_RUN_ID") or os.environ.get("MASTER_PORT", "0")
+        key = job_key or _job_key()
         self._store = store if store is not None else _store_client(f"ddl_amd/abort/{key}/", 30.0)
         self._stop = threading.Event()
         self._thread: threading.Thread | None = None
@@ -170,6 +178,68 @@ class JobWatchdog:
                 if self._stop.wait(4 * self.poll_s + 1.0):
                     return
                 return self._fire(f"rendezvous store unreachable ({type(e).__name__}: {e})")
+
+
+def _death_watch_main(pipe, parent_pid: int, rank: int, job_key: str, host: str, port: int) -> None:
+    """Body of a rank's ``DeathWatch`` child: wait on the pipe to the rank. "done" = the rank shuts down
+    cleanly; EOF (or a new parent) = it died: publish the job-wide abort under the watchdogs' prefix."""
+    os.environ["HIP_VISIBLE_DEVICES"] = "-1"  # never touches a GPU
+    while True:
+        try:
+            if pipe.poll(1.0):
+                if pipe.recv() == "done":
+                    return
+            elif os.getppid() != parent_pid:
+                break
+        except (EOFError, OSError):
+            break
+    msg = f"rank {rank}: process {parent_pid} died without a clean shutdown (killed or crashed)"
+    print(f"ddl_amd: {msg}; aborting the job", file=sys.stderr, flush=True)
+    try:
+        import torch.distributed as dist
+
+        store = dist.TCPStore(host, port, is_master=False, timeout=timedelta(seconds=10), wait_for_workers=False)
+        dist.PrefixStore(f"ddl_amd/abort/{job_key}/", store).compare_set("abort", "", msg[:2000])
+    except Exception:  # the store died with the rank that hosted it: the peers' watchdogs see the loss
+        pass
+
+
+class DeathWatch:
+    """The death reporter of one rank (see the module docstring). ``spawn`` before the rank touches the GPU
+    (a process must never be spawned from a GPU-initialised parent); ``done()`` on a clean shutdown."""
+
+    def __init__(self, proc, pipe):
+        self.proc, self._pipe = proc, pipe
+
+    @classmethod
+    def spawn(cls, rank: int) -> "DeathWatch | None":
+        import multiprocessing as mp
+
+        if os.environ.get("DDL_PRODUCER_MODE", "process") == "thread":
+            # thread-mode producers mean "spawn no process" (under rocprofv3 the GPU may be initialised before
+            # main): the heartbeat alone covers deaths then
+            return None
+        host, port = os.environ.get("MASTER_ADDR"), os.environ.get("MASTER_PORT")
+        if not host or not port:
+            logger.debug("no MASTER_ADDR / MASTER_PORT: no death watch (the heartbeat still covers deaths)")
+            return None
+        ctx = mp.get_context("spawn")
+        reader, writer = ctx.Pipe(duplex=False)
+        proc = ctx.Process(target=_death_watch_main, name=f"ddl-deathwatch-{rank}", daemon=True,
+                           args=(reader, os.getpid(), rank, _job_key(), host, int(port)))
+        proc.start()
+        reader.close()  # the child reads; this process keeps the only write end: EOF when it dies
+        return cls(proc, writer)
+
+    def done(self) -> None:
+        try:
+            self._pipe.send("done")
+            self._pipe.close()
+        except (BrokenPipeError, OSError):
+            pass
+        self.proc.join(5.0)
+        if self.proc.is_alive():
+            self.proc.kill()
 
 
 def abort_on_exception(watchdog: JobWatchdog | None, exc: BaseException, cleanup: Callable[[], None] | None = None,

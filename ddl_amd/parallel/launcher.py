@@ -24,7 +24,7 @@ from typing import Any, Callable, Iterator
 from ..connection import DEFAULT_TIMEOUT_S, Connection
 from ..types import DDLEnv
 from ..utils.logging import configure, logger
-from .abort import DEFAULT_PEER_TIMEOUT_S, JobWatchdog, abort_on_exception
+from .abort import DEFAULT_PEER_TIMEOUT_S, DeathWatch, JobWatchdog, abort_on_exception
 from .env import destroy_distributed, init_distributed, read_env
 
 
@@ -104,6 +104,8 @@ def start(n_producers: int | None = None, init_dist: bool = True, backend: str |
         layout = partition_after_spawn(pids, len(pids)) if len(pids) == env.n_producers * len(every) else None
         for c in every:
             c.cpu_layout = layout
+    # the death reporter is a process too: spawned before anything touches the GPU
+    death_watch = DeathWatch.spawn(env.rank) if abort_on_error and init_dist and env.world_size > 1 else None
     created_pg = False
     watchdog = None
     try:
@@ -126,6 +128,8 @@ def start(n_producers: int | None = None, init_dist: bool = True, backend: str |
     finally:
         if watchdog is not None:
             watchdog.finishing()
+        if death_watch is not None:  # a clean shutdown from here on (a raise already published its abort)
+            death_watch.done()
         for c in spares:
             c.finalize()
         if conn is not None:

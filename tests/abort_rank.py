@@ -1,6 +1,7 @@
 """One rank of the job-abort tests (``test_job_abort.py``): a loop of control-group all-reduces inside
 ``ddl_amd.start``; ``--stop-rank`` SIGSTOPs itself mid-loop (a silent hang: sockets open, no heartbeat),
-``--raise-rank`` raises mid-loop."""
+``--raise-rank`` raises mid-loop; ``--kill-rank`` SIGKILLs itself mid-loop while the others compute (no
+collective in flight: only the library can notice the death)."""
 
 import argparse
 import os
@@ -17,6 +18,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--stop-rank", type=int, default=-1)
     ap.add_argument("--raise-rank", type=int, default=-1)
+    ap.add_argument("--kill-rank", type=int, default=-1)
     ap.add_argument("--iters", type=int, default=400)
     ap.add_argument("--peer-timeout", type=float, default=3.0)
     ap.add_argument("--timeout", type=float, default=600.0, help="start(timeout_s=): shm waits + process groups")
@@ -30,6 +32,10 @@ def main() -> None:
                 os.kill(os.getpid(), signal.SIGSTOP)
             if i == 10 and env.rank == args.raise_rank:
                 raise RuntimeError("abort_rank: injected failure")
+            if i == 10 and args.kill_rank >= 0:
+                if env.rank == args.kill_rank:
+                    os.kill(os.getpid(), signal.SIGKILL)
+                time.sleep(120)  # "compute": no collective that could notice the dead peer
             dist.all_reduce(t, group=env.control_group)
             time.sleep(0.02)
     print(f"rank {env.rank} done", flush=True)

@@ -174,6 +174,24 @@ def test_silent_hang_detected_by_heartbeat():
 
 
 @pytest.mark.timeout(200)
+def test_killed_rank_ends_the_job_at_once():
+    """Rank 1 is SIGKILLed while the others compute (no collective in flight, so no socket error can
+    tell them): its death watch sees the pipe to the dead rank close and publishes the abort, and the
+    peers exit PEER_ABORT_EXIT within seconds -- long before the 60 s heartbeat timeout."""
+    script = os.path.join(REPO, "tests", "abort_rank.py")
+    procs = _launch_plain(3, [script, "--kill-rank", "1", "--peer-timeout", "60"], _base_env())
+    try:
+        codes, took = _wait_all(procs, 150)
+        errs = [p.communicate(timeout=30)[1] for p in procs]
+    finally:
+        _kill_all(procs)
+    assert codes[1] == -signal.SIGKILL, codes
+    assert codes[0] == PEER_ABORT_EXIT and codes[2] == PEER_ABORT_EXIT, (codes, errs[0][-1500:])
+    assert "died without a clean shutdown" in errs[0] and "died without a clean shutdown" in errs[2]
+    assert took < 30 < 60
+
+
+@pytest.mark.timeout(200)
 def test_clean_run_exits_zero_with_watchdog():
     """No fault: every rank finishes, the watchdog never fires (ranks finish at different times)."""
     script = os.path.join(REPO, "tests", "abort_rank.py")
