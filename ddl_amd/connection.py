@@ -339,6 +339,8 @@ class Connection:
         """Job abort (``parallel/abort.py``): stop the producers NOW -- no joins, no device sync (the
         GPU may be stuck behind a collective that will never complete). The arena file is already
         unlinked, so nothing is left in /dev/shm."""
+        if self._closed:  # finalized already (its arena may be unmapped): nothing left to stop
+            return
         self._closed = True
         if self.arena is not None:
             self.arena.request_shutdown()

@@ -23,8 +23,13 @@ partial global batch is completed from the start of the epoch's order, which is 
 ``DistributedSampler(drop_last=False)`` does under DDP (torch's single-process DataLoader instead
 yields a shorter last batch). ``drop_last=True`` drops the partial batch. Like torch's DataLoader
 with worker processes, construct it before the first CUDA call of the process: the workers are
-spawned processes (on a box whose policy forbids spawning after GPU initialisation, that ordering
-is required).
+spawned processes, and a process must never be spawned from a GPU-initialised parent (a loader
+created after that runs its workers as threads of the process, with a warning).
+
+Every loader alive in a process shares one launcher session (``_Session``): a training loader and an
+evaluation loader are opened the usual way, one after the other, and the process groups, the job
+watchdog and the death watch live until the LAST loader closes -- closing the training loader leaves
+a DDP model built on the group, and the evaluation loader, working.
 
 Mirrors the reference's drop-in entry (``ddl/mpi_dataloader.py:107-249``: ``len``, indexing,
 iteration) for users who start from a torch ``Dataset`` rather than a producer function.
@@ -32,7 +37,65 @@ iteration) for users who start from a torch ``Dataset`` rather than a producer f
 
 from __future__ import annotations
 
+import copy
 from typing import Any, Iterator
+
+from .utils.logging import logger
+
+
+class _Session:
+    """The launcher context that every ``DataLoader`` alive in this process shares: the rank's environment,
+    the process groups, the job watchdog and the death watch (``parallel.launcher.start``), opened by the
+    first loader and closed with the last one. A training loader and an evaluation loader of one program are
+    two loaders of ONE session: closing the first leaves the process groups (and a DDP model built on them)
+    and the job-wide abort in place for the second."""
+
+    current: "_Session | None" = None
+
+    def __init__(self, cm, env, first_conn):
+        self.cm, self.env, self.first_conn = cm, env, first_conn
+        self.refs = 0
+
+    @classmethod
+    def acquire(cls, num_workers: int, device: str | None):
+        """(session, this loader's producer connection)."""
+        from .parallel.launcher import spawn_producers, start
+
+        s = cls.current
+        if s is None:
+            cm = start(n_producers=num_workers, device=device)
+            env, conn = cm.__enter__()
+            s = cls.current = cls(cm, env, conn)
+        else:
+            if device is not None and str(device) != s.env.device:
+                raise ValueError(f"a DataLoader on {device!r} while the process's loaders run on {s.env.device!r}")
+            mode = None
+            import torch
+
+            if torch.cuda.is_initialized():
+                # a process must never be spawned from a GPU-initialised parent: this loader's workers run as
+                # threads of this process (construct every loader before the first CUDA call for processes)
+                logger.warning("DataLoader created after the GPU was initialised: its %d workers run as threads",
+                               num_workers)
+                mode = "thread"
+            env = copy.copy(s.env)
+            env.n_producers = int(num_workers)
+            conn = spawn_producers(env, mode=mode)
+            # the session's job abort stops these producers too (start() kills the first connection's spares)
+            s.first_conn.spares.append(conn)
+        s.refs += 1
+        return s, conn
+
+    def release(self, conn) -> None:
+        try:
+            conn.finalize()
+            if conn is not self.first_conn and conn in self.first_conn.spares:
+                self.first_conn.spares.remove(conn)
+        finally:
+            self.refs -= 1
+            if self.refs == 0:
+                type(self).current = None
+                self.cm.__exit__(None, None, None)
 
 
 class DataLoader:
@@ -42,21 +105,20 @@ class DataLoader:
         from .dataloader import DistributedDataLoader
         from .models.datasets import MapDatasetSource
         from .models.producers import IndexedProducer
-        from .parallel.launcher import start
 
         if num_workers < 1:
             raise ValueError("num_workers must be >= 1 (producer processes fill the pinned windows)")
-        self._cm = start(n_producers=int(num_workers), device=device)
-        self.env, conn = self._cm.__enter__()
+        self._session, self._conn = _Session.acquire(int(num_workers), device)
+        self.env = self._session.env
         try:
             gb = int(batch_size) * self.env.world_size
             producer = IndexedProducer(MapDatasetSource(dataset), gb, seed=int(seed), drop_last=drop_last,
                                        host_threads=host_threads, shuffle=shuffle)
             self.loader = DistributedDataLoader(
-                producer, int(batch_size), conn, epochs if epochs is not None else 1_000_000, mode="indexed",
+                producer, int(batch_size), self._conn, epochs if epochs is not None else 1_000_000, mode="indexed",
                 env=self.env, auto_mark=True, seed=int(seed), resume_state=resume_state, **loader_kw)
         except BaseException:
-            self._cm.__exit__(None, None, None)
+            self._session.release(self._conn)
             raise
         self.dataset = dataset
         self.batch_size = int(batch_size)
@@ -90,7 +152,7 @@ class DataLoader:
         try:
             self.loader.close()
         finally:
-            self._cm.__exit__(None, None, None)
+            self._session.release(self._conn)
 
     def __enter__(self) -> "DataLoader":
         return self

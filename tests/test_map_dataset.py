@@ -188,6 +188,59 @@ def test_dataloader_front_end_cpu(monkeypatch):
                            resume_state=sd43)
 
 
+def _train_and_eval_rank(rank, world, bs):
+    """A training loader and an evaluation loader alive together (the usual torch program): one launcher
+    session; closing the training loader keeps the process group (a DDP model's) and the eval loader working."""
+    import torch.distributed as dist
+
+    import ddl_amd
+    from ddl_amd import frontend
+
+    train, val = TupleDataset(48), DictDataset(40)
+    tl = ddl_amd.DataLoader(train, batch_size=bs, shuffle=True, num_workers=2, seed=1)
+    vl = ddl_amd.DataLoader(val, batch_size=bs, shuffle=False, drop_last=True, num_workers=1)
+    assert frontend._Session.current.refs == 2 and tl.env is vl.env
+    got_train = [b[1].tolist() for b in tl]
+    tl.close()
+    assert dist.is_initialized()  # the eval loader's session keeps the group
+    t = torch.ones(1)
+    dist.all_reduce(t)
+    got_val = [b["label"].tolist() for b in vl]
+    vl.close()
+    assert frontend._Session.current is None and not dist.is_initialized()
+    return got_train, got_val, float(t)
+
+
+def test_dataloader_front_end_train_and_eval():
+    bs, world = 4, 2
+    res = run_ranks(_train_and_eval_rank, world, bs, env={"DDL_DEVICE": "cpu"})
+    tr, va = EpochOrder(48, bs * world, 1), EpochOrder(40, bs * world, 0, shuffle=False)
+    for r, (got_train, got_val, total) in enumerate(res):
+        assert total == world
+        assert got_train == [[7 * int(i) for i in tr.indices(0, g)[r * bs:(r + 1) * bs]]
+                             for g in range(tr.batches_per_epoch)]
+        assert got_val == [[7 * int(i) for i in va.indices(0, g)[r * bs:(r + 1) * bs]]
+                           for g in range(va.batches_per_epoch)]
+
+
+def test_dataloader_front_end_late_loader_uses_threads(monkeypatch):
+    """A loader created after the GPU was initialised spawns no process: its workers are threads."""
+    import threading
+
+    from ddl_amd import frontend
+
+    monkeypatch.setenv("DDL_DEVICE", "cpu")
+    ds, bs = TupleDataset(16), 4
+    with ddl_amd.DataLoader(ds, batch_size=bs, num_workers=1) as first:
+        monkeypatch.setattr(torch.cuda, "is_initialized", lambda: True)
+        with ddl_amd.DataLoader(ds, batch_size=bs, num_workers=2) as late:
+            assert all(isinstance(p, threading.Thread) for p in late._conn.processes)
+            assert late._conn in first._conn.spares
+            assert [x for b in late for x in b[1].tolist()] == [7 * i for i in range(16)]
+        assert late._conn not in first._conn.spares and frontend._Session.current.refs == 1
+    assert frontend._Session.current is None
+
+
 @pytest.mark.gpu
 def test_dataloader_front_end_gpu():
     ds, bs = TupleDataset(64), 16
