@@ -147,9 +147,10 @@ class IndexedProducer(ProducerFunctionSkeleton):
     """Producer of the world-size-invariant global order (one window = one local batch)."""
 
     def __init__(self, source, global_batch: int, seed: int | None = None, drop_last: bool = True,
-                 host_threads: int = 4, shuffle: bool = True):
+                 host_threads: int = 4, shuffle: bool = True, worker_init_fn=None):
         super().__init__()
         self.source = source
+        self.worker_init_fn = worker_init_fn  # torch's: called with the worker (producer) index in the worker
         self.global_batch = int(global_batch)
         self.seed = seed  # None: use the loader's seed
         self.drop_last = drop_last
@@ -161,6 +162,9 @@ class IndexedProducer(ProducerFunctionSkeleton):
     def on_init(self, *args, **kwargs):
         super().on_init(*args, **kwargs)
         self.world_size = int(kwargs.get("world_size", 1))
+        init_fn = getattr(self, "worker_init_fn", None)
+        if init_fn is not None:
+            init_fn(int(self.producer_index or 0))
         if self.seed is None:
             self.seed = int(kwargs.get("seed", 0))
         self.order = EpochOrder(self.source.n, self.global_batch, int(self.seed), self.drop_last, self.shuffle)

@@ -184,6 +184,8 @@ def _death_watch_main(pipe, parent_pid: int, rank: int, job_key: str, host: str,
     """Body of a rank's ``DeathWatch`` child: wait on the pipe to the rank. "done" = the rank shuts down
     cleanly; EOF (or a new parent) = it died: publish the job-wide abort under the watchdogs' prefix."""
     os.environ["HIP_VISIBLE_DEVICES"] = "-1"  # never touches a GPU
+    import torch.distributed as dist  # now, not at the rank's death: the report must not wait for an import
+
     while True:
         try:
             if pipe.poll(1.0):
@@ -196,17 +198,16 @@ def _death_watch_main(pipe, parent_pid: int, rank: int, job_key: str, host: str,
     msg = f"rank {rank}: process {parent_pid} died without a clean shutdown (killed or crashed)"
     print(f"ddl_amd: {msg}; aborting the job", file=sys.stderr, flush=True)
     try:
-        import torch.distributed as dist
-
-        store = dist.TCPStore(host, port, is_master=False, timeout=timedelta(seconds=10), wait_for_workers=False)
+        # short: when the store's host is gone too, the peers' watchdogs see that loss themselves
+        store = dist.TCPStore(host, port, is_master=False, timeout=timedelta(seconds=5), wait_for_workers=False)
         dist.PrefixStore(f"ddl_amd/abort/{job_key}/", store).compare_set("abort", "", msg[:2000])
     except Exception:  # the store died with the rank that hosted it: the peers' watchdogs see the loss
         pass
 
 
 class DeathWatch:
-    """The death reporter of one rank (see the module docstring). ``spawn`` before the rank touches the GPU
-    (a process must never be spawned from a GPU-initialised parent); ``done()`` on a clean shutdown."""
+    """The death reporter of one rank (see the module docstring). ``spawn`` when the rank starts (``start()``
+    does, with the producers); ``done()`` on a clean shutdown."""
 
     def __init__(self, proc, pipe):
         self.proc, self._pipe = proc, pipe
@@ -231,12 +232,20 @@ class DeathWatch:
         reader.close()  # the child reads; this process keeps the only write end: EOF when it dies
         return cls(proc, writer)
 
-    def done(self) -> None:
+    def disarm(self) -> None:
+        """This rank is leaving on purpose (a clean shutdown, or an abort it already published or acted on):
+        the child exits without reporting a death. Does not wait for it."""
+        if self._pipe is None:
+            return
         try:
             self._pipe.send("done")
             self._pipe.close()
         except (BrokenPipeError, OSError):
             pass
+        self._pipe = None
+
+    def done(self) -> None:
+        self.disarm()
         self.proc.join(5.0)
         if self.proc.is_alive():
             self.proc.kill()

@@ -70,7 +70,8 @@ def start(n_producers: int | None = None, init_dist: bool = True, backend: str |
           timeout_s: float = DEFAULT_TIMEOUT_S, env_overrides: dict | None = None,
           device: str | None = None, abort_on_error: bool = True,
           peer_timeout_s: float = DEFAULT_PEER_TIMEOUT_S,
-          spare_connections: int = 0) -> Iterator[tuple[DDLEnv, Connection | None]]:
+          spare_connections: int = 0,
+          producer_mode: str | None = None) -> Iterator[tuple[DDLEnv, Connection | None]]:
     """Context-manager form of the launcher: ``with start() as (env, conn): ...``.
 
     ``timeout_s`` bounds every wait: the shm hand-offs with the producers AND the process groups'
@@ -82,10 +83,12 @@ def start(n_producers: int | None = None, init_dist: bool = True, backend: str |
     the GIL, so a rank holding it longer than that in one call counts as hung).
 
     ``spare_connections``: that many more independent sets of ``n_producers`` producers, spawned with the
-    first (before anything touches the GPU -- a process must never be spawned from a GPU-initialised
-    parent), as ``conn.spares``: one per later ``DistributedDataLoader`` of the same program (an evaluation
-    loader after the training loader, a second order). A producer set serves one loader; an unused spare
+    first (the rank's CPU slice is then split over all of them at once), as ``conn.spares``: one per later
+    ``DistributedDataLoader`` of the same program (an evaluation loader after the training loader, a second
+    order). A producer set serves one loader; an unused spare
     shuts down cleanly at exit.
+
+    ``producer_mode``: ``"process"`` or ``"thread"`` (``spawn_producers``; default ``$DDL_PRODUCER_MODE``).
     """
     configure()
     env = read_env(n_producers)
@@ -93,9 +96,9 @@ def start(n_producers: int | None = None, init_dist: bool = True, backend: str |
 
     # before spawning: the producers inherit the rank's CPU slice of its GPU's NUMA node
     node = bind_to_gpu_numa(env.local_rank, env.local_world_size)
-    conn = spawn_producers(env, timeout_s, env_overrides) if env.n_producers > 0 else None
-    spares = [spawn_producers(env, timeout_s, env_overrides) for _ in range(int(spare_connections))] \
-        if conn is not None else []
+    conn = spawn_producers(env, timeout_s, env_overrides, producer_mode) if env.n_producers > 0 else None
+    spares = [spawn_producers(env, timeout_s, env_overrides, producer_mode)
+              for _ in range(int(spare_connections))] if conn is not None else []
     if conn is not None:
         conn.spares = spares
     if conn is not None and node is not None:  # a GPU host: split the slice between consumer and producers
@@ -106,6 +109,16 @@ def start(n_producers: int | None = None, init_dist: bool = True, backend: str |
             c.cpu_layout = layout
     # the death reporter is a process too: spawned before anything touches the GPU
     death_watch = DeathWatch.spawn(env.rank) if abort_on_error and init_dist and env.world_size > 1 else None
+
+    def stop_helpers() -> None:
+        """Job abort (this rank failed, or a peer did): the producers stop now, the death watch stands down
+        (the abort is published already; this exit is no silent death)."""
+        if death_watch is not None:
+            death_watch.disarm()
+        if conn is not None:
+            for c in (conn, *spares):
+                c.kill()
+
     created_pg = False
     watchdog = None
     try:
@@ -117,13 +130,11 @@ def start(n_producers: int | None = None, init_dist: bool = True, backend: str |
             created_pg = not was and dist.is_initialized()  # a named backend builds a group at world size 1 too
             if abort_on_error and env.world_size > 1 and env.control_group is not None:
                 watchdog = JobWatchdog(env.rank, env.world_size, peer_timeout_s=peer_timeout_s,
-                                       on_abort=(lambda: [c.kill() for c in (conn, *spares)]) if conn is not None
-                                       else None).start()
+                                       on_abort=stop_helpers).start()
         yield env, conn
     except BaseException as e:
         if watchdog is not None and not (isinstance(e, SystemExit) and e.code in (None, 0)):
-            abort_on_exception(watchdog, e, cleanup=(lambda: [c.kill() for c in (conn, *spares)]) if conn is not None
-                               else None)
+            abort_on_exception(watchdog, e, cleanup=stop_helpers)
         raise
     finally:
         if watchdog is not None:

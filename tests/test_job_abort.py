@@ -188,6 +188,8 @@ def test_killed_rank_ends_the_job_at_once():
     assert codes[1] == -signal.SIGKILL, codes
     assert codes[0] == PEER_ABORT_EXIT and codes[2] == PEER_ABORT_EXIT, (codes, errs[0][-1500:])
     assert "died without a clean shutdown" in errs[0] and "died without a clean shutdown" in errs[2]
+    # the peers' own death watches stand down when they exit on the abort: no second, false death report
+    assert "rank 0: process" not in errs[0] and "rank 2: process" not in errs[2]
     assert took < 30 < 60
 
 

@@ -1,6 +1,8 @@
 """Map-style Dataset drop-in: ``IndexedProducer(MapDatasetSource(ds))`` delivers batches in the
 dataset's own sample structure, in the world-size-invariant global order."""
 
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -223,22 +225,45 @@ def test_dataloader_front_end_train_and_eval():
                            for g in range(va.batches_per_epoch)]
 
 
-def test_dataloader_front_end_late_loader_uses_threads(monkeypatch):
-    """A loader created after the GPU was initialised spawns no process: its workers are threads."""
+def _mark_worker(path, worker_id):
+    open(os.path.join(path, f"worker{worker_id}"), "w").close()
+
+
+def test_dataloader_front_end_torch_arguments(monkeypatch, tmp_path):
+    """torch's DataLoader signature: positional (dataset, batch_size, shuffle), num_workers=0 (one in-process
+    worker thread), worker_init_fn in every worker, generator as the seed, the no-op pinning / persistence
+    arguments; sampler / collate_fn / iterable datasets are refused with the reason."""
+    import functools
     import threading
 
+    monkeypatch.setenv("DDL_DEVICE", "cpu")
+    ds, bs = TupleDataset(24), 4
+    g = torch.Generator().manual_seed(11)
+    kw = dict(pin_memory=True, persistent_workers=True, prefetch_factor=2, multiprocessing_context="spawn",
+              timeout=30)
+    with ddl_amd.DataLoader(ds, bs, True, num_workers=0, generator=g, **kw) as dl:
+        assert all(isinstance(p, threading.Thread) for p in dl._conn.processes)
+        got = [b[1].tolist() for b in dl]
+    order = EpochOrder(len(ds), bs, 11)
+    assert got == [[7 * int(i) for i in order.indices(0, k)] for k in range(order.batches_per_epoch)]
+    with ddl_amd.DataLoader(ds, batch_size=bs, num_workers=2, collate_fn=torch.utils.data.default_collate,
+                            worker_init_fn=functools.partial(_mark_worker, str(tmp_path))) as dl:
+        assert [x for b in dl for x in b[1].tolist()] == [7 * i for i in range(len(ds))]  # shuffle defaults off
+    assert sorted(os.listdir(tmp_path)) == ["worker0", "worker1"]
+    with pytest.raises(ValueError, match="sampler"):
+        ddl_amd.DataLoader(ds, batch_size=bs, sampler=torch.utils.data.SequentialSampler(ds))
+    with pytest.raises(ValueError, match="collate_fn"):
+        ddl_amd.DataLoader(ds, batch_size=bs, collate_fn=lambda b: b)
+
+    class Stream(torch.utils.data.IterableDataset):
+        def __iter__(self):
+            return iter(range(3))
+
+    with pytest.raises(TypeError, match="map-style"):
+        ddl_amd.DataLoader(Stream(), batch_size=bs)
     from ddl_amd import frontend
 
-    monkeypatch.setenv("DDL_DEVICE", "cpu")
-    ds, bs = TupleDataset(16), 4
-    with ddl_amd.DataLoader(ds, batch_size=bs, num_workers=1) as first:
-        monkeypatch.setattr(torch.cuda, "is_initialized", lambda: True)
-        with ddl_amd.DataLoader(ds, batch_size=bs, num_workers=2) as late:
-            assert all(isinstance(p, threading.Thread) for p in late._conn.processes)
-            assert late._conn in first._conn.spares
-            assert [x for b in late for x in b[1].tolist()] == [7 * i for i in range(16)]
-        assert late._conn not in first._conn.spares and frontend._Session.current.refs == 1
-    assert frontend._Session.current is None
+    assert frontend._Session.current is None  # refused loaders leave no session behind
 
 
 @pytest.mark.gpu
@@ -250,3 +275,24 @@ def test_dataloader_front_end_gpu():
             for g, b in enumerate(dl):
                 assert b[0].is_cuda and b[0].shape == (bs, 3, 5, 7)
                 _check(b, _expected(ds, order.indices(e, g)))
+
+
+@pytest.mark.gpu
+def test_dataloader_front_end_train_and_eval_gpu():
+    """A training loader in use on the GPU, then an evaluation loader created mid-run (its workers spawned
+    after the GPU is initialised) and interleaved with it; closing the training loader first."""
+    ds, val, bs = TupleDataset(64), DictDataset(80), 16
+    order, vorder = EpochOrder(len(ds), bs, 5), EpochOrder(len(val), bs, 0, shuffle=False)
+    tl = ddl_amd.DataLoader(ds, batch_size=bs, shuffle=True, num_workers=2, seed=5)
+    it = iter(tl)
+    _check(next(it), _expected(ds, order.indices(0, 0)))
+    vl = ddl_amd.DataLoader(val, batch_size=bs, num_workers=0)  # shuffle off (eval), an in-process worker
+    vit = iter(vl)
+    for g in range(1, order.batches_per_epoch):
+        _check(next(it), _expected(ds, order.indices(0, g)))
+        _check(next(vit), _expected(val, vorder.indices(0, g - 1)))
+    tl.close()
+    b = next(vit)
+    assert b["image"].is_cuda
+    _check(b, _expected(val, vorder.indices(0, order.batches_per_epoch - 1)))
+    vl.close()
