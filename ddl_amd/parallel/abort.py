@@ -20,10 +20,12 @@ through the (possibly blocked) collectives: a client of the job's rendezvous ``T
   GPU, that holds one end of a pipe to the rank. When the rank dies without a clean shutdown (SIGKILL,
   OOM kill, a crash in native code) the pipe reaches EOF and the child publishes the abort at once, so
   the peers exit within ``poll_s`` -- not after ``peer_timeout_s``. It needs no GIL and no heartbeat.
-* **Silent hang.** Each rank bumps a heartbeat counter; rank r watches rank ``(r + 1) % W`` only (O(W)
-  store traffic). A counter that has not moved for ``peer_timeout_s`` (a hang with the GIL held, a
-  SIGSTOPped process) makes the watcher publish the abort for it. An unreachable store (its host rank
-  died) is an abort too.
+* **Frozen rank.** Each rank's heartbeat counter is bumped by its watchdog thread AND by its death watch,
+  which bumps only while the rank exists and is not stopped (``/proc``: SIGSTOP, a debugger, a frozen
+  cgroup). Rank r watches rank ``(r + 1) % W`` only (O(W) store traffic). A counter that has not moved for
+  ``peer_timeout_s`` (a stopped or frozen process, a lost node) makes the watcher publish the abort for
+  it. A healthy rank holding the GIL in one long C call keeps beating through its death watch, so it is
+  not mistaken for a dead one. An unreachable store (its host rank died) is an abort too.
 * **Clean exit.** ``stop()`` marks the rank done (watchers of a finished rank stop checking it) before
   the final barrier, so a slow rank is never mistaken for a dead one once its neighbour finished.
 
@@ -44,11 +46,11 @@ from typing import Any, Callable
 from ..utils.logging import logger
 
 PEER_ABORT_EXIT = 75  # exit status of a rank torn down because ANOTHER rank failed
-# A rank is declared dead when its heartbeat has not moved for this long. The heartbeat is bumped by a Python
-# daemon thread, so it needs the GIL: a HEALTHY rank whose main thread holds the GIL longer than this in one
-# call (a long C extension call that does not release it, unpickling a huge object) is indistinguishable from
-# a hung one and takes the job down with PEER_ABORT_EXIT. The loader's own waits all release the GIL. Raise it
-# (``start(peer_timeout_s=)``, ``distributed_dataloader(peer_timeout_s=)``) for such workloads.
+# A rank is declared dead when its heartbeat has not moved for this long. With a death watch (the default
+# process-mode launch) the heartbeat needs no GIL: a rank holding it in one long C call still beats. Without
+# one (thread-mode producers, no MASTER_ADDR / MASTER_PORT) only the Python thread beats, and a rank holding
+# the GIL longer than this counts as hung; raise it (``start(peer_timeout_s=)``,
+# ``distributed_dataloader(peer_timeout_s=)``) for such workloads.
 DEFAULT_PEER_TIMEOUT_S = 60.0
 
 
@@ -79,13 +81,23 @@ def _store_client(prefix: str, timeout_s: float):
     return dist.PrefixStore(prefix, store)
 
 
+def _linger_if_store_host(rank: int, poll_s: float) -> None:
+    """Rank 0 hosts the rendezvous TCPStore under a plain launch (torchrun's agent hosts it otherwise): its exit
+    takes the store down, and a peer that polls after that sees "store unreachable" instead of the abort's
+    reason. Stay up for two polls first, so every peer reads the reason."""
+    if rank == 0 and not os.environ.get("TORCHELASTIC_RUN_ID"):
+        time.sleep(2 * poll_s + 0.5)
+
+
 class JobWatchdog:
     """One per rank; see the module docstring. ``on_abort`` runs (best effort) before the exit."""
 
     def __init__(self, rank: int, world_size: int, *, peer_timeout_s: float = DEFAULT_PEER_TIMEOUT_S,
                  poll_s: float = 0.25, on_abort: Callable[[], None] | None = None, store: Any = None,
-                 job_key: str | None = None, exit_fn: Callable[[int], None] | None = None):
+                 job_key: str | None = None, exit_fn: Callable[[int], None] | None = None,
+                 death_watch: "DeathWatch | None" = None):
         self.rank, self.world = int(rank), int(world_size)
+        self.death_watch = death_watch  # beats for this rank too (alive and not stopped), GIL or not
         self.peer_timeout_s = float(peer_timeout_s)
         self.poll_s = float(poll_s)
         self.on_abort = on_abort
@@ -104,6 +116,8 @@ class JobWatchdog:
 
     def start(self) -> "JobWatchdog":
         self._store.set(self._hb(self.rank), "0")
+        if self.death_watch is not None:
+            self.death_watch.beat(self.poll_s)
         self._thread = threading.Thread(target=self._run, name=f"ddl-watchdog-{self.rank}", daemon=True)
         self._thread.start()
         return self
@@ -120,6 +134,8 @@ class JobWatchdog:
         """This rank's work is done: watchers of this rank stop watching it (a rank that finished
         first is not 'dead'), but this rank keeps acting on aborts -- a peer can still fail while
         this one waits in the final barrier."""
+        if self.death_watch is not None:
+            self.death_watch.finishing()  # its beats stop; its last write is "done" too (after any beat in flight)
         try:
             self._store.set(self._hb(self.rank), "done")
         except Exception:  # pragma: no cover - the thread reports a lost store
@@ -147,6 +163,7 @@ class JobWatchdog:
                 self.on_abort()
             except Exception:  # pragma: no cover - best effort
                 pass
+        _linger_if_store_host(self.rank, self.poll_s)
         self._exit(PEER_ABORT_EXIT)
 
     def _run(self) -> None:
@@ -180,37 +197,72 @@ class JobWatchdog:
                 return self._fire(f"rendezvous store unreachable ({type(e).__name__}: {e})")
 
 
+def _process_stopped(pid: int) -> bool:
+    """Is ``pid`` stopped (SIGSTOP, a debugger, a frozen cgroup)? Linux /proc; False where unknown."""
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            state = f.read().rsplit(")", 1)[1].split()[0]
+        if state in ("T", "t"):
+            return True
+        with open(f"/proc/{pid}/cgroup") as f:  # cgroup v2 freezer: the tasks are in "S" state, the cgroup frozen
+            rel = f.read().strip().split("::", 1)[-1]
+        with open(f"/sys/fs/cgroup{rel}/cgroup.events") as f:
+            return "frozen 1" in f.read()
+    except (OSError, IndexError):
+        return False
+
+
 def _death_watch_main(pipe, parent_pid: int, rank: int, job_key: str, host: str, port: int) -> None:
-    """Body of a rank's ``DeathWatch`` child: wait on the pipe to the rank. "done" = the rank shuts down
-    cleanly; EOF (or a new parent) = it died: publish the job-wide abort under the watchdogs' prefix."""
+    """Body of a rank's ``DeathWatch`` child. Messages from the rank: ``("beat", period_s)`` -- keep the rank's
+    heartbeat going from here (while the rank exists and is not stopped), ``"finishing"`` -- mark it done and
+    stop, ``"done"`` -- a clean shutdown, exit. EOF (or a new parent) = the rank died: publish the job-wide
+    abort under the watchdogs' prefix."""
     os.environ["HIP_VISIBLE_DEVICES"] = "-1"  # never touches a GPU
     import torch.distributed as dist  # now, not at the rank's death: the report must not wait for an import
 
+    prefix, hb = f"ddl_amd/abort/{job_key}/", f"hb/{rank}"
+    store, period, beat = None, 1.0, 0
     while True:
         try:
-            if pipe.poll(1.0):
-                if pipe.recv() == "done":
+            if pipe.poll(period):
+                msg = pipe.recv()
+                if msg == "done":
                     return
+                if msg == "finishing":
+                    if store is not None:
+                        store.set(hb, "done")
+                    store = None
+                elif isinstance(msg, tuple) and msg[0] == "beat":
+                    period = float(msg[1])
+                    store = dist.PrefixStore(prefix, dist.TCPStore(host, port, is_master=False,
+                                                                   timeout=timedelta(seconds=30),
+                                                                   wait_for_workers=False))
             elif os.getppid() != parent_pid:
                 break
+            if store is not None and not _process_stopped(parent_pid):
+                beat += 1
+                store.set(hb, f"w{beat}")
         except (EOFError, OSError):
             break
+        except Exception:  # the store is gone: the peers' watchdogs report that loss; keep watching for a death
+            store = None
     msg = f"rank {rank}: process {parent_pid} died without a clean shutdown (killed or crashed)"
     print(f"ddl_amd: {msg}; aborting the job", file=sys.stderr, flush=True)
     try:
         # short: when the store's host is gone too, the peers' watchdogs see that loss themselves
         store = dist.TCPStore(host, port, is_master=False, timeout=timedelta(seconds=5), wait_for_workers=False)
-        dist.PrefixStore(f"ddl_amd/abort/{job_key}/", store).compare_set("abort", "", msg[:2000])
+        dist.PrefixStore(prefix, store).compare_set("abort", "", msg[:2000])
     except Exception:  # the store died with the rank that hosted it: the peers' watchdogs see the loss
         pass
 
 
 class DeathWatch:
-    """The death reporter of one rank (see the module docstring). ``spawn`` when the rank starts (``start()``
-    does, with the producers); ``done()`` on a clean shutdown."""
+    """The death reporter -- and heartbeat -- of one rank (see the module docstring). ``spawn`` when the rank
+    starts (``start()`` does, with the producers); ``done()`` on a clean shutdown."""
 
     def __init__(self, proc, pipe):
         self.proc, self._pipe = proc, pipe
+        self._lock = threading.Lock()  # the watchdog thread and the main thread both send
 
     @classmethod
     def spawn(cls, rank: int) -> "DeathWatch | None":
@@ -232,17 +284,30 @@ class DeathWatch:
         reader.close()  # the child reads; this process keeps the only write end: EOF when it dies
         return cls(proc, writer)
 
+    def _send(self, msg, close: bool = False) -> bool:
+        with self._lock:
+            if self._pipe is None:
+                return False
+            try:
+                self._pipe.send(msg)
+                if close:
+                    self._pipe.close()
+                    self._pipe = None
+                return True
+            except (BrokenPipeError, OSError):
+                return False
+
+    def beat(self, period_s: float) -> bool:
+        """Heartbeat this rank from the child from now on (the rendezvous store is up)."""
+        return self._send(("beat", float(period_s)))
+
+    def finishing(self) -> bool:
+        return self._send("finishing")
+
     def disarm(self) -> None:
         """This rank is leaving on purpose (a clean shutdown, or an abort it already published or acted on):
         the child exits without reporting a death. Does not wait for it."""
-        if self._pipe is None:
-            return
-        try:
-            self._pipe.send("done")
-            self._pipe.close()
-        except (BrokenPipeError, OSError):
-            pass
-        self._pipe = None
+        self._send("done", close=True)
 
     def done(self) -> None:
         self.disarm()
@@ -266,4 +331,5 @@ def abort_on_exception(watchdog: JobWatchdog | None, exc: BaseException, cleanup
             cleanup()
         except Exception:  # pragma: no cover - best effort
             pass
+    _linger_if_store_host(getattr(watchdog, "rank", -1), getattr(watchdog, "poll_s", 0.25))
     (exit_fn or os._exit)(1)

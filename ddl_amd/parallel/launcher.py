@@ -78,9 +78,9 @@ def start(n_producers: int | None = None, init_dist: bool = True, backend: str |
     collectives (``init_distributed``). With ``abort_on_error`` (default) and more than one rank, a
     failure on any rank ends the whole job, as the reference's ``Abort(1)`` does
     (``/root/reference/ddl/ddl_env.py:25-30``): the failing rank publishes the error and exits 1, its
-    peers exit ``PEER_ABORT_EXIT`` within a fraction of a second, and a rank that dies silently is
-    declared dead after ``peer_timeout_s`` without a heartbeat (``parallel/abort.py``; the heartbeat needs
-    the GIL, so a rank holding it longer than that in one call counts as hung).
+    peers exit ``PEER_ABORT_EXIT`` within a fraction of a second; a rank that is killed or crashes ends the
+    job as fast (its death watch reports it), and a stopped or frozen rank after ``peer_timeout_s`` without
+    a heartbeat (``parallel/abort.py``).
 
     ``spare_connections``: that many more independent sets of ``n_producers`` producers, spawned with the
     first (the rank's CPU slice is then split over all of them at once), as ``conn.spares``: one per later
@@ -130,7 +130,7 @@ def start(n_producers: int | None = None, init_dist: bool = True, backend: str |
             created_pg = not was and dist.is_initialized()  # a named backend builds a group at world size 1 too
             if abort_on_error and env.world_size > 1 and env.control_group is not None:
                 watchdog = JobWatchdog(env.rank, env.world_size, peer_timeout_s=peer_timeout_s,
-                                       on_abort=stop_helpers).start()
+                                       on_abort=stop_helpers, death_watch=death_watch).start()
         yield env, conn
     except BaseException as e:
         if watchdog is not None and not (isinstance(e, SystemExit) and e.code in (None, 0)):

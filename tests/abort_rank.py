@@ -1,7 +1,8 @@
 """One rank of the job-abort tests (``test_job_abort.py``): a loop of control-group all-reduces inside
 ``ddl_amd.start``; ``--stop-rank`` SIGSTOPs itself mid-loop (a silent hang: sockets open, no heartbeat),
 ``--raise-rank`` raises mid-loop; ``--kill-rank`` SIGKILLs itself mid-loop while the others compute (no
-collective in flight: only the library can notice the death)."""
+collective in flight: only the library can notice the death); ``--gil-hold-rank`` holds the GIL in one C call
+for ``--gil-hold-s`` seconds mid-loop (alive and healthy, but no Python thread of it can run)."""
 
 import argparse
 import os
@@ -19,6 +20,8 @@ def main() -> None:
     ap.add_argument("--stop-rank", type=int, default=-1)
     ap.add_argument("--raise-rank", type=int, default=-1)
     ap.add_argument("--kill-rank", type=int, default=-1)
+    ap.add_argument("--gil-hold-rank", type=int, default=-1)
+    ap.add_argument("--gil-hold-s", type=int, default=8)
     ap.add_argument("--iters", type=int, default=400)
     ap.add_argument("--peer-timeout", type=float, default=3.0)
     ap.add_argument("--timeout", type=float, default=600.0, help="start(timeout_s=): shm waits + process groups")
@@ -30,6 +33,10 @@ def main() -> None:
         for i in range(args.iters):
             if i == 10 and env.rank == args.stop_rank:
                 os.kill(os.getpid(), signal.SIGSTOP)
+            if i == 10 and env.rank == args.gil_hold_rank:
+                import ctypes
+
+                ctypes.PyDLL(None).sleep(args.gil_hold_s)  # a PyDLL call keeps the GIL for its whole duration
             if i == 10 and env.rank == args.raise_rank:
                 raise RuntimeError("abort_rank: injected failure")
             if i == 10 and args.kill_rank >= 0:

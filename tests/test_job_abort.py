@@ -36,8 +36,10 @@ def _launch_plain(world: int, argv: list[str], env: dict) -> list[subprocess.Pop
     for r in range(world):
         e = dict(env, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
                  MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        # own session per rank: _kill_all ends the rank's helpers too (producers, death watch), which hold
+        # its output pipes
         procs.append(subprocess.Popen([sys.executable, *argv], env=e, stdout=subprocess.PIPE,
-                                      stderr=subprocess.PIPE, text=True))
+                                      stderr=subprocess.PIPE, text=True, start_new_session=True))
     return procs
 
 
@@ -49,11 +51,24 @@ def _wait_all(procs, timeout_s: float) -> tuple[list[int | None], float]:
     return codes, time.monotonic() - t0
 
 
+def _communicate(p):
+    """The rank's (stdout, stderr) once it has exited; a helper of the rank still holding its pipes after 30 s
+    (on a loaded host, a death watch still importing) is killed with the rank's session."""
+    try:
+        return p.communicate(timeout=30)
+    except subprocess.TimeoutExpired:
+        try:
+            os.killpg(p.pid, signal.SIGKILL)
+        except ProcessLookupError:
+            pass
+        return p.communicate(timeout=30)
+
+
 def _kill_all(procs):
     for p in procs:
         if p.poll() is None:
             p.kill()
-        p.communicate(timeout=30)
+        _communicate(p)
 
 
 # ---------------------------------------------------------------- in-process unit tests
@@ -118,7 +133,7 @@ def test_raise_in_window_aborts_every_rank_plain_launch():
     procs = _launch_plain(4, BENCH + ["--gpus", "4"], _base_env(DDL_FAULT_RANK="2:3"))
     try:
         codes, took = _wait_all(procs, 150)
-        errs = [p.communicate(timeout=30)[1] for p in procs]
+        errs = [_communicate(p)[1] for p in procs]
     finally:
         _kill_all(procs)
     assert codes[2] == 1, errs[2][-2000:]
@@ -182,7 +197,7 @@ def test_killed_rank_ends_the_job_at_once():
     procs = _launch_plain(3, [script, "--kill-rank", "1", "--peer-timeout", "60"], _base_env())
     try:
         codes, took = _wait_all(procs, 150)
-        errs = [p.communicate(timeout=30)[1] for p in procs]
+        errs = [_communicate(p)[1] for p in procs]
     finally:
         _kill_all(procs)
     assert codes[1] == -signal.SIGKILL, codes
@@ -194,13 +209,30 @@ def test_killed_rank_ends_the_job_at_once():
 
 
 @pytest.mark.timeout(200)
+def test_gil_holding_rank_is_not_declared_dead():
+    """Rank 1 holds the GIL for 8 s in one C call, with peer_timeout_s = 3 s: its Python threads cannot run,
+    but it is alive -- the heartbeat comes from its death-watch process (which checks that the rank exists
+    and is not stopped), so the job is not aborted and every rank finishes."""
+    script = os.path.join(REPO, "tests", "abort_rank.py")
+    procs = _launch_plain(3, [script, "--gil-hold-rank", "1", "--gil-hold-s", "8", "--iters", "40",
+                              "--peer-timeout", "3"], _base_env())
+    try:
+        codes, _ = _wait_all(procs, 150)
+        outs = [_communicate(p) for p in procs]
+    finally:
+        _kill_all(procs)
+    assert codes == [0, 0, 0], (codes, [o[1][-1500:] for o in outs])
+    assert all(f"rank {r} done" in outs[r][0] for r in range(3))
+
+
+@pytest.mark.timeout(200)
 def test_clean_run_exits_zero_with_watchdog():
     """No fault: every rank finishes, the watchdog never fires (ranks finish at different times)."""
     script = os.path.join(REPO, "tests", "abort_rank.py")
     procs = _launch_plain(3, [script, "--iters", "60", "--peer-timeout", "2"], _base_env())
     try:
         codes, _ = _wait_all(procs, 150)
-        outs = [p.communicate(timeout=30) for p in procs]
+        outs = [_communicate(p) for p in procs]
     finally:
         _kill_all(procs)
     assert codes == [0, 0, 0], [o[1][-1500:] for o in outs]
