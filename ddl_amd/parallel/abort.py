@@ -186,7 +186,8 @@ class JobWatchdog:
                     elif v != last_val:
                         last_val, last_change = v, time.monotonic()
                     elif time.monotonic() - last_change > self.peer_timeout_s:
-                        msg = f"no heartbeat from rank {target} for {self.peer_timeout_s:.0f}s (stopped, frozen or lost)"
+                        msg = (f"no heartbeat from rank {target} for {self.peer_timeout_s:.0f}s "
+                               "(stopped, frozen or lost)")
                         self.abort(msg)
                         return self._fire(f"rank {self.rank}: {msg}")
             except Exception as e:  # store unreachable: its host rank (or the agent) is gone
