@@ -19,9 +19,9 @@
 // global memory: 48 one-byte VMEM instructions per lane for 4 uint8 pixels,
 // which PMC showed to be memory-instruction-issue bound (SQ_WAIT_INST_ANY
 // ~2.6x the active cycles, archive/profiles/r1_augment/). Consecutive lanes write
-// consecutive output pixels of each channel plane (8 B / 16 B stores,
-// coalesced). A geometry whose band does not fit the LDS budget runs the same
-// kernel with the taps read from global memory.
+// consecutive output pixels of each channel plane (a wave store covers 128 B of
+// bf16 / 256 B of f32). A geometry whose band does not fit the LDS budget runs
+// the same kernel with the taps read from global memory.
 #include <algorithm>
 
 #include "common.h"
@@ -181,82 +181,94 @@ __device__ __forceinline__ void resample_band(void* __restrict__ dst, int64_t im
   }
 }
 
-// Fast form of resample_band over an LDS band whose rows all start at the same
-// offset `head` within their 16 B chunk (row pitch and plane size multiples of
-// 16 B: every standard image geometry) and whose output rows are a multiple of
-// kPx wide. A thread's kPx pixels then share one output row, so the vertical
-// coordinate and both source-row offsets are computed once instead of per
-// pixel, the horizontal offsets once per pixel instead of per tap and channel,
-// and every tap is one add + one LDS read (PMC of the generic form: ~1960 VALU
-// instructions per wave, issue-stalled 44% of its cycles, archive/profiles/r1_augment_v2/).
-// Same float math in the same order as resample_band: bit-identical output.
+// Fast form of resample_band over an LDS band whose rows all start at the same offset `head` within their
+// 16 B chunk (row pitch and plane size multiples of 16 B: every standard image geometry). A wave covers 64
+// consecutive output columns of one output row per step, its 4 waves take every 4th row of the band.
+// The horizontal taps (x0, x1, weight) of a lane's columns are computed once per band and held in
+// registers (up to kColGroups groups of 64 columns); the vertical ones once per row and wave. A half-wave's
+// 32 lanes then read 32 consecutive output columns' taps: <= 32 * fx bytes of one LDS row (12 dwords at
+// fx = 1.43), so the byte reads no longer conflict on LDS banks (4 consecutive pixels per lane spanned
+// 128 * fx bytes: up to 2-way CHW, 4-way HWC). uint8 rows read tap x0 + 1 even at the crop's right edge,
+// with its weight zeroed there: v00 + (v01 - v00) * 0 == v00 exactly, as the clamped tap gives (a finite
+// garbage byte times zero), and the two taps of a row are one address with an immediate offset. Same
+// float math in the same order as resample_band: bit-identical output. Against the row-major form
+// (4 consecutive pixels per lane): 40.9 vs 44.0 us CHW, 38.4 vs 42.9 us HWC per 256-image batch
+// (profiles/r5_configs/rrc_cols.jsonl); what remains is VALU-bound (~16 VALU per output value, 4 of them
+// the byte -> float conversions of the taps).
+constexpr int kColGroups = 4;  // out_w <= 256 in one pass of the band's rows
+
 template <int OUT_BF16, typename Tin, int HWC, int NC>
-__device__ __forceinline__ void resample_band_rows(void* __restrict__ dst, int64_t img, const AugmentSpec& a,
+__device__ __forceinline__ void resample_band_cols(void* __restrict__ dst, int64_t img, const AugmentSpec& a,
                                                    const CropBox& b, int oy0, int oy1, const Affine& aff,
                                                    const uint8_t* __restrict__ lds, uint32_t head, uint32_t stride,
                                                    uint32_t nrows, int ylo) {
   constexpr uint32_t kSz = static_cast<uint32_t>(sizeof(Tin));
+  constexpr bool kEdgeByWeight = sizeof(Tin) == 1;  // garbage taps are finite only for uint8
+  constexpr int kWaves = kThreads / 64;
+  constexpr int kC = NC > 0 ? NC : kMaxAffineChannels;
   const int ow = a.out_w;
-  const int C = NC > 0 ? NC : a.channels;  // NC: channel count known at compile time (3), 0: runtime
+  const int C = NC > 0 ? NC : a.channels;
   const uint32_t cin = HWC ? static_cast<uint32_t>(C) : 1u;
   const uint32_t cstep = HWC ? kSz : nrows * stride;  // LDS bytes from one channel to the next
   const int64_t opix = static_cast<int64_t>(a.out_h) * ow;
-  const int n = (oy1 - oy0) * ow;
   const float fy = static_cast<float>(b.h) / a.out_h, fx = static_cast<float>(b.w) / a.out_w;
-  const FastDiv div_ow(static_cast<uint32_t>(ow));
-  for (int q0 = static_cast<int>(threadIdx.x) * kPx; q0 < n; q0 += kThreads * kPx) {
-    const int r = static_cast<int>(div_ow.div(static_cast<uint32_t>(q0)));
-    const int ox0 = q0 - r * ow;
-    const float sy = src_coord(oy0 + r, fy);
-    const int y0 = min(static_cast<int>(sy), b.h - 1);
-    const int y1 = y0 + (y0 < b.h - 1 ? 1 : 0);
-    const float wy = sy - static_cast<float>(y0);
-    const uint32_t ra = static_cast<uint32_t>(y0 - ylo) * stride + head;
-    const uint32_t rb = static_cast<uint32_t>(y1 - ylo) * stride + head;
-    uint32_t xa[kPx], xb[kPx];
-    float wx[kPx];
+  const int lane = static_cast<int>(threadIdx.x & 63u);
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  const int64_t img_o = img * C * opix;
+  for (int cg0 = 0; cg0 < ow; cg0 += 64 * kColGroups) {
+    const int ng = min(kColGroups, (ow - cg0 + 63) / 64);  // uniform
+    uint32_t xa[kColGroups], xb[kColGroups];
+    float wx[kColGroups];
 #pragma unroll
-    for (int k = 0; k < kPx; ++k) {
-      int ox = ox0 + k;
-      if (b.flip) ox = ow - 1 - ox;
-      const float sx = src_coord(ox, fx);
+    for (int g = 0; g < kColGroups; ++g) {
+      int sxo = min(cg0 + 64 * g + lane, ow - 1);
+      if (b.flip) sxo = ow - 1 - sxo;
+      const float sx = src_coord(sxo, fx);
       const int x0 = min(static_cast<int>(sx), b.w - 1);
-      const int x1 = x0 + (x0 < b.w - 1 ? 1 : 0);
-      wx[k] = sx - static_cast<float>(x0);
-      xa[k] = static_cast<uint32_t>(x0) * cin * kSz;
-      xb[k] = static_cast<uint32_t>(x1) * cin * kSz;
+      const bool edge = x0 >= b.w - 1;
+      wx[g] = kEdgeByWeight && edge ? 0.f : sx - static_cast<float>(x0);
+      xa[g] = static_cast<uint32_t>(x0) * cin * kSz + head;
+      xb[g] = kEdgeByWeight ? xa[g] + cin * kSz : static_cast<uint32_t>(x0 + (edge ? 0 : 1)) * cin * kSz + head;
     }
-    const int64_t o = img * C * opix + static_cast<int64_t>(oy0) * ow + q0;
-    for (int c = 0; c < C; ++c) {  // fully unrolled by the compiler when NC > 0
-      const uint32_t cb = static_cast<uint32_t>(c) * cstep;
-      const uint8_t* la = lds + (cb + ra);
-      const uint8_t* lb = lds + (cb + rb);
-      float v00[kPx], v01[kPx], v10[kPx], v11[kPx];
+    for (int r = oy0 + wave; r < oy1; r += kWaves) {  // wave-uniform
+      const float sy = src_coord(r, fy);
+      const int y0 = min(static_cast<int>(sy), b.h - 1);
+      const int y1 = y0 + (y0 < b.h - 1 ? 1 : 0);
+      const float wy = sy - static_cast<float>(y0);
+      const uint32_t ra = static_cast<uint32_t>(y0 - ylo) * stride;
+      const uint32_t rb = static_cast<uint32_t>(y1 - ylo) * stride;
+      const int64_t orow = img_o + static_cast<int64_t>(r) * ow + cg0 + lane;
 #pragma unroll
-      for (int k = 0; k < kPx; ++k) {  // all 4 * kPx taps issued before any use
-        v00[k] = ld(reinterpret_cast<const Tin*>(la + xa[k]));
-        v01[k] = ld(reinterpret_cast<const Tin*>(la + xb[k]));
-        v10[k] = ld(reinterpret_cast<const Tin*>(lb + xa[k]));
-        v11[k] = ld(reinterpret_cast<const Tin*>(lb + xb[k]));
-      }
-      float v[kPx];
+      for (int g = 0; g < kColGroups; ++g) {
+        if (g >= ng) break;
+        float v[kC];
 #pragma unroll
-      for (int k = 0; k < kPx; ++k) {
-        const float top = v00[k] + (v01[k] - v00[k]) * wx[k];
-        const float bot = v10[k] + (v11[k] - v10[k]) * wx[k];
-        v[k] = top + (bot - top) * wy;
-      }
-      if (aff.enabled) {  // kernel-uniform
-        const float sc = aff.scale[c], bi = aff.bias[c];
+        for (int c = 0; c < kC; ++c) {  // all taps of all channels issued before any store
+          if (NC == 0 && c >= C) break;
+          const uint8_t* la = lds + (static_cast<uint32_t>(c) * cstep + ra);
+          const uint8_t* lb = lds + (static_cast<uint32_t>(c) * cstep + rb);
+          const float v00 = ld(reinterpret_cast<const Tin*>(la + xa[g]));
+          const float v01 = ld(reinterpret_cast<const Tin*>(la + xb[g]));
+          const float v10 = ld(reinterpret_cast<const Tin*>(lb + xa[g]));
+          const float v11 = ld(reinterpret_cast<const Tin*>(lb + xb[g]));
+          const float top = v00 + (v01 - v00) * wx[g];
+          const float bot = v10 + (v11 - v10) * wx[g];
+          v[c] = top + (bot - top) * wy;
+        }
+        if (cg0 + 64 * g + lane < ow) {
+          const int64_t o = orow + 64 * g;
 #pragma unroll
-        for (int k = 0; k < kPx; ++k) v[k] = fmaf(v[k], sc, bi);
-      }
-      const int64_t oc = o + static_cast<int64_t>(c) * opix;
-      if constexpr (OUT_BF16) {
-        *reinterpret_cast<uint2*>(static_cast<uint16_t*>(dst) + oc) =
-            make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-      } else {
-        *reinterpret_cast<float4*>(static_cast<float*>(dst) + oc) = make_float4(v[0], v[1], v[2], v[3]);
+          for (int c = 0; c < kC; ++c) {
+            if (NC == 0 && c >= C) break;
+            // uint8 taps give v >= +0, and fma(v, 1, 0) == v for those: no per-element select
+            const float y = kEdgeByWeight ? fmaf(v[c], aff.enabled ? aff.scale[c] : 1.f, aff.enabled ? aff.bias[c] : 0.f)
+                                          : (aff.enabled ? fmaf(v[c], aff.scale[c], aff.bias[c]) : v[c]);
+            if constexpr (OUT_BF16)
+              static_cast<uint16_t*>(dst)[o + static_cast<int64_t>(c) * opix] = f32_to_bf16_bits(y);
+            else
+              static_cast<float*>(dst)[o + static_cast<int64_t>(c) * opix] = y;
+          }
+        }
       }
     }
   }
@@ -344,12 +356,12 @@ __global__ void __launch_bounds__(kThreads) rrc_band_kernel(void* __restrict__ d
   // low bits of the per-row global addresses (mod 2^32 is enough for & 15)
   const uint32_t base_lo = static_cast<uint32_t>(band_base);
   const uint32_t plane_lo = static_cast<uint32_t>(plane_b), pitch_lo = static_cast<uint32_t>(pitch_b);
-  if ((pitch_lo & 15u) == 0 && (planes == 1 || (plane_lo & 15u) == 0) && (a.out_w % kPx) == 0) {
+  if ((pitch_lo & 15u) == 0 && (planes == 1 || (plane_lo & 15u) == 0)) {
     // every LDS row starts `base_lo & 15` bytes into its first chunk (kernel-uniform branch)
     if (a.channels == 3)
-      resample_band_rows<OUT_BF16, Tin, HWC, 3>(dst, img, a, b, oy0, oy1, aff, lds, base_lo & 15u, stride, nrows, ylo);
+      resample_band_cols<OUT_BF16, Tin, HWC, 3>(dst, img, a, b, oy0, oy1, aff, lds, base_lo & 15u, stride, nrows, ylo);
     else
-      resample_band_rows<OUT_BF16, Tin, HWC, 0>(dst, img, a, b, oy0, oy1, aff, lds, base_lo & 15u, stride, nrows, ylo);
+      resample_band_cols<OUT_BF16, Tin, HWC, 0>(dst, img, a, b, oy0, oy1, aff, lds, base_lo & 15u, stride, nrows, ylo);
     return;
   }
   resample_band<OUT_BF16>(dst, img, a, b, oy0, oy1, aff, [&](int c, int y, int x) {
