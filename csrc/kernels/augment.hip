@@ -182,20 +182,24 @@ __device__ __forceinline__ void resample_band(void* __restrict__ dst, int64_t im
 }
 
 // Fast form of resample_band over an LDS band whose rows all start at the same offset `head` within their
-// 16 B chunk (row pitch and plane size multiples of 16 B: every standard image geometry). A wave covers 64
-// consecutive output columns of one output row per step, its 4 waves take every 4th row of the band.
-// The horizontal taps (x0, x1, weight) of a lane's columns are computed once per band and held in
-// registers (up to kColGroups groups of 64 columns); the vertical ones once per row and wave. A half-wave's
-// 32 lanes then read 32 consecutive output columns' taps: <= 32 * fx bytes of one LDS row (12 dwords at
-// fx = 1.43), so the byte reads no longer conflict on LDS banks (4 consecutive pixels per lane spanned
-// 128 * fx bytes: up to 2-way CHW, 4-way HWC). uint8 rows read tap x0 + 1 even at the crop's right edge,
-// with its weight zeroed there: v00 + (v01 - v00) * 0 == v00 exactly, as the clamped tap gives (a finite
-// garbage byte times zero), and the two taps of a row are one address with an immediate offset. Same
-// float math in the same order as resample_band: bit-identical output. Against the row-major form
-// (4 consecutive pixels per lane): 40.9 vs 44.0 us CHW, 38.4 vs 42.9 us HWC per 256-image batch
-// (profiles/r5_configs/rrc_cols.jsonl); what remains is VALU-bound (~16 VALU per output value, 4 of them
-// the byte -> float conversions of the taps).
-constexpr int kColGroups = 4;  // out_w <= 256 in one pass of the band's rows
+// 16 B chunk (row pitch and plane size multiples of 16 B: every standard image geometry). A wave covers
+// 64 * kCpl consecutive output columns of one output row per step (kCpl adjacent columns per lane), its 4
+// waves take every 4th row of the band. The horizontal taps (x0, x1, weight) of a lane's columns are
+// computed once per band and held in registers (kColGroups groups: out_w <= 256 in one pass); the vertical
+// ones once per row and wave. A half-wave's byte taps then span 32 * kCpl * fx bytes of one LDS row
+// (23 dwords at fx = 1.43: no bank conflicts for CHW rows; the row-major form's 4 pixels per lane spanned
+// 128 * fx bytes, up to 2-way CHW / 4-way HWC), and a lane stores its kCpl values of a channel in one
+// 4 B (bf16) / 8 B (f32) store. Against the row-major form on one box: 41.1 vs 44.5 us (CHW), 38.8 vs
+// 44.4 us (HWC) per 256-image batch; the HBM-resident loader with augmentation, whose consumer kernel runs
+// next to it, unchanged (4.78-4.81M vs 4.68-4.89M samples/s). One column per lane (2 B stores) was as fast
+// in isolation but 4.5% slower in that loader; 4 per lane doubled the CHW time (profiles/r5_configs/).
+// uint8 rows read tap x0 + 1 even at the crop's right edge, with its weight zeroed there:
+// v00 + (v01 - v00) * 0 == v00 exactly, as the clamped tap gives (a finite garbage byte times zero), and
+// the two taps of a row are one address with an immediate offset. Same float math in the same order as
+// resample_band: bit-identical output.
+constexpr int kCpl = 2;        // adjacent output columns per lane
+constexpr int kColGroups = 2;  // groups of 64 * kCpl columns held in registers: out_w <= 256 per pass
+static_assert(kCpl == 2 || kCpl == 4, "the vector stores below pack 2 or 4 values");
 
 template <int OUT_BF16, typename Tin, int HWC, int NC>
 __device__ __forceinline__ void resample_band_cols(void* __restrict__ dst, int64_t img, const AugmentSpec& a,
@@ -205,6 +209,7 @@ __device__ __forceinline__ void resample_band_cols(void* __restrict__ dst, int64
   constexpr uint32_t kSz = static_cast<uint32_t>(sizeof(Tin));
   constexpr bool kEdgeByWeight = sizeof(Tin) == 1;  // garbage taps are finite only for uint8
   constexpr int kWaves = kThreads / 64;
+  constexpr int kGw = 64 * kCpl;  // columns per group
   constexpr int kC = NC > 0 ? NC : kMaxAffineChannels;
   const int ow = a.out_w;
   const int C = NC > 0 ? NC : a.channels;
@@ -215,20 +220,25 @@ __device__ __forceinline__ void resample_band_cols(void* __restrict__ dst, int64
   const int lane = static_cast<int>(threadIdx.x & 63u);
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
   const int64_t img_o = img * C * opix;
-  for (int cg0 = 0; cg0 < ow; cg0 += 64 * kColGroups) {
-    const int ng = min(kColGroups, (ow - cg0 + 63) / 64);  // uniform
-    uint32_t xa[kColGroups], xb[kColGroups];
-    float wx[kColGroups];
+  const bool pair_stores = (ow % kCpl) == 0;  // every lane's first column then sits at an aligned offset
+  for (int cg0 = 0; cg0 < ow; cg0 += kGw * kColGroups) {
+    const int ng = min(kColGroups, (ow - cg0 + kGw - 1) / kGw);  // uniform
+    uint32_t xa[kColGroups][kCpl], xb[kColGroups][kCpl];
+    float wx[kColGroups][kCpl];
 #pragma unroll
     for (int g = 0; g < kColGroups; ++g) {
-      int sxo = min(cg0 + 64 * g + lane, ow - 1);
-      if (b.flip) sxo = ow - 1 - sxo;
-      const float sx = src_coord(sxo, fx);
-      const int x0 = min(static_cast<int>(sx), b.w - 1);
-      const bool edge = x0 >= b.w - 1;
-      wx[g] = kEdgeByWeight && edge ? 0.f : sx - static_cast<float>(x0);
-      xa[g] = static_cast<uint32_t>(x0) * cin * kSz + head;
-      xb[g] = kEdgeByWeight ? xa[g] + cin * kSz : static_cast<uint32_t>(x0 + (edge ? 0 : 1)) * cin * kSz + head;
+#pragma unroll
+      for (int j = 0; j < kCpl; ++j) {
+        int sxo = min(cg0 + kGw * g + kCpl * lane + j, ow - 1);
+        if (b.flip) sxo = ow - 1 - sxo;
+        const float sx = src_coord(sxo, fx);
+        const int x0 = min(static_cast<int>(sx), b.w - 1);
+        const bool edge = x0 >= b.w - 1;
+        wx[g][j] = kEdgeByWeight && edge ? 0.f : sx - static_cast<float>(x0);
+        xa[g][j] = static_cast<uint32_t>(x0) * cin * kSz + head;
+        xb[g][j] = kEdgeByWeight ? xa[g][j] + cin * kSz
+                                 : static_cast<uint32_t>(x0 + (edge ? 0 : 1)) * cin * kSz + head;
+      }
     }
     for (int r = oy0 + wave; r < oy1; r += kWaves) {  // wave-uniform
       const float sy = src_coord(r, fy);
@@ -237,36 +247,61 @@ __device__ __forceinline__ void resample_band_cols(void* __restrict__ dst, int64
       const float wy = sy - static_cast<float>(y0);
       const uint32_t ra = static_cast<uint32_t>(y0 - ylo) * stride;
       const uint32_t rb = static_cast<uint32_t>(y1 - ylo) * stride;
-      const int64_t orow = img_o + static_cast<int64_t>(r) * ow + cg0 + lane;
+      const int64_t orow = img_o + static_cast<int64_t>(r) * ow + cg0 + kCpl * lane;
 #pragma unroll
       for (int g = 0; g < kColGroups; ++g) {
         if (g >= ng) break;
-        float v[kC];
+        const int col = cg0 + kGw * g + kCpl * lane;  // this lane's first column
+        if (col >= ow) continue;
+        const int64_t o = orow + kGw * g;
+        float v[kC][kCpl];
 #pragma unroll
         for (int c = 0; c < kC; ++c) {  // all taps of all channels issued before any store
           if (NC == 0 && c >= C) break;
           const uint8_t* la = lds + (static_cast<uint32_t>(c) * cstep + ra);
           const uint8_t* lb = lds + (static_cast<uint32_t>(c) * cstep + rb);
-          const float v00 = ld(reinterpret_cast<const Tin*>(la + xa[g]));
-          const float v01 = ld(reinterpret_cast<const Tin*>(la + xb[g]));
-          const float v10 = ld(reinterpret_cast<const Tin*>(lb + xa[g]));
-          const float v11 = ld(reinterpret_cast<const Tin*>(lb + xb[g]));
-          const float top = v00 + (v01 - v00) * wx[g];
-          const float bot = v10 + (v11 - v10) * wx[g];
-          v[c] = top + (bot - top) * wy;
-        }
-        if (cg0 + 64 * g + lane < ow) {
-          const int64_t o = orow + 64 * g;
 #pragma unroll
-          for (int c = 0; c < kC; ++c) {
-            if (NC == 0 && c >= C) break;
-            // uint8 taps give v >= +0, and fma(v, 1, 0) == v for those: no per-element select
-            const float y = kEdgeByWeight ? fmaf(v[c], aff.enabled ? aff.scale[c] : 1.f, aff.enabled ? aff.bias[c] : 0.f)
-                                          : (aff.enabled ? fmaf(v[c], aff.scale[c], aff.bias[c]) : v[c]);
-            if constexpr (OUT_BF16)
-              static_cast<uint16_t*>(dst)[o + static_cast<int64_t>(c) * opix] = f32_to_bf16_bits(y);
-            else
-              static_cast<float*>(dst)[o + static_cast<int64_t>(c) * opix] = y;
+          for (int j = 0; j < kCpl; ++j) {
+            const float v00 = ld(reinterpret_cast<const Tin*>(la + xa[g][j]));
+            const float v01 = ld(reinterpret_cast<const Tin*>(la + xb[g][j]));
+            const float v10 = ld(reinterpret_cast<const Tin*>(lb + xa[g][j]));
+            const float v11 = ld(reinterpret_cast<const Tin*>(lb + xb[g][j]));
+            const float top = v00 + (v01 - v00) * wx[g][j];
+            const float bot = v10 + (v11 - v10) * wx[g][j];
+            v[c][j] = top + (bot - top) * wy;
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < kC; ++c) {
+          if (NC == 0 && c >= C) break;
+          float y[kCpl];
+#pragma unroll
+          for (int j = 0; j < kCpl; ++j)  // uint8 taps give v >= +0, and fma(v, 1, 0) == v for those
+            y[j] = kEdgeByWeight ? fmaf(v[c][j], aff.enabled ? aff.scale[c] : 1.f, aff.enabled ? aff.bias[c] : 0.f)
+                                 : (aff.enabled ? fmaf(v[c][j], aff.scale[c], aff.bias[c]) : v[c][j]);
+          const int64_t oc = o + static_cast<int64_t>(c) * opix;
+          if (pair_stores && col + kCpl <= ow) {
+            if constexpr (OUT_BF16) {
+              if constexpr (kCpl == 2)
+                *reinterpret_cast<uint32_t*>(static_cast<uint16_t*>(dst) + oc) = pack_bf16x2(y[0], y[1]);
+              else
+                *reinterpret_cast<uint2*>(static_cast<uint16_t*>(dst) + oc) =
+                    make_uint2(pack_bf16x2(y[0], y[1]), pack_bf16x2(y[2], y[3]));
+            } else {
+              if constexpr (kCpl == 2)
+                *reinterpret_cast<float2*>(static_cast<float*>(dst) + oc) = make_float2(y[0], y[1]);
+              else
+                *reinterpret_cast<float4*>(static_cast<float*>(dst) + oc) = make_float4(y[0], y[1], y[2], y[3]);
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < kCpl; ++j) {
+              if (col + j >= ow) break;
+              if constexpr (OUT_BF16)
+                static_cast<uint16_t*>(dst)[oc + j] = f32_to_bf16_bits(y[j]);
+              else
+                static_cast<float*>(dst)[oc + j] = y[j];
+            }
           }
         }
       }
