@@ -115,3 +115,43 @@ def test_bench_multirank_device_path(n, launch):
         assert r["dispatch"]["host_us_per_batch"]["get"] > 0
     assert out["config"]["dispatch"] == out["per_rank"][0]["dispatch"]["mode"]
     assert out["indexed"] and "error" not in out["indexed"] and out["indexed"]["value"] > 0
+
+
+@pytest.mark.timeout(240)
+def test_killed_rank_on_the_card_ends_the_job():
+    """Two ranks on the card streaming a device loader with the exchange on; rank 1 is SIGKILLed mid-epoch
+    (H2D copies, kernels and collectives in flight). Its death watch publishes the abort; rank 0 -- blocked
+    in or heading into the next exchange -- exits with the peer-abort status (or 1 if the collective's own
+    error reaches it first) within seconds, with no leftover processes."""
+    import signal
+    import time
+
+    from ddl_amd.parallel.abort import PEER_ABORT_EXIT
+
+    script = os.path.join(REPO, "tests", "abort_rank.py")
+    port = str(free_port())
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, PYTHONPATH=REPO, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2",
+                   LOCAL_WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=port, **GPU_GLOO)
+        procs.append(subprocess.Popen([sys.executable, script, "--gpu-loader", "--kill-rank", "1",
+                                       "--peer-timeout", "60"], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True, start_new_session=True))
+    t0 = time.monotonic()
+    try:
+        while time.monotonic() - t0 < 150 and any(p.poll() is None for p in procs):
+            time.sleep(0.1)
+        took = time.monotonic() - t0
+        codes = [p.poll() for p in procs]
+    finally:
+        for p in procs:
+            try:
+                os.killpg(p.pid, signal.SIGKILL)  # the rank and its helpers (producers, death watch)
+            except ProcessLookupError:
+                pass
+        outs = [p.communicate(timeout=30) for p in procs]
+    assert "killing itself mid-epoch on cuda" in outs[1][0], outs[1][1][-2000:]
+    assert codes[1] == -signal.SIGKILL, codes
+    assert codes[0] in (PEER_ABORT_EXIT, 1), (codes, outs[0][1][-2000:])
+    assert "died without a clean shutdown" in outs[0][1] or codes[0] == 1, outs[0][1][-2000:]
+    assert took < 120, took
