@@ -26,7 +26,7 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--n-samples", type=int, default=1000)
     ap.add_argument("--global-batch", type=int, default=100)
-    ap.add_argument("--epochs", type=int, default=20)
+    ap.add_argument("--epochs", type=int, default=100)
     ap.add_argument("--producers", type=int, default=2)
     a = ap.parse_args(argv)
     os.environ.setdefault("DDL_DEVICE", "cpu")
@@ -51,7 +51,9 @@ def main(argv=None):
             if not creator:
                 src = SharedArraySource(name, a.n_samples, shape, "float32")
             lb = a.global_batch // env.world_size
-            dl = ddl_amd.DistributedDataLoader(IndexedProducer(src, a.global_batch, seed=3), lb, conn, a.epochs,
+            # one epoch more than is timed: the loader shuts its producers down at the end of its last epoch,
+            # and that teardown (process exits) is not plumbing throughput
+            dl = ddl_amd.DistributedDataLoader(IndexedProducer(src, a.global_batch, seed=3), lb, conn, a.epochs + 1,
                                                mode="indexed", env=env, auto_mark=True)
             bpe = dl.windows_per_epoch
             exact = True

@@ -232,6 +232,7 @@ def producer_main(pipe, producer_index: int, consumer_pid: int, rank: int, world
     try:
         pusher = DataPusher(conn, rank_global=rank, world_size=world_size)
         pusher.push_data()
+        del pusher
     except ShutdownError:  # closed before any loader used this producer (e.g. an unused spare connection)
         logger.debug("producer %d: shut down before a loader used it", producer_index)
     except BaseException as e:  # report, then exit non-zero
@@ -239,3 +240,23 @@ def producer_main(pipe, producer_index: int, consumer_pid: int, rank: int, world
         conn.report_error(e)
         if not in_thread:
             raise SystemExit(1)
+    if not in_thread:
+        _exit_quickly()
+
+
+def _exit_quickly() -> None:
+    """End a producer process after its clean shutdown without the interpreter teardown: with torch loaded
+    that teardown (module and C++ static destructors) took ~0.8 s, which the consumer waited out at the end of
+    its last epoch (``connection.finalize`` joins the producers). The producer object has been released
+    already (its ``__del__``, and its files' close and flush, ran), and the ``atexit`` handlers run first
+    (logging flushes, the user's own handlers)."""
+    import atexit
+    import sys
+
+    atexit._run_exitfuncs()
+    for f in (sys.stdout, sys.stderr):
+        try:
+            f.flush()
+        except Exception:  # pragma: no cover - a closed stream
+            pass
+    os._exit(0)
