@@ -127,6 +127,30 @@ def test_watchdog_finished_peer_is_not_dead():
 
 # ---------------------------------------------------------------- multi-process
 @pytest.mark.timeout(200)
+def test_process_stopped_reads_the_state():
+    """The death watch beats only for a rank that is not stopped: /proc state T after SIGSTOP, not after SIGCONT;
+    a process that is gone is not 'stopped' (its death is the pipe's EOF)."""
+    from ddl_amd.parallel.abort import _process_stopped
+
+    p = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(60)"])
+    try:
+        assert not _process_stopped(p.pid)
+        os.kill(p.pid, signal.SIGSTOP)
+        t0 = time.monotonic()
+        while not _process_stopped(p.pid) and time.monotonic() - t0 < 5:
+            time.sleep(0.01)
+        assert _process_stopped(p.pid)
+        os.kill(p.pid, signal.SIGCONT)
+        t0 = time.monotonic()
+        while _process_stopped(p.pid) and time.monotonic() - t0 < 5:
+            time.sleep(0.01)
+        assert not _process_stopped(p.pid)
+    finally:
+        p.kill()
+        p.wait()
+    assert not _process_stopped(p.pid)
+
+
 def test_raise_in_window_aborts_every_rank_plain_launch():
     """gloo W=4, exchange on: rank 2 raises when its cursor enters window 3. Rank 2 exits 1, every
     other rank exits PEER_ABORT_EXIT within seconds (not the 600 s process-group timeout)."""
