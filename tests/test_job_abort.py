@@ -125,6 +125,38 @@ def test_watchdog_finished_peer_is_not_dead():
     a.stop()
 
 
+def test_watchdog_store_loss_is_an_abort():
+    """The rendezvous store's host died (its rank, or the agent): every store call fails; after a grace period
+    (a clean job end could have raced the final barrier) the watchdog exits with the peer-abort status."""
+    import torch.distributed as dist
+
+    class Dying:
+        def __init__(self):
+            self.inner, self.dead = dist.PrefixStore("t/", dist.HashStore()), False
+
+        def __getattr__(self, name):
+            fn = getattr(self.inner, name)
+
+            def call(*a, **kw):
+                if self.dead:
+                    raise RuntimeError("Connection reset by peer")
+                return fn(*a, **kw)
+
+            return call
+
+    store, fired = Dying(), {}
+    w = JobWatchdog(0, 2, poll_s=0.05, store=store, exit_fn=lambda code: fired.setdefault(0, code))
+    w.start()
+    try:
+        time.sleep(0.2)
+        assert fired == {}
+        store.dead = True
+        assert _until(lambda: 0 in fired, 5.0)
+        assert fired[0] == PEER_ABORT_EXIT and "store unreachable" in w.aborted
+    finally:
+        w.stop()
+
+
 # ---------------------------------------------------------------- multi-process
 @pytest.mark.timeout(200)
 def test_process_stopped_reads_the_state():
