@@ -41,3 +41,22 @@ class IdProducer(ProducerFunctionSkeleton):
 class FailingProducer(IdProducer):
     def on_init(self, *args, **kwargs):
         raise ValueError("boom in on_init")
+
+
+class AtexitProducer(IdProducer):
+    """IdProducer whose worker registers an atexit handler that writes ``path`` (the quick producer exit
+    must still run it) and keeps a file open, written but not flushed (released with the producer object)."""
+
+    def __init__(self, path, **kw):
+        super().__init__(**kw)
+        self.path = path
+
+    def on_init(self, *args, **kwargs):
+        import atexit
+
+        ret = super().on_init(*args, **kwargs)
+        idx = kwargs.get("producer_index", 0)
+        atexit.register(lambda: open(f"{self.path}.atexit{idx}", "w").write("ran"))
+        self._log = open(f"{self.path}.log{idx}", "w")
+        self._log.write("buffered")  # flushed only when the file object is released
+        return ret

@@ -285,6 +285,33 @@ def test_producer_preferred_slots(monkeypatch):
         dl.close()
 
 
+def test_producers_exit_quickly_but_run_their_cleanup(monkeypatch, tmp_path):
+    """Producer processes skip the interpreter teardown at their clean shutdown (os._exit after it): the
+    loader's last epoch no longer waits ~0.8 s per producer; their atexit handlers still run, and a file the
+    producer object held is flushed when the object is released; exit status 0."""
+    import time
+
+    from tests.helpers import AtexitProducer
+
+    monkeypatch.setenv("DDL_DEVICE", "cpu")
+    base = str(tmp_path / "p")
+    with ddl_amd.start(n_producers=2) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(AtexitProducer(base, n=64, width=6), 16, conn, 2, env=env,
+                                           auto_mark=True)
+        for _ in range(2):
+            for _b in dl:
+                pass
+        t0 = time.perf_counter()
+        dl.close()
+        took = time.perf_counter() - t0
+        procs = list(conn.processes)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    for i in range(2):
+        assert open(f"{base}.atexit{i}").read() == "ran"
+        assert open(f"{base}.log{i}").read() == "buffered"
+    assert took < 5.0
+
+
 def test_spare_connections_serve_later_loaders_and_unused_ones_exit_cleanly():
     """``start(spare_connections=)`` spawns more producer sets up front (before the GPU is touched): a second
     loader after the first runs on ``conn.spares[0]`` (its own producers, its own arena) and delivers every row
