@@ -276,16 +276,6 @@ def pressure_phase(args, env, dev, it, feed_per_rank: float, barrier, sync, dl=N
     return out
 
 
-def _quiet_gc() -> None:
-    """Before a timed region: collect now and move every object that exists into the permanent generation
-    (``gc.freeze``), so a full collection inside the region scans only what the region allocates -- a
-    multi-ms gen-2 pause over the setup's objects would otherwise land in a ~27 ms region. No work is skipped."""
-    import gc
-
-    gc.collect()
-    gc.freeze()
-
-
 def _timed_feed(args, env, it, acc, barrier, sync, label: str) -> tuple[float, float]:
     """Warmup, then exactly ``args.steps`` checksum-consumed batches bracketed by barrier + synchronize;
     (samples/s over all ranks from the max elapsed time, ms per step)."""
@@ -296,7 +286,6 @@ def _timed_feed(args, env, it, acc, barrier, sync, label: str) -> tuple[float, f
 
     for _ in range(args.warmup):
         acc.add(next(it))
-    _quiet_gc()
     barrier()
     t0 = time.perf_counter()
     with trace_range(label):
@@ -520,7 +509,6 @@ def main(argv=None) -> int:
         wait_prod0 = dl.stats().get("stager_wait_producer_s", 0.0)
         host_log = args.debug_log
         ticks = []
-        _quiet_gc()
         barrier()
         # the region's H2D work, on the GPU clock: events bracket the region on the (idle) compute stream, and
         # every window copy is timed on the device, so exactly the bytes that crossed PCIe inside the region
