@@ -276,9 +276,12 @@ def pressure_phase(args, env, dev, it, feed_per_rank: float, barrier, sync, dl=N
     return out
 
 
-def _timed_feed(args, env, it, acc, barrier, sync, label: str) -> tuple[float, float]:
+def _timed_feed(args, env, it, acc, barrier, sync, label: str, dl=None) -> tuple[float, float, dict]:
     """Warmup, then exactly ``args.steps`` checksum-consumed batches bracketed by barrier + synchronize;
-    (samples/s over all ranks from the max elapsed time, ms per step)."""
+    (samples/s over all ranks from the max elapsed time, ms per step, accounting). With ``dl`` (a loader that
+    stages windows of ``args.batch`` samples through the H2D stager, copy timing on) the rate is the smaller of
+    the delivered rate and the landed one -- the window bytes that crossed PCIe inside the region, on the device
+    clock, pro rata -- as for the headline: windows staged before the region opened do not count."""
     import torch
     import torch.distributed as dist
 
@@ -286,19 +289,41 @@ def _timed_feed(args, env, it, acc, barrier, sync, label: str) -> tuple[float, f
 
     for _ in range(args.warmup):
         acc.add(next(it))
+    stager = getattr(dl, "_stager", None) if dl is not None else None
+    ev0 = ev1 = None
+    if stager is not None:
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
     t0 = time.perf_counter()
+    if ev0 is not None:
+        ev0.record()
     with trace_range(label):
         for _ in range(args.steps):
             acc.add(next(it))
         sync()
     el = time.perf_counter() - t0
+    if ev1 is not None:
+        ev1.record()
+    landed = None
+    if stager is not None:
+        pro = stager.bytes_in_interval(ev0, ev1)
+        landed = pro["windows"] * args.batch if pro.get("ok") else None
     barrier()
+    t = torch.tensor([el, -1.0 if landed is None else landed], dtype=torch.float64)
     if env.world_size > 1:
-        t = torch.tensor([el], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=env.control_group)
-        el = float(t.item())
-    return args.batch * args.steps * env.world_size / el, 1000 * el / args.steps
+        parts = [torch.empty_like(t) for _ in range(env.world_size)]
+        dist.all_gather(parts, t, group=env.control_group)
+    else:
+        parts = [t]
+    el = max(float(p[0]) for p in parts)
+    delivered = args.batch * args.steps * env.world_size / el
+    info = {"delivered_samples_per_s": round(delivered, 1)}
+    rate = delivered
+    if all(float(p[1]) >= 0 for p in parts):
+        landed_rate = sum(float(p[1]) for p in parts) / el
+        info["landed_samples_per_s"] = round(landed_rate, 1)
+        rate = min(delivered, landed_rate)
+    return rate, 1000 * el / args.steps, info
 
 
 def _idle_behind_step(args, env, dev, it, barrier, sync) -> float | None:
@@ -384,14 +409,15 @@ def indexed_phase(args, env, dev, barrier, sync, spare=None) -> dict:
             total = args.warmup + args.steps + (max(1, args.warmup // 2) + idle_steps if idle_steps else 0)
             dl = ddl_amd.DistributedDataLoader(
                 IndexedProducer(src, gb, seed=args.seed, host_threads=args.index_threads), args.batch, spare,
-                math.ceil(total / bpe) + 2, mode="indexed", env=env, device=dev, n_slots=2, auto_mark=True)
+                math.ceil(total / bpe) + 2, mode="indexed", env=env, device=dev, n_slots=2, auto_mark=True,
+                copy_timing=True)  # the landed-bytes accounting of the timed region
             it = forever(dl)
             w0 = dl.stats().get("stager_wait_producer_s", 0.0)
-            rate, ms = _timed_feed(args, env, it, acc, barrier, sync, "bench.indexed")
+            rate, ms, acct = _timed_feed(args, env, it, acc, barrier, sync, "bench.indexed", dl=dl)
             st = dl.stats()
             out.update({"path": f"producers (IndexedProducer: host gather in the epoch order, 2 slots x "
                                 f"{args.index_threads} threads, direct-DMA staging)",
-                        "value": round(rate, 1), "ms_per_step": round(ms, 4),
+                        "value": round(rate, 1), "ms_per_step": round(ms, 4), **acct,
                         "h2d_direct_dma": bool(st.get("direct_dma", False)),
                         # the stager's waits for producers over warmup + timed steps (diagnostic)
                         "stager_wait_producer_s": round(st.get("stager_wait_producer_s", 0.0) - w0, 4),
@@ -402,7 +428,7 @@ def indexed_phase(args, env, dev, barrier, sync, spare=None) -> dict:
         zc = ZeroCopyLoader(src, args.batch * env.world_size, env, seed=args.seed, out_dtype=torch.bfloat16,
                             device=dev, prefault=not args.index_no_prefault)
         it = forever(zc)
-        rate, ms = _timed_feed(args, env, it, acc, barrier, sync, "bench.indexed_zero_copy")
+        rate, ms, _ = _timed_feed(args, env, it, acc, barrier, sync, "bench.indexed_zero_copy")
         zres = {"path": "zero-copy gfx950 gather over PCIe from the pinned, device-mapped source",
                 "value": round(rate, 1), "ms_per_step": round(ms, 4), "prefault_s": zc.stats().get("prefault_s")}
         if spare is None:
