@@ -410,7 +410,9 @@ def indexed_phase(args, env, dev, barrier, sync, spare=None) -> dict:
             dl = ddl_amd.DistributedDataLoader(
                 IndexedProducer(src, gb, seed=args.seed, host_threads=args.index_threads), args.batch, spare,
                 math.ceil(total / bpe) + 2, mode="indexed", env=env, device=dev, n_slots=2, auto_mark=True,
-                copy_timing=True)  # the landed-bytes accounting of the timed region
+                copy_timing=True,  # the landed-bytes accounting of the timed region
+                copy_batches=False)  # views, as the headline's batches are: the checksum reads them in stream
+            # order before the window's release (auto_mark would otherwise copy every batch, 77 MB D2D each)
             it = forever(dl)
             w0 = dl.stats().get("stager_wait_producer_s", 0.0)
             rate, ms, acct = _timed_feed(args, env, it, acc, barrier, sync, "bench.indexed", dl=dl)
