@@ -25,7 +25,8 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kUnroll = 4;
 
 // ------------------------------ raw byte moves ------------------------------
-// Store policy of the raw row moves: plain stores, which leave the batch in the 256 MB MALL for a consumer
+// Load policy: non-temporal loads of the gathered source rows (below). Store policy of the raw row moves:
+// plain stores, which leave the batch in the 256 MB MALL for a consumer
 // that reads it right away. Streaming stores measured +7.8% on the isolated 1024-image gather (5.39 vs 5.00
 // TB/s) but 5.49M vs 5.74M samples/s in the HBM-resident loader, which reads the batch right after it is
 // written (profiles/r4_second/resident_*.json): plain stores only.
@@ -51,7 +52,11 @@ __global__ void __launch_bounds__(kThreads) move_rows_chunked(uint8_t* __restric
 #pragma unroll
   for (int k = 0; k < kUnroll; ++k) {
     const int64_t u = u0 + k * kThreads;
-    if (u < units_per_row) v[k] = s[u];
+    // gather: the source rows stream through once (a shard far larger than the 256 MB MALL): non-temporal
+    // loads keep them from evicting the batch just written, which the consumer reads next (the HBM-resident
+    // loader: bf16 5.50 -> 6.04M samples/s, kernel 5.00 -> 5.20 TB/s; profiles/r5_configs/nt_loads/).
+    // scatter reads a contiguous receive buffer: plain loads (non-temporal there: 5.01 -> 4.91 TB/s)
+    if (u < units_per_row) v[k] = scatter ? s[u] : __builtin_nontemporal_load(s + u);
   }
 #pragma unroll
   for (int k = 0; k < kUnroll; ++k) {
@@ -252,7 +257,13 @@ __global__ void __launch_bounds__(kThreads) convert_u8_rows_chunked(Tout* __rest
 #pragma unroll
   for (int k = 0; k < kU8Loads; ++k) {
     const int64_t e = e0 + static_cast<int64_t>(k) * kThreads * 8;
-    raw[k] = e < row_elems ? *reinterpret_cast<const uint2*>(s + e) : uint2{};
+    if (e < row_elems) {  // non-temporal, as in move_rows_chunked (uint8 resident loader 5.99 -> 6.21M samples/s)
+      typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+      const u32x2 t = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(s + e));
+      raw[k] = make_uint2(t.x, t.y);
+    } else {
+      raw[k] = uint2{};
+    }
   }
 #pragma unroll
   for (int k = 0; k < kU8Loads; ++k) {
