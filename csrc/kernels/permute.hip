@@ -31,7 +31,7 @@ constexpr int kUnroll = 4;
 // TB/s) but 5.49M vs 5.74M samples/s in the HBM-resident loader, which reads the batch right after it is
 // written (profiles/r4_second/resident_*.json): plain stores only.
 
-template <typename U>
+template <typename U, bool kNtLoads>
 __global__ void __launch_bounds__(kThreads) move_rows_chunked(uint8_t* __restrict__ dst,
                                                               const uint8_t* __restrict__ src,
                                                               int64_t units_per_row, int64_t chunks_per_row,
@@ -52,11 +52,17 @@ __global__ void __launch_bounds__(kThreads) move_rows_chunked(uint8_t* __restric
 #pragma unroll
   for (int k = 0; k < kUnroll; ++k) {
     const int64_t u = u0 + k * kThreads;
-    // gather: the source rows stream through once (a shard far larger than the 256 MB MALL): non-temporal
-    // loads keep them from evicting the batch just written, which the consumer reads next (the HBM-resident
-    // loader: bf16 5.50 -> 6.04M samples/s, kernel 5.00 -> 5.20 TB/s; profiles/r5_configs/nt_loads/).
-    // scatter reads a contiguous receive buffer: plain loads (non-temporal there: 5.01 -> 4.91 TB/s)
-    if (u < units_per_row) v[k] = scatter ? s[u] : __builtin_nontemporal_load(s + u);
+    // kNtLoads (gathers): the source rows stream through once (a shard far larger than the 256 MB MALL):
+    // non-temporal loads keep them from evicting the batch just written, which the consumer reads next (the
+    // HBM-resident loader: bf16 5.50 -> 6.04M samples/s, kernel 5.00 -> 5.20 TB/s; profiles/r5_configs/
+    // nt_loads/). Scatters read a contiguous receive buffer: plain loads (non-temporal there: 5.01 -> 4.91).
+    // A template flag, not a runtime select: the compiler merges `c ? s[u] : nt_load(s + u)` into one plain load.
+    if (u < units_per_row) {
+      if constexpr (kNtLoads)
+        v[k] = __builtin_nontemporal_load(s + u);
+      else
+        v[k] = s[u];
+    }
   }
 #pragma unroll
   for (int k = 0; k < kUnroll; ++k) {
@@ -318,7 +324,8 @@ void launch_move(void* dst, const void* src, int64_t n_rows, int64_t row_bytes, 
   const int64_t units = row_bytes / static_cast<int64_t>(sizeof(U));
   if (units >= kThreads) {
     const int64_t chunks = (units + kThreads * kUnroll - 1) / (kThreads * kUnroll);
-    hipLaunchKernelGGL(move_rows_chunked<U>, tile_grid(n_rows * chunks, max_blocks), dim3(kThreads), 0, st,
+    auto kernel = scatter ? move_rows_chunked<U, false> : move_rows_chunked<U, true>;
+    hipLaunchKernelGGL(kernel, tile_grid(n_rows * chunks, max_blocks), dim3(kThreads), 0, st,
                        static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), units, chunks, n_rows * chunks,
                        ri, scatter);
   } else {
