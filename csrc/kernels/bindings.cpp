@@ -576,17 +576,18 @@ PYBIND11_MODULE(_ddl_hip, m) {
       [](uintptr_t dst, int out_dt, uintptr_t src, int in_dt, int64_t n_rows, int64_t row_elems, int mode,
          uintptr_t idx, int64_t base, std::vector<uint64_t> keys, uint64_t n_domain, uint32_t half_bits,
          std::vector<float> scale, std::vector<float> bias, int64_t plane, bool scatter, uintptr_t stream,
-         int64_t max_blocks) {
+         int64_t max_blocks, bool host_src) {
         const ddl::RowIndex ri = make_index(mode, idx, base, keys, n_domain, half_bits);
         const ddl::Affine aff = make_affine(scale, bias, plane);
         check_rc(ddl::gather_rows(as_ptr<void>(dst), out_dt, as_ptr<const void>(src), in_dt, n_rows, row_elems, ri,
-                                  aff, scatter ? 1 : 0, max_blocks, as_stream(stream)),
+                                  aff, (scatter ? 1 : 0) | (host_src ? ddl::kHostSource : 0), max_blocks,
+                                  as_stream(stream)),
                  "gather_rows");
       },
       py::arg("dst"), py::arg("out_dt"), py::arg("src"), py::arg("in_dt"), py::arg("n_rows"), py::arg("row_elems"),
       py::arg("mode"), py::arg("idx"), py::arg("base"), py::arg("keys"), py::arg("n_domain"), py::arg("half_bits"),
       py::arg("scale"), py::arg("bias"), py::arg("plane"), py::arg("scatter"), py::arg("stream"),
-      py::arg("max_blocks") = 0);
+      py::arg("max_blocks") = 0, py::arg("host_src") = false);
   m.def(
       "feistel_indices",
       [](uintptr_t out, int64_t count, int64_t base, std::vector<uint64_t> keys, uint64_t n_domain,

@@ -13,8 +13,11 @@ namespace ddl {
 // permute.hip ---------------------------------------------------------------
 // dst[r, :] = cast(src[source_row(ri, r), :]) (scatter=0)
 // dst[source_row(ri, r), :] = src[r, :]       (scatter=1, same dtype only)
+// scatter | kHostSource: src is pinned, device-mapped host memory (a zero-copy gather): plain loads; device
+// sources are gathered with non-temporal loads (they stream through once; the fresh batch stays in the MALL)
 // max_blocks > 0 caps the grid (grid-stride over tiles), e.g. to keep a
 // zero-copy gather out of pinned host memory on a few CUs.
+constexpr int kHostSource = 2;
 int gather_rows(void* dst, int32_t out_dt, const void* src, int32_t in_dt, int64_t n_rows, int64_t row_elems,
                 const RowIndex& ri, const Affine& aff, int scatter, int64_t max_blocks, hipStream_t st);
 // out[i] = feistel_perm(base + i), i < count

@@ -246,7 +246,7 @@ __global__ void __launch_bounds__(kThreads) convert_rows_chunked(Tout* __restric
 // bytes in flight per CU (16 KB of loads per workgroup).
 constexpr int kU8Loads = 8;
 
-template <typename Tout>
+template <typename Tout, bool kNtLoads>
 __global__ void __launch_bounds__(kThreads) convert_u8_rows_chunked(Tout* __restrict__ dst,
                                                                     const uint8_t* __restrict__ src, int64_t row_elems,
                                                                     int64_t chunks_per_row, int64_t n_tiles, RowIndex ri,
@@ -263,9 +263,10 @@ __global__ void __launch_bounds__(kThreads) convert_u8_rows_chunked(Tout* __rest
 #pragma unroll
   for (int k = 0; k < kU8Loads; ++k) {
     const int64_t e = e0 + static_cast<int64_t>(k) * kThreads * 8;
-    if (e < row_elems) {  // non-temporal, as in move_rows_chunked (uint8 resident loader 5.99 -> 6.21M samples/s)
-      typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-      const u32x2 t = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(s + e));
+    if (e < row_elems) {  // non-temporal for device sources, as in move_rows_chunked (uint8 resident loader
+      typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));  // 5.99 -> 6.21M samples/s)
+      const u32x2 t = kNtLoads ? __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(s + e))
+                               : *reinterpret_cast<const u32x2*>(s + e);
       raw[k] = make_uint2(t.x, t.y);
     } else {
       raw[k] = uint2{};
@@ -320,11 +321,11 @@ int flat_grid_capped(int64_t work, int64_t max_blocks) {
 
 template <typename U>
 void launch_move(void* dst, const void* src, int64_t n_rows, int64_t row_bytes, const RowIndex& ri, int scatter,
-                 int64_t max_blocks, hipStream_t st) {
+                 bool nt_loads, int64_t max_blocks, hipStream_t st) {
   const int64_t units = row_bytes / static_cast<int64_t>(sizeof(U));
   if (units >= kThreads) {
     const int64_t chunks = (units + kThreads * kUnroll - 1) / (kThreads * kUnroll);
-    auto kernel = scatter ? move_rows_chunked<U, false> : move_rows_chunked<U, true>;
+    auto kernel = nt_loads ? move_rows_chunked<U, true> : move_rows_chunked<U, false>;
     hipLaunchKernelGGL(kernel, tile_grid(n_rows * chunks, max_blocks), dim3(kThreads), 0, st,
                        static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), units, chunks, n_rows * chunks,
                        ri, scatter);
@@ -337,11 +338,12 @@ void launch_move(void* dst, const void* src, int64_t n_rows, int64_t row_bytes, 
 
 template <typename Tin, typename Tout>
 void launch_convert(void* dst, const void* src, int64_t n_rows, int64_t row_elems, const RowIndex& ri, const Affine& aff,
-                    bool vec_ok, int64_t max_blocks, hipStream_t st) {
+                    bool vec_ok, bool nt_loads, int64_t max_blocks, hipStream_t st) {
   if constexpr (sizeof(Tin) == 1) {
     if (vec_ok && row_elems >= kThreads * 8) {  // vec_ok: row_elems % 8 == 0, 16 B aligned
       const int64_t chunks = (row_elems + kThreads * kU8Loads * 8 - 1) / (kThreads * kU8Loads * 8);
-      hipLaunchKernelGGL((convert_u8_rows_chunked<Tout>), tile_grid(n_rows * chunks, max_blocks), dim3(kThreads), 0,
+      auto kernel = nt_loads ? convert_u8_rows_chunked<Tout, true> : convert_u8_rows_chunked<Tout, false>;
+      hipLaunchKernelGGL(kernel, tile_grid(n_rows * chunks, max_blocks), dim3(kThreads), 0,
                          st, static_cast<Tout*>(dst), static_cast<const uint8_t*>(src), row_elems, chunks,
                          n_rows * chunks, ri, aff);
       return;
@@ -361,11 +363,11 @@ void launch_convert(void* dst, const void* src, int64_t n_rows, int64_t row_elem
 
 template <typename Tin>
 int dispatch_out(int32_t out_dt, void* dst, const void* src, int64_t n_rows, int64_t row_elems, const RowIndex& ri,
-                 const Affine& aff, bool vec_ok, int64_t mb, hipStream_t st) {
+                 const Affine& aff, bool vec_ok, bool nt, int64_t mb, hipStream_t st) {
   switch (out_dt) {
-    case kBF16: launch_convert<Tin, BF16Tag>(dst, src, n_rows, row_elems, ri, aff, vec_ok, mb, st); return 0;
-    case kF16: launch_convert<Tin, F16Tag>(dst, src, n_rows, row_elems, ri, aff, vec_ok, mb, st); return 0;
-    case kF32: launch_convert<Tin, float>(dst, src, n_rows, row_elems, ri, aff, vec_ok, mb, st); return 0;
+    case kBF16: launch_convert<Tin, BF16Tag>(dst, src, n_rows, row_elems, ri, aff, vec_ok, nt, mb, st); return 0;
+    case kF16: launch_convert<Tin, F16Tag>(dst, src, n_rows, row_elems, ri, aff, vec_ok, nt, mb, st); return 0;
+    case kF32: launch_convert<Tin, float>(dst, src, n_rows, row_elems, ri, aff, vec_ok, nt, mb, st); return 0;
   }
   return -1;
 }
@@ -380,8 +382,10 @@ __global__ void __launch_bounds__(kThreads) feistel_fill(int64_t* __restrict__ o
 }  // namespace
 
 int gather_rows(void* dst, int32_t out_dt, const void* src, int32_t in_dt, int64_t n_rows, int64_t row_elems,
-                const RowIndex& ri, const Affine& aff, int scatter, int64_t max_blocks, hipStream_t st) {
+                const RowIndex& ri, const Affine& aff, int flags, int64_t max_blocks, hipStream_t st) {
   if (n_rows <= 0 || row_elems <= 0) return 0;
+  const int scatter = flags & 1;
+  const bool nt = (flags & (1 | kHostSource)) == 0;  // a device-source gather: non-temporal source loads
   // the chunked kernels index tiles and in-row elements with 32-bit arithmetic
   if (n_rows >= (int64_t{1} << 31) || n_rows * row_elems >= (int64_t{1} << 40)) return -4;
   const bool same = (out_dt == in_dt) && !aff.enabled;
@@ -389,11 +393,11 @@ int gather_rows(void* dst, int32_t out_dt, const void* src, int32_t in_dt, int64
     const int64_t row_bytes = row_elems * dtype_size(in_dt);
     const uintptr_t align = reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src);
     if (row_bytes % 16 == 0 && align % 16 == 0)
-      launch_move<u32x4>(dst, src, n_rows, row_bytes, ri, scatter, max_blocks, st);
+      launch_move<u32x4>(dst, src, n_rows, row_bytes, ri, scatter, nt, max_blocks, st);
     else if (row_bytes % 4 == 0 && align % 4 == 0)
-      launch_move<uint32_t>(dst, src, n_rows, row_bytes, ri, scatter, max_blocks, st);
+      launch_move<uint32_t>(dst, src, n_rows, row_bytes, ri, scatter, nt, max_blocks, st);
     else
-      launch_move<uint8_t>(dst, src, n_rows, row_bytes, ri, scatter, max_blocks, st);
+      launch_move<uint8_t>(dst, src, n_rows, row_bytes, ri, scatter, nt, max_blocks, st);
     return static_cast<int>(hipGetLastError());
   }
   if (scatter) return -2;  // converting scatters are not needed by the loader
@@ -403,10 +407,10 @@ int gather_rows(void* dst, int32_t out_dt, const void* src, int32_t in_dt, int64
   if (aff.enabled && (aff.plane % 8 != 0)) vec_ok = false;
   int rc = -1;
   switch (in_dt) {
-    case kU8: rc = dispatch_out<uint8_t>(out_dt, dst, src, n_rows, row_elems, ri, aff, vec_ok, max_blocks, st); break;
-    case kF32: rc = dispatch_out<float>(out_dt, dst, src, n_rows, row_elems, ri, aff, vec_ok, max_blocks, st); break;
-    case kBF16: rc = dispatch_out<BF16Tag>(out_dt, dst, src, n_rows, row_elems, ri, aff, vec_ok, max_blocks, st); break;
-    case kF16: rc = dispatch_out<F16Tag>(out_dt, dst, src, n_rows, row_elems, ri, aff, vec_ok, max_blocks, st); break;
+    case kU8: rc = dispatch_out<uint8_t>(out_dt, dst, src, n_rows, row_elems, ri, aff, vec_ok, nt, max_blocks, st); break;
+    case kF32: rc = dispatch_out<float>(out_dt, dst, src, n_rows, row_elems, ri, aff, vec_ok, nt, max_blocks, st); break;
+    case kBF16: rc = dispatch_out<BF16Tag>(out_dt, dst, src, n_rows, row_elems, ri, aff, vec_ok, nt, max_blocks, st); break;
+    case kF16: rc = dispatch_out<F16Tag>(out_dt, dst, src, n_rows, row_elems, ri, aff, vec_ok, nt, max_blocks, st); break;
   }
   if (rc != 0) return -3;
   return static_cast<int>(hipGetLastError());

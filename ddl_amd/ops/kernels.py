@@ -187,7 +187,8 @@ def gather_rows(src, index: torch.Tensor | None = None, *, perm: FeistelPermutat
     _native.hip().gather_rows(
         dst=out.data_ptr(), out_dt=_dtypes.code(out_dtype), src=_src_addr(src), in_dt=_dtypes.code(src.dtype),
         n_rows=n_rows, row_elems=row_elems, scale=sc, bias=bi, plane=int(plane or 0), scatter=False,
-        stream=_stream_handle(stream), max_blocks=int(max_blocks), **_index_kw(index, perm, base))
+        stream=_stream_handle(stream), max_blocks=int(max_blocks), host_src=isinstance(src, HostRows),
+        **_index_kw(index, perm, base))
     return out
 
 
