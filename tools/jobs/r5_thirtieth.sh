@@ -5,7 +5,7 @@ source tools/gpu_job.sh
 unset DDL_BACKEND
 TOK="benchmarks/bench_tokens.py --batch 2048 --steps 2000 --warmup 100 --idle-steps 0 --token-dtype uint16"
 for i in 1 2 3; do
-  run 250 tok_$i python $TOK --json-out gpurun_out/fin_tok_$i.json
+  run 250 tok_$i python $TOK
 done
 for i in 1 2; do
   run 200 u8_$i python bench.py --steps 100 --warmup 10 --source-dtype uint8 --idle-steps 0 --pressure-ratio 0 --order window --json-out gpurun_out/fin_u8_$i.json
