@@ -43,6 +43,12 @@ events (idle = 1 - busy/wall). That step is ~4x slower than the feed, so phase 3
 step whose capacity is 0.9x the phase-1 feed: the loader as the near-bottleneck.
 ``benchmarks/bench_idle_sweep.py`` sweeps that step across the whole ratio range.
 
+The line proves its own layout (``dist``, ``ddl_amd/parallel/report.py``): the DP group's backend and
+size, the RCCL version, each rank's device index, PCI bus ID and UUID, and a device-timed all-to-all of
+``--a2a-probe-mb`` on the DP group per rank (its xGMI egress rate). An N > 1 run that is not RCCL over N
+distinct GPUs exits 3 before measuring anything, unless it is labelled a rehearsal (``DDL_REHEARSAL=1``:
+gloo ranks sharing one card, or CPU ranks); ``dist.rehearsal`` says which.
+
 vs_baseline = value / (28,500 samples/s x N): BASELINE.md's reference
 ceiling for this shape (P=3 host producers, f32, no H2D) scaled linearly.
 """
@@ -108,6 +114,9 @@ def parse(argv=None):
                     help="indexed order: skip the one-word-per-page touch of the mapped source (A/B)")
     ap.add_argument("--dispatch", default="auto", choices=["auto", "inline", "lookahead", "python"],
                     help="per-batch dispatch: the native engine (auto / inline / lookahead) or the Python path")
+    ap.add_argument("--a2a-probe-mb", type=float, default=32.0,
+                    help="size of the device-timed all-to-all on the DP group that opens the run (the 'dist' block's "
+                         "per-rank xGMI rate); 0 skips it")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--debug-log", action="store_true",
                     help="slow host iterations of the timed loop and long per-window stager waits in the JSON line")
@@ -209,7 +218,7 @@ def pressure_phase(args, env, dev, it, feed_per_rank: float, barrier, sync, dl=N
     sync()
     t0 = time.perf_counter()
     for _ in range(n_feed):
-        acc.add(next(it)[0])
+        acc.add(next(it)[0])  # the loaders' iterators here yield a tuple (the batch's column groups)
     sync()
     feed = B * n_feed / (time.perf_counter() - t0)
     step = CalibratedStep(dev, step_ms=1000.0 * B / (r * feed))
@@ -406,7 +415,8 @@ def indexed_phase(args, env, dev, barrier, sync, spare=None) -> dict:
         if spare is not None:
             gb = args.batch * env.world_size
             bpe = n // gb
-            total = args.warmup + args.steps + (max(1, args.warmup // 2) + idle_steps if idle_steps else 0)
+            total = args.warmup + args.steps + (max(1, args.warmup // 2) + idle_steps if idle_steps else 0) \
+                + _pressure_batches(args)
             dl = ddl_amd.DistributedDataLoader(
                 IndexedProducer(src, gb, seed=args.seed, host_threads=args.index_threads), args.batch, spare,
                 math.ceil(total / bpe) + 2, mode="indexed", env=env, device=dev, n_slots=2, auto_mark=True,
@@ -426,6 +436,7 @@ def indexed_phase(args, env, dev, barrier, sync, spare=None) -> dict:
                         "producer_fill_us_per_round": [round(p["fill_ns_total"] / max(1, p["rounds"]) / 1e3, 1)
                                                        for p in st.get("producers", [])]})
             out["gpu_idle_pct"] = _idle_behind_step(args, env, dev, it, barrier, sync)
+            out.update(_pressure_sub(args, env, dev, it, rate, barrier, sync, dl=dl))
             dl.close()
         zc = ZeroCopyLoader(src, args.batch * env.world_size, env, seed=args.seed, out_dtype=torch.bfloat16,
                             device=dev, prefault=not args.index_no_prefault)
@@ -435,6 +446,10 @@ def indexed_phase(args, env, dev, barrier, sync, spare=None) -> dict:
                 "value": round(rate, 1), "ms_per_step": round(ms, 4), "prefault_s": zc.stats().get("prefault_s")}
         if spare is None:
             zres["gpu_idle_pct"] = _idle_behind_step(args, env, dev, it, barrier, sync)
+        # the zero-copy gather holds CUs for its whole PCIe transfer: its idle behind a step at 0.9x the feed
+        # is the number that compares it with the producer path
+        zres.update(_pressure_sub(args, env, dev, it, rate, barrier, sync))
+        if spare is None:
             out.update(zres)
         else:
             out["zero_copy"] = zres
@@ -446,6 +461,28 @@ def indexed_phase(args, env, dev, barrier, sync, spare=None) -> dict:
 
             dist.barrier(group=env.control_group)  # every rank has unmapped its view before the unlink
         src.close()
+
+
+def _pressure_batches(args) -> int:
+    """Batches ``pressure_phase`` draws (an upper bound: calibration, tune passes, at most 3 timed loops)."""
+    if args.pressure_ratio <= 0:
+        return 0
+    return 1 + max(2, args.warmup // 2) + 60 + max(args.steps, 100) + 3 * max(args.steps, 300)
+
+
+def _pressure_sub(args, env, dev, it, feed_total: float, barrier, sync, dl=None) -> dict:
+    """Phase 3 on a sub-path's batches (``it`` yields tensors): ``gpu_idle_pct_r090`` + the pressure record."""
+    if args.pressure_ratio <= 0 or dev.type != "cuda":
+        return {}
+    key = f"gpu_idle_pct_r{round(100 * args.pressure_ratio):03d}"
+    try:
+        pr = pressure_phase(args, env, dev, ((x,) for x in it), feed_total / env.world_size, barrier, sync, dl=dl)
+    except Exception as e:  # the sub-path's feed rate is still reported
+        import traceback
+
+        traceback.print_exc()
+        return {key: None, "pressure": {"error": repr(e)[:300]}}
+    return {key: pr["gpu_idle_pct"], "pressure": pr}
 
 
 def _landed(dl) -> tuple[int, int]:
@@ -474,6 +511,7 @@ def main(argv=None) -> int:
     from ddl_amd import Marker, ops
     from ddl_amd.models.producers import ImageWindowProducer
     from ddl_amd.parallel.order import LEDGER, check_same_order
+    from ddl_amd.parallel.report import dist_block, require_verified
     from ddl_amd import _native
     from ddl_amd.utils.numa import gpu_numa_node
     from ddl_amd.utils.tracing import trace_range
@@ -485,8 +523,7 @@ def main(argv=None) -> int:
     if args.exchange is None:
         args.exchange = 0.5 if n_world > 1 else 0.0
     total_steps = args.warmup + args.steps + (args.warmup // 2 + idle_steps if idle_steps else 0)
-    if args.pressure_ratio > 0:
-        total_steps += 1 + max(2, args.warmup // 2) + 60 + max(args.steps, 100) + 3 * max(args.steps, 300)
+    total_steps += _pressure_batches(args)
     bpw = args.window // args.batch
     if bpw < 1:
         raise SystemExit("--window must hold at least one --batch")
@@ -498,6 +535,16 @@ def main(argv=None) -> int:
     spares = 1 if args.order == "window+indexed" and args.producers > 0 else 0
     with ddl_amd.start(n_producers=args.producers, spare_connections=spares) as (env, conn):
         dev = torch.device(env.device)
+        # the run proves its own layout: RCCL over N distinct GPUs (or a labelled rehearsal), with a
+        # device-timed all-to-all on the DP group as the per-rank xGMI rate (parallel/report.py)
+        dist_info = dist_block(env, int(args.a2a_probe_mb * (1 << 20)))
+        refuse = require_verified(dist_info)
+        if refuse is not None:
+            print(f"bench: {refuse}; refusing to report an unverified dp{env.world_size} number", file=sys.stderr)
+            if env.rank == 0:
+                print("bench: dist = " + json.dumps({k: v for k, v in dist_info.items() if k != "ranks"}),
+                      file=sys.stderr)
+            return 3
         producer = ImageWindowProducer(args.window, shape, args.source_dtype, seed=args.seed, refill=args.refill,
                                        host_threads=args.producer_threads)
         norm = None
@@ -552,6 +599,7 @@ def main(argv=None) -> int:
         w_land0, b_land0 = _landed(dl)
         w_cur0 = dl.window
         bytes_enq0 = dl._stager.bytes_h2d if dl._stager is not None else 0
+        n_post0 = len(dl._stager.post_waits) if dl._stager is not None else 0
         with trace_range("bench.phase1"):  # roctx: lets tools/trace_idle.py find the timed region
             for _ in range(args.steps):
                 (x,) = next(it)
@@ -567,8 +615,10 @@ def main(argv=None) -> int:
         cb = dl._stager._native.copies_between(t0_ns, t1_ns) if dl._stager is not None else None
         w_land1, b_land1 = _landed(dl)
         bytes_enq1 = dl._stager.bytes_h2d if dl._stager is not None else 0
+        post_waits = dl._stager.post_waits[n_post0:] if dl._stager is not None else []
         # CPU rehearsal: the host path has no H2D; every delivered window counts
         n_in, b_in = cb[:2] if cb is not None else (w_land1 - w_land0, 0)
+        cb_complete = bool(cb[2]) if cb is not None else None  # False: the copy log was trimmed in the region
         pro = dl._stager.bytes_in_interval(ev0, ev1) if dl._stager is not None and ev0 is not None else None
         if pro is not None and pro["ok"]:
             # the device interval is the region as the GPU saw it; its length next to the host's is a check
@@ -586,7 +636,9 @@ def main(argv=None) -> int:
             "landed_per_s": landed_samples / elapsed,
             "h2d_bytes_timed": int(b_in_prorata),
             "h2d_gbps_timed": b_in_prorata / elapsed / 1e9,
-            "h2d_accounting": "device-timed pro rata" if pro is not None and pro["ok"] else "whole windows",
+            "h2d_accounting": ("device-timed pro rata" if pro is not None and pro["ok"] else
+                               "whole windows" if cb_complete is not False else "whole windows (INCOMPLETE log)"),
+            "h2d_copy_log_complete": cb_complete,
             "device_region_ms": round(pro["t1_ms"] - pro["t0_ms"], 4) if pro is not None and pro["ok"] else None,
             "h2d_copies_overlapping_region": pro["copies"] if pro is not None else None,
             # device-timed link occupancy in the region: share of it with >= 1 / 2 window copies running
@@ -633,6 +685,10 @@ def main(argv=None) -> int:
                             "compute_waits": nd.get("compute_waits")} if nd else {"mode": "python"}
         mine["stager_wait_producer_s"] = round(stats.get("stager_wait_producer_s", 0.0), 4)
         mine["exchange_issue_wait_s"] = stats.get("exchange_issue_wait_s", 0.0)
+        if post_waits:  # the timed region's per-window host waits at the exchange's issue point
+            from ddl_amd.staging import issue_wait_summary
+
+            mine["exchange_issue_wait_timed"] = issue_wait_summary(post_waits)
         mine["consumer_wait_s"] = round(stats["consumer_wait_s"], 4)
         ex = getattr(dl, "_exchange_fn", None)
         if ex is not None:
@@ -733,6 +789,7 @@ def main(argv=None) -> int:
                 f"gpu_idle_pct_r{round(100 * args.pressure_ratio):03d}": (pressure or {}).get("gpu_idle_pct"),
                 "pressure": pressure,
                 "collective_order": order,
+                "dist": dist_info,
                 "indexed": indexed,
                 "per_rank": per_rank,
             }

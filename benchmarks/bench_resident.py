@@ -6,6 +6,10 @@ sharded across the ranks and loaded into HBM once; every step assembles a
 batch of the world-size-invariant global permutation (gfx950 gather kernels +
 RCCL all-to-all over xGMI for W > 1). Sweeps the prefetch depth; reports
 samples/s fed (checksum consumer) per depth. torchrun-compatible.
+
+``--replicate`` picks the layout at W > 1 (``ResidentGlobalLoader(replicate=)``): replicated (default when the
+dataset fits in HBM: an all-gather over xGMI at bring-up, then no per-step collective) or sharded (a per-step
+RCCL all-to-all of (W-1)/W of every batch).
 """
 
 import argparse
@@ -23,6 +27,11 @@ def main(argv=None):
     ap.add_argument("--n-samples", type=int, default=16384, help="global dataset size")
     ap.add_argument("--dtype", default="bfloat16", choices=["bfloat16", "uint8"])
     ap.add_argument("--depths", default="1,2,4")
+    ap.add_argument("--replicate", default="auto", choices=["auto", "true", "false"],
+                    help="replicated: every rank holds the whole dataset (1/W loaded from host per rank, the rest "
+                         "all-gathered over xGMI once; no per-step collective); sharded: rank r holds rows "
+                         "[r*S, (r+1)*S) and every step all-to-alls (W-1)/W of its batch; auto: replicated when "
+                         "it fits in 80%% of free HBM")
     ap.add_argument("--augment", action="store_true",
                     help="RandomResizedCrop(224) + flip + normalise on the device instead of the plain gather")
     a = ap.parse_args(argv)
@@ -33,6 +42,7 @@ def main(argv=None):
     import ddl_amd
     from ddl_amd import ops
     from ddl_amd.models.datasets import SharedArraySource
+    from ddl_amd.parallel.report import dist_block, require_verified
     from ddl_amd.resident import ResidentGlobalLoader
 
     shape = (3, 224, 224)
@@ -56,11 +66,21 @@ def main(argv=None):
                 del base
             if env.world_size > 1:
                 dist.barrier(group=env.control_group)
+            dist_info = dist_block(env, 32 << 20)  # backend, GPUs, per-rank all-to-all rate (parallel/report.py)
+            refuse = require_verified(dist_info)
+            if refuse is not None:
+                print(f"bench_resident: {refuse}", file=sys.stderr)
+                return 3
             norm = {"mean": [0.485, 0.456, 0.406], "std": [0.229, 0.224, 0.225]} if a.dtype == "uint8" else None
             dev = torch.device(env.device)
+
+            def sync():
+                if dev.type == "cuda":
+                    torch.cuda.synchronize(dev)
             for depth in [int(x) for x in a.depths.split(",")]:
+                rep = {"auto": "auto", "true": True, "false": False}[a.replicate]
                 dl = ResidentGlobalLoader(src, a.batch * env.world_size, env, seed=1, depth=depth,
-                                          out_dtype=torch.bfloat16, normalize=norm,
+                                          out_dtype=torch.bfloat16, normalize=norm, replicate=rep,
                                           augment={"size": (224, 224)} if a.augment else None)
                 acc = ops.ChecksumAccumulator(dev)  # one streaming launch per batch
 
@@ -71,13 +91,13 @@ def main(argv=None):
                 it = gen()
                 for _ in range(a.warmup):
                     acc.add(next(it))
-                torch.cuda.synchronize()
+                sync()
                 if env.world_size > 1:
                     dist.barrier(group=env.control_group)
                 t0 = time.perf_counter()
                 for _ in range(a.steps):
                     acc.add(next(it))
-                torch.cuda.synchronize()
+                sync()
                 el = time.perf_counter() - t0
                 if env.world_size > 1:
                     tt = torch.tensor([el], dtype=torch.float64)
@@ -86,13 +106,19 @@ def main(argv=None):
                 st = dl.stats()
                 dl.close()  # frees the shard; `it` still references dl
                 results.append({"depth": depth, "samples_per_s": round(a.batch * a.steps * env.world_size / el, 1),
-                                "ms_per_step": round(1000 * el / a.steps, 4), "load_s": round(st["load_s"], 2),
-                                "shard_GB": round(st["shard_bytes"] / 1e9, 2),
-                                "xgmi_GB_sent_per_rank": round(st["bytes_exchanged"] / 1e9, 3)})
+                                "ms_per_step": round(1000 * el / a.steps, 4),
+                                "mode": "replicated" if st["replicated"] else "sharded",
+                                # bring-up: host -> HBM of this rank's rows, then (replicated) the all-gather
+                                "load_s": round(st["load_s"], 2), "replicate_s": round(st["replicate_s"], 2),
+                                "resident_GB": round(st["shard_bytes"] / 1e9, 2),
+                                "xgmi_GB_sent_per_rank_steps": round(st["bytes_exchanged"] / 1e9, 3),
+                                "xgmi_GB_sent_per_rank_bringup": round(st["bytes_replicated"] / 1e9, 3)})
                 del dl, it, acc
-                torch.cuda.empty_cache()  # hand the freed shard back before the next depth allocates its own
+                if dev.type == "cuda":
+                    torch.cuda.empty_cache()  # hand the freed shard back before the next depth allocates its own
             if env.rank == 0:
                 print(json.dumps({"metric": "samples/s fed to GPU, HBM-resident exact global shuffle",
+                                  "dist": dist_info,
                                   "augment": "RandomResizedCrop(224)+flip+normalise" if a.augment else None,
                                   "n_gpus": env.world_size, "batch_per_gpu": a.batch, "dtype_src": a.dtype,
                                   "dtype_out": "bf16", "n_samples": a.n_samples, "sweep": results}), flush=True)

@@ -315,6 +315,11 @@ PYBIND11_MODULE(_ddl_hip, m) {
       .def_property_readonly("reanchors", &ddl::NativeStager::reanchors)
       .def("inject_stuck_copy", &ddl::NativeStager::inject_stuck_copy, py::arg("window"),
            "fault injection: window w's copy never reads as landed (its completion signal is armed one too high)")
+      .def("inject_slow_retire", &ddl::NativeStager::inject_slow_retire, py::arg("extra_ms"),
+           "fault injection: the retire thread waits extra_ms longer than the timeout (the consumer times out first)")
+      .def_property_readonly("poisoned", &ddl::NativeStager::poisoned,
+                             "a copy wait failed with copies pending: keep the ring and the arena alive")
+      .def_property_readonly("leaked_signals", &ddl::NativeStager::leaked_signals)
       .def(
           "copies_between",
           [](const ddl::NativeStager& st, uint64_t t0, uint64_t t1) {

@@ -395,13 +395,12 @@ int NativeStager::wait_retired(const Retire& r) {
     return direct_ ? wait_signal(copy_sig_[r.ev], t, stop_aware) : wait_event(retire_ev_[r.ev], t, stop_aware);
   };
   const auto t0 = std::chrono::steady_clock::now();
-  int rc = wait(timeout_ms_, true);
+  int rc = wait(timeout_ms_ < 0 ? timeout_ms_ : timeout_ms_ + retire_extra_ms_.load(), true);
   if (rc == kShutdown) {
     const int64_t left = timeout_ms_ < 0 ? kCloseGraceMs : std::max<int64_t>(0, timeout_ms_ - ms_since(t0));
     rc = wait(std::min(left, kCloseGraceMs), false);
   }
   if (rc == kTimeout) {
-    if (direct_) sig_leaked_[r.ev] = true;  // the engine may still write it: never destroyed
     StagedInfo info;
     info.window = r.window;
     info.producer = static_cast<int32_t>(r.producer);
@@ -416,6 +415,20 @@ int NativeStager::wait_retired(const Retire& r) {
   return rc;
 }
 
+void NativeStager::quarantine_pending() {
+  // every copy still queued -- the one whose wait failed, the ones behind it on the same (possibly hung)
+  // engine, and any the stager thread enqueues before it sees the failure (run() leaks those at enqueue) --
+  // may complete later: its signal is never destroyed, and the owner keeps the ring and the arena (poisoned)
+  std::lock_guard<std::mutex> lk(mu_);
+  for (const Retire& q : retire_q_) {
+    if (direct_ && !sig_leaked_[q.ev]) {
+      sig_leaked_[q.ev] = true;
+      leaked_.fetch_add(1);
+    }
+  }
+  if (!retire_q_.empty()) poisoned_ = true;
+}
+
 void NativeStager::retire_loop() {
   if (hipSetDevice(device_) != hipSuccess) return fail(-1, -1, "hipSetDevice failed in the retire thread");
   for (;;) {
@@ -426,7 +439,10 @@ void NativeStager::retire_loop() {
       if (retire_q_.empty()) return;  // stopped and drained
       r = retire_q_.front();
     }
-    if (wait_retired(r) != 0) return;  // the stager failed (the copy never landed): its slot stays held
+    if (wait_retired(r) != 0) {  // the stager failed (a copy never landed): its slot stays held
+      quarantine_pending();
+      return;
+    }
     bytes_landed_.fetch_add(r.bytes, std::memory_order_relaxed);
     windows_landed_.fetch_add(1, std::memory_order_release);
     arena_->set_state(r.producer, r.slot, kEmpty);  // slot back to its producer (release store + futex wake)
@@ -628,6 +644,10 @@ void NativeStager::run() {
     {
       std::lock_guard<std::mutex> lk(mu_);
       retire_q_.push_back(Retire{w, p, s, info.used_bytes, rev, si, !direct_ || copy_timing_.load()});
+      if (poisoned_.load() && direct_ && !sig_leaked_[rev]) {  // the retire thread is gone: nobody retires it
+        sig_leaked_[rev] = true;
+        leaked_.fetch_add(1);
+      }
     }
     retire_cv_.notify_all();
     if (!direct_) info.copy_event = retire_ev_[rev];

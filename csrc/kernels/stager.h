@@ -161,6 +161,15 @@ class NativeStager {
   // fault injection (tests): window w's copy completion signal is armed one too high, so it never reads as
   // landed although the data arrives -- what a hung SDMA engine looks like to every waiter
   void inject_stuck_copy(int64_t w) { stuck_window_ = w; }
+  // fault injection (tests): the retire thread's copy wait gets extra_ms more than the loader's timeout, so a
+  // consumer waiting on the same stuck copy times out first
+  void inject_slow_retire(int64_t extra_ms) { retire_extra_ms_ = extra_ms < 0 ? 0 : extra_ms; }
+  // A copy wait failed (timed out, or a HIP error) while copies were still queued or in flight: their engines
+  // may still write the ring buffers (and complete their signals) at any later time. Every such copy's signal
+  // is then leaked on purpose (never destroyed), and poisoned() tells the owner to keep the ring buffers and
+  // the pinned arena alive for the life of the process instead of freeing them under a pending copy.
+  bool poisoned() const { return poisoned_.load(); }
+  uint64_t leaked_signals() const { return leaked_.load(); }
   double wait_producer_s() const { return wait_producer_ns_.load() * 1e-9; }
   // free-event waits actually enqueued on a copy stream (the rest had completed and were skipped)
   uint64_t free_waits() const { return free_waits_.load(); }
@@ -217,6 +226,7 @@ class NativeStager {
     bool timed;  // its device times are known (stream mode, or copy timing on when it was enqueued)
   };
   int wait_retired(const Retire& r);  // retire thread: the copy of `r`, bounded (with the close grace)
+  void quarantine_pending();          // retire thread, after a failed wait: leak every queued copy's signal
   static constexpr int kRetireEvents = 16;
   std::vector<hipEvent_t> retire_ev_, start_ev_;
   hipEvent_t epoch_ev_ = nullptr;  // recorded once at construction: the zero of every copy's device times
@@ -283,6 +293,9 @@ class NativeStager {
   std::atomic<uint64_t> windows_landed_{0}, bytes_landed_{0}, free_waits_{0};
   std::atomic<bool> free_on_host_{false}, record_ready_{true}, copy_timing_{false};
   std::atomic<int64_t> stuck_window_{-1};
+  std::atomic<int64_t> retire_extra_ms_{0};
+  std::atomic<bool> poisoned_{false};  // set under mu_ (with the leaks of every queued copy)
+  std::atomic<uint64_t> leaked_{0};
   // direct-DMA state (set in the constructor, read-only afterwards)
   bool direct_ = false;
   std::string direct_reason_;

@@ -296,6 +296,11 @@ class Connection:
             except (BrokenPipeError, OSError):
                 pass
 
+    def quarantine(self) -> None:
+        """A stager closed with copies out of the arena still pending (a hung engine): keep the arena pinned
+        and mapped for the life of the process (``finalize`` skips the unregistration)."""
+        self._quarantined = True
+
     def add_finalizer(self, fn) -> None:
         """Run ``fn()`` in ``finalize`` after the shutdown signal and before the arena is
         unpinned: consumers with native threads on the arena (the stager) stop there,
@@ -327,7 +332,7 @@ class Connection:
                 logger.warning("producer pid %s did not exit; terminating", proc.pid)
                 proc.terminate()
                 proc.join(5)
-        if self._registered and self.arena is not None:
+        if self._registered and self.arena is not None and not getattr(self, "_quarantined", False):
             try:
                 torch.cuda.synchronize()
                 _native.hip().host_unregister(self.arena.base_address)

@@ -72,6 +72,85 @@ def read_env(n_producers: int | None = None) -> DDLEnv:
     )
 
 
+_VISIBILITY_VARS = ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL")
+
+
+def rehearsal() -> bool:
+    """``DDL_REHEARSAL=1``: this multi-rank run is a rehearsal (several ranks on one GPU over gloo, or ranks
+    on the CPU), not a measurement of N GPUs. Without it a layout that shares a device is refused
+    (:func:`check_device_count`, :func:`check_node_locality`) and ``bench.py`` exits non-zero at N > 1 unless
+    the DP group is RCCL over N distinct GPUs."""
+    return os.environ.get("DDL_REHEARSAL", "0") == "1"
+
+
+def check_device_count(env: DDLEnv, n_dev: int) -> None:
+    """Raise ``TopologyError`` when this node has more ranks than visible GPUs: ``local_rank % n_dev`` would
+    wrap and put two ranks on one device silently (gloo runs that way; RCCL fails later with "Duplicate GPU").
+
+    With a ``*_VISIBLE_DEVICES`` mask (per-task GPU isolation, e.g. SLURM ``--gpus-per-task``) every rank
+    legitimately sees fewer devices than the node has ranks; the PCI-bus-ID all-gather of
+    :func:`check_node_locality` then catches a shared device instead."""
+    if env.local_world_size <= n_dev or rehearsal():
+        return
+    if n_dev >= 1 and any(os.environ.get(v) for v in _VISIBILITY_VARS):
+        return
+    raise TopologyError((env.local_world_size, n_dev),
+                        f"{env.local_world_size} ranks on host {env.hostname} but only {n_dev} visible GPU(s): ranks "
+                        "would share a device. One rank per GPU; set DDL_REHEARSAL=1 for a deliberate rehearsal")
+
+
+def device_identity(device: str | None) -> dict:
+    """PCI location and UUID of ``device`` (``{}`` on the CPU): the key that tells two GPUs apart even when
+    per-task visibility masks make every rank call its GPU ``cuda:0``."""
+    if not device or not str(device).startswith("cuda"):
+        return {}
+    import torch
+
+    idx = torch.device(device).index
+    idx = torch.cuda.current_device() if idx is None else idx
+    p = torch.cuda.get_device_properties(idx)
+    bus = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"
+    uuid = str(getattr(p, "uuid", "") or "")
+    return {"device_index": idx, "pci_bus_id": bus, "uuid": uuid, "name": p.name,
+            "arch": getattr(p, "gcnArchName", "")}
+
+
+_CLAIMED: dict = {}  # PCI bus ID -> fd of the held lock (kept open for the life of the process)
+
+
+def claim_device(env: DDLEnv) -> None:
+    """Take this job's exclusive claim on the rank's GPU before any group exists: a non-blocking ``flock`` on
+    a per-job, per-PCI-bus-ID file in the node's temp directory. A second rank of the same job that lands on
+    the same GPU (a wrapped index, a visibility mask handing every task the same device) gets a
+    ``TopologyError`` naming the holder, instead of RCCL's "Duplicate GPU" deep inside the first collective or
+    gloo's silent sharing. The kernel drops the lock when the process exits. Skipped under
+    ``DDL_REHEARSAL=1``."""
+    import fcntl
+    import tempfile
+    import zlib
+
+    if rehearsal():
+        return
+    bus = device_identity(env.device).get("pci_bus_id")
+    if not bus or bus in _CLAIMED:
+        return
+    job = f"{os.environ.get('MASTER_ADDR', '')}:{os.environ.get('MASTER_PORT', '')}"
+    path = os.path.join(tempfile.gettempdir(),
+                        f"ddl_amd_gpu_{bus.replace(':', '_')}_{zlib.crc32(job.encode()):08x}.lock")
+    fd = os.open(path, os.O_CREAT | os.O_RDWR, 0o666)
+    try:
+        fcntl.flock(fd, fcntl.LOCK_EX | fcntl.LOCK_NB)
+    except OSError:
+        holder = os.pread(fd, 64, 0).decode(errors="replace").strip()
+        os.close(fd)
+        raise TopologyError((env.rank, bus, holder),
+                            f"rank {env.rank} and {holder or 'another rank'} of this job share a device (GPU at PCI "
+                            f"{bus}): one rank per GPU; set DDL_REHEARSAL=1 for a deliberate rehearsal") from None
+    os.ftruncate(fd, 0)
+    os.pwrite(fd, f"rank {env.rank} (pid {os.getpid()})".encode(), 0)
+    _CLAIMED[bus] = fd
+
+
 def _free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -96,9 +175,12 @@ def init_distributed(env: DDLEnv, backend: str | None = None, timeout_s: float =
     use_gpu = device != "cpu" and torch.cuda.is_available()
     if use_gpu:
         n_dev = torch.cuda.device_count()
+        check_device_count(env, n_dev)
         dev_index = env.local_rank % max(n_dev, 1)
         torch.cuda.set_device(dev_index)
         env.device = f"cuda:{dev_index}"
+        if env.world_size > 1:
+            claim_device(env)
     else:
         env.device = "cpu"
     backend = backend or os.environ.get("DDL_BACKEND") or None
@@ -169,13 +251,21 @@ def check_node_locality(env: DDLEnv) -> None:
 
     if env.world_size == 1 or env.control_group is None:
         return
+    ident = device_identity(env.device)
     infos: list = [None] * env.world_size
-    dist.all_gather_object(infos, (env.hostname, env.local_rank, env.local_world_size), group=env.control_group)
+    dist.all_gather_object(infos, (env.hostname, env.local_rank, env.local_world_size,
+                                   ident.get("pci_bus_id"), ident.get("uuid")), group=env.control_group)
     mine = [i for i in infos if i[0] == env.hostname]
     local_ranks = sorted(i[1] for i in mine)
     if local_ranks != list(range(len(mine))) or len(mine) != env.local_world_size:
         raise TopologyError(infos, f"ranks on host {env.hostname} have local ranks {local_ranks}, "
                                    f"expected 0..{env.local_world_size - 1}")
+    # one GPU per rank: no two ranks of a host on the same PCI device (a wrapped device index, or a
+    # visibility mask that hands every task the same GPU)
+    buses = [i[3] for i in mine if i[3] is not None]
+    if len(set(buses)) != len(buses) and not rehearsal():
+        raise TopologyError(infos, f"ranks on host {env.hostname} share GPUs (PCI bus IDs {buses}); one rank per "
+                                   "GPU, or DDL_REHEARSAL=1 for a deliberate rehearsal")
     logger.debug("node locality ok: %s", infos)
 
 

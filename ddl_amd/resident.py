@@ -251,7 +251,8 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
                  drop_last: bool = True, out_dtype: Any = None, normalize: dict | None = None, depth: int = 2,
                  device: str | torch.device | None = None, n_epochs: int | None = None,
                  resume_state: dict | None = None, chunk_bytes: int = 256 << 20, host_threads: int = 8,
-                 scatter_from: int | None = None, augment: dict | None = None):
+                 scatter_from: int | None = None, augment: dict | None = None, replicate: bool | str = "auto",
+                 hbm_fraction: float = 0.8):
         import torch.distributed as dist
 
         aug_keys = {"size", "scale", "ratio", "flip_p", "layout"}
@@ -301,18 +302,104 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
             # the DP group: one communicator / RCCL stream with the trainer's DDP (parallel/order.py)
             self.group = loader_group(self.env)
         self.bytes_exchanged = 0
+        self.bytes_replicated = 0
+        self.replicated = self._decide_replicate(replicate, chunk_bytes, hbm_fraction)
+        self.replicate_s = 0.0
         t0 = time.perf_counter()
-        if scatter_from is not None and self.W > 1:
+        if self.replicated:
+            self.shard = self._load_replica(reader, chunk_bytes, host_threads, scatter_from)
+        elif scatter_from is not None and self.W > 1:
             self.shard = self._scatter_shards(reader, chunk_bytes, host_threads, scatter_from)
         else:
             self.shard = self._load_shard(reader, chunk_bytes, host_threads)
         self.load_s = time.perf_counter() - t0
         self.prep_stream = streams.batch_stream(self.device) if self.device.type == "cuda" else None
-        if self.device.type == "cuda" and self.W > 1:  # owner-bucketing outputs, reused every step (prep stream)
+        if self.device.type == "cuda" and self.W > 1 and not self.replicated:  # owner-bucketing outputs (prep stream)
             self._send_idx = torch.empty(self.GB, dtype=torch.int64, device=self.device)
             self._inv_idx = torch.empty(self.LB, dtype=torch.int64, device=self.device)
 
     # ----------------------------------------------------------------- load
+    def _decide_replicate(self, replicate: bool | str, chunk_bytes: int, hbm_fraction: float) -> bool:
+        """``replicate``: True / False, or "auto" = a whole replica (plus the bring-up's gather staging) fits in
+        ``hbm_fraction`` of the free HBM of EVERY rank (MIN over the control group, so all ranks agree). At
+        W = 1 the two modes are the same layout; "auto" on the CPU keeps the sharded layout."""
+        if replicate not in (True, False, "auto"):
+            raise ValueError("replicate must be True, False or 'auto'")
+        if self.W == 1:
+            return False
+        if replicate != "auto":
+            return bool(replicate)
+        if self.device.type != "cuda":
+            return False
+        import torch.distributed as dist
+
+        free, _ = torch.cuda.mem_get_info(self.device)
+        need = self.S * self.W * self.row_bytes + self.W * self._chunk_rows(chunk_bytes) * self.row_bytes
+        t = torch.tensor([1 if need <= hbm_fraction * free else 0], dtype=torch.int64)
+        if self.env.control_group is not None:
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.env.control_group)
+        logger.info("resident loader: replica %.1f GB vs %.1f GB free HBM -> %s", need / 1e9, free / 1e9,
+                    "replicated" if t.item() else "sharded")
+        return bool(t.item())
+
+    def _chunk_rows(self, chunk_bytes: int) -> int:
+        return max(1, min(self.S, chunk_bytes // max(self.row_bytes, 1)))
+
+    def _load_replica(self, reader, chunk_bytes: int, host_threads: int, scatter_from: int | None) -> torch.Tensor:
+        """The whole dataset resident on every rank, built without a host read of more than 1/W of it per rank.
+
+        Each rank loads its slice [r*S, (r+1)*S) from the host exactly as the sharded mode does (pinned bounce
+        buffers, PCIe, all ranks in parallel), straight into its place in the replica; then chunked RCCL
+        ``all_gather``s over xGMI fill the other W-1 slices (chunk_bytes per rank per round: the collective's
+        flat staging stays at W x chunk_bytes of HBM). With ``scatter_from`` only that rank holds the dataset:
+        it streams chunks H2D and ``broadcast``s each one. The replica has S*W rows (<= W-1 padding rows past
+        N, never addressed: the epoch permutation ranges over [0, N)). Steps then gather the rank's slice of
+        every global batch from its own replica: no per-step collective at all."""
+        import torch.distributed as dist
+
+        rows_total = self.S * self.W
+        replica = torch.empty((rows_total,) + self.sample_shape, dtype=self.src_dtype, device=self.device)
+        probe = torch.zeros(1, device=self.device)
+        issue(self.env, self.group, "resident.bringup")
+        dist.all_reduce(probe, group=self.group)  # communicator bring-up on every rank before the timed parts
+        cr = self._chunk_rows(chunk_bytes)
+        if scatter_from is None:
+            self._load_rows(reader, replica, self.lo, self.hi - self.lo, chunk_bytes, host_threads)
+            t0 = time.perf_counter()
+            with trace_range("ddl.resident.replicate"):
+                for k, c0 in enumerate(range(0, self.S, cr)):
+                    c1 = min(self.S, c0 + cr)
+                    outs = [replica[q * self.S + c0:q * self.S + c1] for q in range(self.W)]
+                    issue(self.env, self.group, "resident.replicate", k)
+                    dist.all_gather(outs, outs[self.rank], group=self.group)
+                    self.bytes_replicated += (self.W - 1) * (c1 - c0) * self.row_bytes
+        else:
+            t0 = time.perf_counter()
+            src = self.rank == scatter_from
+            with trace_range("ddl.resident.replicate"):
+                for k, c0 in enumerate(range(0, self.N, cr)):
+                    c1 = min(self.N, c0 + cr)
+                    if src:
+                        self._load_rows(reader, replica, c0, c1 - c0, chunk_bytes, host_threads)
+                    issue(self.env, self.group, "resident.replicate", k)
+                    dist.broadcast(replica[c0:c1], scatter_from, group=self.group)
+                    self.bytes_replicated += (c1 - c0) * self.row_bytes * (self.W - 1 if src else 0)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        self.replicate_s = time.perf_counter() - t0
+        return replica
+
+    def _load_rows(self, reader, dst: torch.Tensor, row0: int, rows: int, chunk_bytes: int,
+                   host_threads: int) -> None:
+        """Source rows [row0, row0 + rows) into ``dst[row0:row0 + rows]`` (device or host tensor)."""
+        if rows <= 0:
+            return
+        out = dst[row0:row0 + rows].view(-1).view(torch.uint8)
+        if self.device.type != "cuda":
+            reader(row0, rows, out.data_ptr(), host_threads)
+            return
+        self._h2d_rows(reader, out, row0, rows, chunk_bytes, host_threads)
+
     def _load_shard(self, reader, chunk_bytes: int, host_threads: int) -> torch.Tensor:
         rows = self.hi - self.lo
         shard = torch.empty((rows,) + self.sample_shape, dtype=self.src_dtype, device=self.device)
@@ -322,7 +409,13 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
         if self.device.type != "cuda":
             reader(self.lo, rows, dst_bytes.data_ptr(), host_threads)
             return shard
-        # double-buffered pinned bounce buffers: host read (memcpy / pread) || SDMA H2D
+        self._h2d_rows(reader, dst_bytes, self.lo, rows, chunk_bytes, host_threads)
+        return shard
+
+    def _h2d_rows(self, reader, dst_bytes: torch.Tensor, row0: int, rows: int, chunk_bytes: int,
+                  host_threads: int) -> None:
+        """Source rows [row0, row0 + rows) into the HBM bytes ``dst_bytes``: double-buffered pinned bounce
+        buffers, host read (memcpy / pread) || SDMA H2D."""
         hip = _native.hip()
         chunk_rows = max(1, min(chunk_bytes // max(self.row_bytes, 1), rows))
         bufs = [torch.empty(chunk_rows * self.row_bytes, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
@@ -336,7 +429,7 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
                 b = i % 2
                 if used[b]:
                     evs[b].synchronize()
-                reader(self.lo + r, n, bufs[b].data_ptr(), host_threads)
+                reader(row0 + r, n, bufs[b].data_ptr(), host_threads)
                 hip.memcpy_h2d(dst_bytes.data_ptr() + r * self.row_bytes, bufs[b].data_ptr(), n * self.row_bytes,
                                s.cuda_stream)
                 evs[b].record(s)
@@ -344,7 +437,6 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
                 r += n
                 i += 1
             s.synchronize()
-        return shard
 
     def _scatter_shards(self, reader, chunk_bytes: int, host_threads: int, src_rank: int) -> torch.Tensor:
         """Rank ``src_rank`` streams the dataset H2D chunk by chunk and sends every
@@ -444,11 +536,14 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
         kw = self._norm_kw()
         ctx = streams.on_stream(self.prep_stream) if self.prep_stream is not None else contextlib.nullcontext()
         with ctx, trace_range("ddl.resident.assemble"):
-            if self.W == 1:
-                if self.augment is not None:  # rows of the shard ARE global sample ids at W = 1
-                    batch = self._crop(self.shard, e, perm=perm, base=g * self.GB, n_rows=self.LB)
+            if self.W == 1 or self.replicated:
+                # the resident rows ARE global sample ids (W = 1, or a whole replica): the rank's slice of
+                # global batch g straight from HBM, the permutation evaluated inside the kernel
+                base = g * self.GB + self.rank * self.LB
+                if self.augment is not None:
+                    batch = self._crop(self.shard, e, perm=perm, base=base, n_rows=self.LB)
                 else:
-                    batch = ops.gather_rows(self.shard, perm=perm, base=g * self.GB, n_rows=self.LB,
+                    batch = ops.gather_rows(self.shard, perm=perm, base=base, n_rows=self.LB,
                                             out_dtype=self.out_dtype, **kw)
             else:
                 # W split counts on the host (native Feistel over the GB positions, no numpy); the send list
@@ -501,8 +596,11 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
             mean=norm.get("mean"), std=norm.get("std"), **kw)
 
     def stats(self) -> dict:
-        return {"batches": self.batches, "bytes_exchanged": self.bytes_exchanged, "shard_rows": self.hi - self.lo,
-                "shard_bytes": (self.hi - self.lo) * self.row_bytes, "load_s": self.load_s}
+        rows = self.S * self.W if self.replicated else self.hi - self.lo
+        return {"batches": self.batches, "replicated": self.replicated, "bytes_exchanged": self.bytes_exchanged,
+                "bytes_replicated": self.bytes_replicated, "resident_rows": rows,
+                "shard_rows": self.hi - self.lo, "shard_bytes": rows * self.row_bytes,
+                "load_s": self.load_s, "replicate_s": self.replicate_s}
 
     def close(self) -> None:
         """Drain the prep stream and release the HBM shard (a 150-190 GB shard must be

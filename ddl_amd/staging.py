@@ -73,6 +73,8 @@ class StagedWindow:
 
 
 _SDMA_WARM: set = set()
+# (ring buffers, arena, native stager) of stagers closed with copies still pending on a stuck engine: never freed
+_QUARANTINE: list = []
 
 
 def warm_copy_engines(device: torch.device, n_engines: int = 4, nbytes: int = 512 << 20) -> float:
@@ -154,6 +156,7 @@ class WindowStager:
         self._closed = False
         self._n_released = 0
         self.post_wait_s = 0.0  # host time blocked at a collective issue point waiting for its window
+        self.post_waits: list[float] = []  # ... per posted window (seconds), for the p50 / p99 in stats()
         self._native = hip.NativeStager(
             arena=connection.arena.address, n_producers=connection.n_producers, n_slots=n_slots,
             first=first_window, total=total_windows, buffers=[b.data_ptr() for b in self.buffers],
@@ -235,11 +238,13 @@ class WindowStager:
             return
         t0 = time.perf_counter()
         sw = self._wait_staged(w)
-        self.post_wait_s += time.perf_counter() - t0
         if self.direct_dma:  # no HIP event behind the copy: the host waits for it, then enqueues the stage
             self._wait_copy(w)
         else:
             self.stream.wait_event(self._copy_done[sw.buffer])
+        dt = time.perf_counter() - t0  # the issue point's host wait: producer publish + (direct DMA) the copy
+        self.post_wait_s += dt
+        self.post_waits.append(dt)
         with streams.on_stream(self.stream), trace_range("ddl.stage.post_copy"):
             self.post_copy(sw.data, w, {"seq": sw.seq, "used_bytes": sw.nbytes, "tag": list(sw.tags)})
         self.ready_events[sw.buffer].record(self.stream)
@@ -297,6 +302,11 @@ class WindowStager:
             return
         self._closed = True
         self._native.close()
+        if self._native.poisoned:
+            # a copy never landed and copies were still queued behind it: an engine may write the ring (and
+            # read the arena) at any later time, so neither is freed -- nor are the copy streams waited for
+            self._quarantine()
+            return
         self.copy_stream.synchronize()
         self.copy_stream2.synchronize()
         self.stream.synchronize()
@@ -307,6 +317,25 @@ class WindowStager:
         if tok is not None:
             tok.drop_cached_views(b.data_ptr() for b in self.buffers)
         self.buffers = []
+
+    def _quarantine(self) -> None:
+        """Keep the HBM ring and the pinned arena alive for the life of the process (module-level refs; the
+        connection skips the arena's hipHostUnregister) -- the price of a hung copy engine is a leak, never a
+        late DMA write into freed or reused memory."""
+        _QUARANTINE.append((self.buffers, self.conn.arena, self._native))
+        quarantine = getattr(self.conn, "quarantine", None)
+        if quarantine is not None:
+            quarantine()
+        logger.warning("stager closed with copies pending on a stuck engine: %d ring buffers (%.1f MB) and the "
+                       "arena stay allocated; %d completion signals leaked", len(self.buffers),
+                       len(self.buffers) * self.max_window_bytes / 1e6, int(self._native.leaked_signals))
+        self._staged.clear()
+        self.buffers = []
+
+    @property
+    def poisoned(self) -> bool:
+        """A copy wait failed with copies pending (see ``_quarantine``)."""
+        return bool(self._native.poisoned)
 
     @property
     def bytes_h2d(self) -> int:
@@ -375,4 +404,18 @@ class WindowStager:
                 "copy_streams": self.copy_streams, "free_waits_enqueued": int(self._native.free_waits),
                 "free_on_host": bool(self._native.free_on_host), "direct_dma": self.direct_dma,
                 "direct_dma_reason": self._native.direct_dma_reason,
-                "exchange_issue_wait_s": round(self.post_wait_s, 6)}
+                "exchange_issue_wait_s": round(self.post_wait_s, 6),
+                **issue_wait_summary(self.post_waits)}
+
+
+def issue_wait_summary(waits: list[float]) -> dict:
+    """p50 / p99 / max (ms) of the per-window host waits at the exchange's issue point (empty without one)."""
+    if not waits:
+        return {}
+    s = sorted(waits)
+
+    def q(p: float) -> float:
+        return round(1e3 * s[min(len(s) - 1, int(p * (len(s) - 1) + 0.5))], 4)
+
+    return {"exchange_issue_wait_n": len(s), "exchange_issue_wait_p50_ms": q(0.50),
+            "exchange_issue_wait_p99_ms": q(0.99), "exchange_issue_wait_max_ms": round(1e3 * s[-1], 4)}

@@ -40,17 +40,28 @@ def expected_batch(w: int, local: int) -> torch.Tensor:
     return ops.ref_gather_rows(producer_window(p, rnd), perm=perm, base=local * B, n_rows=B)
 
 
+@pytest.fixture(params=[True, False], ids=["direct_dma", "hip_streams"])
+def direct(request, monkeypatch):
+    """Both staging paths: window copies straight onto SDMA engines through ROCr, and the HIP copy-stream
+    fallback (what runs whenever ROCr refuses direct DMA)."""
+    from ddl_amd import staging
+
+    monkeypatch.setattr(staging, "DIRECT_DMA", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("dispatch", ["lookahead", "inline", "python"])
 @pytest.mark.parametrize("slow", [False, True])
-def test_direct_dma_batches_equal_the_producers_bytes(dispatch, slow):
+def test_direct_dma_batches_equal_the_producers_bytes(dispatch, slow, direct):
     """Every batch, fast or slow consumer (the ring refills a 2-buffer ring many times), through the native
-    engine and the Python dispatch path, equals the producer's window rows in the window's order, bitwise."""
+    engine and the Python dispatch path, on direct DMA and on the HIP copy-stream fallback, equals the
+    producer's window rows in the window's order, bitwise."""
     with ddl_amd.start(n_producers=P) as (env, conn):
         dl = ddl_amd.DistributedDataLoader(IdProducer(N, WIDTH), B, conn, 8, env=env, device=torch.device("cuda"),
                                            shuffle="device", seed=SEED, prefetch_depth=2, copy_batches=True,
                                            native_dispatch=dispatch if dispatch != "python" else False)
         st = dl.stats()
-        assert st["direct_dma"], st.get("direct_dma_reason")
+        assert st["direct_dma"] is direct, st.get("direct_dma_reason")
         w = 0
         for e in range(8):
             for i in range(len(dl)):
@@ -103,6 +114,51 @@ def test_stuck_copy_raises_within_the_timeout_and_close_returns(dispatch):
         assert time.monotonic() - t1 < 15.0
 
 
+@pytest.mark.parametrize("dispatch", ["lookahead", "python"])
+def test_consumer_times_out_first_and_pending_copies_are_quarantined(dispatch):
+    """The consumer's wait on a stuck copy times out BEFORE the retire thread's (which is given 30 s more):
+    the retire thread then gives up on that copy too, and every copy still queued -- the stuck one and the
+    ones behind it -- is quarantined: its completion signal is never destroyed, and close() keeps the HBM
+    ring and the pinned arena allocated (an engine that recovers later writes into live memory, not into
+    freed or reused memory). close() still returns promptly."""
+    from ddl_amd import staging
+    from ddl_amd.exceptions import DDLTimeoutError
+
+    timeout_s = 2.0
+    with ddl_amd.start(n_producers=P) as (env, conn):
+        dl = ddl_amd.DistributedDataLoader(IdProducer(N, WIDTH), B, conn, 8, env=env, device=torch.device("cuda"),
+                                           shuffle="device", seed=SEED, prefetch_depth=2, copy_batches=True,
+                                           timeout_s=timeout_s,
+                                           native_dispatch=dispatch if dispatch != "python" else False)
+        st = dl._stager
+        if not st.direct_dma:
+            pytest.skip(f"no direct DMA here: {dl.stats()['direct_dma_reason']}")
+        st._native.inject_slow_retire(30000)
+        st._native.inject_stuck_copy(3)
+        ring = [b.data_ptr() for b in st.buffers]
+        n_q = len(staging._QUARANTINE)
+        t0 = time.monotonic()
+        with pytest.raises(DDLTimeoutError) as ei:
+            for e in range(8):
+                for i in range(len(dl)):
+                    dl[i]
+                    dl.mark(Marker.END_OF_BATCH)
+                dl.mark(Marker.END_OF_EPOCH)
+        assert "window 3" in str(ei.value)
+        assert time.monotonic() - t0 < 4 * timeout_s + 5.0  # the consumer's own timeout, not the retire's 32 s
+        deadline = time.monotonic() + 5.0
+        while not st.poisoned and time.monotonic() < deadline:  # the retire thread sees the stuck flag
+            time.sleep(0.01)
+        assert st.poisoned and st._native.leaked_signals >= 1
+        t1 = time.monotonic()
+        dl.close()
+        assert time.monotonic() - t1 < 15.0
+        assert len(staging._QUARANTINE) == n_q + 1
+        kept, arena, _ = staging._QUARANTINE[-1]
+        assert [b.data_ptr() for b in kept] == ring and arena is conn.arena
+        assert getattr(conn, "_quarantined", False)
+
+
 def test_direct_dma_copy_timing_is_off_unless_asked():
     """ROCr's async-copy profiling is process-wide: a loader turns it on only with copy_timing=True, and its
     stager turns it off again when it is done with it (reference counted)."""
@@ -121,10 +177,11 @@ def test_direct_dma_copy_timing_is_off_unless_asked():
         dl.close()
 
 
-def test_close_interrupts_a_pending_free_event_wait():
+def test_close_interrupts_a_pending_free_event_wait(direct):
     """The stager waits for a ring buffer's free event (recorded behind the consumer's reads) by polling, so
     close() ends that wait at once even while the consumer's stream is still busy: here a ~3 s spin kernel
-    sits in front of window 0's free event while the stager wants its buffer back for window 2."""
+    sits in front of window 0's free event while the stager wants its buffer back for window 2. Same on the
+    HIP copy-stream fallback (its free-event wait is polled on the host too)."""
     with ddl_amd.start(n_producers=P) as (env, conn):
         # calibrate the spin kernel (its clock is the shader clock): cycles per second
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -136,6 +193,7 @@ def test_close_interrupts_a_pending_free_event_wait():
         dl = ddl_amd.DistributedDataLoader(IdProducer(N, WIDTH), B, conn, 8, env=env, device=torch.device("cuda"),
                                            shuffle="device", seed=SEED, prefetch_depth=2, copy_batches=True,
                                            native_dispatch=False)
+        assert dl._stager.direct_dma is direct and dl._stager._native.free_on_host
         for i in range(len(dl)):
             dl[i]
             if i + 1 < len(dl):

@@ -46,7 +46,8 @@ def test_bench_contract_two_ranks_torchrun():
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(REPO, "bench.py"),
            "--gpus", "2", "--steps", "6", "--warmup", "2", "--window", "64", "--batch", "16", "--idle-steps", "3",
            "--model-dim", "64", "--model-depth", "1"]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=dict(_env(), DDL_DEVICE="cpu"))
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280,
+                       env=dict(_env(), DDL_DEVICE="cpu", DDL_REHEARSAL="1"))
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1
@@ -76,22 +77,58 @@ def test_bench_eight_ranks(method, launch):
     if launch == "torchrun":
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
                "--master-addr", "127.0.0.1", "--master-port", str(free_port()), *args]
-        env = dict(_env(), DDL_DEVICE="cpu")
+        env = dict(_env(), DDL_DEVICE="cpu", DDL_REHEARSAL="1")
     else:
         cmd = [sys.executable, *args]
         env = {k: v for k, v in _env().items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-        env["DDL_DEVICE"] = "cpu"
+        env.update(DDL_DEVICE="cpu", DDL_REHEARSAL="1")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1
     out = json.loads(lines[0])
     assert out["n_gpus"] == 8 and out["config"]["parallelism"] == "dp8" and out["config"]["global_batch"] == 128
+    # the line says what it is: a gloo rehearsal on 8 CPU ranks, not RCCL over 8 GPUs
+    d = out["dist"]
+    assert d["backend"] == "gloo" and d["group_size"] == 8 and d["world_size"] == 8
+    assert d["verified"] is False and d["rehearsal"] is True and d["problems"]
+    assert [r_["rank"] for r_ in d["ranks"]] == list(range(8))
+    assert all(r_["alltoall"]["data_ok"] and r_["alltoall"]["bytes"] > 0 for r_ in d["ranks"])
     assert out["config"]["exchange_fraction"] == 0.5 and out["value"] > 0
     order = out["collective_order"]
     assert order["same_order"] is True and order["groups"] == 1
     assert order["by_kind"]["loader.exchange"] >= 4 and order["by_kind"]["ddp.allreduce"] >= 4
     assert len(out["per_rank"]) == 8 and all(r_["exchange_calls"] >= 3 for r_ in out["per_rank"])
+
+
+@pytest.mark.timeout(300)
+def test_bench_refuses_unverified_eight_ranks():
+    """The driver's N=8 line must prove RCCL over 8 distinct GPUs: 8 ranks that are not (here gloo on the
+    CPU) exit non-zero before measuring, print no JSON line, and say why -- unless DDL_REHEARSAL=1."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(REPO, "bench.py"),
+           "--gpus", "8", "--steps", "4", "--warmup", "1", "--window", "64", "--batch", "16", "--producers", "1",
+           "--a2a-probe-mb", "1"]
+    env = {k: v for k, v in _env().items() if k != "DDL_REHEARSAL"}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=dict(env, DDL_DEVICE="cpu"))
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert "not RCCL" in r.stderr and "'gloo'" in r.stderr and '"group_size": 8' in r.stderr
+
+
+def test_dist_block_single_rank_and_checks():
+    """dist_block / require_verified on hand-made layouts: N=1 needs nothing; N>1 needs RCCL over N distinct
+    GPUs, or the rehearsal label."""
+    from ddl_amd.parallel.report import dist_block, require_verified
+    from ddl_amd.types import DDLEnv
+
+    b = dist_block(DDLEnv(rank=0, world_size=1, hostname="h", device="cpu"))
+    assert b["world_size"] == 1 and b["backend"] is None and b["verified"] is False
+    assert require_verified(b) is None and b["rccl_version"]
+    fake = dict(b, world_size=8, verified=False, rehearsal=False, problems=["8 ranks on 1 distinct GPU(s)"])
+    assert "distinct GPU" in require_verified(fake)
+    assert require_verified(dict(fake, rehearsal=True)) is None
+    assert require_verified(dict(fake, verified=True)) is None
 
 
 @pytest.mark.timeout(60)
@@ -121,6 +158,27 @@ def test_bench_tokens_two_ranks(token_dtype):
     assert out["n_gpus"] == 2 and out["value"] > 0
     assert out["token_wire_dtype"] == ("uint16" if token_dtype == "auto" else "int32")
     assert abs(out["value"] / out["value_est_from_mean_len"] - 1) < 0.2
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("replicate", ["true", "false"])
+def test_bench_resident_two_ranks(replicate):
+    """BASELINE config 5's bench at 2 ranks (CPU/gloo rehearsal): both layouts run, say which they are, and
+    the replicated one moves nothing per step."""
+    import json
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(REPO, "benchmarks", "bench_resident.py"), "--steps", "6", "--warmup", "2", "--batch", "8",
+           "--n-samples", "256", "--depths", "1", "--replicate", replicate]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280,
+                       env=dict(_env(), DDL_DEVICE="cpu", DDL_REHEARSAL="1"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    (res,) = out["sweep"]
+    assert out["n_gpus"] == 2 and res["samples_per_s"] > 0 and out["dist"]["rehearsal"] is True
+    assert res["mode"] == ("replicated" if replicate == "true" else "sharded")
+    assert (res["xgmi_GB_sent_per_rank_steps"] == 0) == (replicate == "true")
 
 
 @pytest.mark.timeout(200)

@@ -41,18 +41,20 @@ def shared_source():
     src.close()
 
 
-@pytest.mark.parametrize("world", [1, 2, 4])
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
 def test_indexed_order_is_world_size_invariant(shared_source, world):
     from ddl_amd.permutation import EpochOrder
 
     n, gb, epochs = shared_source.n, 64, 2
-    res = run_ranks(_indexed_rank, world, n, gb, epochs, shared_source.name)
+    res = run_ranks(_indexed_rank, world, n, gb, epochs, shared_source.name, timeout=280)
     order = EpochOrder(n, gb, seed=7)
     for e in range(epochs):
         ref = order.perm(e).full()[: order.batches_per_epoch * gb].reshape(-1, gb)
         per_rank = [r[0][e].reshape(-1, gb // world) for r in res]
         merged = np.concatenate(per_rank, axis=1)  # global batch g = concat of rank slices
         assert np.array_equal(merged, ref)
+        assert len(np.unique(merged)) == merged.size  # exactly once per epoch
 
 
 def test_indexed_resume_at_different_world_size(shared_source):
@@ -73,17 +75,17 @@ def test_indexed_resume_at_different_world_size(shared_source):
     assert np.array_equal(out[1], ref1)
 
 
-def _exchange_rank(rank, world, method, fraction):
+def _exchange_rank(rank, world, method, fraction, epochs=3):
     import ddl_amd
     from ddl_amd import Marker
     from tests.helpers import IdProducer
 
     eps = []
     with ddl_amd.start(n_producers=2) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(IdProducer(40, 6), 8, conn, 3, fraction, method, env=env,
+        dl = ddl_amd.DistributedDataLoader(IdProducer(40, 6), 8, conn, epochs, fraction, method, env=env,
                                            copy_batches=True, seed=1)
         assert dl._exchange_fn is not None
-        for e in range(3):
+        for e in range(epochs):
             rows = []
             for i, (a, b) in enumerate(dl):
                 rows.append(torch.cat([a, b], 1))
@@ -94,13 +96,38 @@ def _exchange_rank(rank, world, method, fraction):
     return eps, n_ex
 
 
-@pytest.mark.parametrize("method,world", [("alltoall", 2), ("alltoall", 4), ("sendrecv_replace", 2),
-                                          ("sendrecv_replace", 3)])
+def _partner_cycles(n: int, seed: int, window: int) -> list[int]:
+    """Cycle lengths of the sendrecv_replace partner permutation of ``window`` (send_to of every rank)."""
+    from ddl_amd.parallel.shuffle import derangement_partners
+
+    to = [derangement_partners(n, r, np.random.default_rng([seed & 0xFFFFFFFF, window]))[0] for r in range(n)]
+    seen, out = set(), []
+    for r in range(n):
+        c, x = 0, r
+        while x not in seen:
+            seen.add(x)
+            x, c = to[x], c + 1
+        if c:
+            out.append(c)
+    return sorted(out)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("method,world", [("alltoall", 2), ("alltoall", 4), ("alltoall", 8), ("sendrecv_replace", 2),
+                                          ("sendrecv_replace", 3), ("sendrecv_replace", 8)])
 def test_global_shuffle_exchange_conserves_rows(method, world):
-    res = run_ranks(_exchange_rank, world, method, 0.5)
+    """Exactly-once delivery across the exchange: every (rank, producer, row) key of every window is delivered
+    once, by some rank, every epoch. At W = 8 the reference's partner rule can split the ranks into several
+    cycles (5 + 3); the run covers such a window (window 3 with seed 1), where the reference's
+    "prevents split graph" comment would have it deadlock or lose rows."""
+    epochs = 4 if world == 8 else 3
+    if method == "sendrecv_replace" and world == 8:
+        assert _partner_cycles(8, 1, 3) == [3, 5]  # a split pattern among the exchanged windows
+        assert _partner_cycles(8, 1, 0) == [8]
+    res = run_ranks(_exchange_rank, world, method, 0.5, epochs, timeout=280)
     n_ex = res[0][1]
     assert n_ex > 0
-    for e in range(3):
+    for e in range(epochs):
         all_rows = np.concatenate([r[0][e] for r in res])
         # every rank's window rows (rank, producer, i) are still delivered exactly once overall
         keys = {tuple(x) for x in all_rows[:, :3].tolist()}

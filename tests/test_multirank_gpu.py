@@ -24,7 +24,8 @@ from tests.mp_harness import free_port, run_ranks
 pytestmark = pytest.mark.gpu
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-GPU_GLOO = {"DDL_DEVICE": "", "DDL_BACKEND": "gloo"}  # "" = not forced to the CPU
+# "" = not forced to the CPU; several ranks share the one card of a gpurun box: a labelled rehearsal
+GPU_GLOO = {"DDL_DEVICE": "", "DDL_BACKEND": "gloo", "DDL_REHEARSAL": "1"}
 
 
 def _exchange_rank_gpu(rank, world, method, fraction, slow=0.0):
@@ -115,6 +116,31 @@ def test_bench_multirank_device_path(n, launch):
         assert r["dispatch"]["host_us_per_batch"]["get"] > 0
     assert out["config"]["dispatch"] == out["per_rank"][0]["dispatch"]["mode"]
     assert out["indexed"] and "error" not in out["indexed"] and out["indexed"]["value"] > 0
+    # the line labels itself: gloo ranks sharing one card, a rehearsal (not an N-GPU RCCL measurement)
+    d = out["dist"]
+    assert d["backend"] == "gloo" and d["group_size"] == n and d["distinct_gpus"] == 1
+    assert d["rehearsal"] is True and d["verified"] is False and len(d["problems"]) >= 2
+    assert all(r_["alltoall"]["data_ok"] for r_ in d["ranks"])
+    for r in out["per_rank"]:
+        w = r["exchange_issue_wait_timed"]
+        assert w["exchange_issue_wait_n"] > 0 and w["exchange_issue_wait_p99_ms"] >= w["exchange_issue_wait_p50_ms"]
+
+
+@pytest.mark.timeout(120)
+def test_ranks_sharing_the_card_are_refused_without_rehearsal():
+    """Two ranks on one GPU without DDL_REHEARSAL: the layout is refused at start (TopologyError: more ranks
+    than visible GPUs), bench exits non-zero and prints no JSON line -- no silent device sharing."""
+    args = [os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "1", "--idle-steps", "0",
+            "--pressure-ratio", "0", "--order", "window"]
+    env = {k: v for k, v in os.environ.items() if k not in ("DDL_REHEARSAL", "DDL_BACKEND", "WORLD_SIZE", "RANK",
+                                                            "LOCAL_RANK", "MASTER_PORT")}
+    env.update(PYTHONPATH=REPO, DDL_DEVICE="")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), *args]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=100, env=env)
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert "TopologyError" in r.stderr and "share a device" in r.stderr
 
 
 @pytest.mark.timeout(240)

@@ -7,15 +7,20 @@ import torch
 from tests.mp_harness import run_ranks
 
 
-def _resident_rank(rank, world, name, n, gb, epochs, depth, resume=None, stop=None):
+def _resident_rank(rank, world, name, n, gb, epochs, depth, resume=None, stop=None, replicate=False):
     import ddl_amd
     from ddl_amd.models import SharedArraySource
     from ddl_amd.resident import ResidentGlobalLoader
 
     src = SharedArraySource(name, n, (3,), "int64")
     with ddl_amd.start(n_producers=0) as (env, _):
-        dl = ResidentGlobalLoader(src, gb, env, seed=11, depth=depth, n_epochs=epochs, resume_state=resume)
-        assert dl.shard.shape[0] == dl.hi - dl.lo
+        dl = ResidentGlobalLoader(src, gb, env, seed=11, depth=depth, n_epochs=epochs, resume_state=resume,
+                                  replicate=replicate)
+        if dl.replicated:  # the whole dataset (plus <= W-1 padding rows) on every rank, bit-exact
+            assert dl.shard.shape[0] == dl.S * world >= n
+            assert torch.equal(dl.shard[:n], src.tensor())
+        else:
+            assert dl.shard.shape[0] == dl.hi - dl.lo
         out = []
         while dl.epoch < epochs:
             e = dl.epoch
@@ -41,57 +46,78 @@ def src():
     s.close()
 
 
-@pytest.mark.parametrize("world,depth", [(1, 1), (2, 2), (3, 3), (4, 2)])
-def test_resident_exact_global_order(src, world, depth):
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("replicate", [False, True])
+@pytest.mark.parametrize("world,depth", [(1, 1), (2, 2), (3, 3), (4, 2), (8, 2)])
+def test_resident_exact_global_order(src, world, depth, replicate):
+    """Sharded (per-step all-to-all) and replicated (all-gather bring-up, no per-step collective) deliver the
+    identical union order -- global batch g of the epoch permutation -- at W = 1..8: every sample exactly
+    once per epoch."""
     from ddl_amd.permutation import EpochOrder
 
     gb = 48
-    res = run_ranks(_resident_rank, world, src.name, src.n, gb, 2, depth)
+    res = run_ranks(_resident_rank, world, src.name, src.n, gb, 2, depth, None, None, replicate, timeout=280)
     order = EpochOrder(src.n, gb, 11)
     bpe = order.batches_per_epoch
     for e in range(2):
         ref = order.perm(e).full()[: bpe * gb].reshape(bpe, gb)
         merged = np.concatenate([r[0][e].reshape(bpe, gb // world) for r in res], axis=1)
         assert np.array_equal(merged, ref)
-    if world > 1:
-        assert sum(r[2]["bytes_exchanged"] for r in res) > 0
+        assert len(np.unique(merged)) == merged.size  # exactly once
+    st = [r[2] for r in res]
+    if world > 1 and not replicate:
+        assert sum(s_["bytes_exchanged"] for s_ in st) > 0
+    if world > 1 and replicate:  # the per-step traffic is gone; the bring-up moved (W-1)/W of the data
+        assert all(s_["replicated"] and s_["bytes_exchanged"] == 0 for s_ in st)
+        assert all(s_["bytes_replicated"] >= (world - 1) * (src.n // world) * 24 for s_ in st)
 
 
-def test_resident_resume_across_world_sizes(src):
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("save,resume", [((2, False), (1, False)), ((8, True), (2, False)), ((4, False), (8, True))])
+def test_resident_resume_across_world_sizes(src, save, resume):
+    """A checkpoint taken at one (W, mode) resumes at another: sharded <-> replicated, 1 <-> 8 ranks."""
     from ddl_amd.permutation import EpochOrder
 
     gb = 48
-    (_, sd, _), _ = run_ranks(_resident_rank, 2, src.name, src.n, gb, 2, 2, None, (0, 3))
-    assert sd["global_batch_cursor"] == 4
-    (out, _, _), = run_ranks(_resident_rank, 1, src.name, src.n, gb, 2, 1, sd)
+    (w0, rep0), (w1, rep1) = save, resume
+    res = run_ranks(_resident_rank, w0, src.name, src.n, gb, 2, 2, None, (0, 3), rep0, timeout=280)
+    sd = res[0][1]
+    assert sd["global_batch_cursor"] == 4 and all(r[1] == sd for r in res)
+    out = run_ranks(_resident_rank, w1, src.name, src.n, gb, 2, 1, sd, None, rep1, timeout=280)
     order = EpochOrder(src.n, gb, 11)
     bpe = order.batches_per_epoch
-    assert np.array_equal(out[0], order.perm(0).full()[4 * gb: bpe * gb])
-    assert np.array_equal(out[1], order.perm(1).full()[: bpe * gb])
+    for e, first in ((0, 4), (1, 0)):
+        merged = np.concatenate([r[0][e].reshape(-1, gb // w1) for r in out], axis=1).reshape(-1)
+        assert np.array_equal(merged, order.perm(e).full()[first * gb: bpe * gb])
 
 
-def _scatter_rank(rank, world, name, n, gb):
+def _scatter_rank(rank, world, name, n, gb, replicate=False):
     import ddl_amd
     from ddl_amd.models import SharedArraySource
     from ddl_amd.resident import ResidentGlobalLoader
 
     src = SharedArraySource(name, n, (3,), "int64") if rank == 0 else None
     with ddl_amd.start(n_producers=0) as (env, _):
-        dl = ResidentGlobalLoader(src, gb, env, seed=11, n_epochs=1, scatter_from=0, chunk_bytes=24 * 50)
-        shard = dl.shard.clone()
+        dl = ResidentGlobalLoader(src, gb, env, seed=11, n_epochs=1, scatter_from=0, chunk_bytes=24 * 50,
+                                  replicate=replicate)
+        shard = dl.shard[:n].clone() if dl.replicated else dl.shard.clone()
         rows = torch.cat([b[:, 0].clone() for b in dl]).numpy()
-        return shard.numpy(), rows, dl.lo, dl.hi, dl.stats()["bytes_exchanged"]
+        lo, hi = (0, n) if dl.replicated else (dl.lo, dl.hi)
+        st = dl.stats()
+        return shard.numpy(), rows, lo, hi, st["bytes_exchanged"] + st["bytes_replicated"]
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_resident_scatter_from_one_rank(src, world):
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("replicate", [False, True])
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_resident_scatter_from_one_rank(src, world, replicate):
     from ddl_amd.permutation import EpochOrder
 
     gb = 48
-    res = run_ranks(_scatter_rank, world, src.name, src.n, gb)
+    res = run_ranks(_scatter_rank, world, src.name, src.n, gb, replicate, timeout=280)
     full = src.tensor().numpy()
     for shard, _, lo, hi, _ in res:
-        assert np.array_equal(shard, full[lo:hi])  # every rank received exactly its shard
+        assert np.array_equal(shard, full[lo:hi])  # every rank received exactly its shard (or the whole set)
     order = EpochOrder(src.n, gb, 11)
     bpe = order.batches_per_epoch
     ref = order.perm(0).full()[: bpe * gb].reshape(bpe, gb)
