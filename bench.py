@@ -419,10 +419,11 @@ def indexed_phase(args, env, dev, barrier, sync, spare=None) -> dict:
                 + _pressure_batches(args)
             dl = ddl_amd.DistributedDataLoader(
                 IndexedProducer(src, gb, seed=args.seed, host_threads=args.index_threads), args.batch, spare,
-                math.ceil(total / bpe) + 2, mode="indexed", env=env, device=dev, n_slots=2, auto_mark=True,
-                copy_timing=True,  # the landed-bytes accounting of the timed region
-                copy_batches=False)  # views, as the headline's batches are: the checksum reads them in stream
-            # order before the window's release (auto_mark would otherwise copy every batch, 77 MB D2D each)
+                math.ceil(total / bpe) + 2, env=env, device=dev, auto_mark=True,
+                order=ddl_amd.OrderSpec(mode="indexed"),
+                staging=ddl_amd.StagingSpec(n_slots=2, copy_timing=True),  # copy timing: the landed-bytes accounting
+                output=ddl_amd.OutputSpec(copy_batches=False))  # views, as the headline's batches are: the checksum
+            # reads them in stream order before the window's release (auto_mark would copy every batch, 77 MB D2D)
             it = forever(dl)
             w0 = dl.stats().get("stager_wait_producer_s", 0.0)
             rate, ms, acct = _timed_feed(args, env, it, acc, barrier, sync, "bench.indexed", dl=dl)
@@ -552,10 +553,12 @@ def main(argv=None) -> int:
             norm = {"mean": [0.485, 0.456, 0.406], "std": [0.229, 0.224, 0.225], "layout": "chw"}
         dl = ddl_amd.DistributedDataLoader(
             producer, args.batch, conn, n_epochs, args.exchange, args.exchange_method, env.rank, env.world_size,
-            env=env, device=dev, out_dtype=torch.bfloat16, shuffle=args.shuffle, seed=args.seed,
-            n_slots=args.slots, prefetch_depth=args.depth, normalize=norm,
-            native_dispatch=False if args.dispatch == "python" else args.dispatch,
-            copy_timing=True)  # device times of every window copy: the pro-rata H2D accounting below
+            env=env, device=dev, output=ddl_amd.OutputSpec(dtype=torch.bfloat16, normalize=norm),
+            order=ddl_amd.OrderSpec(shuffle=args.shuffle, seed=args.seed),
+            staging=ddl_amd.StagingSpec(
+                n_slots=args.slots, prefetch_depth=args.depth,
+                native_dispatch=False if args.dispatch == "python" else args.dispatch,
+                copy_timing=True))  # device times of every window copy: the pro-rata H2D accounting below
         acc = ops.ChecksumAccumulator(dev)  # one streaming launch per batch
 
         def batches():

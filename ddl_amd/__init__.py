@@ -20,6 +20,9 @@ __all__ = [
     "EpochOrder",
     "IndexedProducer",
     "DataLoader",
+    "OutputSpec",
+    "StagingSpec",
+    "OrderSpec",
     "ops",
 ]
 
@@ -29,6 +32,7 @@ from .dataloader import DistributedDataLoader
 from .datasetwrapper import ProducerFunctionSkeleton
 from .parallel.launcher import distributed_dataloader, start
 from .permutation import EpochOrder, FeistelPermutation
+from .specs import OrderSpec, OutputSpec, StagingSpec
 from .types import DDLEnv, Marker
 
 

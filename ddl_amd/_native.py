@@ -8,6 +8,12 @@ If an extension is missing, or STALE -- the source hash it embeds differs from
 the ``csrc/`` tree's (``_build.is_stale``) -- it is (re)built in-tree before the
 import (under a file lock, so concurrently starting producer processes do not
 race); with ``DDL_AMD_NO_AUTOBUILD=1`` either case raises instead.
+
+A process that has loaded an extension pins it for its children: ``DDL_NATIVE_PIN`` (set here, inherited
+by every producer or helper process spawned later) names each loaded ``.so`` and the source hash it
+carries. A child loading the same file never rebuilds it -- it loads exactly that binary, or raises
+``NativeExtensionError`` when the file changed under the job (``csrc/`` edited and rebuilt mid-run), so a
+consumer and its producers never run different builds over one shared arena.
 """
 
 from __future__ import annotations
@@ -56,11 +62,53 @@ def _check_fresh(name: str, which: str) -> None:
         raise NativeExtensionError(f"ddl_amd.{name} is stale and failed to rebuild: {e}") from e
 
 
+_PIN_ENV = "DDL_NATIVE_PIN"
+
+
+def _pins() -> dict[str, str]:
+    """``{realpath of a loaded .so: its source hash}`` pinned by an ancestor process."""
+    out = {}
+    for item in filter(None, os.environ.get(_PIN_ENV, "").split(";")):
+        path, _, digest = item.rpartition("=")
+        if path:
+            out[path] = digest
+    return out
+
+
+def _pin(path: str) -> None:
+    from . import _build
+
+    digest = _build.embedded_hash(path)
+    if digest is None:
+        return
+    pins = _pins()
+    pins[os.path.realpath(path)] = digest
+    os.environ[_PIN_ENV] = ";".join(f"{p}={d}" for p, d in pins.items())
+
+
+def _check_pinned(name: str, which: str) -> bool:
+    """True when an ancestor pinned this extension's file: it is loaded as is (no staleness check, no rebuild),
+    provided it still carries the pinned hash; a file that changed under the job raises."""
+    from . import _build
+
+    target = _build.runtime_target() if which == "runtime" else _build.hip_target()
+    want = _pins().get(os.path.realpath(target))
+    if want is None:
+        return False
+    have = _build.embedded_hash(target)
+    if have != want:
+        raise NativeExtensionError(
+            f"ddl_amd.{name} changed under the running job: the parent process loaded the build of source hash "
+            f"{want[:12]}, the file now holds {str(have)[:12]} (rebuilt mid-run?); restart the job")
+    return True
+
+
 def _load(name: str, which: str) -> ModuleType:
     with _lock:
         if name in _cache:
             return _cache[name]
-        _check_fresh(name, which)
+        if not _check_pinned(name, which):
+            _check_fresh(name, which)
         try:
             mod = importlib.import_module(f"ddl_amd.{name}")
         except ImportError as first:
@@ -72,6 +120,8 @@ def _load(name: str, which: str) -> ModuleType:
             except Exception as e:  # pragma: no cover - depends on toolchain
                 raise NativeExtensionError(f"ddl_amd.{name} failed to build/load: {e}") from e
         _cache[name] = mod
+        if getattr(mod, "__file__", None):
+            _pin(mod.__file__)
         return mod
 
 

@@ -42,34 +42,22 @@ from typing import Any, Iterator
 import torch
 
 from . import ops
+from .batching import WindowBatchMixin, window_perm_key
 from .checkpoint import CheckpointMixin
 from .connection import Connection
 from .engine_dispatch import NativeDispatchMixin
 from .datasetwrapper import ProducerFunctionSkeleton
 from .exceptions import ShapeMismatchError
 from .ops import _dtypes
-from .permutation import FeistelPermutation
+from .specs import MODES, OrderSpec, OutputSpec, StagingSpec, resolve
 from .types import DDLEnv, Marker, MetaData_Consumer_To_Producer, MetaData_Producer_To_Consumer
-from .utils.logging import for_all_methods, with_logging
+from .utils.logging import with_logging
 from .utils import streams
 from .utils.tracing import LoaderMetrics, trace_range
+from .verify import OrderVerifyMixin
 
 _FAULT_RANK = bool(os.environ.get("DDL_FAULT_RANK"))  # test hook (utils/faults.py)
-MODES = ("do_not_split_along_epoch", "split_along_epoch", "window", "indexed")
-
-
-def _mix(a: int, b: int) -> int:
-    """64-bit mix of two ints (splitmix64 finaliser over a*phi + b)."""
-    z = (int(a) * 0x9E3779B97F4A7C15 + int(b) + 0x632BE59BD9B4E019) & ((1 << 64) - 1)
-    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & ((1 << 64) - 1)
-    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & ((1 << 64) - 1)
-    return z ^ (z >> 31)
-
-
-def window_perm_key(producer: int, round_: int) -> int:
-    """Key of the device permutation of one window visit (producer ``p``, round ``seq``): a 64-bit
-    mix of both, so every (producer, round) pair has its own order at any producer count."""
-    return _mix(producer, round_) & ((1 << 63) - 1)
+__all__ = ["DistributedDataLoader", "DistributedDataloaderABC", "MODES", "window_perm_key"]
 
 
 class DistributedDataloaderABC(ABC):
@@ -105,12 +93,16 @@ class DistributedDataloaderABC(ABC):
     def mark(self, mark: Marker) -> None: ...
 
 
-@for_all_methods(with_logging, exclude=["__getitem__", "__len__", "__iter__", "mark", "_on_batch_end",
-                                        "_window", "_batch_from_window", "_schedule", "_engine_batch",
-                                        "_engine_provide", "_release_window", "_advance_window",
-                                        "_advance_to_next_producer", "_begin_window", "_update_len",
-                                        "_end_access_epoch", "_device_batch", "_enqueue_batch"])
-class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDataloaderABC):
+class DistributedDataLoader(WindowBatchMixin, OrderVerifyMixin, NativeDispatchMixin, CheckpointMixin,
+                            DistributedDataloaderABC):
+    """The reference's eight arguments (reference ddl/mpi_dataloader.py:108-118), then the rank environment,
+    the device, the three option records of ``specs.py`` (``output=OutputSpec(...)``,
+    ``staging=StagingSpec(...)``, ``order=OrderSpec(...)``), ``auto_mark`` (iteration marks the batches:
+    a torch DataLoader drop-in) and ``resume_state`` (a ``state_dict()``). The flat keywords of earlier
+    releases (``out_dtype=``, ``seed=``, ``prefetch_depth=`` ...) are deprecated aliases of the records'
+    fields."""
+
+    @with_logging
     def __init__(
         self,
         producer_function: ProducerFunctionSkeleton,
@@ -122,35 +114,18 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
         instance_idx: int = 0,
         n_instances: int = 1,
         *,
-        device: str | torch.device | None = None,
-        out_dtype: Any = None,
-        shuffle: str = "none",
-        seed: int = 0,
-        n_slots: int | None = None,
-        prefetch_depth: int = 4,
-        mode: str = "window",
-        normalize: dict | None = None,
-        augment: dict | None = None,
-        contiguous: bool = False,
         env: DDLEnv | None = None,
+        device: str | torch.device | None = None,
+        output: OutputSpec | None = None,
+        staging: StagingSpec | None = None,
+        order: OrderSpec | None = None,
         auto_mark: bool = False,
         resume_state: dict | None = None,
-        timeout_s: float | None = None,
-        host_threads: int = 4,
         debug_checksum: bool = False,
-        copy_batches: bool | None = None,
-        collate: str | None = None,
-        pad_id: int = 0,
-        native_dispatch: bool | str = True,
-        token_rows: str = "exact",
-        verify_order: bool | None = None,
-        max_ahead: int | None = None,
-        copy_timing: bool = False,
+        **legacy: Any,
     ):
-        if mode not in MODES:
-            raise ValueError(f"unknown mode {mode!r}; one of {MODES}")
-        if shuffle not in ("none", "device"):
-            raise ValueError("shuffle must be 'none' or 'device'")
+        out, stg, odr = resolve(output, staging, order, legacy)
+        self.output_spec, self.staging_spec, self.order_spec = out, stg, odr
         self.batch_size = int(batch_size)
         self.connection = connection
         self.n_epochs = int(n_epochs)
@@ -158,41 +133,34 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
         self.exchange_method = exchange_method
         self.instance_idx = instance_idx
         self.n_instances = n_instances
-        self.shuffle = shuffle
-        self.seed = int(seed)
+        self.shuffle = odr.shuffle
+        self.seed = int(odr.seed)
         # default: what the producer asks for (ProducerFunctionSkeleton.preferred_slots, 1 unless its rounds
         # rewrite the whole window)
+        n_slots = stg.n_slots
         self.n_slots = int(n_slots if n_slots is not None else getattr(producer_function, "preferred_slots", 1))
-        self.prefetch_depth = int(prefetch_depth)
-        self.mode = "do_not_split_along_epoch" if mode == "window" else mode
-        self.normalize = normalize
-        # on-device RandomResizedCrop + flip (GPU only): {"size": (224, 224), "scale": (0.08, 1.0),
-        # "ratio": (3/4, 4/3), "flip_p": 0.5, "layout": "chw" | "hwc"}; normalize's mean/std apply after it
-        aug_keys = {"size", "scale", "ratio", "flip_p", "layout"}
-        if augment is not None and not set(augment) <= aug_keys:
-            raise ValueError(f"unknown augment keys {sorted(set(augment) - aug_keys)}")
-        self.augment = augment
-        self.contiguous = contiguous
+        self.prefetch_depth = int(stg.prefetch_depth)
+        self.mode = "do_not_split_along_epoch" if odr.mode == "window" else odr.mode
+        self.normalize = out.normalize
+        self.augment = out.augment  # on-device RandomResizedCrop + flip (GPU only); normalize applies after it
+        self.contiguous = out.contiguous
         self.env = env
         self.auto_mark = auto_mark
         # Zero-copy views alias the window and die when it is released (reference
         # semantics, ddl/mpi_dataloader.py:193). With auto_mark the caller does not
         # control the release, so batches are owned copies by default.
-        self.copy_batches = auto_mark if copy_batches is None else bool(copy_batches)
-        if collate not in (None, "tokens"):
-            raise ValueError("collate must be None or 'tokens'")
-        self.collate = collate
-        self.pad_id = pad_id
+        self.copy_batches = auto_mark if out.copy_batches is None else bool(out.copy_batches)
+        self.collate = out.collate
+        self.pad_id = out.pad_id
         # collate="tokens", pack mode: "exact" -> [packed rows, S] per batch; "fixed" -> every batch has the
         # window layout's max rows (padding rows past the packed ones): static shapes, and no per-batch
         # slicing of four [R, S] outputs on the host (~2 us per tensor view)
-        if token_rows not in ("exact", "fixed"):
-            raise ValueError("token_rows must be 'exact' or 'fixed'")
-        self.token_rows = token_rows
+        self.token_rows = out.token_rows
         self.debug_checksum = debug_checksum
         # device times of every window copy from the first one (WindowStager.copy_timing: bytes_in_interval and
         # copy_summary need them; direct DMA takes them from a process-wide ROCr switch, so off by default)
-        self.copy_timing = bool(copy_timing)
+        self.copy_timing = bool(stg.copy_timing)
+        timeout_s, host_threads, out_dtype = stg.timeout_s, stg.host_threads, out.dtype
         self.metrics = LoaderMetrics()
         self.timeout_s = timeout_s if timeout_s is not None else (connection.timeout_s if connection else 600.0)
         self._timeout_ms = int(self.timeout_s * 1000)
@@ -234,9 +202,7 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
         # under 16 MB -- "window" (one kernel builds all of a window's batches at its first get) when a
         # window holds several small gather/split batches -- and lookahead (one batch ahead on the batch
         # stream) above 16 MB; False: the Python dispatch path
-        if native_dispatch not in (True, False, "auto", "inline", "lookahead", "window"):
-            raise ValueError("native_dispatch must be a bool or 'auto' / 'inline' / 'lookahead' / 'window'")
-        self.native_dispatch = "auto" if native_dispatch is True else native_dispatch
+        self.native_dispatch = "auto" if stg.native_dispatch is True else stg.native_dispatch
         self._engine = None                   # native per-batch dispatch (csrc/kernels/engine.cpp)
         self._fields = None                   # MapDatasetSource rows: (fields, kind) to unpack batches into
         # Run-ahead bound (GPU device path): a host that never synchronises with its step (no .item(), no
@@ -246,9 +212,7 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
         # fetching batch i waits (on the host) for the event of batch i - max_ahead: the copies then follow
         # the step's pace when the step is the bottleneck. 0 disables. (Default 16; off with the
         # global-shuffle exchange, see _setup_exchange.)
-        ma = 16 if max_ahead is None else int(max_ahead)
-        if ma < 0:
-            raise ValueError("max_ahead must be >= 0")
+        ma = 16 if stg.max_ahead is None else int(stg.max_ahead)
         self.max_ahead = ma
         # an event every max_ahead / 4 batches (one per batch raised the GPU idle behind a slow step from
         # 0.12% to 0.17-0.18%: archive/profiles/r4_eleventh); a small ring of them is reused
@@ -308,7 +272,7 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
             self.windows_per_epoch = P
         else:
             self.windows_per_epoch = 1
-        self._setup_verify(verify_order, md, env.rank if env else instance_idx, env.world_size if env else n_instances)
+        self._setup_verify(odr.verify, md, env.rank if env else instance_idx, env.world_size if env else n_instances)
         self.sample_shape = self.shapes[0][1:]
         self.window_dtype = self.dtypes[0]
         # MapDatasetSource rows: batches come back in the dataset's sample structure (typed views)
@@ -364,6 +328,7 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
         return self._len
 
     # --------------------------------------------------------------- exchange
+    @with_logging
     def _setup_exchange(self) -> None:
         self._exchange_fn = None
         world = self.env.world_size if self.env else 1
@@ -382,50 +347,6 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
         # another rank's progress (the same rule as the device hand-off below). The exchange itself
         # bounds the run-ahead: window w + 2 is not exchanged before every rank has posted it.
         self._ahead_q = None
-
-    # ----------------------------------------------------------------- verification
-    def _setup_verify(self, verify_order: bool | None, md, rank, world) -> None:
-        """``verify_order`` (default ``$DDL_VERIFY_ORDER=1``): check every window of the indexed order
-        against the epoch order before its batches are used. ``IndexedProducer`` publishes (epoch,
-        global batch, digest of the sample ids) in the slot tags of each window; the consumer recomputes
-        them from its own cursor and ``EpochOrder``, so a producer/consumer cursor disagreement, a stale
-        or reused slot, or a wrong resume position raises ``DataIntegrityError`` instead of silently
-        training on the wrong samples (race detection). Costs one host-side Feistel
-        evaluation of the local batch and a hash per window."""
-        import os
-
-        self._verify = None
-        self.verified_windows = 0
-        want = verify_order if verify_order is not None else os.environ.get("DDL_VERIFY_ORDER") == "1"
-        if not want:
-            return
-        ex = md[0].extra if md else {}
-        ok = (self.mode == "indexed" and self.collate is None and "order_seed" in ex
-              and "windows_per_epoch" not in ex)  # one global batch per window (IndexedProducer)
-        if not ok:
-            if verify_order:
-                raise ValueError("verify_order needs mode='indexed' windows from IndexedProducer")
-            return
-        from .permutation import EpochOrder
-
-        self._verify = EpochOrder(int(ex["n_samples"]), int(ex["global_batch"]), int(ex["order_seed"]),
-                                  bool(ex.get("order_drop_last", True)), bool(ex.get("order_shuffle", True)))
-        self._verify_rank = (int(rank or 0), int(world or 1))
-
-    def _verify_window(self, w: int, tags) -> None:
-        from .exceptions import DataIntegrityError
-        from .permutation import ids_digest
-
-        epoch, g = divmod(int(w), self.windows_per_epoch)
-        ids = self._verify.indices(epoch, g, *self._verify_rank)
-        want = (epoch, g, ids_digest(ids))
-        got = tuple(int(x) for x in tuple(tags)[:3])
-        if got != want:
-            raise DataIntegrityError(
-                f"window {w}: the epoch order expects (epoch {epoch}, global batch {g}, ids digest {want[2]:#x}); "
-                f"the producer published (epoch {got[0] if got else None}, global batch "
-                f"{got[1] if len(got) > 1 else None}, ids digest {got[2] if len(got) > 2 else 0:#x})")
-        self.verified_windows += 1
 
     # ----------------------------------------------------------------- access
     def _ensure_posted(self, w: int) -> None:
@@ -546,122 +467,6 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
             self.checksums.append(int(ops.checksum(out[0] if isinstance(out, tuple) else out).item()))
         return out if self._fields is None else self._unpack(out)
 
-    def _unpack(self, out):
-        from .models.datasets import unpack_fields
-
-        rows = out[0] if isinstance(out, (tuple, list)) else out
-        return unpack_fields(rows, *self._fields)
-
-    # ---------------------------------------------------------- batch stream
-    def _produces_copy(self) -> bool:
-        """True when a batch is built by a kernel (not a zero-copy view of the window)."""
-        return (self.shuffle == "device" or self.out_dtype not in (None, self.window_dtype) or self.augment is not None
-                or self.normalize is not None or self.copy_batches or self.contiguous or self.collate is not None)
-
-    def _enqueue_batch(self, sw, p: int, s: int, local: int):
-        """Build batch ``local`` of window ``sw`` on the batch stream; returns (outputs, ready event)."""
-        bs = self._batch_stream
-        self._stager.wait_ready(sw, bs)
-        with streams.on_stream(bs):
-            out = self._batch_from_window(sw, p, s, local)
-            ev = torch.cuda.Event()
-            ev.record(bs)
-        if local + 1 == self.batches_per_window[p]:
-            # the window's free event: right after its last batch kernel, NOT at release time behind the
-            # next window's lookahead kernel (which waits for that window's copy: the copy after it would
-            # then wait for a copy plus a gather)
-            self._win_done[sw.index] = ev
-        return out, ev
-
-    def _device_batch(self, sw, p: int, s: int, local: int, bpw: int):
-        """Batch kernels run on their own stream one batch ahead of the consumer:
-        batch l+1's gather overlaps the training step on batch l, and the compute
-        stream only waits on an event (no host sync)."""
-        hit = self._lookahead.pop((self.window, local), None)
-        out, ev = hit if hit is not None else self._enqueue_batch(sw, p, s, local)
-        cur = streams.current(self.device.index)
-        cur.wait_event(ev)
-        for t in (out.values() if isinstance(out, dict) else out):
-            if isinstance(t, torch.Tensor) and t.is_cuda:
-                t.record_stream(cur)
-        if local + 1 < bpw:
-            if (self.window, local + 1) not in self._lookahead:
-                self._lookahead[(self.window, local + 1)] = self._enqueue_batch(sw, p, s, local + 1)
-        elif self.window_in_epoch + 1 < self.windows_per_epoch or self.epoch + 1 < self.n_epochs:
-            # last batch of this window: start the next window's first batch if it is already in HBM
-            nxt = self._stager.peek(self.window + 1)
-            if nxt is not None and (self.window + 1, 0) not in self._lookahead:
-                np_, ns = self._schedule(self.window + 1)
-                self._lookahead[(self.window + 1, 0)] = self._enqueue_batch(nxt, np_, ns, 0)
-        return out
-
-    def _perm_for(self, p: int, seq: int) -> FeistelPermutation | None:
-        if self.shuffle != "device":
-            return None
-        # key = (seed, producer, round): every window visit gets a fresh order.
-        return FeistelPermutation(self.metadata_from_producer[p].nData, self.seed, window_perm_key(p, seq))
-
-    def _batch_from_window(self, sw, p: int, s: int, local: int):
-        B = self.batch_size
-        n_data = self.shapes[p][0]
-        wdt = self.window_dtype
-        if sw is None:  # host path: zero-copy views of the shm window
-            _, win = self.arys[p][s]
-            seq, tags = self._host_seq, self._host_tags
-            meta = getattr(self, "_host_meta", ())
-        else:
-            win = sw.data.view(wdt).view((n_data,) + self.sample_shape) if self.collate is None else sw.data
-            seq, tags, meta = sw.seq, sw.tags, sw.meta
-        if self.collate == "tokens":
-            from .models.tokens import TokenWindowLayout, collate_token_window
-
-            ex = self.metadata_from_producer[p].extra
-            with trace_range("ddl.consumer.tokens"):
-                return collate_token_window(win.reshape(-1), TokenWindowLayout(**ex["token_layout"]),
-                                            ex["token_mode"], meta, self.pad_id, sub=local,
-                                            fixed_rows=self.token_rows == "fixed")
-        perm = self._perm_for(p, seq)
-        out_dtype = self.out_dtype or (torch.float32 if self.normalize is not None else wdt)
-        if self.augment is not None:
-            aug, norm = self.augment, self.normalize or {}
-            # crop randomness keyed by (seed, epoch OF THIS WINDOW) and the row's identity (producer, round, row);
-            # the window's epoch, not the cursor's: a lookahead batch of the next window is built a step early
-            w = sw.index if sw is not None else self.window
-            epoch = self.epoch + (w - (self.window - self.window_in_epoch)) // self.windows_per_epoch
-            return (ops.random_resized_crop(
-                win, perm=perm, base=local * B, n_rows=B, size=aug.get("size", (224, 224)),
-                scale=aug.get("scale", (0.08, 1.0)), ratio=aug.get("ratio", (3.0 / 4.0, 4.0 / 3.0)),
-                flip_p=aug.get("flip_p", 0.5), seed=_mix(self.seed, epoch),
-                sample_base=_mix(p, seq) & ~0xFFFFFFFF & ((1 << 63) - 1), layout=aug.get("layout", "chw"),
-                out_dtype=self.out_dtype or torch.bfloat16, mean=norm.get("mean"), std=norm.get("std")),)
-        splits = list(self.splits[p])
-        norm = self.normalize
-        with trace_range("ddl.consumer.batch"):
-            if norm is not None and norm.get("layout", "chw") == "hwc":
-                x = ops.collate_hwc_to_chw(win, perm=perm, base=local * B, n_rows=B, out_dtype=out_dtype,
-                                           mean=norm.get("mean"), std=norm.get("std"))
-                return (x,)
-            if (self.contiguous or self.copy_batches) and len(splits) > 1 and len(self.sample_shape) == 1 \
-                    and norm is None:
-                return ops.split_columns(win, splits, perm=perm, base=local * B, n_rows=B, out_dtype=out_dtype)
-            if perm is None and out_dtype == wdt and norm is None and not self.copy_batches:
-                x = win[local * B:(local + 1) * B]  # zero-copy view (reference semantics)
-            else:
-                kw = {}
-                if norm is not None:
-                    plane = int(math.prod(self.sample_shape[1:])) if len(self.sample_shape) > 1 else 1
-                    c = self.sample_shape[0] if len(self.sample_shape) > 1 else len(norm.get("mean", [0]))
-                    sc, bi = ops.norm_affine(c, norm.get("mean"), norm.get("std"), norm.get("scale"),
-                                             norm.get("bias"), ops.pixel_max(wdt))
-                    kw = dict(scale=sc, bias=bi, plane=plane)
-                x = ops.gather_rows(win, perm=perm, base=local * B, n_rows=B, out_dtype=out_dtype, **kw)
-        if len(splits) == 1:
-            return (x,)
-        parts = torch.split(x.reshape(B, -1), splits, dim=1)
-        if self.contiguous or self.copy_batches:  # normalised tabular rows: own each column group
-            return tuple(t.contiguous() for t in parts)
-        return parts
-
     def __iter__(self) -> Iterator:
         n = self._len
         start = self.epoch_batch  # 0 at an epoch start; the resumed cursor after load_state_dict
@@ -725,6 +530,7 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
             self._host_window = None
 
     # reference protocol names (ddl/mpi_dataloader.py:200-218): the same state machine
+    @with_logging
     def _start_access_epoch(self, target_rank: int = 0) -> None:
         """Take the current window (staged in HBM, or the shm slot on the host path)."""
         if self.connection is not None and self.connection.n_producers and not self._finalized:
@@ -780,6 +586,7 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
                 # the window's last END_OF_BATCH too, ddl/mpi_dataloader.py:223-227)
                 self._release_window()
 
+    @with_logging
     def _on_epoch_end(self) -> None:
         if self._finalized or self.connection is None or self.connection.n_producers == 0:
             self.epoch += 1
@@ -811,6 +618,7 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
 
 
     # --------------------------------------------------------------- teardown
+    @with_logging
     def _finalize(self) -> None:
         if self._finalized:
             return
@@ -828,6 +636,7 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
         if self.connection is not None:
             self.connection.finalize()
 
+    @with_logging
     def _drop_engine(self) -> None:
         if self._engine is not None:
             self.metrics.consumer_wait_s += self._engine.wait_s
@@ -838,32 +647,13 @@ class DistributedDataLoader(NativeDispatchMixin, CheckpointMixin, DistributedDat
             self._engine = None
             self._eng_slots.clear()
 
+    @with_logging
     def close(self) -> None:
         self._finalize()
 
     def stats(self) -> dict:
         d = self.metrics.as_dict()
-        done = getattr(self, "_native_done", None)
-        if self._engine is not None or done is not None:
-            nd = dict(done or {"batches": 0, "lookahead_hits": 0})
-            if self._engine is not None:
-                d["consumer_wait_s"] += self._engine.wait_s
-                nd["batches"] += int(self._engine.batches)
-                nd["lookahead_hits"] += int(self._engine.lookahead_hits)
-                g, la, rec, sw = self._engine.timing_ns
-                n = max(1, int(self._engine.batches))
-                nd["compute_waits"] = int(self._engine.compute_waits)
-                nd["ready_host_waits"] = int(self._engine.ready_host_waits)
-                wait_ns = self._engine.wait_s * 1e9
-                nd["host_us_per_batch"] = {"get": round(g / n / 1e3, 2),
-                                           "get_excl_staging_wait": round(max(0.0, g - wait_ns) / n / 1e3, 2),
-                                           "kernel_launch": round(la / n / 1e3, 2),
-                                           "event_record": round(rec / n / 1e3, 2),
-                                           "stream_wait": round(sw / n / 1e3, 2)}
-            nd["mode"] = getattr(self, "_eng_mode", None)
-            if self._engine is not None:
-                nd["handoff"] = "host" if self._engine.host_handoff else "device"
-            d["native_dispatch"] = nd
+        self._native_stats(d)
         if self._stager is not None:
             d.update(self._stager.stats())
         if self.connection is not None:

@@ -351,3 +351,27 @@ class NativeDispatchMixin:
         return {"input_ids": out[0][:n_rows], "attention_mask": out[1][:n_rows], "position_ids": out[2][:n_rows],
                 "segment_ids": out[3][:n_rows], "cu_seqlens": out[4][:n_seg + 1], "max_seqlen": max_seg,
                 "n_tokens": n_tokens}
+
+    def _native_stats(self, d: dict) -> None:
+        """The native engine's counters into the loader's ``stats()`` dict ``d`` (``native_dispatch``)."""
+        done = getattr(self, "_native_done", None)
+        if self._engine is not None or done is not None:
+            nd = dict(done or {"batches": 0, "lookahead_hits": 0})
+            if self._engine is not None:
+                d["consumer_wait_s"] += self._engine.wait_s
+                nd["batches"] += int(self._engine.batches)
+                nd["lookahead_hits"] += int(self._engine.lookahead_hits)
+                g, la, rec, sw = self._engine.timing_ns
+                n = max(1, int(self._engine.batches))
+                nd["compute_waits"] = int(self._engine.compute_waits)
+                nd["ready_host_waits"] = int(self._engine.ready_host_waits)
+                wait_ns = self._engine.wait_s * 1e9
+                nd["host_us_per_batch"] = {"get": round(g / n / 1e3, 2),
+                                           "get_excl_staging_wait": round(max(0.0, g - wait_ns) / n / 1e3, 2),
+                                           "kernel_launch": round(la / n / 1e3, 2),
+                                           "event_record": round(rec / n / 1e3, 2),
+                                           "stream_wait": round(sw / n / 1e3, 2)}
+            nd["mode"] = getattr(self, "_eng_mode", None)
+            if self._engine is not None:
+                nd["handoff"] = "host" if self._engine.host_handoff else "device"
+            d["native_dispatch"] = nd

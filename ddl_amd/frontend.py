@@ -122,6 +122,7 @@ class DataLoader:
 
         from .dataloader import DistributedDataLoader
         from .models.datasets import MapDatasetSource
+        from .specs import from_flat
         from .models.producers import IndexedProducer
 
         if sampler is not None or batch_sampler is not None:
@@ -153,9 +154,10 @@ class DataLoader:
             producer = IndexedProducer(MapDatasetSource(dataset), gb, seed=int(seed), drop_last=drop_last,
                                        host_threads=host_threads, shuffle=bool(shuffle),
                                        worker_init_fn=worker_init_fn)
+            specs = from_flat(loader_kw, mode="indexed", seed=int(seed))
             self.loader = DistributedDataLoader(
-                producer, int(batch_size), self._conn, epochs if epochs is not None else 1_000_000, mode="indexed",
-                env=self.env, auto_mark=True, seed=int(seed), resume_state=resume_state, **loader_kw)
+                producer, int(batch_size), self._conn, epochs if epochs is not None else 1_000_000, env=self.env,
+                auto_mark=True, resume_state=resume_state, **specs, **loader_kw)
         except BaseException:
             self._session.release(self._conn)
             raise

@@ -24,8 +24,14 @@ through the (possibly blocked) collectives: a client of the job's rendezvous ``T
   which bumps only while the rank exists and is not stopped (``/proc``: SIGSTOP, a debugger, a frozen
   cgroup). Rank r watches rank ``(r + 1) % W`` only (O(W) store traffic). A counter that has not moved for
   ``peer_timeout_s`` (a stopped or frozen process, a lost node) makes the watcher publish the abort for
-  it. A healthy rank holding the GIL in one long C call keeps beating through its death watch, so it is
-  not mistaken for a dead one. An unreachable store (its host rank died) is an abort too.
+  it. An unreachable store (its host rank died) is an abort too.
+* **Hung rank.** The death watch relays its beats only while the rank's watchdog thread keeps sending it
+  liveness tokens (one per poll). A healthy rank holding the GIL in one long C call stops the tokens but
+  keeps beating through the death watch for ``hang_timeout_s`` (default 5 x ``peer_timeout_s``, at least
+  300 s), so it is not mistaken for a dead one; a rank that holds the GIL longer -- deadlocked or hung --
+  stops beating and is aborted then, before the collective timeout (``timeout_s``, 600 s) would end it.
+  A rank blocked in a collective with the GIL released keeps beating: its peers are blocked in the same
+  collective, which the collective timeout bounds.
 * **Clean exit.** ``stop()`` marks the rank done (watchers of a finished rank stop checking it) before
   the final barrier, so a slow rank is never mistaken for a dead one once its neighbour finished.
 
@@ -52,6 +58,11 @@ PEER_ABORT_EXIT = 75  # exit status of a rank torn down because ANOTHER rank fai
 # the GIL longer than this counts as hung; raise it (``start(peer_timeout_s=)``,
 # ``distributed_dataloader(peer_timeout_s=)``) for such workloads.
 DEFAULT_PEER_TIMEOUT_S = 60.0
+
+
+def default_hang_timeout_s(peer_timeout_s: float) -> float:
+    """How long a rank's death watch keeps beating for it without a liveness token from its watchdog thread."""
+    return max(300.0, 5.0 * float(peer_timeout_s))
 
 
 def _job_key() -> str:
@@ -95,10 +106,12 @@ class JobWatchdog:
     def __init__(self, rank: int, world_size: int, *, peer_timeout_s: float = DEFAULT_PEER_TIMEOUT_S,
                  poll_s: float = 0.25, on_abort: Callable[[], None] | None = None, store: Any = None,
                  job_key: str | None = None, exit_fn: Callable[[int], None] | None = None,
-                 death_watch: "DeathWatch | None" = None):
+                 death_watch: "DeathWatch | None" = None, hang_timeout_s: float | None = None):
         self.rank, self.world = int(rank), int(world_size)
         self.death_watch = death_watch  # beats for this rank too (alive and not stopped), GIL or not
         self.peer_timeout_s = float(peer_timeout_s)
+        self.hang_timeout_s = float(hang_timeout_s if hang_timeout_s is not None
+                                    else default_hang_timeout_s(peer_timeout_s))
         self.poll_s = float(poll_s)
         self.on_abort = on_abort
         self._exit = exit_fn or os._exit
@@ -117,7 +130,7 @@ class JobWatchdog:
     def start(self) -> "JobWatchdog":
         self._store.set(self._hb(self.rank), "0")
         if self.death_watch is not None:
-            self.death_watch.beat(self.poll_s)
+            self.death_watch.beat(self.poll_s, self.hang_timeout_s)
         self._thread = threading.Thread(target=self._run, name=f"ddl-watchdog-{self.rank}", daemon=True)
         self._thread.start()
         return self
@@ -175,6 +188,8 @@ class JobWatchdog:
                 if not self._done:
                     self._beat += 1
                     self._store.set(self._hb(self.rank), str(self._beat))
+                    if self.death_watch is not None:
+                        self.death_watch.alive()  # the token the death watch needs to keep beating for us
                 if self._store.check(["abort"]):
                     msg = self._store.get("abort").decode(errors="replace")
                     if msg:
@@ -214,33 +229,40 @@ def _process_stopped(pid: int) -> bool:
 
 
 def _death_watch_main(pipe, parent_pid: int, rank: int, job_key: str, host: str, port: int) -> None:
-    """Body of a rank's ``DeathWatch`` child. Messages from the rank: ``("beat", period_s)`` -- keep the rank's
-    heartbeat going from here (while the rank exists and is not stopped), ``"finishing"`` -- mark it done and
-    stop, ``"done"`` -- a clean shutdown, exit. EOF (or a new parent) = the rank died: publish the job-wide
-    abort under the watchdogs' prefix."""
+    """Body of a rank's ``DeathWatch`` child. Messages from the rank: ``("beat", period_s, hang_s)`` -- keep the
+    rank's heartbeat going from here (while the rank exists, is not stopped, and sent a liveness token within
+    ``hang_s``), ``"alive"`` -- a liveness token from the rank's watchdog thread, ``"finishing"`` -- mark it
+    done and stop, ``"done"`` -- a clean shutdown, exit. EOF (or a new parent) = the rank died: publish the
+    job-wide abort under the watchdogs' prefix."""
     os.environ["HIP_VISIBLE_DEVICES"] = "-1"  # never touches a GPU
     import torch.distributed as dist  # now, not at the rank's death: the report must not wait for an import
 
     prefix, hb = f"ddl_amd/abort/{job_key}/", f"hb/{rank}"
     store, period, beat = None, 1.0, 0
+    hang_s, last_alive = float("inf"), time.monotonic()
     while True:
         try:
             if pipe.poll(period):
                 msg = pipe.recv()
                 if msg == "done":
                     return
-                if msg == "finishing":
+                if msg == "alive":
+                    last_alive = time.monotonic()
+                elif msg == "finishing":
                     if store is not None:
                         store.set(hb, "done")
                     store = None
                 elif isinstance(msg, tuple) and msg[0] == "beat":
                     period = float(msg[1])
+                    hang_s = float(msg[2]) if len(msg) > 2 else float("inf")
+                    last_alive = time.monotonic()
                     store = dist.PrefixStore(prefix, dist.TCPStore(host, port, is_master=False,
                                                                    timeout=timedelta(seconds=30),
                                                                    wait_for_workers=False))
             elif os.getppid() != parent_pid:
                 break
-            if store is not None and not _process_stopped(parent_pid):
+            if (store is not None and not _process_stopped(parent_pid)
+                    and time.monotonic() - last_alive <= hang_s):
                 beat += 1
                 store.set(hb, f"w{beat}")
         except (EOFError, OSError):
@@ -298,9 +320,14 @@ class DeathWatch:
             except (BrokenPipeError, OSError):
                 return False
 
-    def beat(self, period_s: float) -> bool:
-        """Heartbeat this rank from the child from now on (the rendezvous store is up)."""
-        return self._send(("beat", float(period_s)))
+    def beat(self, period_s: float, hang_timeout_s: float = float("inf")) -> bool:
+        """Heartbeat this rank from the child from now on (the rendezvous store is up), as long as a liveness
+        token (``alive``) arrived within ``hang_timeout_s``."""
+        return self._send(("beat", float(period_s), float(hang_timeout_s)))
+
+    def alive(self) -> bool:
+        """A liveness token: this rank's Python threads still run (sent by the watchdog thread every poll)."""
+        return self._send("alive")
 
     def finishing(self) -> bool:
         return self._send("finishing")

@@ -585,7 +585,7 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
         return batch, ev
 
     def _crop(self, src: torch.Tensor, epoch: int, **kw) -> torch.Tensor:
-        from .dataloader import _mix
+        from .batching import _mix
 
         aug, norm = self.augment, self.normalize or {}
         return ops.random_resized_crop(

@@ -62,7 +62,8 @@ class Params:
 def main(cfg: Params, env, conn):
     producer = PointCloudProducer(cfg.nData, env.rank, env.world_size)
     loader = ddl_amd.DistributedDataLoader(producer, cfg.batch_size, conn, cfg.nepoch, cfg.fraction_exchange,
-                                           "alltoall", env.rank, env.world_size, env=env, shuffle="device")
+                                           "alltoall", env.rank, env.world_size, env=env,
+                                           order=ddl_amd.OrderSpec(shuffle="device"))
     model = torch.nn.Linear(3, 5).to(loader.device)
     opt = torch.optim.SGD(model.parameters(), lr=1e-2)
     t0 = time.time()

@@ -59,8 +59,9 @@ def main() -> None:
             producer = TokenBatchProducer(src, a.global_batch, a.seq_len, a.mode,
                                           pack_order="ffd" if a.mode == "pack" else "in_order",
                                           batches_per_window=a.batches_per_window)
-            dl = ddl_amd.DistributedDataLoader(producer, a.global_batch // env.world_size, conn, a.epochs,
-                                               mode="indexed", env=env, collate="tokens", auto_mark=True)
+            dl = ddl_amd.DistributedDataLoader(producer, a.global_batch // env.world_size, conn, a.epochs, env=env,
+                                               order=ddl_amd.OrderSpec(mode="indexed"),
+                                               output=ddl_amd.OutputSpec(collate="tokens"), auto_mark=True)
             for epoch in range(a.epochs):
                 real = rows = 0
                 for b in dl:

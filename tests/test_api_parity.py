@@ -67,3 +67,59 @@ def test_reference_protocol_methods_drive_the_window_round_robin():
         assert dl._can_continue()
         dl.close()
         assert dl._finalized
+
+
+def test_constructor_keeps_the_reference_eight_and_groups_the_rest():
+    """The reference's eight arguments come first, positionally (reference ddl/mpi_dataloader.py:108-118);
+    everything the MI355X loader adds is keyword-only, and its ~20 options live in three records."""
+    import inspect
+
+    params = list(inspect.signature(ddl_amd.DistributedDataLoader.__init__).parameters.values())[1:]
+    positional = [p.name for p in params if p.kind is p.POSITIONAL_OR_KEYWORD]
+    assert positional == ["producer_function", "batch_size", "connection", "n_epochs", "fraction_exchange",
+                          "exchange_method", "instance_idx", "n_instances"]
+    keyword = [p.name for p in params if p.kind is p.KEYWORD_ONLY]
+    assert keyword == ["env", "device", "output", "staging", "order", "auto_mark", "resume_state", "debug_checksum"]
+
+
+def test_specs_validate_and_legacy_keywords_are_deprecated_aliases():
+    from ddl_amd.specs import OrderSpec, OutputSpec, StagingSpec, resolve
+
+    with pytest.raises(ValueError):
+        OrderSpec(mode="bogus")
+    with pytest.raises(ValueError):
+        OutputSpec(augment={"bogus": 1})
+    with pytest.raises(ValueError):
+        StagingSpec(native_dispatch="sideways")
+    with pytest.raises(ValueError):
+        StagingSpec(max_ahead=-1)
+    with pytest.raises(TypeError):
+        resolve(None, None, None, {"not_an_option": 1})
+    with pytest.warns(DeprecationWarning, match=r"order=OrderSpec\(seed=...\)"):
+        out, stg, odr = resolve(None, StagingSpec(prefetch_depth=2), None, {"seed": 5, "out_dtype": torch.bfloat16})
+    assert odr.seed == 5 and out.dtype is torch.bfloat16 and stg.prefetch_depth == 2
+    with pytest.raises(dataclasses_frozen_error()):
+        odr.seed = 1  # records are frozen
+
+
+def dataclasses_frozen_error():
+    import dataclasses
+
+    return dataclasses.FrozenInstanceError
+
+
+def test_spec_and_legacy_construction_deliver_the_same_batches():
+    def run(**kw):
+        with ddl_amd.start(n_producers=2) as (env, conn):
+            dl = ddl_amd.DistributedDataLoader(IdProducer(16, 4), 4, conn, 2, env=env, auto_mark=True, **kw)
+            got = [torch.cat(b, 1).clone() for _ in range(2) for b in dl]
+            opts = (dl.seed, dl.shuffle, dl.mode, dl.copy_batches, dl.prefetch_depth)
+            dl.close()
+        return got, opts
+
+    new, o1 = run(order=ddl_amd.OrderSpec(shuffle="device", seed=9, mode="split_along_epoch"),
+                  staging=ddl_amd.StagingSpec(prefetch_depth=2))
+    with pytest.warns(DeprecationWarning):
+        old, o2 = run(shuffle="device", seed=9, mode="split_along_epoch", prefetch_depth=2)
+    assert o1 == o2 == (9, "device", "split_along_epoch", True, 2)
+    assert len(new) == len(old) > 0 and all(torch.equal(a, b) for a, b in zip(new, old))

@@ -2,7 +2,8 @@
 
 Knobs covered elsewhere: DDL_BACKEND (test_multirank_*), DDL_DEVICE (everywhere), DDL_PRODUCERS_PER_RANK
 (test_utils), DDL_PRODUCER_MODE / DDL_FAULT_PRODUCER (test_loader_cpu), DDL_HOSTNAME (test_multirank_cpu),
-DDL_FAULT_RANK (test_job_abort). The rest are tested here.
+DDL_FAULT_RANK (test_job_abort), DDL_REHEARSAL (test_examples, test_multirank_gpu), DDL_NATIVE_PIN
+(test_stale_build). The rest are tested here.
 """
 
 import os

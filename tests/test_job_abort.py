@@ -26,7 +26,7 @@ PG_TIMEOUT_S = 600  # what the peers would otherwise wait for
 
 def _base_env(**kw):
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    env.update(PYTHONPATH=REPO, DDL_DEVICE="cpu", **kw)
+    env.update(PYTHONPATH=REPO, DDL_DEVICE="cpu", DDL_REHEARSAL="1", **kw)  # CPU ranks: a labelled rehearsal
     return env
 
 
@@ -313,3 +313,50 @@ def test_start_timeout_reaches_the_process_group():
         _kill_all(procs)
     assert codes[0] not in (None, 0, PEER_ABORT_EXIT) and codes[2] not in (None, 0, PEER_ABORT_EXIT), codes
     assert took < 90  # start-up + ~6 s, far from the 600 s default
+
+
+@pytest.mark.timeout(120)
+def test_death_watch_beats_only_while_liveness_tokens_arrive(monkeypatch):
+    """The death watch keeps a rank's heartbeat going while its Python threads cannot run (a long C call holding
+    the GIL) -- but only for hang_timeout_s after the last liveness token: a rank hung for longer stops beating,
+    so its watcher aborts the job before the collective timeout would."""
+    import time
+    from datetime import timedelta
+
+    import torch.distributed as dist
+
+    from ddl_amd.parallel.abort import DeathWatch, _job_key
+    from tests.mp_harness import free_port
+
+    port = free_port()
+    master = dist.TCPStore("127.0.0.1", port, is_master=True, timeout=timedelta(seconds=30), wait_for_workers=False)
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", str(port))
+    monkeypatch.delenv("DDL_PRODUCER_MODE", raising=False)
+    store = dist.PrefixStore(f"ddl_amd/abort/{_job_key()}/", master)
+    dw = DeathWatch.spawn(7)
+    assert dw is not None
+    try:
+        def hb():
+            return store.get("hb/7") if store.check(["hb/7"]) else b""
+
+        def moving(seconds: float, tokens: bool) -> bool:
+            t_end, seen = time.monotonic() + seconds, {hb()}
+            while time.monotonic() < t_end:
+                if tokens:
+                    dw.alive()
+                time.sleep(0.05)
+                seen.add(hb())
+            return len(seen) > 2
+
+        assert dw.beat(0.05, 1.0)
+        t0 = time.monotonic()
+        while hb() == b"" and time.monotonic() - t0 < 60:  # the child imports torch first
+            dw.alive()
+            time.sleep(0.05)
+        assert moving(1.5, tokens=True)        # tokens arrive: the death watch beats
+        time.sleep(1.5)                          # no token for longer than hang_timeout_s ...
+        assert not moving(1.0, tokens=False)    # ... the beats stop: the rank counts as hung
+        assert moving(1.5, tokens=True)         # tokens again: beating again
+    finally:
+        dw.done()

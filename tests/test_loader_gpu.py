@@ -234,7 +234,7 @@ def test_gpu_resident_augment_matches_direct_crop():
     """ResidentGlobalLoader(augment=...) crops every epoch's global order out of the HBM shard,
     keyed by (seed, epoch, sample id): identical to cropping the dataset directly."""
     from ddl_amd import ops
-    from ddl_amd.dataloader import _mix
+    from ddl_amd.batching import _mix
     from ddl_amd.models import SharedArraySource
     from ddl_amd.resident import ResidentGlobalLoader
 

@@ -55,3 +55,31 @@ def test_edited_csrc_is_reported_or_rebuilt(tmp_path):
     rebuilt = _run(root)
     assert rebuilt.returncode == 0 and "STALE False" in rebuilt.stdout, rebuilt.stderr[-2000:]
     assert so.read_bytes() != before
+
+
+def test_children_load_the_parents_build_or_refuse(tmp_path):
+    """A producer spawned mid-job loads exactly the binary its consumer loaded (DDL_NATIVE_PIN, inherited): it
+    never rebuilds a stale one under a live job, and a file that changed under the job is an error -- the
+    consumer and its producers never run different builds over one arena."""
+    root = _copy_tree(tmp_path)
+    first = _run(root, DDL_AMD_NO_AUTOBUILD="1")
+    assert first.returncode == 0 and "STALE False" in first.stdout, first.stderr[-2000:]
+    so = next((root / "ddl_amd").glob("_ddl_runtime*.so"))
+    code = "import os, ddl_amd._native as n; n.runtime(); print(os.environ['DDL_NATIVE_PIN'])"
+    e = {k: v for k, v in os.environ.items() if k not in ("DDL_AMD_NO_AUTOBUILD", "DDL_NATIVE_PIN")}
+    r = subprocess.run([sys.executable, "-c", code], cwd=str(root), env=dict(e, PYTHONPATH=str(root)),
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    pin = r.stdout.strip().splitlines()[-1]
+    assert str(so.resolve()) in pin
+    # csrc/ edited after the consumer loaded its build: a child with the pin loads that build, no rebuild
+    src = root / "csrc" / "runtime" / "arena.cpp"
+    src.write_text(src.read_text() + "\n// edited mid-job\n")
+    before = so.read_bytes()
+    child = _run(root, DDL_NATIVE_PIN=pin)
+    assert child.returncode == 0 and "STALE True" in child.stdout, child.stderr[-2000:]
+    assert so.read_bytes() == before
+    # the .so itself replaced under the job (a rebuild by someone else): the child refuses
+    digest = pin.rpartition("=")[2]
+    bad = _run(root, DDL_NATIVE_PIN=f"{so.resolve()}={'0' * len(digest)}")
+    assert bad.returncode != 0 and "changed under the running job" in bad.stderr, bad.stderr[-2000:]
