@@ -137,7 +137,11 @@ def claim_device(env: DDLEnv) -> None:
     job = f"{os.environ.get('MASTER_ADDR', '')}:{os.environ.get('MASTER_PORT', '')}"
     path = os.path.join(tempfile.gettempdir(),
                         f"ddl_amd_gpu_{bus.replace(':', '_')}_{zlib.crc32(job.encode()):08x}.lock")
-    fd = os.open(path, os.O_CREAT | os.O_RDWR, 0o666)
+    try:
+        fd = os.open(path, os.O_CREAT | os.O_RDWR, 0o666)
+    except OSError as e:  # no writable temp directory: the PCI-bus-ID all-gather still checks (after the groups)
+        logger.warning("cannot claim GPU %s (%s): relying on the bus-ID all-gather", bus, e)
+        return
     try:
         fcntl.flock(fd, fcntl.LOCK_EX | fcntl.LOCK_NB)
     except OSError:

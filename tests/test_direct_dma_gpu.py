@@ -179,9 +179,12 @@ def test_direct_dma_copy_timing_is_off_unless_asked():
 
 def test_close_interrupts_a_pending_free_event_wait(direct):
     """The stager waits for a ring buffer's free event (recorded behind the consumer's reads) by polling, so
-    close() ends that wait at once even while the consumer's stream is still busy: here a ~3 s spin kernel
-    sits in front of window 0's free event while the stager wants its buffer back for window 2. Same on the
-    HIP copy-stream fallback (its free-event wait is polled on the host too)."""
+    close() ends that wait at once even while the consumer's stream is still busy: here a ~3 s spin kernel sits
+    on the batch stream in front of the last batch kernel of window 0, and so in front of window 0's free
+    event, while the stager wants buffer 0 back for window 2. Same on the HIP copy-stream fallback (its
+    free-event wait is polled on the host too)."""
+    from ddl_amd.utils import streams
+
     with ddl_amd.start(n_producers=P) as (env, conn):
         # calibrate the spin kernel (its clock is the shader clock): cycles per second
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -190,22 +193,26 @@ def test_close_interrupts_a_pending_free_event_wait(direct):
         e1.record()
         e1.synchronize()
         cycles_per_s = 1e8 / max(1e-4, e0.elapsed_time(e1) / 1e3)
-        dl = ddl_amd.DistributedDataLoader(IdProducer(N, WIDTH), B, conn, 8, env=env, device=torch.device("cuda"),
-                                           shuffle="device", seed=SEED, prefetch_depth=2, copy_batches=True,
-                                           native_dispatch=False)
+        dl = ddl_amd.DistributedDataLoader(
+            IdProducer(N, WIDTH), B, conn, 8, env=env, device=torch.device("cuda"),
+            order=ddl_amd.OrderSpec(shuffle="device", seed=SEED), output=ddl_amd.OutputSpec(copy_batches=True),
+            staging=ddl_amd.StagingSpec(prefetch_depth=2, native_dispatch=False))
         assert dl._stager.direct_dma is direct and dl._stager._native.free_on_host
-        for i in range(len(dl)):
+        bs, n = dl._batch_stream, len(dl)
+        assert n == 4
+        for i in range(n):
+            if i == n - 2:  # batch n-1 (the window's last kernel) is enqueued when batch n-2 is fetched
+                with streams.on_stream(bs):
+                    torch.cuda._sleep(int(3.0 * cycles_per_s))
             dl[i]
-            if i + 1 < len(dl):
-                dl.mark(Marker.END_OF_BATCH)
-        torch.cuda._sleep(int(3.0 * cycles_per_s))  # ~3 s of spinning ahead of window 0's free event
-        dl.mark(Marker.END_OF_BATCH)  # window 0 released behind the spin: its free event stays pending
+            dl.mark(Marker.END_OF_BATCH)  # the last mark releases window 0 with its (pending) free event
         time.sleep(0.3)  # the stager is now waiting for that free event (window 2 needs buffer 0)
-        assert not torch.cuda.current_stream().query(), "the spin kernel finished too early for this test"
+        assert not bs.query(), "the spin kernel finished too early for this test"
+        assert dl._stager.windows_staged == 2  # window 2's copy is held by the pending free event
         t0 = time.monotonic()
         dl._stager._native.close()
         assert time.monotonic() - t0 < 1.0
-        assert not torch.cuda.current_stream().query()  # the wait was interrupted, not satisfied
+        assert not bs.query()  # the wait was interrupted, not satisfied
         dl.close()
 
 

@@ -116,6 +116,10 @@ def test_bench_multirank_device_path(n, launch):
         assert r["dispatch"]["host_us_per_batch"]["get"] > 0
     assert out["config"]["dispatch"] == out["per_rank"][0]["dispatch"]["mode"]
     assert out["indexed"] and "error" not in out["indexed"] and out["indexed"]["value"] > 0
+    # phase 3 (loader pressure) ran on all three paths, in step on every rank
+    for sub in (out, out["indexed"], out["indexed"]["zero_copy"]):
+        assert sub["pressure"] and "error" not in sub["pressure"], sub["pressure"]
+        assert sub["gpu_idle_pct_r090"] is not None
     # the line labels itself: gloo ranks sharing one card, a rehearsal (not an N-GPU RCCL measurement)
     d = out["dist"]
     assert d["backend"] == "gloo" and d["group_size"] == n and d["distinct_gpus"] == 1

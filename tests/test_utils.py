@@ -336,3 +336,40 @@ def test_compute_idle_meter_gap_distribution():
     assert abs(g["p50"] - 10.0) < 0.1 and abs(g["max"] - 1000.0) < 0.1
     assert abs(g["top1pct_share"] - 1000.0 / (1000.0 + 98 * 10.0)) < 1e-3
     assert abs(r["gpu_idle_pct"] - 100.0 * (1.0 - 100.0 / (100.0 + 1.0 + 0.98))) < 1e-6
+
+
+def test_one_gpu_per_rank_is_enforced(monkeypatch):
+    """More ranks on a node than visible GPUs, or a second rank of the job on a GPU (a per-job flock on its PCI
+    bus ID), is a TopologyError -- unless DDL_REHEARSAL=1 labels the run a rehearsal."""
+    import os
+
+    from ddl_amd.exceptions import TopologyError
+    from ddl_amd.parallel import env as env_mod
+    from ddl_amd.types import DDLEnv
+
+    for v in env_mod._VISIBILITY_VARS:
+        monkeypatch.delenv(v, raising=False)
+    monkeypatch.delenv("DDL_REHEARSAL", raising=False)
+    e = DDLEnv(rank=1, world_size=8, local_rank=1, local_world_size=8, hostname="h")
+    env_mod.check_device_count(e, 8)
+    with pytest.raises(TopologyError, match="share a device"):
+        env_mod.check_device_count(e, 1)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "3")  # per-task masks: the bus-ID checks decide instead
+    env_mod.check_device_count(e, 1)
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    monkeypatch.setenv("DDL_REHEARSAL", "1")
+    env_mod.check_device_count(e, 1)
+    monkeypatch.delenv("DDL_REHEARSAL")
+
+    bus = f"0000:{os.getpid() % 251:02x}:1f"
+    monkeypatch.setattr(env_mod, "device_identity", lambda device: {"pci_bus_id": bus})
+    monkeypatch.setenv("MASTER_PORT", str(40000 + os.getpid() % 20000))
+    env_mod.claim_device(DDLEnv(rank=0, world_size=2, device="cuda:0"))
+    fd = env_mod._CLAIMED.pop(bus)  # as if rank 0 were another process still holding the claim
+    try:
+        with pytest.raises(TopologyError, match=r"rank 1 and rank 0 \(pid"):
+            env_mod.claim_device(DDLEnv(rank=1, world_size=2, device="cuda:0"))
+        monkeypatch.setenv("DDL_REHEARSAL", "1")
+        env_mod.claim_device(DDLEnv(rank=1, world_size=2, device="cuda:0"))  # a rehearsal may share
+    finally:
+        os.close(fd)
