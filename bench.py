@@ -115,6 +115,8 @@ def parse(argv=None):
     ap.add_argument("--zc-blocks", type=int, default=None,
                     help="indexed order, zero-copy path: workgroups of the PCIe gather (ZeroCopyLoader max_blocks; "
                          "default: its own choice, 32 for bf16)")
+    ap.add_argument("--zc-handoff", default="host", choices=["host", "device"],
+                    help="indexed order, zero-copy path: how a batch is handed to the consumer's stream")
     ap.add_argument("--dispatch", default="auto", choices=["auto", "inline", "lookahead", "python"],
                     help="per-batch dispatch: the native engine (auto / inline / lookahead) or the Python path")
     ap.add_argument("--a2a-probe-mb", type=float, default=32.0,
@@ -443,12 +445,13 @@ def indexed_phase(args, env, dev, barrier, sync, spare=None) -> dict:
             out.update(_pressure_sub(args, env, dev, it, rate, barrier, sync, dl=dl))
             dl.close()
         zc = ZeroCopyLoader(src, args.batch * env.world_size, env, seed=args.seed, out_dtype=torch.bfloat16,
-                            device=dev, prefault=not args.index_no_prefault, max_blocks=args.zc_blocks)
+                            device=dev, prefault=not args.index_no_prefault, max_blocks=args.zc_blocks,
+                            handoff=args.zc_handoff)
         it = forever(zc)
         rate, ms, _ = _timed_feed(args, env, it, acc, barrier, sync, "bench.indexed_zero_copy")
         zres = {"path": "zero-copy gfx950 gather over PCIe from the pinned, device-mapped source",
                 "value": round(rate, 1), "ms_per_step": round(ms, 4), "prefault_s": zc.stats().get("prefault_s"),
-                "max_blocks": zc.max_blocks}
+                "max_blocks": zc.max_blocks, "handoff": zc.handoff}
         if spare is None:
             zres["gpu_idle_pct"] = _idle_behind_step(args, env, dev, it, barrier, sync)
         # the zero-copy gather holds CUs for its whole PCIe transfer: its idle behind a step at 0.9x the feed

@@ -55,7 +55,11 @@ class ZeroCopyLoader(PrefetchedIndexedLoader):
                  drop_last: bool = True, out_dtype: Any = None, normalize: dict | None = None, depth: int = 2,
                  max_blocks: int | None = None, device: str | torch.device | None = None,
                  n_epochs: int | None = None,
-                 resume_state: dict | None = None, prep_streams: int = 1, prefault: bool = True):
+                 resume_state: dict | None = None, prep_streams: int = 1, prefault: bool = True,
+                 handoff: str = "host"):
+        if handoff not in ("host", "device"):
+            raise ValueError("handoff must be 'host' or 'device'")
+        self.handoff = handoff  # PCIe-paced batches (~1.4 ms each): no barrier packet in the caller's queue
         self.env = env or DDLEnv()
         self.W, self.rank = self.env.world_size, self.env.rank
         self.sample_shape, self.src_dtype = _source_geometry(source)
@@ -148,6 +152,7 @@ class ZeroCopyLoader(PrefetchedIndexedLoader):
 
     def stats(self) -> dict:
         return {"batches": self.batches, "source_bytes": self.nbytes, "max_blocks": self.max_blocks,
+                "handoff": self.handoff, "host_waits": self.host_waits,
                 "prefault_s": getattr(self, "prefault_s", 0.0),
                 "prep_streams": len(self._prep) if self.prep_stream is not None else 0}
 

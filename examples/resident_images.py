@@ -6,10 +6,13 @@
 
 The dataset lives in node-shared memory here (``SharedArraySource``); with a
 real dataset use ``FileRowsSource.from_npy(path)`` or ``FileRowsSource(path,
-shape, "uint8")`` instead. Each rank loads its shard into HBM once (an ImageNet-size
-uint8 set is 193 GB at 3x224x224, which fits one MI355X). Then every epoch the
-loader delivers rank r's slice of the world-size-invariant global order. With
-W > 1 the rows are exchanged over RCCL all-to-all. On a GPU each batch is
+shape, "uint8")`` instead. The dataset goes into HBM once: an ImageNet-size uint8
+set is 193 GB at 3x224x224, which fits one MI355X, so by default (``replicate="auto"``)
+every rank holds a full replica -- it loads 1/W of it from the host and RCCL
+all-gathers over xGMI fill in the rest -- and no step moves a row between GPUs.
+(``--replicate false``, or a dataset too big for HBM: each rank holds a shard and
+every step all-to-alls 7/8 of its batch over xGMI.) Every epoch the loader
+delivers rank r's slice of the world-size-invariant global order. On a GPU each batch is
 RandomResizedCrop + flip + normalise + cast to bf16, in one kernel. The loader
 state is a checkpointable cursor: resume with ``resume_state=``, at any world
 size.
@@ -34,6 +37,7 @@ def main() -> None:
     ap.add_argument("--crop", type=int, default=64, help="crop side (a multiple of the 16-px patch)")
     ap.add_argument("--global-batch", type=int, default=128)
     ap.add_argument("--epochs", type=int, default=2)
+    ap.add_argument("--replicate", default="auto", choices=["auto", "true", "false"])
     a = ap.parse_args()
 
     name = f"ddl_amd_example_imgs_{os.environ.get('MASTER_PORT', os.getpid())}"
@@ -52,7 +56,8 @@ def main() -> None:
         norm = {"mean": [0.485, 0.456, 0.406], "std": [0.229, 0.224, 0.225]}
         dl = ResidentGlobalLoader(src, a.global_batch, env, seed=0, n_epochs=a.epochs, depth=2,
                                   out_dtype=torch.bfloat16 if gpu else torch.float32, normalize=norm,
-                                  augment={"size": (a.crop, a.crop)} if gpu else None)
+                                  augment={"size": (a.crop, a.crop)} if gpu else None,
+                                  replicate={"auto": "auto", "true": True, "false": False}[a.replicate])
         step = TrainStep(env.device, dim=64, depth=1, dtype=torch.bfloat16 if gpu else torch.float32,
                          process_group=env.process_group if env.world_size > 1 else None) if gpu else None
         for epoch in range(a.epochs):
@@ -63,7 +68,8 @@ def main() -> None:
                 n += batch.shape[0]
             if env.rank == 0:
                 print(f"epoch {epoch}: {n} samples on rank 0, batch {tuple(batch.shape)} {batch.dtype}, "
-                      f"cursor {dl.state_dict()['epoch']}/{dl.state_dict()['global_batch_cursor']}", flush=True)
+                      f"cursor {dl.state_dict()['epoch']}/{dl.state_dict()['global_batch_cursor']}, "
+                      f"{'replicated' if dl.replicated else 'sharded'}", flush=True)
         dl.close()
     src.close()  # unlinks the segment only in the process that created it
 

@@ -197,6 +197,8 @@ def test_bench_plumbing_config1_two_ranks():
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("script,args", [("resident_images.py", ["--n-samples", "512", "--epochs", "2"]),
+                                         ("resident_images.py", ["--n-samples", "512", "--epochs", "1",
+                                                                 "--replicate", "true"]),
                                          ("tokens_packed.py", ["--n-seqs", "256", "--epochs", "2"]),
                                          ("tokens_packed.py", ["--n-seqs", "256", "--epochs", "1", "--mode", "pad"]),
                                          ("torch_dataset.py", ["--n-samples", "256", "--epochs", "2", "--batch-size", "16"])])

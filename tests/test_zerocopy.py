@@ -53,6 +53,28 @@ def test_zerocopy_gpu_matches_reference(max_blocks, prep_streams, dtype):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("handoff", ["host", "device"])
+def test_zerocopy_handoff_modes_deliver_the_same_bytes_behind_a_busy_stream(handoff):
+    """Host hand-off (the default: the host waits for the gather's event, the consumer's stream gets no barrier)
+    and device hand-off deliver the same batches, bitwise -- also when the consumer's stream is busy with a long
+    kernel while the gathers run ahead, and the consumer reads each batch right after it is handed over."""
+    n, shape = 1024, (3, 64, 64)
+    src = (torch.rand((n, *shape)) * 100).to(torch.bfloat16)
+    dl = ZeroCopyLoader(src, 64, seed=2, n_epochs=1, depth=3, handoff=handoff)
+    order = EpochOrder(n, 64, 2)
+    idx = torch.from_numpy(order.perm(0).full()[: order.batches_per_epoch * 64]).view(-1, 64)
+    outs = []
+    for g, b in enumerate(dl):
+        if g % 4 == 0:
+            torch.cuda._sleep(2_000_000)  # the consumer's stream is busy; later gathers finish first
+        outs.append(b.clone())  # read on the consumer's stream, right away
+    assert torch.equal(torch.cat(outs).cpu(), src[idx.reshape(-1)])
+    st = dl.stats()
+    assert st["handoff"] == handoff and (st["host_waits"] == 0 or handoff == "host")
+    dl.close()
+
+
+@pytest.mark.gpu
 def test_touch_pages_reads_every_page():
     """touch_pages: one 4 B read per page; the per-block xor of the words lands in the sink (the loads are real)."""
     from ddl_amd import _native
