@@ -72,10 +72,11 @@ def main(argv=None) -> int:
             n_epochs = total // bpe + 2
             norm = {"mean": [0.485, 0.456, 0.406], "std": [0.229, 0.224, 0.225]}
             dev = torch.device(env.device)
-            dl = ddl_amd.DistributedDataLoader(
-                IndexedProducer(src, gb, seed=1, host_threads=a.host_threads), a.batch, conn, n_epochs,
-                mode="indexed", env=env, device=dev, out_dtype=torch.bfloat16, normalize=norm, n_slots=a.slots,
-                auto_mark=True)
+            dl = ddl_amd.DistributedDataLoader(IndexedProducer(src, gb, seed=1, host_threads=a.host_threads), a.batch,
+                                               conn, n_epochs, env=env, device=dev, auto_mark=True,
+                                               output=ddl_amd.OutputSpec(dtype=torch.bfloat16, normalize=norm),
+                                               staging=ddl_amd.StagingSpec(n_slots=a.slots),
+                                               order=ddl_amd.OrderSpec(mode="indexed"))
             acc = ops.ChecksumAccumulator(dev)
 
             def gen():

@@ -108,12 +108,14 @@ def _image_loader(a, env, conn, n_steps):
     if a.source_dtype == "uint8":
         norm = {"mean": [0.485, 0.456, 0.406], "std": [0.229, 0.224, 0.225], "layout": "chw"}
     n_epochs = math.ceil(n_steps / max(1, a.window // B)) + 2
-    dl = ddl_amd.DistributedDataLoader(
-        ImageWindowProducer(a.window, (3, 224, 224), a.source_dtype, refill="stamp"), B, conn, n_epochs,
-        env=env, device=torch.device(env.device), out_dtype=torch.bfloat16, shuffle="device", normalize=norm,
-        native_dispatch=False if a.dispatch == "python" else a.dispatch,
-        **({"prefetch_depth": a.depth} if a.depth else {}),
-        **({"max_ahead": a.max_ahead} if a.max_ahead is not None else {}), copy_timing=True)
+    dl = ddl_amd.DistributedDataLoader(ImageWindowProducer(a.window, (3, 224, 224), a.source_dtype, refill="stamp"), B,
+                                       conn, n_epochs, env=env, device=torch.device(env.device),
+                                       **{"prefetch_depth": a.depth} if a.depth else {},
+                                       **{"max_ahead": a.max_ahead} if a.max_ahead is not None else {},
+                                       output=ddl_amd.OutputSpec(dtype=torch.bfloat16, normalize=norm),
+                                       staging=ddl_amd.StagingSpec(
+                                           native_dispatch=a.dispatch != "python" and a.dispatch, copy_timing=True),
+                                       order=ddl_amd.OrderSpec(shuffle="device"))
 
     def gen():
         while True:
@@ -162,11 +164,11 @@ def _token_loader(a, env, conn, n_steps, src):
 
     B = a.batch or 2048
     n_epochs = n_steps // (src.n // B) + 2
-    dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(src, B, 4096, "pack", pack_order="ffd", host_threads=4,
-                                                          batches_per_window=a.tokens_k), B, conn,
-                                       n_epochs, mode="indexed", env=env, collate="tokens", auto_mark=True,
-                                       n_slots=2,
-                                       copy_timing=True, **({"prefetch_depth": a.depth} if a.depth else {}))
+    dl = ddl_amd.DistributedDataLoader(
+        TokenBatchProducer(src, B, 4096, "pack", pack_order="ffd", host_threads=4,
+                                                          batches_per_window=a.tokens_k), B, conn, n_epochs, env=env,
+        auto_mark=True, **{"prefetch_depth": a.depth} if a.depth else {}, output=ddl_amd.OutputSpec(collate="tokens"),
+        staging=ddl_amd.StagingSpec(n_slots=2, copy_timing=True), order=ddl_amd.OrderSpec(mode="indexed"))
 
     def gen():
         while True:

@@ -54,7 +54,7 @@ def main(argv=None):
             # one epoch more than is timed: the loader shuts its producers down at the end of its last epoch,
             # and that teardown (process exits) is not plumbing throughput
             dl = ddl_amd.DistributedDataLoader(IndexedProducer(src, a.global_batch, seed=3), lb, conn, a.epochs + 1,
-                                               mode="indexed", env=env, auto_mark=True)
+                                               env=env, auto_mark=True, order=ddl_amd.OrderSpec(mode="indexed"))
             bpe = dl.windows_per_epoch
             exact = True
             t0 = time.perf_counter()

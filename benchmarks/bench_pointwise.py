@@ -50,8 +50,11 @@ def main(argv=None) -> None:
         dev = torch.device(env.device)
         producer = PointwiseProducer(n_timesteps=a.timesteps, host_shuffle=a.host_shuffle)
         dl = ddl_amd.DistributedDataLoader(producer, 4096, conn, 10 ** 6, 0.0, "alltoall", env.rank, env.world_size,
-                                           env=env, shuffle="device", contiguous=True, seed=1,
-                                           native_dispatch={"native": True, "python": False}.get(a.dispatch, a.dispatch))
+                                           env=env, output=ddl_amd.OutputSpec(contiguous=True),
+                                           staging=ddl_amd.StagingSpec(
+                                               native_dispatch={"native": True, "python": False}.get(a.dispatch,
+                                                                                                     a.dispatch)),
+                                           order=ddl_amd.OrderSpec(shuffle="device", seed=1))
         acc = ops.ChecksumAccumulator(dev)
 
         def consume(groups):

@@ -90,10 +90,12 @@ def main(argv=None):
             producer = TokenBatchProducer(source, gb, a.seq_len, a.mode,
                                           pack_order=a.pack_order if a.mode == "pack" else "in_order",
                                           batches_per_window=a.batches_per_window, host_threads=a.host_threads)
-            dl = ddl_amd.DistributedDataLoader(producer, a.batch, conn,
-                                               n_epochs, mode="indexed", env=env, collate="tokens", auto_mark=True,
-                                               n_slots=a.slots, token_rows=a.token_rows,
-                                               native_dispatch=False if a.dispatch == "python" else a.dispatch)
+            dispatch = False if a.dispatch == "python" else a.dispatch
+            dl = ddl_amd.DistributedDataLoader(producer, a.batch, conn, n_epochs, env=env, auto_mark=True,
+                                               output=ddl_amd.OutputSpec(collate="tokens", token_rows=a.token_rows),
+                                               staging=ddl_amd.StagingSpec(n_slots=a.slots,
+                                                                           native_dispatch=dispatch),
+                                               order=ddl_amd.OrderSpec(mode="indexed"))
             dev = torch.device(env.device)
             acc = ops.ChecksumAccumulator(dev)  # one streaming launch per batch
 

@@ -30,8 +30,10 @@ def main(argv=None) -> int:
         res["indexed_first"] = bench.indexed_phase(args, env, dev, sync, sync)["value"]
         res["indexed_second"] = bench.indexed_phase(args, env, dev, sync, sync)["value"]
         dl = ddl_amd.DistributedDataLoader(ImageWindowProducer(256, (3, 224, 224), "bfloat16"), 256, conn,
-                                           math.ceil(300 / 1) + 1, env=env, device=dev, out_dtype=torch.bfloat16,
-                                           shuffle="device", prefetch_depth=4)
+                                           math.ceil(300 / 1) + 1, env=env, device=dev,
+                                           output=ddl_amd.OutputSpec(dtype=torch.bfloat16),
+                                           staging=ddl_amd.StagingSpec(prefetch_depth=4),
+                                           order=ddl_amd.OrderSpec(shuffle="device"))
         acc = ops.ChecksumAccumulator(dev)
         for e in range(300):
             (x,) = dl[0]

@@ -328,6 +328,7 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
         else:
             self.shard = self._load_shard(reader, chunk_bytes, host_threads)
         self.load_s = time.perf_counter() - t0
+        self.resident_rows = int(self.shard.shape[0])
         self.prep_stream = streams.batch_stream(self.device) if self.device.type == "cuda" else None
         if self.device.type == "cuda" and self.W > 1 and not self.replicated:  # owner-bucketing outputs (prep stream)
             self._send_idx = torch.empty(self.GB, dtype=torch.int64, device=self.device)
@@ -367,12 +368,16 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
         buffers, PCIe, all ranks in parallel), straight into its place in the replica; then chunked RCCL
         ``all_gather``s over xGMI fill the other W-1 slices (chunk_bytes per rank per round: the collective's
         flat staging stays at W x chunk_bytes of HBM). With ``scatter_from`` only that rank holds the dataset:
-        it streams chunks H2D and ``broadcast``s each one. The replica has S*W rows (<= W-1 padding rows past
+        it streams chunks H2D and distributes each one as a scatter + all-gather -- grouped point-to-point
+        sends of piece q of the chunk to rank q (every xGMI link of the source carries 1/W of the chunk at
+        once), then an all-gather of the pieces -- instead of a ring broadcast, which is bound by one link
+        (SURVEY §5, MI355X-native communication design). The replica has at least S*W rows (padding rows past
         N, never addressed: the epoch permutation ranges over [0, N)). Steps then gather the rank's slice of
         every global batch from its own replica: no per-step collective at all."""
         import torch.distributed as dist
 
-        rows_total = self.S * self.W
+        W = self.W
+        rows_total = max(self.S * W, self.N + W)  # + the last scatter chunk's piece padding
         replica = torch.empty((rows_total,) + self.sample_shape, dtype=self.src_dtype, device=self.device)
         probe = torch.zeros(1, device=self.device)
         issue(self.env, self.group, "resident.bringup")
@@ -384,21 +389,31 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
             with trace_range("ddl.resident.replicate"):
                 for k, c0 in enumerate(range(0, self.S, cr)):
                     c1 = min(self.S, c0 + cr)
-                    outs = [replica[q * self.S + c0:q * self.S + c1] for q in range(self.W)]
+                    outs = [replica[q * self.S + c0:q * self.S + c1] for q in range(W)]
                     issue(self.env, self.group, "resident.replicate", k)
                     dist.all_gather(outs, outs[self.rank], group=self.group)
-                    self.bytes_replicated += (self.W - 1) * (c1 - c0) * self.row_bytes
+                    self.bytes_replicated += (W - 1) * (c1 - c0) * self.row_bytes
         else:
             t0 = time.perf_counter()
             src = self.rank == scatter_from
+            span = W * max(1, -(-cr // W))  # chunk rows: W pieces
             with trace_range("ddl.resident.replicate"):
-                for k, c0 in enumerate(range(0, self.N, cr)):
-                    c1 = min(self.N, c0 + cr)
+                for k, c0 in enumerate(range(0, self.N, span)):
+                    n_rows = min(span, self.N - c0)
+                    pr = -(-n_rows // W)  # piece rows (the last piece may run into the padding)
+                    pieces = [replica[c0 + q * pr:c0 + (q + 1) * pr] for q in range(W)]
                     if src:
-                        self._load_rows(reader, replica, c0, c1 - c0, chunk_bytes, host_threads)
+                        self._load_rows(reader, replica, c0, n_rows, chunk_bytes, host_threads)
+                        p2p = [dist.P2POp(dist.isend, pieces[q], q, group=self.group) for q in range(W)
+                               if q != scatter_from]
+                    else:
+                        p2p = [dist.P2POp(dist.irecv, pieces[self.rank], scatter_from, group=self.group)]
+                    check_group(self.env, self.group, "resident.replicate_scatter")
+                    for req in dist.batch_isend_irecv(p2p):
+                        req.wait()
                     issue(self.env, self.group, "resident.replicate", k)
-                    dist.broadcast(replica[c0:c1], scatter_from, group=self.group)
-                    self.bytes_replicated += (c1 - c0) * self.row_bytes * (self.W - 1 if src else 0)
+                    dist.all_gather(pieces, pieces[self.rank], group=self.group)
+                    self.bytes_replicated += (W - 1) * pr * self.row_bytes * (2 if src else 1)
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
         self.replicate_s = time.perf_counter() - t0
@@ -611,7 +626,7 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
             mean=norm.get("mean"), std=norm.get("std"), **kw)
 
     def stats(self) -> dict:
-        rows = self.S * self.W if self.replicated else self.hi - self.lo
+        rows = self.resident_rows
         return {"batches": self.batches, "replicated": self.replicated, "bytes_exchanged": self.bytes_exchanged,
                 "bytes_replicated": self.bytes_replicated, "resident_rows": rows,
                 "shard_rows": self.hi - self.lo, "shard_bytes": rows * self.row_bytes,

@@ -59,8 +59,10 @@ def gpu_loader(args) -> None:
 
     with ddl_amd.start(n_producers=2, peer_timeout_s=args.peer_timeout, timeout_s=args.timeout) as (env, conn):
         dl = ddl_amd.DistributedDataLoader(IdProducer(64, 6), 16, conn, 1000, 0.5, "alltoall", env=env,
-                                           copy_batches=True, seed=1, device=torch.device(env.device),
-                                           prefetch_depth=2)
+                                           device=torch.device(env.device),
+                                           output=ddl_amd.OutputSpec(copy_batches=True),
+                                           staging=ddl_amd.StagingSpec(prefetch_depth=2),
+                                           order=ddl_amd.OrderSpec(seed=1))
         n = 0
         for epoch in range(1000):
             for a, _ in dl:

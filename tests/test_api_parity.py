@@ -54,7 +54,8 @@ def test_reference_protocol_methods_drive_the_window_round_robin():
     consumer to the next producer's window exactly as mark(END_OF_BATCH) does at a window's end
     (reference ddl/mpi_dataloader.py:220-227)."""
     with ddl_amd.start(n_producers=3) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(IdProducer(8, 4), 4, conn, 1, env=env, mode="split_along_epoch")
+        dl = ddl_amd.DistributedDataLoader(IdProducer(8, 4), 4, conn, 1, env=env,
+                                           order=ddl_amd.OrderSpec(mode="split_along_epoch"))
         assert len(dl) == 6 and dl.target_rank == 1
         _, rest = dl[0]
         dl.mark(Marker.END_OF_BATCH)
@@ -95,8 +96,10 @@ def test_specs_validate_and_legacy_keywords_are_deprecated_aliases():
         StagingSpec(max_ahead=-1)
     with pytest.raises(TypeError):
         resolve(None, None, None, {"not_an_option": 1})
-    with pytest.warns(DeprecationWarning, match=r"order=OrderSpec\(seed=...\)"):
+    with pytest.warns(DeprecationWarning) as rec:
         out, stg, odr = resolve(None, StagingSpec(prefetch_depth=2), None, {"seed": 5, "out_dtype": torch.bfloat16})
+    msgs = sorted(str(w.message) for w in rec)
+    assert any("order=OrderSpec(seed=...)" in m for m in msgs) and any("output=OutputSpec(dtype=...)" in m for m in msgs)
     assert odr.seed == 5 and out.dtype is torch.bfloat16 and stg.prefetch_depth == 2
     with pytest.raises(dataclasses_frozen_error()):
         odr.seed = 1  # records are frozen

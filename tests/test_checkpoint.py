@@ -15,7 +15,7 @@ from ddl_amd.exceptions import ShapeMismatchError
 from tests.helpers import IdProducer
 
 EPOCHS = 3
-KW = dict(copy_batches=True, shuffle="device", seed=7)
+KW = dict(output=ddl_amd.OutputSpec(copy_batches=True), order=ddl_amd.OrderSpec(shuffle="device", seed=7))
 
 
 def _device():
@@ -45,7 +45,8 @@ def _take(dl, n):
 
 def _full(n_slots=1, n_producers=3):
     with ddl_amd.start(n_producers=n_producers) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(IdProducer(16, 4), 4, conn, EPOCHS, env=env, n_slots=n_slots, **KW)
+        dl = ddl_amd.DistributedDataLoader(IdProducer(16, 4), 4, conn, EPOCHS, env=env, **KW,
+                                           staging=ddl_amd.StagingSpec(n_slots=n_slots))
         return _take(dl, 10 ** 9)
 
 
@@ -109,13 +110,14 @@ def test_resume_with_a_different_slot_count():
     full = _full(n_slots=1)
     assert all(torch.equal(a, b) for a, b in zip(_full(n_slots=2), full))
     with ddl_amd.start(n_producers=3) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(IdProducer(16, 4), 4, conn, EPOCHS, env=env, n_slots=1, **KW)
+        dl = ddl_amd.DistributedDataLoader(IdProducer(16, 4), 4, conn, EPOCHS, env=env, **KW,
+                                           staging=ddl_amd.StagingSpec(n_slots=1))
         head = _take(dl, 5)
         sd = dl.state_dict()
         dl.close()
     with ddl_amd.start(n_producers=3) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(IdProducer(16, 4), 4, conn, EPOCHS, env=env, n_slots=3, resume_state=sd,
-                                           **KW)
+        dl = ddl_amd.DistributedDataLoader(IdProducer(16, 4), 4, conn, EPOCHS, env=env, resume_state=sd, **KW,
+                                           staging=ddl_amd.StagingSpec(n_slots=3))
         tail = _take(dl, 10 ** 9)
     assert all(torch.equal(a, b) for a, b in zip(head + tail, full))
 

@@ -135,8 +135,8 @@ def test_verify_order_knob(monkeypatch):
     src = SharedArraySource.create(f"ddl_amd_cfg_{np.random.randint(1 << 30)}", torch.arange(2 * n).view(n, 2))
     try:
         with ddl_amd.start(n_producers=1) as (env, conn):
-            dl = ddl_amd.DistributedDataLoader(IndexedProducer(src, gb), gb, conn, 1, mode="indexed", env=env,
-                                               auto_mark=True, seed=3)
+            dl = ddl_amd.DistributedDataLoader(IndexedProducer(src, gb), gb, conn, 1, env=env, auto_mark=True,
+                                               order=ddl_amd.OrderSpec(mode="indexed", seed=3))
             assert dl._verify is not None
             assert sum(1 for _ in dl) == n // gb
             assert dl.verified_windows == n // gb

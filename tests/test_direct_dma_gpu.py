@@ -25,6 +25,11 @@ pytestmark = pytest.mark.gpu
 N, WIDTH, B, P, SEED = 64, 8, 16, 2, 3
 
 
+def _dispatch(name: str):
+    """StagingSpec.native_dispatch for a test's dispatch id ("python": the Python path)."""
+    return False if name == "python" else name
+
+
 def producer_window(p: int, rnd: int) -> torch.Tensor:
     """The window producer ``p`` writes in round ``rnd`` (IdProducer._write, rank 0), int32 [N, WIDTH]."""
     t = torch.empty(N, WIDTH, dtype=torch.int32)
@@ -58,8 +63,10 @@ def test_direct_dma_batches_equal_the_producers_bytes(dispatch, slow, direct):
     producer's window rows in the window's order, bitwise."""
     with ddl_amd.start(n_producers=P) as (env, conn):
         dl = ddl_amd.DistributedDataLoader(IdProducer(N, WIDTH), B, conn, 8, env=env, device=torch.device("cuda"),
-                                           shuffle="device", seed=SEED, prefetch_depth=2, copy_batches=True,
-                                           native_dispatch=dispatch if dispatch != "python" else False)
+                                           output=ddl_amd.OutputSpec(copy_batches=True),
+                                           staging=ddl_amd.StagingSpec(prefetch_depth=2,
+                                                                       native_dispatch=_dispatch(dispatch)),
+                                           order=ddl_amd.OrderSpec(shuffle="device", seed=SEED))
         st = dl.stats()
         assert st["direct_dma"] is direct, st.get("direct_dma_reason")
         w = 0
@@ -90,9 +97,11 @@ def test_stuck_copy_raises_within_the_timeout_and_close_returns(dispatch):
     timeout_s = 3.0
     with ddl_amd.start(n_producers=P) as (env, conn):
         dl = ddl_amd.DistributedDataLoader(IdProducer(N, WIDTH), B, conn, 8, env=env, device=torch.device("cuda"),
-                                           shuffle="device", seed=SEED, prefetch_depth=2, copy_batches=True,
-                                           timeout_s=timeout_s,
-                                           native_dispatch=dispatch if dispatch != "python" else False)
+                                           output=ddl_amd.OutputSpec(copy_batches=True),
+                                           staging=ddl_amd.StagingSpec(prefetch_depth=2,
+                                                                       timeout_s=timeout_s,
+                                               native_dispatch=_dispatch(dispatch)),
+                                           order=ddl_amd.OrderSpec(shuffle="device", seed=SEED))
         if not dl._stager.direct_dma:
             pytest.skip(f"no direct DMA here: {dl.stats()['direct_dma_reason']}")
         dl._stager._native.inject_stuck_copy(3)  # windows 0 and 1 fill the 2-buffer ring; 3 is not staged yet
@@ -127,9 +136,11 @@ def test_consumer_times_out_first_and_pending_copies_are_quarantined(dispatch):
     timeout_s = 2.0
     with ddl_amd.start(n_producers=P) as (env, conn):
         dl = ddl_amd.DistributedDataLoader(IdProducer(N, WIDTH), B, conn, 8, env=env, device=torch.device("cuda"),
-                                           shuffle="device", seed=SEED, prefetch_depth=2, copy_batches=True,
-                                           timeout_s=timeout_s,
-                                           native_dispatch=dispatch if dispatch != "python" else False)
+                                           output=ddl_amd.OutputSpec(copy_batches=True),
+                                           staging=ddl_amd.StagingSpec(prefetch_depth=2,
+                                                                       timeout_s=timeout_s,
+                                               native_dispatch=_dispatch(dispatch)),
+                                           order=ddl_amd.OrderSpec(shuffle="device", seed=SEED))
         st = dl._stager
         if not st.direct_dma:
             pytest.skip(f"no direct DMA here: {dl.stats()['direct_dma_reason']}")
@@ -164,7 +175,8 @@ def test_direct_dma_copy_timing_is_off_unless_asked():
     stager turns it off again when it is done with it (reference counted)."""
     with ddl_amd.start(n_producers=P) as (env, conn):
         dl = ddl_amd.DistributedDataLoader(IdProducer(N, WIDTH), B, conn, 2, env=env, device=torch.device("cuda"),
-                                           prefetch_depth=2, copy_batches=True)
+                                           output=ddl_amd.OutputSpec(copy_batches=True),
+                                           staging=ddl_amd.StagingSpec(prefetch_depth=2))
         st = dl._stager
         assert not st.copy_timing
         st.copy_timing = True
@@ -231,7 +243,8 @@ def test_long_run_reanchors_and_flags_trimmed_copy_logs():
         e0.record()
         t0_ns = rt.now_ns()
         dl = ddl_amd.DistributedDataLoader(IdProducer(64, 64), 64, conn, n_win, env=env, device=torch.device("cuda"),
-                                           prefetch_depth=4, copy_batches=True, copy_timing=True)
+                                           output=ddl_amd.OutputSpec(copy_batches=True),
+                                           staging=ddl_amd.StagingSpec(prefetch_depth=4, copy_timing=True))
         em = None
         for e in range(n_win):
             if e == n_win - 200:

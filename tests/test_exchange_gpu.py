@@ -56,7 +56,8 @@ def test_loader_with_exchange_enabled_on_gpu(rccl_env, monkeypatch, method):
     conn = launcher.spawn_producers(ddl_amd.parallel.read_env(2), mode="thread")
     try:
         dl = ddl_amd.DistributedDataLoader(IdProducer(64, 8), 16, conn, 4, 0.5, method, env=rccl_env,
-                                           shuffle="device", copy_batches=True, seed=2)
+                                           output=ddl_amd.OutputSpec(copy_batches=True),
+                                           order=ddl_amd.OrderSpec(shuffle="device", seed=2))
         assert dl._exchange_fn is not None and dl._stager.stream is not dl._stager.copy_stream
         for e in range(4):
             rows = []
@@ -84,7 +85,8 @@ def test_partial_epochs_with_exchange_keep_windows_intact(rccl_env):
     conn = launcher.spawn_producers(ddl_amd.parallel.read_env(P), mode="thread")
     try:
         dl = ddl_amd.DistributedDataLoader(IdProducer(256, 8), 16, conn, 12, 0.5, "alltoall", env=rccl_env,
-                                           shuffle="device", copy_batches=True, seed=5, mode="split_along_epoch")
+                                           output=ddl_amd.OutputSpec(copy_batches=True),
+                                           order=ddl_amd.OrderSpec(shuffle="device", seed=5, mode="split_along_epoch"))
         for e in range(12):
             w = dl.window
             for i, (a, b) in enumerate(dl):
@@ -111,7 +113,9 @@ def _exchange_run(env, dispatch, epochs=4, restore_at=None):
     out, sd, n = [], None, 0
     try:
         dl = ddl_amd.DistributedDataLoader(IdProducer(64, 8), 16, conn, epochs, 0.5, "alltoall", env=env,
-                                           shuffle="device", copy_batches=True, seed=2, native_dispatch=dispatch)
+                                           output=ddl_amd.OutputSpec(copy_batches=True),
+                                           staging=ddl_amd.StagingSpec(native_dispatch=dispatch),
+                                           order=ddl_amd.OrderSpec(shuffle="device", seed=2))
         mode = dl.stats().get("native_dispatch", {}).get("mode") if dispatch else "python"
         while dl.epoch < epochs:
             for i in range(dl.epoch_batch, len(dl)):
@@ -176,8 +180,10 @@ def test_exchange_stuck_copy_raises_within_the_timeout(rccl_env, dispatch):
     conn = launcher.spawn_producers(ddl_amd.parallel.read_env(2), mode="thread")
     try:
         dl = ddl_amd.DistributedDataLoader(IdProducer(64, 8), 16, conn, 8, 0.5, "alltoall", env=rccl_env,
-                                           shuffle="device", copy_batches=True, seed=2, prefetch_depth=2,
-                                           timeout_s=3.0, native_dispatch=dispatch)
+                                           output=ddl_amd.OutputSpec(copy_batches=True),
+                                           staging=ddl_amd.StagingSpec(prefetch_depth=2, timeout_s=3.0,
+                                                                       native_dispatch=dispatch),
+                                           order=ddl_amd.OrderSpec(shuffle="device", seed=2))
         if not dl._stager.direct_dma:
             pytest.skip("no direct DMA here")
         dl._stager._native.inject_stuck_copy(4)  # not staged yet: the 3-buffer ring holds windows 0..2

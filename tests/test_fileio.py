@@ -80,8 +80,8 @@ def test_file_source_indexed_loader(npy):
     path, arr = npy
     src = FileRowsSource.from_npy(str(path))
     with ddl_amd.start(n_producers=2, device="cpu") as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(IndexedProducer(src, 100, seed=4), 100, conn, 2, mode="indexed",
-                                           env=env, auto_mark=True)
+        dl = ddl_amd.DistributedDataLoader(IndexedProducer(src, 100, seed=4), 100, conn, 2, env=env, auto_mark=True,
+                                           order=ddl_amd.OrderSpec(mode="indexed"))
         got = [torch.cat([b[0].cpu() for b in dl]).numpy() for _ in range(2)]
     for e in range(2):
         ref = EpochOrder(3001, 100, 4).perm(e).full()[:3000]

@@ -68,8 +68,9 @@ def corpus():
 
 def _token_loader(corpus, conn, env, mode, dispatch, epochs=2):
     return ddl_amd.DistributedDataLoader(TokenBatchProducer(corpus, 16, 256, mode, batches_per_window=4), 16, conn,
-                                         epochs, mode="indexed", env=env, collate="tokens", seed=4,
-                                         native_dispatch=dispatch)
+                                         epochs, env=env, output=ddl_amd.OutputSpec(collate="tokens"),
+                                         staging=ddl_amd.StagingSpec(native_dispatch=dispatch),
+                                         order=ddl_amd.OrderSpec(mode="indexed", seed=4))
 
 
 @pytest.mark.parametrize("dispatch", ["inline", "window", False])
@@ -122,9 +123,10 @@ def test_token_loader_live_set_epoch(corpus, dispatch):
 
 def _image_loader(conn, env, dispatch, epochs=3):
     norm = {"mean": [0.485, 0.456, 0.406], "std": [0.229, 0.224, 0.225]}
-    return ddl_amd.DistributedDataLoader(ImageWindowProducer(16, (3, 8, 8), "uint8", seed=5), 4, conn, epochs,
-                                         env=env, out_dtype=torch.bfloat16, shuffle="device", seed=9,
-                                         normalize=norm, native_dispatch=dispatch)
+    return ddl_amd.DistributedDataLoader(ImageWindowProducer(16, (3, 8, 8), "uint8", seed=5), 4, conn, epochs, env=env,
+                                         output=ddl_amd.OutputSpec(dtype=torch.bfloat16, normalize=norm),
+                                         staging=ddl_amd.StagingSpec(native_dispatch=dispatch),
+                                         order=ddl_amd.OrderSpec(shuffle="device", seed=9))
 
 
 @pytest.mark.parametrize("dispatch", ["auto", "lookahead", False])

@@ -82,8 +82,9 @@ def test_zero_copy_views_alias_the_window():
 
 def test_split_along_epoch_mode():
     with ddl_amd.start(n_producers=3) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(IdProducer(32, 4), 8, conn, 2, env=env, mode="split_along_epoch",
-                                           copy_batches=True)
+        dl = ddl_amd.DistributedDataLoader(IdProducer(32, 4), 8, conn, 2, env=env,
+                                           output=ddl_amd.OutputSpec(copy_batches=True),
+                                           order=ddl_amd.OrderSpec(mode="split_along_epoch"))
         assert len(dl) == 12
         eps = _epochs(dl, 2)
     for e, rows in enumerate(eps):
@@ -94,7 +95,8 @@ def test_split_along_epoch_mode():
 
 def test_auto_mark_dataloader_dropin_with_slots():
     with ddl_amd.start(n_producers=2) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(IdProducer(20, 4), 5, conn, 4, env=env, auto_mark=True, n_slots=2)
+        dl = ddl_amd.DistributedDataLoader(IdProducer(20, 4), 5, conn, 4, env=env, auto_mark=True,
+                                           staging=ddl_amd.StagingSpec(n_slots=2))
         seen = []
         for epoch in range(4):
             seen.append(torch.cat([torch.cat(b, 1) for b in dl]))
@@ -109,7 +111,8 @@ def test_column_normalisation_applies_with_owned_batches(auto_mark):
     mean, std = [1.0, 2.0, 3.0, 4.0], [2.0, 4.0, 0.5, 1.0]
     with ddl_amd.start(n_producers=1) as (env, conn):
         dl = ddl_amd.DistributedDataLoader(IdProducer(20, 4, dtype="float32"), 5, conn, 1, env=env,
-                                           auto_mark=auto_mark, normalize={"mean": mean, "std": std})
+                                           auto_mark=auto_mark,
+                                           output=ddl_amd.OutputSpec(normalize={"mean": mean, "std": std}))
         got = []
         for b in dl:
             assert all(t.is_contiguous() for t in b) or not auto_mark
@@ -130,7 +133,8 @@ def test_host_device_shuffle_uses_feistel_order():
     from ddl_amd.permutation import FeistelPermutation
 
     with ddl_amd.start(n_producers=2) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(IdProducer(40, 4), 8, conn, 2, env=env, shuffle="device", seed=3)
+        dl = ddl_amd.DistributedDataLoader(IdProducer(40, 4), 8, conn, 2, env=env,
+                                           order=ddl_amd.OrderSpec(shuffle="device", seed=3))
         eps = _epochs(dl, 2)
     for e, rows in enumerate(eps):
         perm = FeistelPermutation(40, 3, window_perm_key(e, 0)).full()  # window e: producer e, round 0
@@ -158,24 +162,27 @@ def test_decorator_forwards_kwargs_and_runs_producers():
 def test_thread_mode_producers(monkeypatch):
     monkeypatch.setenv("DDL_PRODUCER_MODE", "thread")
     with ddl_amd.start(n_producers=2) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(IdProducer(16, 4), 4, conn, 3, env=env, copy_batches=True)
+        dl = ddl_amd.DistributedDataLoader(IdProducer(16, 4), 4, conn, 3, env=env,
+                                           output=ddl_amd.OutputSpec(copy_batches=True))
         eps = _epochs(dl, 3)
     assert [r[:, 1].unique().item() for r in eps] == [0, 1, 0]
 
 
 def test_resume_from_state_dict():
     with ddl_amd.start(n_producers=3) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(IdProducer(16, 4), 4, conn, 5, env=env, copy_batches=True)
+        dl = ddl_amd.DistributedDataLoader(IdProducer(16, 4), 4, conn, 5, env=env,
+                                           output=ddl_amd.OutputSpec(copy_batches=True))
         first = _epochs(dl, 2)
         sd = dl.state_dict()
         dl.close()
     assert sd["epoch"] == 2 and sd["window"] == 2 and sd["batch"] == 0
     with ddl_amd.start(n_producers=3) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(IdProducer(16, 4), 4, conn, 5, env=env, copy_batches=True,
-                                           resume_state=sd)
+        dl = ddl_amd.DistributedDataLoader(IdProducer(16, 4), 4, conn, 5, env=env, resume_state=sd,
+                                           output=ddl_amd.OutputSpec(copy_batches=True))
         rest = _epochs(dl, 3)
     with ddl_amd.start(n_producers=3) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(IdProducer(16, 4), 4, conn, 5, env=env, copy_batches=True)
+        dl = ddl_amd.DistributedDataLoader(IdProducer(16, 4), 4, conn, 5, env=env,
+                                           output=ddl_amd.OutputSpec(copy_batches=True))
         full = _epochs(dl, 5)
     for a, b in zip(first + rest, full):
         assert torch.equal(a, b)  # the resumed run continues bit-identically
@@ -184,7 +191,9 @@ def test_resume_from_state_dict():
 @pytest.mark.parametrize("auto_mark", [False, True])
 def test_resume_mid_window_is_exact(auto_mark):
     """Checkpoint after 6 of 12 batches (windows of 4 batches: mid-window of epoch 1), resume in a fresh job."""
-    kw = dict(env=None, copy_batches=True, shuffle="device", seed=7, auto_mark=auto_mark)
+    kw = dict(env=None, output=ddl_amd.OutputSpec(copy_batches=True), order=ddl_amd.OrderSpec(shuffle="device",
+                                                                                              seed=7),
+              auto_mark=auto_mark)
 
     def run(n_batches, resume=None):
         rows, sd = [], None

@@ -7,6 +7,7 @@ import torch
 import ddl_amd
 from ddl_amd import Marker
 from ddl_amd.dataloader import window_perm_key
+from ddl_amd.specs import from_flat
 from ddl_amd.permutation import FeistelPermutation
 from tests.helpers import IdProducer
 
@@ -16,8 +17,10 @@ pytestmark = pytest.mark.gpu
 def _run(n_producers=3, n=64, bs=16, epochs=6, shuffle="device", n_slots=1, depth=2, out_dtype=None):
     seen = []
     with ddl_amd.start(n_producers=n_producers) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(IdProducer(n, 8), bs, conn, epochs, env=env, shuffle=shuffle,
-                                           n_slots=n_slots, prefetch_depth=depth, out_dtype=out_dtype, seed=11)
+        dl = ddl_amd.DistributedDataLoader(IdProducer(n, 8), bs, conn, epochs, env=env,
+                                           output=ddl_amd.OutputSpec(dtype=out_dtype),
+                                           staging=ddl_amd.StagingSpec(n_slots=n_slots, prefetch_depth=depth),
+                                           order=ddl_amd.OrderSpec(shuffle=shuffle, seed=11))
         assert dl.device.type == "cuda"
         for e in range(epochs):
             rows = []
@@ -76,8 +79,8 @@ def test_gpu_indexed_mode_world_size_invariant_order():
     src = SharedArraySource.create(f"ddl_amd_gsrc_{np.random.randint(1 << 30)}", data)
     try:
         with ddl_amd.start(n_producers=3) as (env, conn):
-            dl = ddl_amd.DistributedDataLoader(IndexedProducer(src, gb), gb, conn, 2, mode="indexed", env=env,
-                                               auto_mark=True, seed=9)
+            dl = ddl_amd.DistributedDataLoader(IndexedProducer(src, gb), gb, conn, 2, env=env, auto_mark=True,
+                                               order=ddl_amd.OrderSpec(mode="indexed", seed=9))
             order = EpochOrder(n, gb, 9)
             for e in range(2):
                 got = torch.cat([b[0][:, 0].cpu() for b in dl]).numpy()
@@ -99,8 +102,8 @@ def test_gpu_file_source_indexed_and_resident(tmp_path):
     order = EpochOrder(n, gb, 5)
     ref = arr[order.perm(0).full()[: order.batches_per_epoch * gb]]
     with ddl_amd.start(n_producers=2) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(IndexedProducer(src, gb), gb, conn, 1, mode="indexed", env=env,
-                                           auto_mark=True, seed=5)
+        dl = ddl_amd.DistributedDataLoader(IndexedProducer(src, gb), gb, conn, 1, env=env, auto_mark=True,
+                                           order=ddl_amd.OrderSpec(mode="indexed", seed=5))
         got = torch.cat([b[0].cpu() for b in dl]).numpy()
     assert np.array_equal(got.reshape(ref.shape), ref)
     res = ResidentGlobalLoader(src, gb, seed=5, n_epochs=1, chunk_bytes=64 << 10)
@@ -115,9 +118,11 @@ def test_gpu_uint8_normalised_and_hwc_collate():
 
     mean, std = [0.485, 0.456, 0.406], [0.229, 0.224, 0.225]
     with ddl_amd.start(n_producers=2) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(ImageWindowProducer(32, (3, 24, 24), "uint8", refill="none"), 8, conn,
-                                           2, env=env, out_dtype=torch.bfloat16, shuffle="none",
-                                           normalize={"mean": mean, "std": std})
+        dl = ddl_amd.DistributedDataLoader(ImageWindowProducer(32, (3, 24, 24), "uint8", refill="none"), 8, conn, 2,
+                                           env=env,
+                                           output=ddl_amd.OutputSpec(dtype=torch.bfloat16, normalize={"mean": mean,
+                                                                     "std": std}),
+                                           order=ddl_amd.OrderSpec(shuffle="none"))
         (x,) = dl[0]
         _, win = dl.arys[0][0]
         ref = ((win[:8].float() / 255 - torch.tensor(mean).view(1, 3, 1, 1)) / torch.tensor(std).view(1, 3, 1, 1))
@@ -129,8 +134,10 @@ def test_gpu_uint8_normalised_and_hwc_collate():
             dl.mark(Marker.END_OF_BATCH)
         dl.mark(Marker.END_OF_EPOCH)
     with ddl_amd.start(n_producers=1) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(ImageWindowProducer(16, (20, 20, 3), "uint8", refill="none"), 4, conn,
-                                           1, env=env, normalize={"mean": mean, "std": std, "layout": "hwc"})
+        dl = ddl_amd.DistributedDataLoader(ImageWindowProducer(16, (20, 20, 3), "uint8", refill="none"), 4, conn, 1,
+                                           env=env,
+                                           output=ddl_amd.OutputSpec(normalize={"mean": mean, "std": std,
+                                                                     "layout": "hwc"}))
         (x,) = dl[1]
         _, win = dl.arys[0][0]
         ref = ((win[4:8].float() / 255 - torch.tensor(mean)) / torch.tensor(std)).permute(0, 3, 1, 2)
@@ -145,8 +152,9 @@ def test_gpu_resume_mid_window_is_exact():
     def run(n_batches, resume=None):
         rows, sd = [], None
         with ddl_amd.start(n_producers=3) as (env, conn):
-            dl = ddl_amd.DistributedDataLoader(IdProducer(64, 8), 16, conn, 3, env=env, copy_batches=True,
-                                               shuffle="device", seed=5, auto_mark=True, resume_state=resume)
+            dl = ddl_amd.DistributedDataLoader(IdProducer(64, 8), 16, conn, 3, env=env, auto_mark=True,
+                                               resume_state=resume, output=ddl_amd.OutputSpec(copy_batches=True),
+                                               order=ddl_amd.OrderSpec(shuffle="device", seed=5))
             assert dl.device.type == "cuda"
             done = 0
             while dl.epoch < 3 and done < n_batches:
@@ -177,7 +185,8 @@ def test_gpu_native_stager_surfaces_producer_faults(monkeypatch, fault, exc):
     monkeypatch.setenv("DDL_FAULT_PRODUCER", fault)
     with pytest.raises(getattr(exceptions, exc)):
         with ddl_amd.start(n_producers=2, timeout_s=4) as (env, conn):
-            dl = ddl_amd.DistributedDataLoader(IdProducer(8, 4), 4, conn, 10, env=env, shuffle="device")
+            dl = ddl_amd.DistributedDataLoader(IdProducer(8, 4), 4, conn, 10, env=env,
+                                               order=ddl_amd.OrderSpec(shuffle="device"))
             assert dl._stager is not None
             for _ in range(10):
                 for _b in dl:
@@ -193,10 +202,12 @@ def test_gpu_augment_random_resized_crop_in_loader():
     def run():
         outs = []
         with ddl_amd.start(n_producers=2) as (env, conn):
-            dl = ddl_amd.DistributedDataLoader(
-                ImageWindowProducer(32, (3, 64, 80), "uint8", refill="none"), 8, conn, 2, env=env,
-                shuffle="device", seed=3, normalize={"mean": mean, "std": std}, copy_batches=True,
-                augment={"size": (32, 32), "scale": (0.2, 1.0), "flip_p": 0.5})
+            dl = ddl_amd.DistributedDataLoader(ImageWindowProducer(32, (3, 64, 80), "uint8", refill="none"), 8, conn,
+                                               2, env=env,
+                                               output=ddl_amd.OutputSpec(normalize={"mean": mean, "std": std},
+                                                                         copy_batches=True, augment={"size": (32, 32),
+                                                                         "scale": (0.2, 1.0), "flip_p": 0.5}),
+                                               order=ddl_amd.OrderSpec(shuffle="device", seed=3))
             for _ in range(2):
                 for (x,) in dl:
                     assert x.shape == (8, 3, 32, 32) and x.dtype == torch.bfloat16 and x.is_cuda
@@ -223,7 +234,8 @@ def test_gpu_exception_unwinds_cleanly_with_native_stager():
     with pytest.raises(KeyError):
         with ddl_amd.start(n_producers=2) as (env, conn):
             dl = ddl_amd.DistributedDataLoader(IdProducer(64, 8, delay_s=2.0), 16, conn, 5, env=env,
-                                               shuffle="device", n_slots=2, prefetch_depth=2)
+                                               staging=ddl_amd.StagingSpec(n_slots=2, prefetch_depth=2),
+                                               order=ddl_amd.OrderSpec(shuffle="device"))
             next(iter(dl))
             raise KeyError("user error")
     assert time.monotonic() - t0 < 30
@@ -264,7 +276,8 @@ def _collect(native, make, epochs=4, partial=None, **kw):
     out = []
     with ddl_amd.start(n_producers=3) as (env, conn):
         prod, bs = make()
-        dl = ddl_amd.DistributedDataLoader(prod, bs, conn, epochs, env=env, native_dispatch=native, **kw)
+        dl = ddl_amd.DistributedDataLoader(prod, bs, conn, epochs, env=env,
+                                           **from_flat(dict(kw, native_dispatch=native)))
         for e in range(epochs):
             for i in range(len(dl)):
                 if partial and i >= partial.get(e, 10 ** 9):
@@ -325,7 +338,7 @@ def test_native_dispatch_held_batches_stay_valid():
 
     with ddl_amd.start(n_producers=3) as (env, conn):
         dl = ddl_amd.DistributedDataLoader(ImageWindowProducer(32, (3, 16, 16), "bfloat16", seed=3), 8, conn, 30,
-                                           env=env, shuffle="device", seed=2)
+                                           env=env, order=ddl_amd.OrderSpec(shuffle="device", seed=2))
         held, snap = [], []
         for e in range(30):
             for i in range(len(dl)):
@@ -351,7 +364,8 @@ def test_window_dispatch_batches_on_other_streams():
     out = []
     with ddl_amd.start(n_producers=3) as (env, conn):
         prod, bs = make()
-        dl = ddl_amd.DistributedDataLoader(prod, bs, conn, 2, env=env, native_dispatch="window", **kw)
+        dl = ddl_amd.DistributedDataLoader(prod, bs, conn, 2, env=env,
+                                           **from_flat(dict(kw, native_dispatch="window")))
         for e in range(2):
             for i in range(len(dl)):
                 with torch.cuda.stream(side[i % 2]):
@@ -378,7 +392,8 @@ def test_inline_dispatch_window_read_on_two_streams_is_not_overwritten():
     out = []
     with ddl_amd.start(n_producers=3) as (env, conn):
         prod, bs = make()
-        dl = ddl_amd.DistributedDataLoader(prod, bs, conn, 3, env=env, native_dispatch="inline", **kw)
+        dl = ddl_amd.DistributedDataLoader(prod, bs, conn, 3, env=env,
+                                           **from_flat(dict(kw, native_dispatch="inline")))
         for e in range(3):
             held = []
             for i in range(len(dl)):
@@ -407,8 +422,9 @@ def test_stager_counts_the_copies_of_a_time_window():
     rt = _native.runtime()
     with ddl_amd.start(n_producers=3) as (env, conn):
         t0 = rt.now_ns()
-        dl = ddl_amd.DistributedDataLoader(IdProducer(64, 8), 16, conn, 4, env=env, shuffle="device", seed=2,
-                                           copy_batches=True)
+        dl = ddl_amd.DistributedDataLoader(IdProducer(64, 8), 16, conn, 4, env=env,
+                                           output=ddl_amd.OutputSpec(copy_batches=True),
+                                           order=ddl_amd.OrderSpec(shuffle="device", seed=2))
         st = dl._stager
         for e in range(4):  # every window of the run: nothing is left to stage afterwards
             for i in range(len(dl)):
@@ -437,10 +453,11 @@ def test_stager_bytes_in_interval_is_pro_rata_and_additive(anchor_every):
     with ddl_amd.start(n_producers=2) as (env, conn):
         e0 = ev()
         e0.record()
-        dl = ddl_amd.DistributedDataLoader(ImageWindowProducer(64, (3, 64, 64), "bfloat16", refill="stamp"), 32,
-                                           conn, 6, env=env, device=torch.device("cuda"),
-                                           out_dtype=torch.bfloat16, shuffle="device", prefetch_depth=2,
-                                           copy_timing=True)
+        dl = ddl_amd.DistributedDataLoader(ImageWindowProducer(64, (3, 64, 64), "bfloat16", refill="stamp"), 32, conn,
+                                           6, env=env, device=torch.device("cuda"),
+                                           output=ddl_amd.OutputSpec(dtype=torch.bfloat16),
+                                           staging=ddl_amd.StagingSpec(prefetch_depth=2, copy_timing=True),
+                                           order=ddl_amd.OrderSpec(shuffle="device"))
         st = dl._stager
         assert st.copy_timing
         if anchor_every:
@@ -489,9 +506,11 @@ def test_untimed_direct_copies_make_the_interval_unusable():
     with ddl_amd.start(n_producers=2) as (env, conn):
         e0 = ev()
         e0.record()
-        dl = ddl_amd.DistributedDataLoader(ImageWindowProducer(64, (3, 32, 32), "bfloat16", refill="stamp"), 32,
-                                           conn, 3, env=env, device=torch.device("cuda"),
-                                           out_dtype=torch.bfloat16, shuffle="device", prefetch_depth=2)
+        dl = ddl_amd.DistributedDataLoader(ImageWindowProducer(64, (3, 32, 32), "bfloat16", refill="stamp"), 32, conn,
+                                           3, env=env, device=torch.device("cuda"),
+                                           output=ddl_amd.OutputSpec(dtype=torch.bfloat16),
+                                           staging=ddl_amd.StagingSpec(prefetch_depth=2),
+                                           order=ddl_amd.OrderSpec(shuffle="device"))
         st = dl._stager
         if not st.direct_dma:
             pytest.skip(f"no direct DMA here: {st.stats()['direct_dma_reason']}")
@@ -529,8 +548,9 @@ def test_native_dispatch_refetch_after_last_batch(mode):
 
     with ddl_amd.start(n_producers=2) as (env, conn):
         dl = ddl_amd.DistributedDataLoader(ImageWindowProducer(32, (3, 16, 16), "bfloat16", seed=3), 8, conn, 4,
-                                           env=env, shuffle="device", seed=2, native_dispatch=mode,
-                                           prefetch_depth=2)
+                                           env=env,
+                                           staging=ddl_amd.StagingSpec(native_dispatch=mode, prefetch_depth=2),
+                                           order=ddl_amd.OrderSpec(shuffle="device", seed=2))
         assert len(dl) == 4
         first = [ops.checksum(dl[i][0]).item() for i in range(4)]  # batch 3 is the last: window handed back
         torch.cuda.synchronize()

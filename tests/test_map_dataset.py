@@ -106,7 +106,7 @@ def test_map_dataset_loader_cpu(ds_cls, monkeypatch):
     order = EpochOrder(len(ds), gb, 3)
     with ddl_amd.start(n_producers=2) as (env, conn):
         dl = ddl_amd.DistributedDataLoader(IndexedProducer(MapDatasetSource(ds), gb, host_threads=2), gb, conn, 2,
-                                           mode="indexed", env=env, auto_mark=True, seed=3)
+                                           env=env, auto_mark=True, order=ddl_amd.OrderSpec(mode="indexed", seed=3))
         for e in range(2):
             n = 0
             for g, b in enumerate(dl):
@@ -121,8 +121,8 @@ def _rank(rank, world, n, gb):
     out = []
     ds = TupleDataset(n)
     with ddl_amd.start(n_producers=2) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(IndexedProducer(MapDatasetSource(ds), gb), gb // world, conn, 1,
-                                           mode="indexed", env=env, auto_mark=True, seed=3)
+        dl = ddl_amd.DistributedDataLoader(IndexedProducer(MapDatasetSource(ds), gb), gb // world, conn, 1, env=env,
+                                           auto_mark=True, order=ddl_amd.OrderSpec(mode="indexed", seed=3))
         for b in dl:
             out.append(b[1].tolist())  # labels = 7 * sample id
     return out
@@ -144,8 +144,9 @@ def test_map_dataset_loader_gpu(native):
     ds, gb = TupleDataset(64), 16
     order = EpochOrder(len(ds), gb, 3)
     with ddl_amd.start(n_producers=2) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(IndexedProducer(MapDatasetSource(ds), gb), gb, conn, 2, mode="indexed",
-                                           env=env, auto_mark=True, seed=3, native_dispatch=native)
+        dl = ddl_amd.DistributedDataLoader(IndexedProducer(MapDatasetSource(ds), gb), gb, conn, 2, env=env,
+                                           auto_mark=True, staging=ddl_amd.StagingSpec(native_dispatch=native),
+                                           order=ddl_amd.OrderSpec(mode="indexed", seed=3))
         for e in range(2):
             for g, b in enumerate(dl):
                 assert all(t.is_cuda for t in b)

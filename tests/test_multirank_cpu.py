@@ -16,8 +16,9 @@ def _indexed_rank(rank, world, n, gb, epochs, name, resume=None, stop_after=None
     out = []
     with ddl_amd.start(n_producers=2) as (env, conn):
         assert env.world_size == world and env.rank == rank
-        dl = ddl_amd.DistributedDataLoader(IndexedProducer(src, gb, seed=7), gb // world, conn, epochs,
-                                           mode="indexed", env=env, auto_mark=True, resume_state=resume)
+        dl = ddl_amd.DistributedDataLoader(IndexedProducer(src, gb, seed=7), gb // world, conn, epochs, env=env,
+                                           auto_mark=True, resume_state=resume,
+                                           order=ddl_amd.OrderSpec(mode="indexed"))
         for e in range(dl.epoch, epochs):
             rows = []
             for i, (b,) in enumerate(dl):
@@ -83,7 +84,8 @@ def _exchange_rank(rank, world, method, fraction, epochs=3):
     eps = []
     with ddl_amd.start(n_producers=2) as (env, conn):
         dl = ddl_amd.DistributedDataLoader(IdProducer(40, 6), 8, conn, epochs, fraction, method, env=env,
-                                           copy_batches=True, seed=1)
+                                           output=ddl_amd.OutputSpec(copy_batches=True),
+                                           order=ddl_amd.OrderSpec(seed=1))
         assert dl._exchange_fn is not None
         for e in range(epochs):
             rows = []
@@ -151,8 +153,8 @@ def test_npy_memmap_source_indexed(tmp_path):
     np.save(path, arr)
     src = NpyMemmapSource(str(path))
     with ddl_amd.start(n_producers=2) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(IndexedProducer(src, 50, seed=2), 50, conn, 1, mode="indexed",
-                                           env=env, auto_mark=True)
+        dl = ddl_amd.DistributedDataLoader(IndexedProducer(src, 50, seed=2), 50, conn, 1, env=env, auto_mark=True,
+                                           order=ddl_amd.OrderSpec(mode="indexed"))
         got = torch.cat([b[0].cpu() for b in dl]).numpy()
     ref = EpochOrder(500, 50, 2).perm(0).full()
     assert np.array_equal(got[:, 0], ref) and np.array_equal(got[:, 1], ref * 2)
@@ -166,7 +168,7 @@ def _topology_rank(rank, world, method):
         from tests.helpers import IdProducer
 
         dl = ddl_amd.DistributedDataLoader(IdProducer(40, 4), 8, conn, 2, 0.5, method, env.rank, env.world_size,
-                                           env=env, copy_batches=True)
+                                           env=env, output=ddl_amd.OutputSpec(copy_batches=True))
         rows = []
         for _ in range(2):
             for b in dl:
@@ -278,8 +280,9 @@ def _token_rank(rank, world, name, n, max_len, gb, k, resume=None, stop_after=No
     out = []
     with ddl_amd.start(n_producers=2) as (env, conn):
         dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(src, gb, max_len, "pad", batches_per_window=k),
-                                           gb // world, conn, 1, mode="indexed", env=env, collate="tokens",
-                                           auto_mark=True, seed=5, resume_state=resume)
+                                           gb // world, conn, 1, env=env, auto_mark=True, resume_state=resume,
+                                           output=ddl_amd.OutputSpec(collate="tokens"),
+                                           order=ddl_amd.OrderSpec(mode="indexed", seed=5))
         for i, b in enumerate(dl):
             ids = b["input_ids"]
             # identify each row's sequence by its tokens (synthetic corpus: rows are distinct)

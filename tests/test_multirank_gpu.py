@@ -39,8 +39,10 @@ def _exchange_rank_gpu(rank, world, method, fraction, slow=0.0):
     with ddl_amd.start(n_producers=2) as (env, conn):
         assert env.device.startswith("cuda"), env.device
         dl = ddl_amd.DistributedDataLoader(IdProducer(64, 6), 16, conn, 3, fraction, method, env=env,
-                                           copy_batches=True, seed=1, device=torch.device(env.device),
-                                           prefetch_depth=2)
+                                           device=torch.device(env.device),
+                                           output=ddl_amd.OutputSpec(copy_batches=True),
+                                           staging=ddl_amd.StagingSpec(prefetch_depth=2),
+                                           order=ddl_amd.OrderSpec(seed=1))
         assert dl._exchange_fn is not None
         direct = dl.stats()["direct_dma"]
         for _ in range(3):
@@ -185,3 +187,48 @@ def test_killed_rank_on_the_card_ends_the_job():
     assert codes[0] in (PEER_ABORT_EXIT, 1), (codes, outs[0][1][-2000:])
     assert "died without a clean shutdown" in outs[0][1] or codes[0] == 1, outs[0][1][-2000:]
     assert took < 120, took
+
+
+def _resident_rank_gpu(rank, world, name, n, gb, replicate, scatter):
+    import numpy as np
+
+    import ddl_amd
+    from ddl_amd.models import SharedArraySource
+    from ddl_amd.resident import ResidentGlobalLoader
+
+    src = SharedArraySource(name, n, (3, 8, 8), "uint8") if (rank == 0 or not scatter) else None
+    with ddl_amd.start(n_producers=0) as (env, _):
+        dl = ResidentGlobalLoader(src, gb, env, seed=4, n_epochs=1, replicate=replicate,
+                                  scatter_from=0 if scatter else None, chunk_bytes=192 * 37)
+        assert dl.shard.is_cuda and dl.replicated == replicate
+        ids = [b[:, 0, 0, 0].to(torch.int64).cpu().numpy() for b in dl]
+        st = dl.stats()
+        dl.close()
+        return np.stack(ids), st["bytes_exchanged"], st["bytes_replicated"]
+
+
+@pytest.mark.timeout(200)
+@pytest.mark.parametrize("replicate,scatter", [(True, False), (True, True), (False, False)])
+def test_resident_layouts_on_the_card(replicate, scatter):
+    """The HBM-resident loader's GPU path at W = 2 (gloo on one card): replicated (all-gather bring-up, or
+    scatter + all-gather from one holder) and sharded layouts deliver the same union order -- global batch g of
+    the epoch permutation -- and only the sharded one moves rows per step."""
+    import numpy as np
+
+    from ddl_amd.models import SharedArraySource
+    from ddl_amd.permutation import EpochOrder
+
+    n, gb = 300, 32
+    data = (torch.arange(n) % 251).to(torch.uint8).view(n, 1, 1, 1).expand(n, 3, 8, 8).contiguous()
+    src = SharedArraySource.create(f"ddl_amd_resgpu_{np.random.randint(1 << 30)}", data)
+    try:
+        res = run_ranks(_resident_rank_gpu, 2, src.name, n, gb, replicate, scatter, timeout=180, env=GPU_GLOO)
+    finally:
+        src.close()
+    order = EpochOrder(n, gb, 4)
+    ref = (order.perm(0).full()[: order.batches_per_epoch * gb] % 251).reshape(-1, gb)
+    merged = np.concatenate([r[0] for r in res], axis=1)
+    assert np.array_equal(merged, ref)
+    moved_steps = sum(r[1] for r in res)
+    assert (moved_steps == 0) == replicate
+    assert (sum(r[2] for r in res) > 0) == replicate

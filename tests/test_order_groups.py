@@ -31,7 +31,8 @@ def _all_on_dp_group(rank, world, name):
     src = SharedArraySource(name, 96, (3,), "int64") if rank == 0 else None
     with ddl_amd.start(n_producers=2) as (env, conn):
         dl = ddl_amd.DistributedDataLoader(IdProducer(32, 6), 8, conn, 2, 0.5, "alltoall", env=env,
-                                           copy_batches=True, seed=1)
+                                           output=ddl_amd.OutputSpec(copy_batches=True),
+                                           order=ddl_amd.OrderSpec(seed=1))
         step = TrainStep(torch.device("cpu"), dim=8, depth=1, process_group=env.process_group)
         for _ in range(2):
             for a, b in dl:

@@ -5,6 +5,7 @@ import pytest
 import torch
 
 import ddl_amd
+from ddl_amd.specs import from_flat
 from ddl_amd import ops
 from ddl_amd.models.tokens import SharedTokenSource, TokenBatchProducer, expected_tokens
 from ddl_amd.permutation import EpochOrder
@@ -46,7 +47,9 @@ def test_token_batches_cpu(wire_corpus, mode, k, monkeypatch):
     order = EpochOrder(wire_corpus.n, gb, 4)
     with ddl_amd.start(n_producers=2) as (env, conn):
         prod = TokenBatchProducer(wire_corpus, gb, seq_len, mode, batches_per_window=k)
-        dl = ddl_amd.DistributedDataLoader(prod, gb, conn, 2, mode="indexed", env=env, auto_mark=True, collate="tokens", seed=4)
+        dl = ddl_amd.DistributedDataLoader(prod, gb, conn, 2, env=env, auto_mark=True,
+                                           output=ddl_amd.OutputSpec(collate="tokens"),
+                                           order=ddl_amd.OrderSpec(mode="indexed", seed=4))
         assert dl.batches_per_window == [1 if k == 1 else 4] * 2
         assert len(dl) == order.batches_per_epoch
         for e in range(2):
@@ -73,7 +76,9 @@ def test_token_batches_gpu(wire_corpus, mode, k):
     order = EpochOrder(wire_corpus.n, gb, 4)
     with ddl_amd.start(n_producers=2) as (env, conn):
         prod = TokenBatchProducer(wire_corpus, gb, seq_len, mode, batches_per_window=k)
-        dl = ddl_amd.DistributedDataLoader(prod, gb, conn, 1, mode="indexed", env=env, auto_mark=True, collate="tokens", seed=4)
+        dl = ddl_amd.DistributedDataLoader(prod, gb, conn, 1, env=env, auto_mark=True,
+                                           output=ddl_amd.OutputSpec(collate="tokens"),
+                                           order=ddl_amd.OrderSpec(mode="indexed", seed=4))
         held = None
         for g, batch in enumerate(dl):
             assert batch["input_ids"].is_cuda
@@ -265,8 +270,9 @@ def test_token_batches_ffd_pack_order(corpus, monkeypatch):
     for po in ("in_order", "ffd"):
         with ddl_amd.start(n_producers=2) as (env, conn):
             dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(corpus, gb, seq_len, "pack", pack_order=po), gb,
-                                               conn, 1, mode="indexed", env=env, auto_mark=True, collate="tokens",
-                                               seed=4)
+                                               conn, 1, env=env, auto_mark=True,
+                                               output=ddl_amd.OutputSpec(collate="tokens"),
+                                               order=ddl_amd.OrderSpec(mode="indexed", seed=4))
             rows[po] = 0
             for g, batch in enumerate(dl):
                 seqs = expected_tokens(corpus, order.indices(0, g))
@@ -333,8 +339,9 @@ def test_cu_seqlens_drive_varlen_attention(corpus, monkeypatch):
     order = EpochOrder(corpus.n, gb, 4)
     emb = torch.randn(50257, 16, generator=torch.Generator().manual_seed(0))
     with ddl_amd.start(n_producers=1) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(corpus, gb, seq_len, "pack"), gb, conn, 1,
-                                           mode="indexed", env=env, auto_mark=True, collate="tokens", seed=4)
+        dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(corpus, gb, seq_len, "pack"), gb, conn, 1, env=env,
+                                           auto_mark=True, output=ddl_amd.OutputSpec(collate="tokens"),
+                                           order=ddl_amd.OrderSpec(mode="indexed", seed=4))
         for g, batch in enumerate(dl):
             if g == 3:
                 break
@@ -362,9 +369,10 @@ def test_token_native_dispatch_matches_python_path(corpus, mode, bpw):
         out = []
         with ddl_amd.start(n_producers=2) as (env, conn):
             dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(corpus, gb, seq_len, mode, batches_per_window=bpw),
-                                               gb, conn, 2,
-                                               mode="indexed", env=env, auto_mark=True, collate="tokens", seed=4,
-                                               native_dispatch=native)
+                                               gb, conn, 2, env=env, auto_mark=True,
+                                               output=ddl_amd.OutputSpec(collate="tokens"),
+                                               staging=ddl_amd.StagingSpec(native_dispatch=native),
+                                               order=ddl_amd.OrderSpec(mode="indexed", seed=4))
             for _ in range(2):
                 for b in dl:
                     out.append({k: (v.cpu().clone() if isinstance(v, torch.Tensor) else v) for k, v in b.items()})
@@ -398,8 +406,9 @@ def test_multi_batch_window_resume_mid_window(corpus, live, monkeypatch):
 
     def make(conn, env, sd=None):
         return ddl_amd.DistributedDataLoader(TokenBatchProducer(corpus, gb, seq_len, "pad", batches_per_window=k), gb,
-                                             conn, 2, mode="indexed", env=env, auto_mark=True, collate="tokens",
-                                             seed=4, resume_state=sd)
+                                             conn, 2, env=env, auto_mark=True, resume_state=sd,
+                                             output=ddl_amd.OutputSpec(collate="tokens"),
+                                             order=ddl_amd.OrderSpec(mode="indexed", seed=4))
 
     with ddl_amd.start(n_producers=2) as (env, conn):
         dl = make(conn, env)
@@ -441,8 +450,8 @@ def _token_run(corpus, gb, seq_len, k, epochs=1, **kw):
     out = []
     with ddl_amd.start(n_producers=2) as (env, conn):
         dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(corpus, gb, seq_len, "pack", batches_per_window=k), gb,
-                                           conn, epochs, mode="indexed", env=env, auto_mark=True, collate="tokens",
-                                           seed=4, **kw)
+                                           conn, epochs, env=env, auto_mark=True,
+                                           **from_flat(dict(kw, collate="tokens"), mode="indexed", seed=4))
         for _ in range(epochs):
             for b in dl:
                 out.append({x: (v.cpu().clone() if isinstance(v, torch.Tensor) else v) for x, v in b.items()})

@@ -34,9 +34,9 @@ class SkewedProducer(IndexedProducer):
 def _run(src, gb, epochs, producer_cls=IndexedProducer, resume=None, stop_after=None, verify=True):
     out = []
     with ddl_amd.start(n_producers=2, device="cpu") as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(producer_cls(src, gb, seed=3), gb // env.world_size, conn, epochs,
-                                           mode="indexed", env=env, auto_mark=True, resume_state=resume,
-                                           verify_order=verify)
+        dl = ddl_amd.DistributedDataLoader(producer_cls(src, gb, seed=3), gb // env.world_size, conn, epochs, env=env,
+                                           auto_mark=True, resume_state=resume,
+                                           order=ddl_amd.OrderSpec(mode="indexed", verify=verify))
         for e in range(dl.epoch, epochs):
             for i, (b,) in enumerate(dl):
                 out.append(b[:, 0].clone())
@@ -83,7 +83,7 @@ def test_window_mode_rejects_verify_order(monkeypatch):
     monkeypatch.setenv("DDL_DEVICE", "cpu")
     with ddl_amd.start(n_producers=1, device="cpu") as (env, conn):
         with pytest.raises(ValueError, match="verify_order"):
-            ddl_amd.DistributedDataLoader(IdProducer(16, 4), 8, conn, 1, env=env, verify_order=True)
+            ddl_amd.DistributedDataLoader(IdProducer(16, 4), 8, conn, 1, env=env, order=ddl_amd.OrderSpec(verify=True))
 
 
 def _rank(rank, world, name, n):
@@ -104,8 +104,9 @@ def test_verify_order_on_device(source, native):
     """Staged windows (HBM ring): the native engine's slot tags and the Python stager's are checked."""
     bpe = EpochOrder(source.n, 64, 3).batches_per_epoch
     with ddl_amd.start(n_producers=2) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(IndexedProducer(source, 64, seed=3), 64, conn, 2, mode="indexed",
-                                           env=env, auto_mark=True, verify_order=True, native_dispatch=native)
+        dl = ddl_amd.DistributedDataLoader(IndexedProducer(source, 64, seed=3), 64, conn, 2, env=env, auto_mark=True,
+                                           staging=ddl_amd.StagingSpec(native_dispatch=native),
+                                           order=ddl_amd.OrderSpec(mode="indexed", verify=True))
         n = 0
         for _ in range(2):
             for (b,) in dl:
@@ -114,8 +115,9 @@ def test_verify_order_on_device(source, native):
         assert dl.verified_windows == n == 2 * bpe
         dl.close()
     with ddl_amd.start(n_producers=2) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(SkewedProducer(source, 64, seed=3), 64, conn, 1, mode="indexed",
-                                           env=env, auto_mark=True, verify_order=True, native_dispatch=native)
+        dl = ddl_amd.DistributedDataLoader(SkewedProducer(source, 64, seed=3), 64, conn, 1, env=env, auto_mark=True,
+                                           staging=ddl_amd.StagingSpec(native_dispatch=native),
+                                           order=ddl_amd.OrderSpec(mode="indexed", verify=True))
         with pytest.raises(DataIntegrityError):
             for _ in dl:
                 pass

@@ -12,8 +12,9 @@ from ddl_amd.permutation import EpochOrder
 
 def run(src, gb, native):
     with ddl_amd.start(n_producers=2) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(IndexedProducer(src, gb), gb, conn, 1, mode="indexed", env=env,
-                                           auto_mark=True, seed=5, native_dispatch=native)
+        dl = ddl_amd.DistributedDataLoader(IndexedProducer(src, gb), gb, conn, 1, env=env, auto_mark=True,
+                                           staging=ddl_amd.StagingSpec(native_dispatch=native),
+                                           order=ddl_amd.OrderSpec(mode="indexed", seed=5))
         out = [b[0].cpu().numpy().copy() for b in dl]
     return out
 

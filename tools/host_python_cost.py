@@ -62,8 +62,8 @@ def main() -> int:
 
     n = 200_000
     with ddl_amd.start(n_producers=3) as (env, conn):
-        dl = ddl_amd.DistributedDataLoader(PointwiseProducer(n_timesteps=10, host_shuffle=False), 4096, conn,
-                                           10 ** 6, env=env, seed=1)
+        dl = ddl_amd.DistributedDataLoader(PointwiseProducer(n_timesteps=10, host_shuffle=False), 4096, conn, 10 ** 6,
+                                           env=env, order=ddl_amd.OrderSpec(seed=1))
         # the CUDA-only pieces of the fast path, stubbed (after the loader is built: producers are threads)
         torch._C._cuda_getCurrentStream = lambda i: 1
         streams.current = lambda i: _Stream()

@@ -26,6 +26,7 @@ def run(shape: str, native, steps: int) -> dict:
     import torch
 
     import ddl_amd
+    from ddl_amd.specs import from_flat
     from ddl_amd import Marker
     from ddl_amd.models import PointwiseProducer
     from ddl_amd.models.producers import ImageWindowProducer
@@ -39,8 +40,8 @@ def run(shape: str, native, steps: int) -> dict:
         else:
             prod, bs, kw = ImageWindowProducer(256, (3, 224, 224), "bfloat16", refill="stamp"), 256, \
                 dict(out_dtype=torch.bfloat16)
-        dl = ddl_amd.DistributedDataLoader(prod, bs, conn, 10 ** 6, env=env, device=dev, shuffle="device", seed=1,
-                                           native_dispatch=native, **kw)
+        dl = ddl_amd.DistributedDataLoader(prod, bs, conn, 10 ** 6, env=env, device=dev,
+                                           **from_flat(dict(kw, native_dispatch=native, shuffle="device", seed=1)))
 
         def batches():
             while True:
@@ -75,10 +76,10 @@ def run_tokens(native, steps: int, producers: int = 4, k: int = 8) -> dict:
     src = SharedTokenSource.synthetic(f"ddl_amd_lhc_{os.getpid()}", 8192, 256, 4096, seed=1)
     try:
         with ddl_amd.start(n_producers=producers) as (env, conn):
-            dl = ddl_amd.DistributedDataLoader(TokenBatchProducer(src, 64, 4096, "pack", pack_order="ffd",
-                                                                  batches_per_window=k), 64, conn,
-                                               10 ** 4, mode="indexed", env=env, collate="tokens", auto_mark=True,
-                                               native_dispatch=native)
+            dl = ddl_amd.DistributedDataLoader(
+                TokenBatchProducer(src, 64, 4096, "pack", pack_order="ffd", batches_per_window=k), 64, conn, 10 ** 4,
+                env=env, auto_mark=True, output=ddl_amd.OutputSpec(collate="tokens"),
+                staging=ddl_amd.StagingSpec(native_dispatch=native), order=ddl_amd.OrderSpec(mode="indexed"))
 
             def gen():
                 while True:
