@@ -120,7 +120,7 @@ def dist_block(env: DDLEnv, probe_bytes: int = 32 << 20) -> dict:
         "distinct_gpus": distinct,
         "hosts": len({r["host"] for r in ranks}),
         "alltoall_out_gbps_min": min(a2a) if a2a else None,
-        "verified": env.world_size > 1 and not problems,
+        "verified": (not problems) if env.world_size > 1 else None,  # None: a single rank has nothing to verify
         "rehearsal": rehearsal(),
         "problems": problems,
         "ranks": ranks,

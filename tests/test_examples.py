@@ -123,7 +123,7 @@ def test_dist_block_single_rank_and_checks():
     from ddl_amd.types import DDLEnv
 
     b = dist_block(DDLEnv(rank=0, world_size=1, hostname="h", device="cpu"))
-    assert b["world_size"] == 1 and b["backend"] is None and b["verified"] is False
+    assert b["world_size"] == 1 and b["backend"] is None and b["verified"] is None
     assert require_verified(b) is None and b["rccl_version"]
     fake = dict(b, world_size=8, verified=False, rehearsal=False, problems=["8 ranks on 1 distinct GPU(s)"])
     assert "distinct GPU" in require_verified(fake)

@@ -57,10 +57,12 @@ def test_zerocopy_gpu_matches_reference(max_blocks, prep_streams, dtype):
 def test_zerocopy_handoff_modes_deliver_the_same_bytes_behind_a_busy_stream(handoff):
     """Host hand-off (the default: the host waits for the gather's event, the consumer's stream gets no barrier)
     and device hand-off deliver the same batches, bitwise -- also when the consumer's stream is busy with a long
-    kernel while the gathers run ahead, and the consumer reads each batch right after it is handed over."""
-    n, shape = 1024, (3, 64, 64)
+    kernel while the gathers run ahead, and the consumer reads each batch right after it is handed over. The rows
+    are large enough for the deep-tile PCIe gather, on a grid of 8 workgroups."""
+    # 76,800 B rows: the deep-tile host gather (64 KB per workgroup tile) with a partial second tile per row
+    n, shape = 512, (3, 128, 100)
     src = (torch.rand((n, *shape)) * 100).to(torch.bfloat16)
-    dl = ZeroCopyLoader(src, 64, seed=2, n_epochs=1, depth=3, handoff=handoff)
+    dl = ZeroCopyLoader(src, 64, seed=2, n_epochs=1, depth=3, handoff=handoff, max_blocks=8)
     order = EpochOrder(n, 64, 2)
     idx = torch.from_numpy(order.perm(0).full()[: order.batches_per_epoch * 64]).view(-1, 64)
     outs = []
