@@ -31,13 +31,7 @@ constexpr int kUnroll = 4;
 // TB/s) but 5.49M vs 5.74M samples/s in the HBM-resident loader, which reads the batch right after it is
 // written (profiles/r4_second/resident_*.json): plain stores only.
 
-// Zero-copy gathers out of pinned host memory are PCIe-latency-bound: a workgroup waits one PCIe round trip
-// per tile. Their tiles are 4x deeper (16 accesses in flight per lane, 64 KB per workgroup), so a grid of a
-// few workgroups keeps the link busy while holding a few CUs -- the rest stay with the training step, whose
-// GEMMs otherwise lose CUs to the gather for each batch's whole transfer.
-constexpr int kUnrollHost = 16;
-
-template <typename U, bool kNtLoads, int kU = kUnroll>
+template <typename U, bool kNtLoads>
 __global__ void __launch_bounds__(kThreads) move_rows_chunked(uint8_t* __restrict__ dst,
                                                               const uint8_t* __restrict__ src,
                                                               int64_t units_per_row, int64_t chunks_per_row,
@@ -53,10 +47,10 @@ __global__ void __launch_bounds__(kThreads) move_rows_chunked(uint8_t* __restric
   const int64_t drow = scatter ? mapped : row;
   const U* s = reinterpret_cast<const U*>(src) + srow * units_per_row;
   U* d = reinterpret_cast<U*>(dst) + drow * units_per_row;
-  const int64_t u0 = chunk * (kThreads * kU) + threadIdx.x;
-  U v[kU];
+  const int64_t u0 = chunk * (kThreads * kUnroll) + threadIdx.x;
+  U v[kUnroll];
 #pragma unroll
-  for (int k = 0; k < kU; ++k) {
+  for (int k = 0; k < kUnroll; ++k) {
     const int64_t u = u0 + k * kThreads;
     // kNtLoads (gathers): the source rows stream through once (a shard far larger than the 256 MB MALL):
     // non-temporal loads keep them from evicting the batch just written, which the consumer reads next (the
@@ -71,7 +65,7 @@ __global__ void __launch_bounds__(kThreads) move_rows_chunked(uint8_t* __restric
     }
   }
 #pragma unroll
-  for (int k = 0; k < kU; ++k) {
+  for (int k = 0; k < kUnroll; ++k) {
     const int64_t u = u0 + k * kThreads;
     if (u < units_per_row) {
       d[u] = v[k];
@@ -327,14 +321,9 @@ int flat_grid_capped(int64_t work, int64_t max_blocks) {
 
 template <typename U>
 void launch_move(void* dst, const void* src, int64_t n_rows, int64_t row_bytes, const RowIndex& ri, int scatter,
-                 bool nt_loads, bool host_src, int64_t max_blocks, hipStream_t st) {
+                 bool nt_loads, int64_t max_blocks, hipStream_t st) {
   const int64_t units = row_bytes / static_cast<int64_t>(sizeof(U));
-  if (host_src && units >= kThreads * kUnrollHost) {  // a capped-grid PCIe gather: deep tiles
-    const int64_t chunks = (units + kThreads * kUnrollHost - 1) / (kThreads * kUnrollHost);
-    hipLaunchKernelGGL((move_rows_chunked<U, false, kUnrollHost>), tile_grid(n_rows * chunks, max_blocks),
-                       dim3(kThreads), 0, st, static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), units,
-                       chunks, n_rows * chunks, ri, scatter);
-  } else if (units >= kThreads) {
+  if (units >= kThreads) {
     const int64_t chunks = (units + kThreads * kUnroll - 1) / (kThreads * kUnroll);
     auto kernel = nt_loads ? move_rows_chunked<U, true> : move_rows_chunked<U, false>;
     hipLaunchKernelGGL(kernel, tile_grid(n_rows * chunks, max_blocks), dim3(kThreads), 0, st,
@@ -396,7 +385,6 @@ int gather_rows(void* dst, int32_t out_dt, const void* src, int32_t in_dt, int64
                 const RowIndex& ri, const Affine& aff, int flags, int64_t max_blocks, hipStream_t st) {
   if (n_rows <= 0 || row_elems <= 0) return 0;
   const int scatter = flags & 1;
-  const bool host = (flags & kHostSource) != 0 && !scatter;
   const bool nt = (flags & (1 | kHostSource)) == 0;  // a device-source gather: non-temporal source loads
   // the chunked kernels index tiles and in-row elements with 32-bit arithmetic
   if (n_rows >= (int64_t{1} << 31) || n_rows * row_elems >= (int64_t{1} << 40)) return -4;
@@ -405,11 +393,11 @@ int gather_rows(void* dst, int32_t out_dt, const void* src, int32_t in_dt, int64
     const int64_t row_bytes = row_elems * dtype_size(in_dt);
     const uintptr_t align = reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src);
     if (row_bytes % 16 == 0 && align % 16 == 0)
-      launch_move<u32x4>(dst, src, n_rows, row_bytes, ri, scatter, nt, host, max_blocks, st);
+      launch_move<u32x4>(dst, src, n_rows, row_bytes, ri, scatter, nt, max_blocks, st);
     else if (row_bytes % 4 == 0 && align % 4 == 0)
-      launch_move<uint32_t>(dst, src, n_rows, row_bytes, ri, scatter, nt, host, max_blocks, st);
+      launch_move<uint32_t>(dst, src, n_rows, row_bytes, ri, scatter, nt, max_blocks, st);
     else
-      launch_move<uint8_t>(dst, src, n_rows, row_bytes, ri, scatter, nt, host, max_blocks, st);
+      launch_move<uint8_t>(dst, src, n_rows, row_bytes, ri, scatter, nt, max_blocks, st);
     return static_cast<int>(hipGetLastError());
   }
   if (scatter) return -2;  // converting scatters are not needed by the loader
