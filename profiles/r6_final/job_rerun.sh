@@ -1,0 +1,8 @@
+#!/bin/bash
+# Round 6, the final tree after the zero-copy revert: whole GPU suite, smoke, the driver's command x2.
+source tools/gpu_job.sh
+unset DDL_BACKEND
+run 1000 gpu_tests python -u -m pytest tests -m gpu -q -x --timeout 240 --timeout-method thread
+run 300 smoke python -c "import __graft_entry__ as g; g.smoke()"
+run 200 bench_a python bench.py --steps 20 --warmup 5 --json-out gpurun_out/bench_a.json
+run 200 bench_b python bench.py --steps 20 --warmup 5 --json-out gpurun_out/bench_b.json
