@@ -321,7 +321,7 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
         self.replicated = self._decide_replicate(replicate, chunk_bytes, hbm_fraction)
         self.replicate_s = 0.0
         t0 = time.perf_counter()
-        if self.replicated:
+        if self.replicated and self.W > 1:
             self.shard = self._load_replica(reader, chunk_bytes, host_threads, scatter_from)
         elif scatter_from is not None and self.W > 1:
             self.shard = self._scatter_shards(reader, chunk_bytes, host_threads, scatter_from)
@@ -338,11 +338,13 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
     def _decide_replicate(self, replicate: bool | str, chunk_bytes: int, hbm_fraction: float) -> bool:
         """``replicate``: True / False, or "auto" = a whole replica (plus the bring-up's gather staging) fits in
         ``hbm_fraction`` of the free HBM of EVERY rank (MIN over the control group, so all ranks agree). At
-        W = 1 the two modes are the same layout; "auto" on the CPU keeps the sharded layout."""
+        W = 1 the two layouts are the same (the rank's shard is the whole dataset): reported as replicated
+        unless ``replicate=False``, loaded and stepped as one shard. "auto" on the CPU keeps the sharded layout
+        at W > 1."""
         if replicate not in (True, False, "auto"):
             raise ValueError("replicate must be True, False or 'auto'")
         if self.W == 1:
-            return False
+            return replicate is not False
         if replicate != "auto":
             return bool(replicate)
         if self.device.type != "cuda":
