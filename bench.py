@@ -122,9 +122,6 @@ def parse(argv=None):
     ap.add_argument("--a2a-probe-mb", type=float, default=32.0,
                     help="size of the device-timed all-to-all on the DP group that opens the run (the 'dist' block's "
                          "per-rank xGMI rate); 0 skips it")
-    ap.add_argument("--exchange-handoff", default=None, choices=["device", "host"],
-                    help="A/B: how the native engine hands a lookahead batch to the compute stream when the exchange "
-                         "is on (default: the library's choice)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--debug-log", action="store_true",
                     help="slow host iterations of the timed loop and long per-window stager waits in the JSON line")
@@ -570,8 +567,6 @@ def main(argv=None) -> int:
                 native_dispatch=False if args.dispatch == "python" else args.dispatch,
                 copy_timing=True))  # device times of every window copy: the pro-rata H2D accounting below
         acc = ops.ChecksumAccumulator(dev)  # one streaming launch per batch
-        if args.exchange_handoff is not None and getattr(dl, "_engine", None) is not None:
-            dl._engine.host_handoff = args.exchange_handoff == "host"
 
         def batches():
             while True:

@@ -204,9 +204,12 @@ class NativeDispatchMixin:
         # consumer's release (archive/profiles/r3_early_release); a later out-of-order fetch of that window raises
         self._engine.early_release = True
         # lookahead batches still pending at get(): the host waits for them (no device-side cross-queue
-        # barrier on the compute stream, archive/profiles/r3_handoff) unless the exchange is on -- its kernels wait
-        # on peer ranks, and the host must never block on another rank's progress
-        self._engine.host_handoff = self._exchange_fn is None
+        # barrier on the compute stream, archive/profiles/r3_handoff) -- also with the exchange on (round 6: GPU
+        # idle at r = 0.9 through a 1-rank RCCL group 1.12-1.21% -> 0.84-0.85%, profiles/r6_tenth). The batch
+        # kernel then waits on the exchange, a collective every rank issued at an EARLIER point of the schedule
+        # (entering the previous window, parallel/order.py), so this host wait never closes a cycle across ranks;
+        # a dead or hung peer ends it through the job abort / the process group's timeout
+        self._engine.host_handoff = True
         # the host (not the batch stream) waits for a window's H2D copy before launching its batch kernels
         # (bounded by the loader timeout), so no queue holds a barrier packet on an unfinished copy: GPU idle
         # below the crossover 2.4-2.5% -> 1.1% at r = 0.9 (archive/profiles/r4_sixteenth, r4_seventeenth). Not
