@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round 6: validation of the host hand-off with the exchange on: whole GPU suite, smoke, the driver's command,
+# the exchange through a 1-rank RCCL group (x2), and the N = 4 on-card rehearsal with the exchange.
+source tools/gpu_job.sh
+unset DDL_BACKEND
+run 1000 gpu_tests python -u -m pytest tests -m gpu -q -x --timeout 240 --timeout-method thread
+run 300 smoke python -c "import __graft_entry__ as g; g.smoke()"
+run 200 bench_a python bench.py --steps 20 --warmup 5 --json-out gpurun_out/bench_a.json
+run 200 rccl1_a env DDL_BACKEND=nccl python bench.py --steps 100 --warmup 10 --exchange 0.5 --order window --json-out gpurun_out/rccl1_a.json
+run 200 rccl1_b env DDL_BACKEND=nccl python bench.py --steps 20 --warmup 5 --exchange 0.5 --json-out gpurun_out/rccl1_b.json
+run 300 n4 env DDL_REHEARSAL=1 DDL_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --master-addr 127.0.0.1 --nproc-per-node 4 --master-port 29681 bench.py --gpus 4 --steps 40 --warmup 5 --json-out gpurun_out/n4.json
