@@ -32,6 +32,12 @@ def main(argv=None):
                          "all-gathered over xGMI once; no per-step collective); sharded: rank r holds rows "
                          "[r*S, (r+1)*S) and every step all-to-alls (W-1)/W of its batch; auto: replicated when "
                          "it fits in 80%% of free HBM")
+    ap.add_argument("--idle-step-ms", type=float, default=0.0,
+                    help="after the sweep: GPU idle %% behind a fixed-cost step of this many ms (a batch read + bf16 "
+                         "GEMMs) fed by the loader at --depths' first depth, for each --handoff; 0 skips it")
+    ap.add_argument("--handoffs", default="device",
+                    help="comma list of hand-offs for the idle phase (device: the step's stream waits for the "
+                         "batch's event; host: the host does)")
     ap.add_argument("--augment", action="store_true",
                     help="RandomResizedCrop(224) + flip + normalise on the device instead of the plain gather")
     a = ap.parse_args(argv)
@@ -116,8 +122,45 @@ def main(argv=None):
                 del dl, it, acc
                 if dev.type == "cuda":
                     torch.cuda.empty_cache()  # hand the freed shard back before the next depth allocates its own
+            idle = []
+            if a.idle_step_ms > 0 and dev.type == "cuda":
+                from ddl_amd.models.trainstep import CalibratedStep
+                from ddl_amd.utils.tracing import ComputeIdleMeter
+
+                step = CalibratedStep(dev, step_ms=a.idle_step_ms)
+                for handoff in a.handoffs.split(","):
+                    dl = ResidentGlobalLoader(src, a.batch * env.world_size, env, seed=1,
+                                              depth=int(a.depths.split(",")[0]), out_dtype=torch.bfloat16,
+                                              normalize=norm, replicate={"auto": "auto", "true": True,
+                                                                         "false": False}[a.replicate],
+                                              handoff=handoff)
+
+                    def gen2():
+                        while True:
+                            yield from dl
+
+                    it2 = gen2()
+                    step.calibrate(next(it2))  # size the GEMM chain to step_ms on this GPU (once per loader)
+                    for _ in range(a.warmup):
+                        step(next(it2))
+                    sync()
+                    meter = ComputeIdleMeter()
+                    for _ in range(a.steps):
+                        x = next(it2)
+                        meter.step_begin()
+                        step(x)
+                        meter.step_end()
+                    sync()
+                    res = meter.result()
+                    idle.append({"handoff": handoff, "step_ms": a.idle_step_ms,
+                                 "busy_ms_per_step": round(res["busy_ms"] / max(1, res["steps"]), 4),
+                                 "gpu_idle_pct": res["gpu_idle_pct"],
+                                 "gaps_us": res.get("gaps_us"), "host_waits": dl.host_waits})
+                    dl.close()
+                    del dl, it2
             if env.rank == 0:
                 print(json.dumps({"metric": "samples/s fed to GPU, HBM-resident exact global shuffle",
+                                  "idle_behind_step": idle,
                                   "dist": dist_info,
                                   "augment": "RandomResizedCrop(224)+flip+normalise" if a.augment else None,
                                   "n_gpus": env.world_size, "batch_per_gpu": a.batch, "dtype_src": a.dtype,

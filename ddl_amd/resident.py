@@ -114,7 +114,9 @@ class PrefetchedIndexedLoader:
     queue a ~30 us stall at every step boundary on MI355X when another queue is streaming (the zero-copy
     gather: step-boundary gaps 40 vs 10 us, GPU idle at r = 0.9 2.4% vs 0.7% on the producer path,
     ``profiles/r6_third``), so PCIe-paced loaders hand off on the host; loaders whose batches take
-    microseconds keep the device hand-off, which never makes the host wait.
+    microseconds keep the device hand-off by default, which never makes the host wait (behind a 1.25 ms step
+    the HBM-resident loader idles 0.88-0.93% that way, 0.81% with ``handoff="host"``, ``profiles/r6_twelfth``;
+    a host hand-off paces a host with no step of its own at the gather rate).
     """
 
     handoff = "device"
@@ -267,8 +269,12 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
                  device: str | torch.device | None = None, n_epochs: int | None = None,
                  resume_state: dict | None = None, chunk_bytes: int = 256 << 20, host_threads: int = 8,
                  scatter_from: int | None = None, augment: dict | None = None, replicate: bool | str = "auto",
-                 hbm_fraction: float = 0.8):
+                 hbm_fraction: float = 0.8, handoff: str = "device"):
         import torch.distributed as dist
+
+        if handoff not in ("host", "device"):
+            raise ValueError("handoff must be 'host' or 'device'")
+        self.handoff = handoff
 
         aug_keys = {"size", "scale", "ratio", "flip_p", "layout"}
         if augment is not None and not set(augment) <= aug_keys:
