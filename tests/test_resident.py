@@ -152,6 +152,11 @@ def test_resident_close_releases_shard(src):
 def test_resident_augment_needs_gpu_and_known_keys(src):
     from ddl_amd.resident import ResidentGlobalLoader
 
+    with pytest.raises(ValueError, match="handoff"):
+        ResidentGlobalLoader(src, 48, handoff="sideways", device="cpu")
+    with pytest.raises(ValueError, match="replicate"):
+        ResidentGlobalLoader(src, 48, replicate="sometimes", device="cpu")
+
     with pytest.raises(ValueError):
         ResidentGlobalLoader(src, 48, augment={"size": (4, 4)}, device="cpu")  # CPU, and rows are not images
     with pytest.raises(ValueError):
