@@ -481,6 +481,8 @@ PYBIND11_MODULE(_ddl_hip, m) {
       .def("set_batches_per_window", &ddl::BatchEngine::set_batches_per_window, py::arg("bpw"))
       .def_property("host_handoff", &ddl::BatchEngine::host_handoff, &ddl::BatchEngine::set_host_handoff)
       .def_property("ready_on_host", &ddl::BatchEngine::ready_on_host, &ddl::BatchEngine::set_ready_on_host)
+      .def_property("ready_event_on_host", &ddl::BatchEngine::ready_event_on_host,
+                    &ddl::BatchEngine::set_ready_event_on_host)
       .def_property_readonly("ready_host_waits", &ddl::BatchEngine::ready_host_waits)
       .def_property_readonly("wait_s", &ddl::BatchEngine::wait_s)
       .def_property_readonly("batches", &ddl::BatchEngine::batches)

@@ -265,12 +265,22 @@ TokenSpec BatchEngine::token_spec(const StagedInfo& info, int64_t sub, const std
   return sp;
 }
 
+int BatchEngine::wait_ready_event(int b) {
+  const hipError_t q = hipEventQuery(ready_[b]);
+  if (q == hipSuccess) return 0;
+  if (q != hipErrorNotReady) return -1;
+  ++ready_host_waits_;
+  return hipEventSynchronize(ready_[b]) == hipSuccess ? 0 : -1;
+}
+
 int BatchEngine::launch(int64_t w, int64_t local, int64_t n_batches, const StagedInfo& info, int64_t slot,
                         hipStream_t st) {
   const auto& dst = slots_[slot];
   const void* src = buffers_[info.buffer];
   uint64_t t0 = clock_ns();
-  if (ready_host_) {  // the host waits for the copy (a no-op once it has landed), bounded by the loader timeout
+  if (ready_event_host_) {  // post-copy stage (exchange): the host waits for its ready event, no barrier packet
+    if (wait_ready_event(info.buffer) != 0) return -1;
+  } else if (ready_host_) {  // the host waits for the copy (a no-op once it has landed), bounded by the loader timeout
     const int q = NativeStager::copy_landed(info);
     if (q == 0) {
       if (stager_->wait_copy(info) != 0) return kCopyWaitFailed;
@@ -474,7 +484,10 @@ int BatchEngine::release(int64_t w) {
           return -1;
       }
     }
-    if (ready_host_) {
+    if (ready_event_host_) {
+      // no batch read the window: its post-copy stage must finish before the buffer is reused
+      if (wait_ready_event(b) != 0) return -1;
+    } else if (ready_host_) {
       // no batch read the window: its copy must still land before the buffer is reused
       const int q = NativeStager::copy_landed(it->second);
       if (q == 0 && stager_->wait_copy(it->second) != 0) return kCopyWaitFailed;

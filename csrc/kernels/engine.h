@@ -147,6 +147,12 @@ class BatchEngine {
   // queue never holds a barrier packet on an unfinished copy.
   void set_ready_on_host(bool on) { ready_host_ = on; }
   bool ready_on_host() const { return ready_host_; }
+  // With a post-copy stage (the exchange) a window is ready when the stage's ready event has completed, not
+  // when its copy has landed: true makes the HOST wait for that event before the window's first launch (and
+  // before a never-read window's buffer goes back), so the batch stream's queue holds no barrier packet on a
+  // collective; false (default) makes the batch stream wait for it on the device.
+  void set_ready_event_on_host(bool on) { ready_event_host_ = on; }
+  bool ready_event_on_host() const { return ready_event_host_; }
   uint64_t ready_host_waits() const { return ready_host_waits_; }  // launches whose copy the host waited for
 
   double wait_s() const { return wait_ns_ * 1e-9; }
@@ -224,6 +230,8 @@ class BatchEngine {
   bool early_ = true;
   bool host_wait_ = false;  // host hand-off of lookahead batches (set_host_handoff)
   bool ready_host_ = false;  // host-side wait for a window's copy (set_ready_on_host)
+  bool ready_event_host_ = false;  // host-side wait for a window's post-copy ready event (set_ready_event_on_host)
+  int wait_ready_event(int b);     // 0, or -1 on a HIP error; counts a wait that blocked in ready_host_waits_
   uint64_t ready_host_waits_ = 0;
   std::vector<int64_t> bpw_;
   std::set<int64_t> handed_back_;  // windows whose buffer went back to the stager before release()

@@ -213,8 +213,12 @@ class NativeDispatchMixin:
         # the host (not the batch stream) waits for a window's H2D copy before launching its batch kernels
         # (bounded by the loader timeout), so no queue holds a barrier packet on an unfinished copy: GPU idle
         # below the crossover 2.4-2.5% -> 1.1% at r = 0.9 (archive/profiles/r4_sixteenth, r4_seventeenth). Not
-        # with the exchange: the batch stream waits on the post-copy stage's ready event instead
+        # with the exchange, whose readiness is the post-copy stage's ready event (below)
         self._engine.ready_on_host = self._exchange_fn is None
+        # with the exchange the window is ready when its post-copy stage's ready event completes: the host waits
+        # for that event before the window's first launch, so the batch stream's queue holds no barrier packet on
+        # a collective (GPU idle at r = 0.9 through a 1-rank RCCL group 0.84% -> 0.74-0.78%, profiles/r6_thirteenth)
+        self._engine.ready_event_on_host = self._exchange_fn is not None
         # then the copy's retire event is the only marker behind it in the copy stream's queue
         self._stager._native.record_ready = not self._engine.ready_on_host
         self._eng_mode = mode
