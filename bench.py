@@ -199,6 +199,9 @@ def phase2(args, env, dev, it, idle_steps: int, barrier, sync) -> dict:
     return idle
 
 
+_FEED_DRAIN = 64  # batches: > HBM ring (depth 4 + 1) + producer slots + the indexed paths' prefetch
+
+
 def pressure_phase(args, env, dev, it, feed_per_rank: float, barrier, sync, dl=None) -> dict:
     """GPU idle % with the LOADER as the near-bottleneck: a calibrated step (reads the whole batch, then a
     bf16 GEMM chain, ``CalibratedStep``) sized so its capacity is ``--pressure-ratio`` x this rank's phase-1
@@ -217,8 +220,14 @@ def pressure_phase(args, env, dev, it, feed_per_rank: float, barrier, sync, dl=N
     r, B = args.pressure_ratio, args.batch
     # the feed this phase runs against: re-measured here over >= 100 batches with the checksum consumer
     # (phase 1's region can be as short as 20 steps, and the loader's state after phase 2 -- copy streams,
-    # ring -- is what the step will see); the step is sized from it, and its ratio is reported against it
+    # ring -- is what the step will see); the step is sized from it, and its ratio is reported against it.
+    # Phase 2's step is slower than the feed, so the loader enters this phase with every ring full: the first
+    # batches come out of those rings at kernel speed, not at the feed rate, and a feed timed over them reads
+    # ~4% high on the window path (198.7k vs 191.5k), sizing the step at an effective ratio of ~0.93 instead
+    # of 0.9. _FEED_DRAIN untimed batches (more than the rings of every path hold) empty them first.
     acc = ops.ChecksumAccumulator(dev)
+    for _ in range(_FEED_DRAIN):
+        acc.add(next(it)[0])
     n_feed = max(args.steps, 100)
     sync()
     t0 = time.perf_counter()
@@ -475,7 +484,7 @@ def _pressure_batches(args) -> int:
     """Batches ``pressure_phase`` draws (an upper bound: calibration, tune passes, at most 3 timed loops)."""
     if args.pressure_ratio <= 0:
         return 0
-    return 1 + max(2, args.warmup // 2) + 60 + max(args.steps, 100) + 3 * max(args.steps, 300)
+    return _FEED_DRAIN + 1 + max(2, args.warmup // 2) + 60 + max(args.steps, 100) + 3 * max(args.steps, 300)
 
 
 def _pressure_sub(args, env, dev, it, feed_total: float, barrier, sync, dl=None) -> dict:
