@@ -27,6 +27,7 @@ def run(args, dispatch: str) -> dict:
     from ddl_amd import Marker, ops
     from ddl_amd.models.producers import ImageWindowProducer
     from ddl_amd.models.trainstep import CalibratedStep
+    from ddl_amd.utils.tracing import ComputeIdleMeter
 
     with ddl_amd.start(n_producers=3) as (env, conn):
         dev = torch.device(env.device)
@@ -78,18 +79,30 @@ def run(args, dispatch: str) -> dict:
         for k in host:
             host[k].clear()
         n = args.steps
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
         late = [False] * n
-        for k in range(n):
-            (x,) = next(it)
-            t0 = time.perf_counter()
-            if k > 0:
-                late[k] = evs[k - 1][1].query()  # the GPU already ran out of step k-1 when step k was enqueued
-            evs[k][0].record()
-            step(x)
-            evs[k][1].record()
-            host["step"].append(time.perf_counter() - t0)
-        torch.cuda.synchronize()
+        if args.meter == "bench":  # bench.py's ComputeIdleMeter: a fresh pair of timing events per step
+            meter = ComputeIdleMeter()
+            for k in range(n):
+                (x,) = next(it)
+                t0 = time.perf_counter()
+                meter.step_begin()
+                step(x)
+                meter.step_end()
+                host["step"].append(time.perf_counter() - t0)
+            torch.cuda.synchronize()
+            evs = meter._pairs
+        else:  # events created up front; "late" probes query step k-1's end event before step k is enqueued
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+            for k in range(n):
+                (x,) = next(it)
+                t0 = time.perf_counter()
+                if k > 0 and args.meter == "late":
+                    late[k] = evs[k - 1][1].query()  # the GPU already ran out of step k-1 when step k was enqueued
+                evs[k][0].record()
+                step(x)
+                evs[k][1].record()
+                host["step"].append(time.perf_counter() - t0)
+            torch.cuda.synchronize()
         st = dl.stats()
         dl.close()
     busy = [s.elapsed_time(e) for s, e in evs]
@@ -108,7 +121,8 @@ def run(args, dispatch: str) -> dict:
             "get_us": [round(1e6 * get[j], 1) for j in range(max(0, k - 2), k + 1)],
             "mark_us": [round(1e6 * mark[j], 1) for j in range(max(0, k - 2), min(len(mark), k + 1))],
             "enqueue_us": round(1e6 * enq[k], 1)} for k in top]
-    return {"dispatch": dispatch, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"), "spare_streams": len(spare),
+    return {"dispatch": dispatch, "meter": args.meter, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+            "spare_streams": len(spare),
             "depth": args.depth, "copy_timing": args.copy_timing, "steps": n,
             "feed": round(feed, 1), "ratio_measured": round(1000.0 * 256 / (sum(busy) / n) / feed, 3),
             "idle_pct": round(100.0 * (1.0 - sum(busy) / wall), 3),
@@ -127,6 +141,9 @@ def main() -> int:
     ap.add_argument("--depth", type=int, default=4)
     ap.add_argument("--copy-timing", action="store_true")
     ap.add_argument("--top", type=int, default=8)
+    ap.add_argument("--meter", default="late", choices=["late", "plain", "bench"],
+                    help="late: events made up front + a query of step k-1's end per step; plain: without the "
+                         "query; bench: bench.py's ComputeIdleMeter (events made per step)")
     ap.add_argument("--spare-streams", type=int, default=0,
                     help="idle HIP streams created before the loader's (HIP maps streams round-robin onto "
                          "GPU_MAX_HW_QUEUES hardware queues)")
