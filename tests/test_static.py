@@ -92,3 +92,35 @@ def test_license_file():
     assert text.lstrip().startswith("GNU LESSER GENERAL PUBLIC LICENSE") and "Version 2.1" in text[:200]
     assert "LGPL-2.1" in (ROOT / "pyproject.toml").read_text()
     assert "LGPL-2.1" in (ROOT / "CITATION.cff").read_text()
+
+
+def _expand_braces(path: str) -> list[str]:
+    """``a_{x,y}.json`` -> ``[a_x.json, a_y.json]`` (the docs' shorthand for sibling evidence files)."""
+    import re
+
+    m = re.search(r"\{([^{}]*)\}", path)
+    if m is None:
+        return [path]
+    return [q for opt in m.group(1).split(",") for q in _expand_braces(path[:m.start()] + opt + path[m.end():])]
+
+
+def test_cited_evidence_exists():
+    """Every ``profiles/...`` / ``archive/...`` path the README and docs cite as evidence exists in the tree
+    (brace and glob shorthand allowed; a bare ``r4_tenth/`` continues a range begun with a full path, so it is
+    looked up among the evidence and job directories)."""
+    import re
+
+    docs = [ROOT / "README.md", ROOT / "profiles" / "README.md", *sorted((ROOT / "docs").glob("*.md"))]
+    pat = re.compile(r"`((?:\.\./)?(?:archive/|profiles/|r[1-6]_)[^`\s]*)`")
+    bases = [ROOT, ROOT / "profiles", ROOT / "archive" / "profiles", ROOT / "archive" / "jobs", ROOT / "tools" / "jobs"]
+    missing = []
+    for doc in docs:
+        for m in pat.finditer(doc.read_text()):
+            cited = m.group(1).split("::")[0].rstrip(",.)")
+            names = [p.rstrip("/") for p in _expand_braces(cited)]
+            for base in bases:
+                if any(next(base.glob(n.replace("../", "", 1) if base == ROOT else n), None) for n in names):
+                    break
+            else:
+                missing.append(f"{doc.relative_to(ROOT)}: {cited}")
+    assert not missing, missing
