@@ -115,11 +115,45 @@ class PrefetchedIndexedLoader:
     gather: step-boundary gaps 40 vs 10 us, GPU idle at r = 0.9 2.4% vs 0.7% on the producer path,
     ``profiles/r6_third``), so PCIe-paced loaders hand off on the host; loaders whose batches take
     microseconds keep the device hand-off by default, which never makes the host wait (behind a 1.25 ms step
-    the HBM-resident loader idles 0.88-0.93% that way, 0.81% with ``handoff="host"``, ``profiles/r6_twelfth``;
-    a host hand-off paces a host with no step of its own at the gather rate).
+    the HBM-resident loader idles 0.57% either way since batches come from blocks, ``profiles/r6_twentieth``;
+    0.88-0.93% vs 0.81% before, ``profiles/r6_twelfth``; a host hand-off paces a host with no step of its own
+    at the gather rate).
     """
 
     handoff = "device"
+    block_bytes = 512 << 20  # output batches are carved from blocks of about this size (>= 1 batch, <= 64)
+
+    def _out_batch(self, shape: tuple, dtype) -> torch.Tensor:
+        """An output tensor for one batch, carved (on the current stream: the prep stream) from a block of
+        batches. The caller's stream is recorded on a block once (``__iter__``), not once per batch: the caching
+        allocator then puts one event on the compute stream when the block is freed, instead of one per batch
+        -- each such event is a marker between two steps, and with the zero-copy gather streaming over PCIe a
+        marker costs the compute queue ~14 us (step-boundary gap 32 -> 18 us, idle at r = 0.9 1.69 -> 0.97%
+        without any, ``profiles/r6_nineteenth``). The batch engine's output slots do the same
+        (``engine_dispatch._engine_provide``). A block is freed once every batch carved from it is gone."""
+        n = int(math.prod(shape))
+        blk = self._blk
+        if blk is None or blk[0].dtype != dtype or blk[1] + n > blk[0].numel():
+            per = max(1, min(64, self.block_bytes // max(1, n * torch.empty((), dtype=dtype).element_size())))
+            blk = self._blk = [torch.empty(per * n, dtype=dtype, device=self.device), 0, set()]
+            blk[2].add(streams.current(self.device.index).stream_id)  # the allocating stream
+        cur = streams.current(self.device.index)
+        if cur.stream_id not in blk[2]:  # another prep stream writes into this block: the allocator must know
+            blk[0].record_stream(cur)
+            blk[2].add(cur.stream_id)
+        out = blk[0][blk[1]:blk[1] + n].view(shape)
+        blk[1] += n
+        return out
+
+    def _record_caller(self, batch: torch.Tensor, cur) -> None:
+        """``record_stream`` of the caller's stream on the batch's block (once per block and stream)."""
+        base = batch._base if batch._base is not None else batch
+        rec = self._rec
+        if rec[0] is not base:
+            rec = self._rec = [base, set()]
+        if cur.stream_id not in rec[1]:
+            base.record_stream(cur)
+            rec[1].add(cur.stream_id)
 
     def _init_cursor(self, seed: int, depth: int, n_epochs: int | None, resume_state: dict | None) -> None:
         self.seed = int(seed)
@@ -134,6 +168,8 @@ class PrefetchedIndexedLoader:
         self._generation = 0
         self.batches = 0
         self.host_waits = 0  # host hand-off: batches whose gather was still running when the caller asked
+        self._blk = None  # [block tensor, elements carved] (_out_batch)
+        self._rec = [None, set()]  # [block, caller streams recorded on it] (_record_caller)
 
     def __len__(self) -> int:
         """Batches left in the current epoch."""
@@ -191,7 +227,7 @@ class PrefetchedIndexedLoader:
                         ev.synchronize()  # a gather kernel of this process: it always completes
                 else:
                     cur.wait_event(ev)
-                batch.record_stream(cur)
+                self._record_caller(batch, cur)
             self.cursor = t - self.epoch * bpe
             self._pending = True
             self.batches += 1
@@ -581,7 +617,9 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
                 if self.augment is not None:
                     batch = self._crop(self.shard, e, perm=perm, base=base, n_rows=self.LB)
                 else:
-                    batch = ops.gather_rows(self.shard, perm=perm, base=base, n_rows=self.LB,
+                    out = self._out_batch((self.LB,) + self.sample_shape, self.out_dtype) \
+                        if self.prep_stream is not None else None
+                    batch = ops.gather_rows(self.shard, perm=perm, base=base, n_rows=self.LB, out=out,
                                             out_dtype=self.out_dtype, **kw)
             else:
                 # W split counts on the host (native Feistel over the GB positions, no numpy); the send list
@@ -647,6 +685,7 @@ class ResidentGlobalLoader(PrefetchedIndexedLoader):
         if self.prep_stream is not None:
             self.prep_stream.synchronize()
         self._queue.clear()
+        self._blk, self._rec = None, [None, set()]
         logger.debug("resident loader closed: %s", self.stats())
         self.shard = None
 

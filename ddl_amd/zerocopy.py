@@ -144,7 +144,8 @@ class ZeroCopyLoader(PrefetchedIndexedLoader):
                                    out_dtype=self.out_dtype, **kw), None
         st = self._prep[t % len(self._prep)]
         with streams.on_stream(st):
-            batch = ops.gather_rows(self.rows, perm=self.order.perm(e), base=base, n_rows=self.LB,
+            out = self._out_batch((self.LB,) + self.sample_shape, self.out_dtype)
+            batch = ops.gather_rows(self.rows, perm=self.order.perm(e), base=base, n_rows=self.LB, out=out,
                                     out_dtype=self.out_dtype, max_blocks=self.max_blocks, **kw)
             ev = torch.cuda.Event()
             ev.record(st)
@@ -161,6 +162,7 @@ class ZeroCopyLoader(PrefetchedIndexedLoader):
             for st in self._prep:
                 st.synchronize()
         self._queue.clear()
+        self._blk, self._rec = None, [None, set()]
         if self._reg_base is not None:
             torch.cuda.synchronize(self.device)
             _native.hip().host_unregister(self._reg_base)

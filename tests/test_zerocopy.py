@@ -77,6 +77,33 @@ def test_zerocopy_handoff_modes_deliver_the_same_bytes_behind_a_busy_stream(hand
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("prep_streams", [1, 2])
+def test_batches_carved_from_blocks_stay_intact(prep_streams):
+    """Batches are carved from multi-batch blocks and the consumer's stream is recorded once per block: a batch
+    the consumer holds is never overwritten by later gathers, and a dropped block is reused only after the
+    consumer's reads -- here the consumer's stream is busy before every read, so the gathers run far ahead."""
+    n, shape = 1024, (3, 32, 32)
+    src = (torch.rand((n, *shape)) * 100).to(torch.bfloat16)
+    dl = ZeroCopyLoader(src, 64, seed=3, n_epochs=3, depth=3, prep_streams=prep_streams)
+    dl.block_bytes = 3 * 64 * 3 * 32 * 32 * 2  # 3 batches per block: many blocks, each reused many times
+    order = EpochOrder(n, 64, 3)
+    outs, held, blocks = [], [], 0
+    for e in range(3):
+        idx = torch.from_numpy(order.perm(e).full()[: order.batches_per_epoch * 64]).view(-1, 64)
+        for g, b in enumerate(dl):
+            assert b._base is not None and b._base.numel() == 3 * b.numel()
+            blocks += b.data_ptr() == b._base.data_ptr()
+            torch.cuda._sleep(300_000)  # the consumer reads late
+            outs.append((b.clone(), idx[g]))
+            if g % 4 == 0:
+                held.append((b, idx[g]))  # kept to the end: its block must never be handed out again
+    assert blocks >= len(outs) // 3
+    for got, i in outs + held:
+        assert torch.equal(got.cpu(), src[i])
+    dl.close()
+
+
+@pytest.mark.gpu
 def test_touch_pages_reads_every_page():
     """touch_pages: one 4 B read per page; the per-block xor of the words lands in the sink (the loads are real)."""
     from ddl_amd import _native

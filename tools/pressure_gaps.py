@@ -29,16 +29,35 @@ def run(args, dispatch: str) -> dict:
     from ddl_amd.models.trainstep import CalibratedStep
     from ddl_amd.utils.tracing import ComputeIdleMeter
 
-    with ddl_amd.start(n_producers=3) as (env, conn):
+    if args.no_record_stream:  # A/B only: batches' allocator blocks are then unprotected across streams
+        torch.Tensor.record_stream = lambda self, stream: None
+    with ddl_amd.start(n_producers=3 if args.path == "window" else 0) as (env, conn):
         dev = torch.device(env.device)
         spare = [torch.cuda.Stream(dev) for _ in range(args.spare_streams)]  # shifts the stream -> HW queue map
-        dl = ddl_amd.DistributedDataLoader(
-            ImageWindowProducer(256, (3, 224, 224), "bfloat16", seed=0, refill="stamp"), 256, conn, 10 ** 6,
-            env=env, device=dev, output=ddl_amd.OutputSpec(dtype=torch.bfloat16),
-            order=ddl_amd.OrderSpec(shuffle="device", seed=0),
-            staging=ddl_amd.StagingSpec(prefetch_depth=args.depth, native_dispatch=dispatch,
-                                        copy_timing=args.copy_timing))
         host = {"get": [], "mark": [], "step": []}
+        if args.path == "zero_copy":
+            from ddl_amd.zerocopy import ZeroCopyLoader
+
+            src = torch.empty((4096, 3, 224, 224), dtype=torch.bfloat16).pin_memory()
+            src.view(4096, -1)[:, 0] = torch.arange(4096, dtype=torch.bfloat16)
+            dl = ZeroCopyLoader(src, 256, env, seed=0, out_dtype=torch.bfloat16, device=dev,
+                                max_blocks=args.zc_blocks, handoff="host")
+        else:
+            dl = ddl_amd.DistributedDataLoader(
+                ImageWindowProducer(256, (3, 224, 224), "bfloat16", seed=0, refill="stamp"), 256, conn, 10 ** 6,
+                env=env, device=dev, output=ddl_amd.OutputSpec(dtype=torch.bfloat16),
+                order=ddl_amd.OrderSpec(shuffle="device", seed=0),
+                staging=ddl_amd.StagingSpec(prefetch_depth=args.depth, native_dispatch=dispatch,
+                                            copy_timing=args.copy_timing))
+
+        def zc_batches():
+            while True:
+                t0 = time.perf_counter()
+                for x in dl:
+                    host["get"].append(time.perf_counter() - t0)
+                    host["mark"].append(0.0)
+                    yield (x,)
+                    t0 = time.perf_counter()
 
         def batches():
             while True:
@@ -53,7 +72,7 @@ def run(args, dispatch: str) -> dict:
                     host["mark"].append(time.perf_counter() - t2)
                 dl.mark(Marker.END_OF_EPOCH)
 
-        it = batches()
+        it = zc_batches() if args.path == "zero_copy" else batches()
         acc = ops.ChecksumAccumulator(dev)
         for _ in range(50):
             acc.add(next(it)[0])
@@ -105,6 +124,7 @@ def run(args, dispatch: str) -> dict:
             torch.cuda.synchronize()
         st = dl.stats()
         dl.close()
+        del dl
     busy = [s.elapsed_time(e) for s, e in evs]
     gaps = [1000.0 * evs[k - 1][1].elapsed_time(evs[k][0]) for k in range(1, n)]
     wall = evs[0][0].elapsed_time(evs[-1][1])
@@ -130,7 +150,8 @@ def run(args, dispatch: str) -> dict:
             "late_steps": sum(late), "late_share_of_gap": round(late_gap / max(1e-9, sum(gaps)), 3),
             "host_us_p50": {k: round(1e6 * sorted(v)[len(v) // 2], 1) for k, v in (("get", get), ("mark", mark),
                                                                                   ("enqueue", enq))},
-            "top": ctx, "engine": st.get("native_dispatch")}
+            "top": ctx, "engine": st.get("native_dispatch"), "path": args.path,
+            "record_stream": not args.no_record_stream, "zc_host_waits": st.get("host_waits")}
 
 
 def main() -> int:
@@ -141,6 +162,9 @@ def main() -> int:
     ap.add_argument("--depth", type=int, default=4)
     ap.add_argument("--copy-timing", action="store_true")
     ap.add_argument("--top", type=int, default=8)
+    ap.add_argument("--path", default="window", choices=["window", "zero_copy"])
+    ap.add_argument("--zc-blocks", type=int, default=None)
+    ap.add_argument("--no-record-stream", action="store_true")
     ap.add_argument("--meter", default="late", choices=["late", "plain", "bench"],
                     help="late: events made up front + a query of step k-1's end per step; plain: without the "
                          "query; bench: bench.py's ComputeIdleMeter (events made per step)")
