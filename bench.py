@@ -164,8 +164,18 @@ def self_launch(n: int, argv: list[str]) -> int:
     return rc
 
 
+_T0 = time.perf_counter()
+
+
+def _progress(env, what: str) -> None:
+    """One line on stderr (rank 0) as each phase starts: a run of many phases is never silent for minutes."""
+    if env.rank == 0:
+        print(f"bench: {what} (+{time.perf_counter() - _T0:.1f} s)", file=sys.stderr, flush=True)
+
+
 def phase2(args, env, dev, it, idle_steps: int, barrier, sync) -> dict:
     """GPU idle % behind a fixed-cost bf16 train step (DDP gradient all-reduce over RCCL when N > 1)."""
+    _progress(env, "phase 2: idle behind the PatchMLP step")
     import torch
     import torch.distributed as dist
 
@@ -217,6 +227,7 @@ def pressure_phase(args, env, dev, it, feed_per_rank: float, barrier, sync, dl=N
 
     from ddl_amd import ops
 
+    _progress(env, "pressure phase: step at %.2fx the feed" % args.pressure_ratio)
     r, B = args.pressure_ratio, args.batch
     # the feed this phase runs against: re-measured here over >= 100 batches with the checksum consumer
     # (phase 1's region can be as short as 20 steps, and the loader's state after phase 2 -- copy streams,
@@ -310,6 +321,7 @@ def _timed_feed(args, env, it, acc, barrier, sync, label: str, dl=None) -> tuple
 
     from ddl_amd.utils.tracing import trace_range
 
+    _progress(env, f"feed: {label}")
     for _ in range(args.warmup):
         acc.add(next(it))
     stager = getattr(dl, "_stager", None) if dl is not None else None
@@ -351,6 +363,7 @@ def _timed_feed(args, env, it, acc, barrier, sync, label: str, dl=None) -> tuple
 
 def _idle_behind_step(args, env, dev, it, barrier, sync) -> float | None:
     """GPU idle % behind the PatchMLP step (phase 2's measurement) on the batches of ``it``."""
+    _progress(env, "idle behind the PatchMLP step")
     import torch
     import torch.distributed as dist
 
@@ -596,6 +609,7 @@ def main(argv=None) -> int:
             sync()
 
         # ---------------- phase 1: feed rate
+        _progress(env, f"phase 1: the headline feed over {args.steps} steps")
         for _ in range(args.warmup):
             (x,) = next(it)
             acc.add(x)
