@@ -269,6 +269,7 @@ def pressure_phase(args, env, dev, it, feed_per_rank: float, barrier, sync, dl=N
         # state): then re-size from THIS loop's busy time and time again, at most 3 times. Every rank makes
         # the same decision (MAX over ranks), so all of them fetch the same number of batches.
         attempts += 1
+        _progress(env, f"pressure phase: timed loop {attempts} ({n} steps)")
         meter = ComputeIdleMeter()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         barrier()
