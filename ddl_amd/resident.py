@@ -121,7 +121,7 @@ class PrefetchedIndexedLoader:
     """
 
     handoff = "device"
-    block_bytes = 512 << 20  # output batches are carved from blocks of about this size (>= 1 batch, <= 64)
+    block_bytes = 2 << 30  # output batches are carved from blocks of about this size (>= 1 batch, <= 64)
 
     def _out_batch(self, shape: tuple, dtype) -> torch.Tensor:
         """An output tensor for one batch, carved (on the current stream: the prep stream) from a block of

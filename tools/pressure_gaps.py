@@ -29,6 +29,11 @@ def run(args, dispatch: str) -> dict:
     from ddl_amd.models.trainstep import CalibratedStep
     from ddl_amd.utils.tracing import ComputeIdleMeter
 
+    if args.block_mb:  # output blocks of the batch engine and of the indexed loaders
+        from ddl_amd.engine_dispatch import NativeDispatchMixin
+        from ddl_amd.resident import PrefetchedIndexedLoader
+
+        NativeDispatchMixin.engine_block_bytes = PrefetchedIndexedLoader.block_bytes = args.block_mb << 20
     if args.no_record_stream:  # A/B only: batches' allocator blocks are then unprotected across streams
         torch.Tensor.record_stream = lambda self, stream: None
     with ddl_amd.start(n_producers=3 if args.path == "window" else 0) as (env, conn):
@@ -151,7 +156,8 @@ def run(args, dispatch: str) -> dict:
             "host_us_p50": {k: round(1e6 * sorted(v)[len(v) // 2], 1) for k, v in (("get", get), ("mark", mark),
                                                                                   ("enqueue", enq))},
             "top": ctx, "engine": st.get("native_dispatch"), "path": args.path,
-            "record_stream": not args.no_record_stream, "zc_host_waits": st.get("host_waits")}
+            "record_stream": not args.no_record_stream, "block_mb": args.block_mb,
+            "zc_host_waits": st.get("host_waits")}
 
 
 def main() -> int:
@@ -165,6 +171,7 @@ def main() -> int:
     ap.add_argument("--path", default="window", choices=["window", "zero_copy"])
     ap.add_argument("--zc-blocks", type=int, default=None)
     ap.add_argument("--no-record-stream", action="store_true")
+    ap.add_argument("--block-mb", type=int, default=0, help="output block size (default: the library's)")
     ap.add_argument("--meter", default="late", choices=["late", "plain", "bench"],
                     help="late: events made up front + a query of step k-1's end per step; plain: without the "
                          "query; bench: bench.py's ComputeIdleMeter (events made per step)")
